@@ -1,0 +1,211 @@
+"""Generate the committed golden vectors by running the REFERENCE's own code.
+
+Run in the build container only (it reads /root/reference, which never travels to
+the GPU box):   python tests/golden/make_golden.py
+
+The reference `main.py` is imported with a stub `jiwer` module (jiwer is not
+installed; its `wer` is never called here).  Its `__main__` block does not run.
+Model arithmetic is transformers 5.15.0 `Wav2Vec2ForCTC` on torch 2.10 CPU, fp32,
+eval mode, loaded with the build's seeded synthetic weights (suta_amd.weights),
+so weights are regenerated, not stored (a sha256 digest guards against drift).
+
+Fixtures written next to this file:
+  g1_loss_grad.npz   loss + dL/dlogits through reference forward_and_adapt
+                     (main.py:172-215) with a fake model whose logits are a Parameter
+  g2_adam_mult.npz   reference setup_optimizer('AdamW') (main.py:8-23) stepping a
+                     tensor listed k times (k = 1..5), 3 steps
+  g3_tiny_<variant>.npz  tiny-config episodic SUTA (main.py:327-348): logits after
+                     every step + final trainable tensors
+  g4_base_<N>.npz    base-size (w2v2-base shapes) SUTA, canonical scripts/LS.sh flags:
+                     logits at steps 0,1,3,5,10 + digests of the adapted tensors
+"""
+import contextlib
+import hashlib
+import io
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+import suta_loader  # noqa: E402
+
+suta = suta_loader.load()
+from suta_amd.weights import synth_weights  # noqa: E402
+from suta_amd.config import get_config  # noqa: E402
+
+REF = "/root/reference"
+
+
+def import_reference():
+    jiwer = types.ModuleType("jiwer")
+    jiwer.wer = lambda *a, **k: float("nan")
+    sys.modules["jiwer"] = jiwer
+    sys.path.insert(0, REF)
+    import main as ref  # noqa: E402
+    sys.path.remove(REF)
+    return ref
+
+
+def weights_digest(sd):
+    h = hashlib.sha256()
+    for k in sorted(sd):
+        h.update(k.encode())
+        h.update(np.ascontiguousarray(sd[k], dtype=np.float32).tobytes())
+    return h.hexdigest()
+
+
+def wave(n, i=0, seed=20260415):
+    """Synthetic utterance then HF processor normalisation."""
+    x = np.random.default_rng(seed + i).standard_normal(n, dtype=np.float32) * np.float32(0.05)
+    return ((x - x.mean()) / np.sqrt(x.var() + 1e-7)).astype(np.float32)
+
+
+class _FakeLogits(torch.nn.Module):
+    def __init__(self, L):
+        super().__init__()
+        self.L = torch.nn.Parameter(L.clone())
+
+    def forward(self, x):
+        return types.SimpleNamespace(logits=self.L * 1)
+
+
+def g1(ref):
+    cases = []
+    rng = np.random.default_rng(1)
+    # (name, T, em, reweight, non_blank, div, blank_shift)
+    specs = [("canon_T1", 1, 0.3, True, True, 0.0, 0.0), ("canon_T7", 7, 0.3, True, True, 0.0, 0.0),
+             ("canon_T49", 49, 0.3, True, True, 0.0, 0.0), ("canon_T399", 399, 0.3, True, True, 0.0, 0.0),
+             ("allblank_T49", 49, 0.3, True, True, 0.0, 50.0),
+             ("em1_T49", 49, 1.0, False, True, 0.0, 0.0), ("em0_T49", 49, 0.0, True, False, 0.0, 0.0),
+             ("noblankmask_T49", 49, 0.5, False, False, 0.0, 0.0), ("div_T49", 49, 0.3, True, True, 0.4, 0.0),
+             ("mixed_T120", 120, 0.3, True, True, 0.0, 1.5)]
+    out = {}
+    for name, T, em, rw, nb, div, shift in specs:
+        L = (rng.standard_normal((1, T, 32)) * 3).astype(np.float32)
+        L[..., 0] += shift
+        for dt in (torch.float32, torch.float64):
+            fake = _FakeLogits(torch.from_numpy(L).to(dt))
+            grads, losses = [], []
+            fake.L.register_post_accumulate_grad_hook(lambda p: grads.append(p.grad.detach().clone()))
+            orig = torch.Tensor.backward
+
+            def bw(self, *a, **k):
+                losses.append(self.detach().clone())
+                return orig(self, *a, **k)
+            torch.Tensor.backward = bw
+            try:
+                opt = torch.optim.SGD([fake.L], lr=1.0)
+                ref.forward_and_adapt(None, fake, opt, em, rw, 2.5, nb, None, div)
+            finally:
+                torch.Tensor.backward = orig
+            tag = "f32" if dt == torch.float32 else "f64"
+            out[f"{name}/logits"] = L[0]
+            out[f"{name}/grad_{tag}"] = grads[0][0].numpy()
+            out[f"{name}/loss_{tag}"] = np.array(losses[0].item())
+        out[f"{name}/hp"] = np.array([2.5, em, float(rw), float(nb), div])
+        cases.append(name)
+    out["cases"] = np.array(cases)
+    np.savez_compressed(os.path.join(HERE, "g1_loss_grad.npz"), **out)
+
+
+def g2(ref):
+    out = {}
+    rng = np.random.default_rng(2)
+    p0 = rng.standard_normal(7).astype(np.float32)
+    gs = rng.standard_normal((3, 7)).astype(np.float32)
+    out["p0"], out["grads"] = p0, gs
+    for k in range(1, 6):
+        p = torch.nn.Parameter(torch.from_numpy(p0.copy()))
+        with contextlib.redirect_stdout(io.StringIO()):
+            opt, _ = ref.setup_optimizer([p] * k, "AdamW", 1e-3)
+        traj = []
+        for s in range(3):
+            p.grad = torch.from_numpy(gs[s].copy())
+            opt.step()
+            traj.append(p.detach().numpy().copy())
+        out[f"k{k}"] = np.stack(traj)
+    np.savez_compressed(os.path.join(HERE, "g2_adam_mult.npz"), **out)
+
+
+def run_ref_suta(ref, cfg, sd, x, steps, lr, train_feature=True, bias_only=False, em=0.3, rw=True, nb=True,
+                 temp=2.5, div=0.0, record=None):
+    from transformers import Wav2Vec2Config, Wav2Vec2ForCTC
+    torch.manual_seed(0)
+    model = Wav2Vec2ForCTC(Wav2Vec2Config(**cfg)).eval()
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+    model = ref.configure_model(model)
+    with contextlib.redirect_stdout(io.StringIO()):
+        params, names = ref.collect_params(model, bias_only, train_feature, False, True)
+        opt, sch = ref.setup_optimizer(params, "AdamW", lr, scheduler=None)
+    xt = torch.from_numpy(x)[None]
+    logits = {}
+    with torch.no_grad():
+        logits[0] = model(xt).logits[0].numpy().copy()                    # main.py:331-332
+    for i in range(steps):                                                 # main.py:347-348
+        o = ref.forward_and_adapt(xt, model, opt, em, rw, temp, nb, sch, div)
+        if record is None or (i + 1) in record:
+            logits[i + 1] = o[0].detach().numpy().copy()
+    sdf = model.state_dict()
+    uniq = list(dict.fromkeys(names))
+    return logits, {n: sdf[n].numpy().copy() for n in uniq}, names
+
+
+def g3(ref):
+    variants = [("group", "tiny-group", dict(lr=2e-5)), ("group_lr5e-4", "tiny-group", dict(lr=5e-4)),
+                ("layer", "tiny-layer", dict(lr=2e-5)), ("layer_lr5e-4", "tiny-layer", dict(lr=5e-4)),
+                ("group_lnonly", "tiny-group", dict(lr=5e-4, train_feature=False)),
+                ("group_biasonly", "tiny-group", dict(lr=5e-4, bias_only=True)),
+                ("group_em1", "tiny-group", dict(lr=5e-4, em=1.0, rw=False, nb=False, div=0.2))]
+    for vname, preset, kw in variants:
+        cfg = get_config(preset)
+        sd = synth_weights(cfg)
+        out = {"weights_sha256": np.array(weights_digest(sd))}
+        hp = dict(lr=kw.get("lr"), train_feature=kw.get("train_feature", True), bias_only=kw.get("bias_only", False),
+                  em=kw.get("em", 0.3), rw=kw.get("rw", True), nb=kw.get("nb", True), temp=2.5,
+                  div=kw.get("div", 0.0))
+        out["hp_json"] = np.array(repr(hp))
+        for j, n in enumerate((8000, 12345)):
+            x = wave(n, j)
+            logits, final, names = run_ref_suta(ref, cfg, sd, x, 10, **hp)
+            out[f"N{n}/x"] = x
+            out[f"N{n}/logits"] = np.stack([logits[i] for i in range(11)])
+            for k, v in final.items():
+                out[f"N{n}/final/{k}"] = v
+        out["entries"] = np.array(names)
+        np.savez_compressed(os.path.join(HERE, f"g3_tiny_{vname}.npz"), **out)
+        print("g3", vname, "done")
+
+
+def g4(ref):
+    cfg = get_config("wav2vec2-base")
+    sd = synth_weights(cfg)
+    rec = (1, 3, 5, 10)
+    for j, n in enumerate((16000, 32000)):
+        x = wave(n, j)
+        logits, final, names = run_ref_suta(ref, cfg, sd, x, 10, lr=2e-5, record=rec)
+        out = {"weights_sha256": np.array(weights_digest(sd)), "x_sha256": np.array(hashlib.sha256(x.tobytes()).hexdigest())}
+        out["steps"] = np.array((0,) + rec)
+        out["logits"] = np.stack([logits[i] for i in (0,) + rec])
+        idx_rng = np.random.default_rng(4)
+        for k, v in final.items():
+            flat = v.reshape(-1)
+            idx = np.sort(idx_rng.choice(flat.size, size=min(64, flat.size), replace=False))
+            out[f"final/{k}/idx"] = idx
+            out[f"final/{k}/val"] = flat[idx]
+            out[f"final/{k}/sum"] = np.array(flat.astype(np.float64).sum())
+            out[f"final/{k}/delta_abs_sum"] = np.array(np.abs(flat.astype(np.float64) - sd[k].reshape(-1)).sum())
+        np.savez_compressed(os.path.join(HERE, f"g4_base_{n}.npz"), **out)
+        print("g4", n, "done")
+
+
+if __name__ == "__main__":
+    torch.set_num_threads(8)
+    ref = import_reference()
+    which = sys.argv[1:] or ["g1", "g2", "g3", "g4"]
+    for w in which:
+        globals()[w](ref)

@@ -1,0 +1,32 @@
+"""Shared parity tolerances.
+
+Logits: absolute tolerance stated per test (fp32 end-to-end; the survey's probe measured
+fp32-vs-fp64 logits within 1.04e-5 after 10 steps on a base-size random model).
+
+Adapted tensors: Adam divides the first moment by the root of the second, so a
+gradient element whose true value is ~0 is stepped by up to +-lr per sub-step
+whatever its sign.  Two implementations that differ only in fp32 rounding
+therefore agree to rounding on almost every element but may differ by up to a few
+Adam steps on a handful.  The check bounds both: the fraction of elements outside
+a tight tolerance, and the worst element against the Adam step budget.
+"""
+import numpy as np
+
+
+def assert_params_close(actual, desired, lr, steps, tight=2e-6, max_frac=0.005, name=""):
+    a = np.asarray(actual, dtype=np.float64).reshape(-1)
+    d = np.asarray(desired, dtype=np.float64).reshape(-1)
+    diff = np.abs(a - d)
+    frac = float(np.mean(diff > tight)) if diff.size else 0.0
+    budget = 2.0 * lr * steps * 5 + tight          # <= 5 sub-steps per step (max multiplicity)
+    assert frac <= max_frac, f"{name}: {frac:.4%} elements differ by > {tight} (max {diff.max():.3g})"
+    assert diff.max() <= budget, f"{name}: max |diff| {diff.max():.3g} exceeds Adam step budget {budget:.3g}"
+
+
+def logits_tol(lr):
+    """Absolute logits tolerance after up to 10 SUTA steps at learning rate lr.
+
+    Oracle-vs-reference on the tiny goldens measured <= 2.6e-6 at lr 2e-5 and <= 3.7e-5 at
+    lr 5e-4 (adaptation moves logits by ~5 there), so fp32 reordering noise grows with lr.
+    """
+    return 2e-5 + 0.2 * lr

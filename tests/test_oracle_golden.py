@@ -1,0 +1,129 @@
+"""Pin the CPU oracle (oracle/) against golden vectors made by the reference's own code.
+
+Fixtures: tests/golden/make_golden.py (reference main.py imported with a jiwer stub).
+"""
+import ast
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import w2v2_cpu as W
+from oracle.suta_loss_np import suta_loss_and_grad
+from suta_amd.config import get_config
+from suta_amd.weights import synth_weights
+from tests.parity import assert_params_close, logits_tol
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+G = os.path.join(HERE, "golden")
+
+
+def _load(name):
+    return np.load(os.path.join(G, name), allow_pickle=False)
+
+
+def test_g1_closed_form_loss_grad_matches_reference():
+    z = _load("g1_loss_grad.npz")
+    for case in z["cases"]:
+        L = z[f"{case}/logits"]
+        temp, em, rw, nb, div = z[f"{case}/hp"]
+        loss, g = suta_loss_and_grad(L, temp, em, bool(rw), bool(nb), div)
+        ref_g = z[f"{case}/grad_f64"]
+        ref_loss = float(z[f"{case}/loss_f64"])
+        np.testing.assert_allclose(g, ref_g, rtol=1e-9, atol=1e-14, err_msg=case)
+        if np.isnan(ref_loss):
+            assert np.isnan(loss), case
+        else:
+            assert abs(loss - ref_loss) <= 1e-10 * max(1, abs(ref_loss)), case
+        # the fp32 reference grad is within fp32 rounding of the exact one
+        np.testing.assert_allclose(z[f"{case}/grad_f32"], ref_g, rtol=0, atol=max(2e-6 * np.abs(ref_g).max(), 1e-8), err_msg=case)
+
+
+def test_g1_allblank_is_nan_loss_finite_grad():
+    z = _load("g1_loss_grad.npz")
+    assert np.isnan(float(z["allblank_T49/loss_f32"]))
+    assert np.isfinite(z["allblank_T49/grad_f32"]).all()
+
+
+def test_g1_torch_restatement_matches_reference():
+    z = _load("g1_loss_grad.npz")
+    for case in z["cases"]:
+        L = torch.tensor(z[f"{case}/logits"][None], dtype=torch.float64, requires_grad=True)
+        temp, em, rw, nb, div = z[f"{case}/hp"]
+        loss = W.suta_loss(L, em, bool(rw), temp, bool(nb), div)
+        loss.backward()
+        np.testing.assert_allclose(L.grad[0].numpy(), z[f"{case}/grad_f64"], rtol=1e-12, atol=1e-15, err_msg=case)
+
+
+def test_g2_adam_multiplicity():
+    z = _load("g2_adam_mult.npz")
+    for k in range(1, 6):
+        p = {"w": torch.from_numpy(z["p0"].copy())}
+        st = W.AdamState(["w"], p)
+        for s in range(3):
+            W.adam_step(p, {"w": torch.from_numpy(z["grads"][s].copy())}, st, ["w"] * k, lr=1e-3)
+            np.testing.assert_array_equal(p["w"].numpy(), z[f"k{k}"][s], err_msg=f"k={k} step={s}")
+
+
+def test_collect_params_multiplicity_base():
+    """96 entries / 63 unique / 4 633 856 elements for base + --train_feature."""
+    cfg = get_config("wav2vec2-base")
+    e = W.trainable_entries(cfg, train_feature=True)
+    shapes = dict(__import__("suta_amd.config", fromlist=["param_shapes"]).param_shapes(cfg))
+    assert len(e) == 96
+    u = list(dict.fromkeys(e))
+    assert len(u) == 63
+    assert sum(int(np.prod(shapes[n])) for n in u) == 4633856
+    m = W.multiplicity(e)
+    assert m["wav2vec2.feature_extractor.conv_layers.3.conv.weight"] == 4
+    assert m["wav2vec2.feature_extractor.conv_layers.0.layer_norm.bias"] == 4
+    assert m["wav2vec2.feature_projection.layer_norm.weight"] == 3
+    assert m["wav2vec2.feature_projection.projection.weight"] == 2
+    assert m["wav2vec2.encoder.layers.5.final_layer_norm.bias"] == 1
+
+
+@pytest.mark.parametrize("variant", ["group", "group_lr5e-4", "layer", "layer_lr5e-4", "group_lnonly",
+                                     "group_biasonly", "group_em1"])
+def test_g3_tiny_suta_oracle_matches_reference(variant):
+    z = _load(f"g3_tiny_{variant}.npz")
+    preset = "tiny-group" if variant.startswith("group") else "tiny-layer"
+    cfg = get_config(preset)
+    sd = synth_weights(cfg)
+    from tests.golden.make_golden import weights_digest  # noqa
+    assert weights_digest(sd) == str(z["weights_sha256"]), "seeded weight generator drifted"
+    hp = ast.literal_eval(str(z["hp_json"]))
+    entries = W.trainable_entries(cfg, bias_only=hp["bias_only"], train_feature=hp["train_feature"])
+    assert entries == [str(s) for s in z["entries"]]
+    params = {k: torch.from_numpy(v) for k, v in sd.items()}
+    for n in (8000, 12345):
+        x = torch.from_numpy(z[f"N{n}/x"])[None]
+        out, final = W.run_suta(params, cfg, x, 10, lr=hp["lr"], temp=hp["temp"], em_coef=hp["em"],
+                                reweight=hp["rw"], non_blank=hp["nb"], div_coef=hp["div"],
+                                train_feature=hp["train_feature"], bias_only=hp["bias_only"])
+        ref = z[f"N{n}/logits"]
+        for i in range(11):
+            np.testing.assert_allclose(out[i][0].numpy(), ref[i], rtol=0, atol=logits_tol(hp["lr"]), err_msg=f"{variant} N{n} step {i}")
+        for k, v in final.items():
+            assert_params_close(v.numpy(), z[f"N{n}/final/{k}"], hp["lr"], 10, name=k)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("n", [16000])
+def test_g4_base_oracle_matches_reference(n):
+    path = os.path.join(G, f"g4_base_{n}.npz")
+    if not os.path.exists(path):
+        pytest.skip("g4 fixture missing")
+    z = _load(f"g4_base_{n}.npz")
+    cfg = get_config("wav2vec2-base")
+    sd = synth_weights(cfg)
+    params = {k: torch.from_numpy(v) for k, v in sd.items()}
+    from tests.golden.make_golden import wave
+    x = torch.from_numpy(wave(n, 0 if n == 16000 else 1))[None]
+    steps = [int(s) for s in z["steps"]]
+    out, final = W.run_suta(params, cfg, x, 10, record=steps)
+    for j, s in enumerate(steps):
+        np.testing.assert_allclose(out[s][0].numpy(), z["logits"][j], rtol=0, atol=5e-5, err_msg=f"step {s}")
+    for k, v in final.items():
+        idx = z[f"final/{k}/idx"]
+        assert_params_close(v.numpy().reshape(-1)[idx], z[f"final/{k}/val"], 2e-5, 10, max_frac=0.05, name=k)
