@@ -1,0 +1,84 @@
+// Shared device helpers and kernel launcher declarations for libsuta (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define SUTA_WAVE 64
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ float gelu_f(float x) {
+    return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+}
+__device__ __forceinline__ float dgelu_f(float x) {
+    // d/dx [x Phi(x)] = Phi(x) + x phi(x)
+    const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+    const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
+    return cdf + x * pdf;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// ------------------------------------------------------------------------------------------
+// GEMM:  C[z](m,n) = epi( sum_k A[z](m,k) * B[z](k,n) )         (fp32 in, fp32 MFMA accumulate)
+//   A(m,k) = A[m*lda + k]   (ta = 0)   or A[k*lda + m]   (ta = 1)
+//   conv A mode (ta = 0, segK > 0): k = seg*segK + r, A(m,k) = A[(m + seg - pad)*lda + r],
+//        zero unless 0 <= m + seg - pad < Mvalid   (implicit grouped/positional conv)
+//   B(k,n) = B[k*ldb + n]   (tb = 0)   or B[n*ldb + k]   (tb = 1)
+//   batch z in [0, Z): pointer += (z / zdiv) * s?1 + (z % zdiv) * s?0
+// epilogue flags, applied in this order:  v = alpha*acc; +bias[n]; +C(acc) ; C2 = v (store pre);
+//   GELU; *gelu'(aux(m,n)); +R(m,n); C = v
+// ------------------------------------------------------------------------------------------
+enum {
+    EPI_BIAS = 1,
+    EPI_GELU = 2,
+    EPI_RESID = 4,
+    EPI_STORE_PRE = 8,
+    EPI_DGELU = 16,
+    EPI_ACCUM = 32,
+};
+
+struct GemmParams {
+    const float* A;
+    const float* B;
+    float* C;
+    int M, N, K;
+    long lda, ldb, ldc;
+    int Z, zdiv;
+    long sA0, sA1, sB0, sB1, sC0, sC1;
+    int ta, tb;
+    int segK, pad, Mvalid;  // conv-A mode when segK > 0
+    const float* bias;
+    long sBias0, sBias1;
+    const float* R;
+    long ldr, sR0, sR1;
+    const float* aux;
+    long ldaux, sAux0, sAux1;
+    float* C2;
+    long ldc2, sC20, sC21;
+    float alpha;
+    int epi;
+    // internal
+    int splits, kchunk;
+    float* ws;  // split-K workspace
+    int va, vb; // vector (16 B) loads legal
+};
+
+void gemm_init(GemmParams& p);
+// Launch; ws/ws_floats: scratch for split-K (may be null -> no split).
+void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats);

@@ -1,0 +1,1480 @@
+// libsuta engine: the SUTA adapt loop (reference main.py:172-215, 327-398) on gfx950.
+//
+// Per batch of utterances (same length, one slot each) the engine runs, per step:
+//   forward with saved activations -> fused entropy+MCC loss-and-grad -> hand-written backward
+//   (dX through every frozen op, dW only for collect_params' tensors) -> AdamW with the
+//   duplicate-entry multiplicity -> next step's forward doubles as this step's re-inference.
+// Layout: every activation is time-major [utterance][frame][channel] in HBM; trainable tensors
+// of slot b live in one flat buffer P[b][Pn] (conv weights stored [k][c_in][c_out] so every
+// conv layer is a strided-row GEMM); frozen encoder weights are shared by all slots.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/suta.h"
+#include "common.h"
+#include "ops.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+struct SutaError : std::runtime_error {
+    int code;
+    SutaError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define HIPCHK(x)                                                                                        \
+    do {                                                                                                 \
+        hipError_t _e = (x);                                                                             \
+        if (_e != hipSuccess)                                                                            \
+            throw SutaError(_e == hipErrorOutOfMemory ? SUTA_ERR_OOM : SUTA_ERR_HIP,                      \
+                            std::string(#x) + ": " + hipGetErrorString(_e));                             \
+    } while (0)
+
+inline long rup(long a, long b) { return (a + b - 1) / b * b; }
+
+// shortest decimal of a float, read back as a double (0.9f -> 0.9)
+inline double py_double(float f) {
+    char buf[48];
+    snprintf(buf, sizeof buf, "%.9g", (double)f);
+    double best = atof(buf);
+    for (int prec = 1; prec <= 9; ++prec) {
+        snprintf(buf, sizeof buf, "%.*g", prec, (double)f);
+        const double d = atof(buf);
+        if ((float)d == f) {
+            best = d;
+            break;
+        }
+    }
+    return best;
+}
+
+struct Cfg {
+    int H, L, NH, F, V, nconv;
+    int C[SUTA_MAX_CONV], K[SUTA_MAX_CONV], S[SUTA_MAX_CONV];
+    int conv_bias, layer_mode, stable, posK, posG;
+    float eps;
+};
+
+// trainable tensor descriptor
+struct TP {
+    std::string name;
+    std::vector<long> shape;  // HF shape
+    long off = 0, numel = 0;
+    bool conv_w = false;      // stored permuted [k][cin][cout]
+    bool ln_member = false;   // belongs to an nn.LayerNorm module
+    bool is_bias = false;
+    int feat_depth = 0;       // feature-branch module count containing it (train_feature)
+};
+
+enum Fam { F_GEMM = 0, F_SOFTMAX = 1, F_NORM = 2, F_EW = 3, F_LOSS = 4, F_ADAM = 5, NFAM = 6 };
+
+struct DevBuf {
+    float* p = nullptr;
+    size_t bytes = 0;
+    void alloc(size_t b) {
+        if (b <= bytes) return;
+        if (p) HIPCHK(hipFree(p));
+        p = nullptr;
+        bytes = 0;
+        HIPCHK(hipMalloc(&p, b));
+        bytes = b;
+    }
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+};
+
+struct Arena {
+    char* base = nullptr;
+    size_t off = 0, cap = 0;
+    bool dry = true;
+    template <typename T>
+    T* take(size_t n) {
+        off = rup(off, 256);
+        T* r = dry ? nullptr : reinterpret_cast<T*>(base + off);
+        off += n * sizeof(T);
+        return r;
+    }
+};
+
+struct LayerBufs {
+    float *x_in, *xhat1, *rstd1, *y1, *qkv, *P, *hmid, *xhat2, *rstd2, *y2, *u, *x_out;
+};
+
+struct Plan {
+    int B = 0;
+    long N = 0;
+    int Lc[SUTA_MAX_CONV];
+    int T = 0, Tp = 0;
+    // forward
+    float *xraw, *x;
+    float *z[SUTA_MAX_CONV], *a[SUTA_MAX_CONV], *cxhat[SUTA_MAX_CONV], *crstd[SUTA_MAX_CONV];
+    float *gn_mean, *gn_rstd;
+    float *fp_xhat, *fp_rstd, *fp_y, *h0, *pz, *e, *enc_xhat, *enc_rstd, *enc_y;
+    std::vector<LayerBufs> lay;
+    float *ctx, *gu, *rtmp, *logits;
+    // backward
+    float *dlogits, *d1, *d2, *d3, *dqkv, *dP, *du, *dzc, *dzc2, *dcol, *lnpart, *loss, *loss_scratch;
+    double* dpart;
+    int* ids;
+    float* splitws;
+    long splitws_floats;
+    size_t bytes;
+};
+
+}  // namespace
+
+struct suta_engine {
+    Cfg c;
+    int device = 0;
+    hipStream_t st = nullptr;
+    int max_batch = 0;
+    long max_samples = 0;
+    // frozen weights
+    std::vector<float*> wqkv, bqkv, wo, bo, w1, b1, w2, b2;
+    float *wpos_f = nullptr, *wpos_b = nullptr, *bpos = nullptr, *wlm = nullptr, *blm = nullptr;
+    // trainable
+    std::vector<TP> tps;
+    std::map<std::string, int> tpi;
+    long Pn = 0;
+    float *P0 = nullptr, *P = nullptr, *G = nullptr, *Mo = nullptr, *Vo = nullptr;
+    long opt_steps = 0;
+    // offsets of trainable pieces
+    long o_cw[SUTA_MAX_CONV], o_cb[SUTA_MAX_CONV], o_cg[SUTA_MAX_CONV], o_cbeta[SUTA_MAX_CONV];
+    long o_fpg, o_fpb, o_pw, o_pb, o_eg, o_eb;
+    std::vector<long> o_l1g, o_l1b, o_l2g, o_l2b;
+    // workspace
+    DevBuf ws;
+    Plan plan;
+    // timing
+    bool timing = false;
+    double fam_ms[NFAM] = {0};
+    long fam_n[NFAM] = {0};
+    std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
+    std::vector<hipEvent_t> evpool;
+    bool use_graphs = true;
+    std::vector<float*> owned;
+
+    ~suta_engine();
+
+    // ---------------- helpers ----------------
+    float* dalloc(long n) {
+        float* p = nullptr;
+        HIPCHK(hipMalloc(&p, std::max<long>(n, 1) * sizeof(float)));
+        owned.push_back(p);
+        return p;
+    }
+    hipEvent_t ev() {
+        if (!evpool.empty()) {
+            hipEvent_t e = evpool.back();
+            evpool.pop_back();
+            return e;
+        }
+        hipEvent_t e;
+        HIPCHK(hipEventCreate(&e));
+        return e;
+    }
+    template <typename Fn>
+    void timed(int fam, Fn&& fn) {
+        if (!timing) {
+            fn();
+            return;
+        }
+        hipEvent_t a = ev(), b = ev();
+        HIPCHK(hipEventRecord(a, st));
+        fn();
+        HIPCHK(hipEventRecord(b, st));
+        pending.push_back({fam, {a, b}});
+    }
+    void collect_timing() {
+        for (auto& pe : pending) {
+            float ms = 0.f;
+            HIPCHK(hipEventSynchronize(pe.second.second));
+            HIPCHK(hipEventElapsedTime(&ms, pe.second.first, pe.second.second));
+            fam_ms[pe.first] += ms;
+            fam_n[pe.first] += 1;
+            evpool.push_back(pe.second.first);
+            evpool.push_back(pe.second.second);
+        }
+        pending.clear();
+    }
+    void gemm(const GemmParams& p) {
+        timed(F_GEMM, [&] { gemm_launch(p, st, plan.splitws, plan.splitws_floats); });
+    }
+
+    int multiplicity(const TP& t, int train_feature, int bias_only) const {
+        int k = 0;
+        if (t.ln_member && (!bias_only || t.is_bias)) k += 1;
+        if (train_feature) k += t.feat_depth;
+        return k;
+    }
+
+    void build_plan(int B, long N);
+    void forward(int B);
+    void backward(int B, const suta_hparams& hp);
+    void adam(int B, const suta_hparams& hp);
+    void reset_slots(int B);
+    void stage_input(const float* wav, int on_dev, int norm, int B, long N);
+};
+
+suta_engine::~suta_engine() {
+    for (float* p : owned) (void)hipFree(p);
+    for (auto& pe : pending) {
+        (void)hipEventDestroy(pe.second.first);
+        (void)hipEventDestroy(pe.second.second);
+    }
+    for (auto e : evpool) (void)hipEventDestroy(e);
+    if (st) (void)hipStreamDestroy(st);
+}
+
+// ----------------------------------------------------------------------------------------------
+// workspace plan
+// ----------------------------------------------------------------------------------------------
+void suta_engine::build_plan(int B, long N) {
+    if (plan.B == B && plan.N == N) return;
+    const Cfg& k = c;
+    Plan pl;
+    pl.B = B;
+    pl.N = N;
+    long L = N;
+    for (int i = 0; i < k.nconv; ++i) {
+        L = (L - k.K[i]) / k.S[i] + 1;
+        if (L < 1) throw SutaError(SUTA_ERR_ARG, "utterance too short for the conv feature encoder");
+        pl.Lc[i] = (int)L;
+    }
+    pl.T = pl.Lc[k.nconv - 1];
+    pl.Tp = (int)rup(pl.T, 4);
+    if (pl.T > 2048) throw SutaError(SUTA_ERR_UNSUPPORTED, "T > 2048 frames (max 600000 samples in the reference)");
+    const long T = pl.T, H = k.H, BT = (long)B * T;
+    long maxLC = 0, maxcol = 0;
+    for (int i = 0; i < k.nconv; ++i) {
+        maxLC = std::max(maxLC, (long)pl.Lc[i] * k.C[i]);
+        if (i > 0) maxcol = std::max(maxcol, (long)pl.Lc[i] * k.K[i] * k.C[i - 1]);
+    }
+    for (int pass = 0; pass < 2; ++pass) {
+        Arena ar;
+        ar.dry = pass == 0;
+        ar.base = reinterpret_cast<char*>(ws.p);
+        pl.xraw = ar.take<float>((size_t)B * N);
+        pl.x = ar.take<float>((size_t)B * N);
+        for (int i = 0; i < k.nconv; ++i) {
+            const long n = (long)B * pl.Lc[i] * k.C[i];
+            pl.z[i] = ar.take<float>(n);
+            pl.a[i] = ar.take<float>(n);
+            if (k.layer_mode) {
+                pl.cxhat[i] = ar.take<float>(n);
+                pl.crstd[i] = ar.take<float>((size_t)B * pl.Lc[i]);
+            } else {
+                pl.cxhat[i] = pl.crstd[i] = nullptr;
+            }
+        }
+        pl.gn_mean = ar.take<float>((size_t)B * k.C[0]);
+        pl.gn_rstd = ar.take<float>((size_t)B * k.C[0]);
+        const long C6 = k.C[k.nconv - 1];
+        pl.fp_xhat = ar.take<float>(BT * C6);
+        pl.fp_rstd = ar.take<float>(BT);
+        pl.fp_y = ar.take<float>(BT * C6);
+        pl.h0 = ar.take<float>(BT * H);
+        pl.pz = ar.take<float>(BT * H);
+        pl.e = ar.take<float>(BT * H);
+        pl.enc_xhat = ar.take<float>(BT * H);
+        pl.enc_rstd = ar.take<float>(BT);
+        pl.enc_y = ar.take<float>(BT * H);
+        pl.lay.assign(k.L, LayerBufs{});
+        const long Psz = (long)B * k.NH * T * pl.Tp;
+        for (int l = 0; l < k.L; ++l) {
+            LayerBufs& lb = pl.lay[l];
+            lb.xhat1 = ar.take<float>(BT * H);
+            lb.rstd1 = ar.take<float>(BT);
+            lb.y1 = ar.take<float>(BT * H);
+            lb.qkv = ar.take<float>(BT * 3 * H);
+            lb.P = ar.take<float>(Psz);
+            lb.hmid = k.stable ? ar.take<float>(BT * H) : nullptr;
+            lb.xhat2 = ar.take<float>(BT * H);
+            lb.rstd2 = ar.take<float>(BT);
+            lb.y2 = k.stable ? ar.take<float>(BT * H) : nullptr;
+            lb.u = ar.take<float>(BT * k.F);
+            lb.x_out = ar.take<float>(BT * H);
+        }
+        for (int l = 0; l < k.L; ++l) {
+            pl.lay[l].x_in = l == 0 ? (k.stable ? pl.e : pl.enc_y) : pl.lay[l - 1].x_out;
+            if (!k.stable) pl.lay[l].y2 = pl.lay[l].x_out;
+        }
+        pl.ctx = ar.take<float>(BT * H);
+        pl.gu = ar.take<float>(BT * k.F);
+        pl.rtmp = ar.take<float>(BT * H);
+        pl.logits = ar.take<float>(BT * k.V);
+        pl.dlogits = ar.take<float>(BT * k.V);
+        pl.d1 = ar.take<float>(BT * H);
+        pl.d2 = ar.take<float>(BT * H);
+        pl.d3 = ar.take<float>(BT * H);
+        pl.dqkv = ar.take<float>(BT * 3 * H);
+        pl.dP = ar.take<float>(Psz);
+        pl.du = ar.take<float>(BT * k.F);
+        pl.dzc = ar.take<float>((size_t)B * maxLC);
+        pl.dzc2 = ar.take<float>((size_t)B * maxLC);
+        pl.dcol = ar.take<float>((size_t)B * std::max(maxcol, 1L));
+        const long lnrows = std::max<long>(pl.Lc[0], T);
+        pl.lnpart = ar.take<float>((size_t)B * ((lnrows + 31) / 32) * 2 * std::max<long>(H, maxLC / pl.Lc[0] + 1) + 64);
+        pl.dpart = ar.take<double>((size_t)B * ((pl.Lc[0] + 127) / 128 + 2) * 2 * k.C[0] + (size_t)B * k.C[0] * 2);
+        pl.loss = ar.take<float>(B);
+        pl.loss_scratch = ar.take<float>((size_t)B * T * 66 + 64);
+        pl.ids = ar.take<int>((size_t)BT);
+        pl.splitws_floats = 32L << 20;
+        pl.splitws = ar.take<float>(pl.splitws_floats);
+        pl.bytes = ar.off;
+        if (pass == 0) ws.alloc(ar.off + 256);
+    }
+    plan = pl;
+}
+
+// ----------------------------------------------------------------------------------------------
+// forward (saves everything the backward needs)
+// ----------------------------------------------------------------------------------------------
+void suta_engine::forward(int B) {
+    const Cfg& k = c;
+    Plan& pl = plan;
+    const int T = pl.T, H = k.H, NH = k.NH, d = H / NH;
+    const long BT = (long)B * T;
+    // conv0
+    timed(F_EW, [&] {
+        launch_conv0(pl.x, pl.N, P + o_cw[0], k.conv_bias ? P + o_cb[0] : nullptr, Pn, pl.z[0], B, pl.Lc[0], k.C[0],
+                     k.K[0], k.S[0], st);
+    });
+    if (!k.layer_mode) {
+        timed(F_NORM, [&] {
+            launch_col_stats(pl.z[0], B, pl.Lc[0], k.C[0], 1e-5f, pl.dpart, pl.gn_mean, pl.gn_rstd, st);
+            launch_gn_apply_gelu(pl.z[0], pl.gn_mean, pl.gn_rstd, P + o_cg[0], P + o_cbeta[0], Pn, pl.a[0], B,
+                                 pl.Lc[0], k.C[0], st);
+        });
+    } else {
+        timed(F_NORM, [&] {
+            launch_layernorm_fwd(pl.z[0], P + o_cg[0], P + o_cbeta[0], Pn, pl.Lc[0], pl.a[0], pl.cxhat[0],
+                                 pl.crstd[0], B * pl.Lc[0], k.C[0], 1e-5f, 1, st);
+        });
+    }
+    for (int i = 1; i < k.nconv; ++i) {
+        GemmParams g;
+        gemm_init(g);
+        g.A = pl.a[i - 1];
+        g.lda = (long)k.S[i] * k.C[i - 1];
+        g.M = pl.Lc[i];
+        g.K = k.K[i] * k.C[i - 1];
+        g.N = k.C[i];
+        g.B = P + o_cw[i];
+        g.ldb = k.C[i];
+        g.Z = B;
+        g.sA1 = (long)pl.Lc[i - 1] * k.C[i - 1];
+        g.sB1 = Pn;
+        g.sC1 = (long)pl.Lc[i] * k.C[i];
+        if (k.conv_bias) {
+            g.epi |= EPI_BIAS;
+            g.bias = P + o_cb[i];
+            g.sBias1 = Pn;
+        }
+        if (!k.layer_mode) {
+            g.C = pl.a[i];
+            g.ldc = k.C[i];
+            g.epi |= EPI_STORE_PRE | EPI_GELU;
+            g.C2 = pl.z[i];
+            g.ldc2 = k.C[i];
+            g.sC21 = g.sC1;
+            gemm(g);
+        } else {
+            g.C = pl.z[i];
+            g.ldc = k.C[i];
+            gemm(g);
+            timed(F_NORM, [&] {
+                launch_layernorm_fwd(pl.z[i], P + o_cg[i], P + o_cbeta[i], Pn, pl.Lc[i], pl.a[i], pl.cxhat[i],
+                                     pl.crstd[i], B * pl.Lc[i], k.C[i], 1e-5f, 1, st);
+            });
+        }
+    }
+    const int C6 = k.C[k.nconv - 1];
+    const float* feat = pl.a[k.nconv - 1];
+    timed(F_NORM, [&] {
+        launch_layernorm_fwd(feat, P + o_fpg, P + o_fpb, Pn, T, pl.fp_y, pl.fp_xhat, pl.fp_rstd, (int)BT, C6, k.eps, 0,
+                             st);
+    });
+    {  // projection (per-utterance trainable W, b)
+        GemmParams g;
+        gemm_init(g);
+        g.A = pl.fp_y;
+        g.lda = C6;
+        g.B = P + o_pw;
+        g.tb = 1;
+        g.ldb = C6;
+        g.C = pl.h0;
+        g.ldc = H;
+        g.M = T;
+        g.N = H;
+        g.K = C6;
+        g.Z = B;
+        g.sA1 = (long)T * C6;
+        g.sB1 = Pn;
+        g.sC1 = (long)T * H;
+        g.epi = EPI_BIAS;
+        g.bias = P + o_pb;
+        g.sBias1 = Pn;
+        gemm(g);
+    }
+    {  // positional conv: e = h0 + gelu(posconv(h0)); pz = pre-activation
+        const int Cg = H / k.posG;
+        GemmParams g;
+        gemm_init(g);
+        g.A = pl.h0;
+        g.lda = H;
+        g.segK = Cg;
+        g.pad = k.posK / 2;
+        g.Mvalid = T;
+        g.M = T;
+        g.N = Cg;
+        g.K = k.posK * Cg;
+        g.Z = B * k.posG;
+        g.zdiv = k.posG;
+        g.sA0 = Cg;
+        g.sA1 = (long)T * H;
+        g.B = wpos_f;
+        g.ldb = Cg;
+        g.sB0 = (long)k.posK * Cg * Cg;
+        g.C = pl.e;
+        g.ldc = H;
+        g.sC0 = Cg;
+        g.sC1 = (long)T * H;
+        g.epi = EPI_BIAS | EPI_STORE_PRE | EPI_GELU | EPI_RESID;
+        g.bias = bpos;
+        g.sBias0 = Cg;
+        g.C2 = pl.pz;
+        g.ldc2 = H;
+        g.sC20 = Cg;
+        g.sC21 = (long)T * H;
+        g.R = pl.h0;
+        g.ldr = H;
+        g.sR0 = Cg;
+        g.sR1 = (long)T * H;
+        gemm(g);
+    }
+    if (!k.stable) {
+        timed(F_NORM, [&] {
+            launch_layernorm_fwd(pl.e, P + o_eg, P + o_eb, Pn, T, pl.enc_y, pl.enc_xhat, pl.enc_rstd, (int)BT, H,
+                                 k.eps, 0, st);
+        });
+    }
+    const float scale = 1.0f / std::sqrt((float)d);
+    for (int l = 0; l < k.L; ++l) {
+        LayerBufs& lb = pl.lay[l];
+        const float* attn_in = lb.x_in;
+        if (k.stable) {
+            timed(F_NORM, [&] {
+                launch_layernorm_fwd(lb.x_in, P + o_l1g[l], P + o_l1b[l], Pn, T, lb.y1, lb.xhat1, lb.rstd1, (int)BT, H,
+                                     k.eps, 0, st);
+            });
+            attn_in = lb.y1;
+        }
+        {  // fused QKV
+            GemmParams g;
+            gemm_init(g);
+            g.A = attn_in;
+            g.lda = H;
+            g.B = wqkv[l];
+            g.tb = 1;
+            g.ldb = H;
+            g.C = lb.qkv;
+            g.ldc = 3 * H;
+            g.M = (int)BT;
+            g.N = 3 * H;
+            g.K = H;
+            g.epi = EPI_BIAS;
+            g.bias = bqkv[l];
+            gemm(g);
+        }
+        {  // S = Q K^T * scale
+            GemmParams g;
+            gemm_init(g);
+            g.A = lb.qkv;
+            g.lda = 3 * H;
+            g.B = lb.qkv + H;
+            g.tb = 1;
+            g.ldb = 3 * H;
+            g.C = lb.P;
+            g.ldc = pl.Tp;
+            g.M = T;
+            g.N = T;
+            g.K = d;
+            g.Z = B * NH;
+            g.zdiv = NH;
+            g.sA0 = d;
+            g.sA1 = (long)T * 3 * H;
+            g.sB0 = d;
+            g.sB1 = (long)T * 3 * H;
+            g.sC0 = (long)T * pl.Tp;
+            g.sC1 = (long)NH * T * pl.Tp;
+            g.alpha = scale;
+            gemm(g);
+        }
+        timed(F_SOFTMAX, [&] { launch_softmax_rows(lb.P, (long)B * NH * T, T, pl.Tp, st); });
+        {  // ctx = P V
+            GemmParams g;
+            gemm_init(g);
+            g.A = lb.P;
+            g.lda = pl.Tp;
+            g.B = lb.qkv + 2 * H;
+            g.ldb = 3 * H;
+            g.C = pl.ctx;
+            g.ldc = H;
+            g.M = T;
+            g.N = d;
+            g.K = T;
+            g.Z = B * NH;
+            g.zdiv = NH;
+            g.sA0 = (long)T * pl.Tp;
+            g.sA1 = (long)NH * T * pl.Tp;
+            g.sB0 = d;
+            g.sB1 = (long)T * 3 * H;
+            g.sC0 = d;
+            g.sC1 = (long)T * H;
+            gemm(g);
+        }
+        {  // out projection + residual
+            GemmParams g;
+            gemm_init(g);
+            g.A = pl.ctx;
+            g.lda = H;
+            g.B = wo[l];
+            g.tb = 1;
+            g.ldb = H;
+            g.C = k.stable ? lb.hmid : pl.rtmp;
+            g.ldc = H;
+            g.M = (int)BT;
+            g.N = H;
+            g.K = H;
+            g.epi = EPI_BIAS | EPI_RESID;
+            g.bias = bo[l];
+            g.R = lb.x_in;
+            g.ldr = H;
+            gemm(g);
+        }
+        const float* ffn_in;
+        const float* ffn_res;
+        float* ffn_out;
+        if (k.stable) {
+            timed(F_NORM, [&] {
+                launch_layernorm_fwd(lb.hmid, P + o_l2g[l], P + o_l2b[l], Pn, T, lb.y2, lb.xhat2, lb.rstd2, (int)BT, H,
+                                     k.eps, 0, st);
+            });
+            ffn_in = lb.y2;
+            ffn_res = lb.hmid;
+            ffn_out = lb.x_out;
+        } else {
+            timed(F_NORM, [&] {
+                launch_layernorm_fwd(pl.rtmp, P + o_l1g[l], P + o_l1b[l], Pn, T, lb.y1, lb.xhat1, lb.rstd1, (int)BT, H,
+                                     k.eps, 0, st);
+            });
+            ffn_in = lb.y1;
+            ffn_res = lb.y1;
+            ffn_out = pl.rtmp;
+        }
+        {  // u = in W1^T + b1 (stored), gu = gelu(u)
+            GemmParams g;
+            gemm_init(g);
+            g.A = ffn_in;
+            g.lda = H;
+            g.B = w1[l];
+            g.tb = 1;
+            g.ldb = H;
+            g.C = pl.gu;
+            g.ldc = k.F;
+            g.M = (int)BT;
+            g.N = k.F;
+            g.K = H;
+            g.epi = EPI_BIAS | EPI_STORE_PRE | EPI_GELU;
+            g.bias = b1[l];
+            g.C2 = lb.u;
+            g.ldc2 = k.F;
+            gemm(g);
+        }
+        {  // out = gu W2^T + b2 + residual
+            GemmParams g;
+            gemm_init(g);
+            g.A = pl.gu;
+            g.lda = k.F;
+            g.B = w2[l];
+            g.tb = 1;
+            g.ldb = k.F;
+            g.C = ffn_out;
+            g.ldc = H;
+            g.M = (int)BT;
+            g.N = H;
+            g.K = k.F;
+            g.epi = EPI_BIAS | EPI_RESID;
+            g.bias = b2[l];
+            g.R = ffn_res;
+            g.ldr = H;
+            gemm(g);
+        }
+        if (!k.stable) {
+            timed(F_NORM, [&] {
+                launch_layernorm_fwd(pl.rtmp, P + o_l2g[l], P + o_l2b[l], Pn, T, lb.x_out, lb.xhat2, lb.rstd2, (int)BT,
+                                     H, k.eps, 0, st);
+            });
+        }
+    }
+    const float* hfin = pl.lay[k.L - 1].x_out;
+    if (k.stable) {
+        timed(F_NORM, [&] {
+            launch_layernorm_fwd(hfin, P + o_eg, P + o_eb, Pn, T, pl.enc_y, pl.enc_xhat, pl.enc_rstd, (int)BT, H, k.eps,
+                                 0, st);
+        });
+        hfin = pl.enc_y;
+    }
+    {  // lm_head
+        GemmParams g;
+        gemm_init(g);
+        g.A = hfin;
+        g.lda = H;
+        g.B = wlm;
+        g.tb = 1;
+        g.ldb = H;
+        g.C = pl.logits;
+        g.ldc = k.V;
+        g.M = (int)BT;
+        g.N = k.V;
+        g.K = H;
+        g.epi = EPI_BIAS;
+        g.bias = blm;
+        gemm(g);
+    }
+}
+
+// ----------------------------------------------------------------------------------------------
+// backward: grads of the trainable tensors into G[b] (fully overwritten for every k > 0 tensor)
+// ----------------------------------------------------------------------------------------------
+void suta_engine::backward(int B, const suta_hparams& hp) {
+    const Cfg& k = c;
+    Plan& pl = plan;
+    const int T = pl.T, H = k.H, NH = k.NH, d = H / NH;
+    const long BT = (long)B * T;
+    const float scale = 1.0f / std::sqrt((float)d);
+    LossHP lh{hp.temp, hp.em_coef, hp.div_coef, hp.reweight, hp.non_blank};
+    timed(F_LOSS, [&] { launch_suta_loss(pl.logits, B, T, k.V, lh, pl.dlogits, pl.loss, pl.loss_scratch, st); });
+
+    auto nn_gemm = [&](const float* A, int lda, const float* Bm, int ldb, float* C, int ldc, int M, int N, int K,
+                       int epi, const float* R, int ldr, const float* aux, int ldaux) {
+        GemmParams g;
+        gemm_init(g);
+        g.A = A;
+        g.lda = lda;
+        g.B = Bm;
+        g.ldb = ldb;
+        g.C = C;
+        g.ldc = ldc;
+        g.M = M;
+        g.N = N;
+        g.K = K;
+        g.epi = epi;
+        g.R = R;
+        g.ldr = ldr;
+        g.aux = aux;
+        g.ldaux = ldaux;
+        gemm(g);
+    };
+    // d hfin = dlogits @ Wlm
+    nn_gemm(pl.dlogits, k.V, wlm, H, pl.d1, H, (int)BT, H, k.V, 0, nullptr, 0, nullptr, 0);
+    float* dx = pl.d1;  // grad wrt current residual stream
+    float* t1 = pl.d2;
+    float* t2 = pl.d3;
+    if (k.stable) {
+        timed(F_NORM, [&] {
+            launch_layernorm_bwd(dx, pl.enc_xhat, pl.enc_rstd, P + o_eg, P + o_eb, Pn, T, B, H, 0, nullptr, nullptr, t1,
+                                 G + o_eg, G + o_eb, Pn, pl.lnpart, st);
+        });
+        std::swap(dx, t1);
+    }
+    for (int l = k.L - 1; l >= 0; --l) {
+        LayerBufs& lb = pl.lay[l];
+        float* dhres;  // grad flowing into the attention-block output (residual point)
+        if (!k.stable) {
+            // dr2 = LN2 bwd(dx)
+            timed(F_NORM, [&] {
+                launch_layernorm_bwd(dx, lb.xhat2, lb.rstd2, P + o_l2g[l], P + o_l2b[l], Pn, T, B, H, 0, nullptr,
+                                     nullptr, t1, G + o_l2g[l], G + o_l2b[l], Pn, pl.lnpart, st);
+            });
+            // du = (dr2 @ W2) * gelu'(u)
+            nn_gemm(t1, H, w2[l], k.F, pl.du, k.F, (int)BT, k.F, H, EPI_DGELU, nullptr, 0, lb.u, k.F);
+            // dh1 = du @ W1 + dr2
+            nn_gemm(pl.du, k.F, w1[l], H, t2, H, (int)BT, H, k.F, EPI_RESID, t1, H, nullptr, 0);
+            // dr1 = LN1 bwd(dh1)
+            timed(F_NORM, [&] {
+                launch_layernorm_bwd(t2, lb.xhat1, lb.rstd1, P + o_l1g[l], P + o_l1b[l], Pn, T, B, H, 0, nullptr,
+                                     nullptr, t1, G + o_l1g[l], G + o_l1b[l], Pn, pl.lnpart, st);
+            });
+            dhres = t1;  // dr1
+        } else {
+            // du = (dx @ W2) * gelu'(u); dy2 = du @ W1; dhmid = LN2 bwd(dy2) + dx
+            nn_gemm(dx, H, w2[l], k.F, pl.du, k.F, (int)BT, k.F, H, EPI_DGELU, nullptr, 0, lb.u, k.F);
+            nn_gemm(pl.du, k.F, w1[l], H, t2, H, (int)BT, H, k.F, 0, nullptr, 0, nullptr, 0);
+            timed(F_NORM, [&] {
+                launch_layernorm_bwd(t2, lb.xhat2, lb.rstd2, P + o_l2g[l], P + o_l2b[l], Pn, T, B, H, 0, nullptr, dx,
+                                     t1, G + o_l2g[l], G + o_l2b[l], Pn, pl.lnpart, st);
+            });
+            dhres = t1;  // dhmid
+        }
+        // dctx = dhres @ Wo
+        nn_gemm(dhres, H, wo[l], H, pl.ctx, H, (int)BT, H, H, 0, nullptr, 0, nullptr, 0);
+        {  // dP = dctx_h @ V_h^T
+            GemmParams g;
+            gemm_init(g);
+            g.A = pl.ctx;
+            g.lda = H;
+            g.B = lb.qkv + 2 * H;
+            g.tb = 1;
+            g.ldb = 3 * H;
+            g.C = pl.dP;
+            g.ldc = pl.Tp;
+            g.M = T;
+            g.N = T;
+            g.K = d;
+            g.Z = B * NH;
+            g.zdiv = NH;
+            g.sA0 = d;
+            g.sA1 = (long)T * H;
+            g.sB0 = d;
+            g.sB1 = (long)T * 3 * H;
+            g.sC0 = (long)T * pl.Tp;
+            g.sC1 = (long)NH * T * pl.Tp;
+            gemm(g);
+        }
+        timed(F_SOFTMAX, [&] { launch_softmax_bwd_rows(lb.P, pl.dP, (long)B * NH * T, T, pl.Tp, scale, st); });
+        {  // dQ = dS K_h
+            GemmParams g;
+            gemm_init(g);
+            g.A = pl.dP;
+            g.lda = pl.Tp;
+            g.B = lb.qkv + H;
+            g.ldb = 3 * H;
+            g.C = pl.dqkv;
+            g.ldc = 3 * H;
+            g.M = T;
+            g.N = d;
+            g.K = T;
+            g.Z = B * NH;
+            g.zdiv = NH;
+            g.sA0 = (long)T * pl.Tp;
+            g.sA1 = (long)NH * T * pl.Tp;
+            g.sB0 = d;
+            g.sB1 = (long)T * 3 * H;
+            g.sC0 = d;
+            g.sC1 = (long)T * 3 * H;
+            gemm(g);
+        }
+        {  // dK = dS^T Q_h
+            GemmParams g;
+            gemm_init(g);
+            g.A = pl.dP;
+            g.ta = 1;
+            g.lda = pl.Tp;
+            g.B = lb.qkv;
+            g.ldb = 3 * H;
+            g.C = pl.dqkv + H;
+            g.ldc = 3 * H;
+            g.M = T;
+            g.N = d;
+            g.K = T;
+            g.Z = B * NH;
+            g.zdiv = NH;
+            g.sA0 = (long)T * pl.Tp;
+            g.sA1 = (long)NH * T * pl.Tp;
+            g.sB0 = d;
+            g.sB1 = (long)T * 3 * H;
+            g.sC0 = d;
+            g.sC1 = (long)T * 3 * H;
+            gemm(g);
+        }
+        {  // dV = P^T dctx_h
+            GemmParams g;
+            gemm_init(g);
+            g.A = lb.P;
+            g.ta = 1;
+            g.lda = pl.Tp;
+            g.B = pl.ctx;
+            g.ldb = H;
+            g.C = pl.dqkv + 2 * H;
+            g.ldc = 3 * H;
+            g.M = T;
+            g.N = d;
+            g.K = T;
+            g.Z = B * NH;
+            g.zdiv = NH;
+            g.sA0 = (long)T * pl.Tp;
+            g.sA1 = (long)NH * T * pl.Tp;
+            g.sB0 = d;
+            g.sB1 = (long)T * H;
+            g.sC0 = d;
+            g.sC1 = (long)T * 3 * H;
+            gemm(g);
+        }
+        if (!k.stable) {
+            // dx_in = dqkv @ Wqkv + dr1
+            nn_gemm(pl.dqkv, 3 * H, wqkv[l], H, t2, H, (int)BT, H, 3 * H, EPI_RESID, dhres, H, nullptr, 0);
+            std::swap(dx, t2);
+        } else {
+            // dy1 = dqkv @ Wqkv ; dx_in = LN1 bwd(dy1) + dhmid
+            nn_gemm(pl.dqkv, 3 * H, wqkv[l], H, t2, H, (int)BT, H, 3 * H, 0, nullptr, 0, nullptr, 0);
+            timed(F_NORM, [&] {
+                launch_layernorm_bwd(t2, lb.xhat1, lb.rstd1, P + o_l1g[l], P + o_l1b[l], Pn, T, B, H, 0, nullptr, dhres,
+                                     dx, G + o_l1g[l], G + o_l1b[l], Pn, pl.lnpart, st);
+            });
+            // dx now holds grad wrt x_in; t1/t2 free
+        }
+    }
+    // encoder input
+    float* de = dx;
+    if (!k.stable) {
+        timed(F_NORM, [&] {
+            launch_layernorm_bwd(dx, pl.enc_xhat, pl.enc_rstd, P + o_eg, P + o_eb, Pn, T, B, H, 0, nullptr, nullptr, t1,
+                                 G + o_eg, G + o_eb, Pn, pl.lnpart, st);
+        });
+        de = t1;
+    }
+    float* dpz = (de == pl.d1) ? pl.d2 : (de == pl.d2 ? pl.d3 : pl.d1);
+    float* dh0 = (dpz == pl.d1 || de == pl.d1) ? ((dpz == pl.d2 || de == pl.d2) ? pl.d3 : pl.d2) : pl.d1;
+    timed(F_EW, [&] { launch_dgelu_mul(de, pl.pz, dpz, BT * H, st); });
+    {  // dh0 = posconv^T(dpz) + de
+        const int Cg = H / k.posG;
+        GemmParams g;
+        gemm_init(g);
+        g.A = dpz;
+        g.lda = H;
+        g.segK = Cg;
+        g.pad = k.posK - 1 - k.posK / 2;
+        g.Mvalid = T;
+        g.M = T;
+        g.N = Cg;
+        g.K = k.posK * Cg;
+        g.Z = B * k.posG;
+        g.zdiv = k.posG;
+        g.sA0 = Cg;
+        g.sA1 = (long)T * H;
+        g.B = wpos_b;
+        g.ldb = Cg;
+        g.sB0 = (long)k.posK * Cg * Cg;
+        g.C = dh0;
+        g.ldc = H;
+        g.sC0 = Cg;
+        g.sC1 = (long)T * H;
+        g.epi = EPI_RESID;
+        g.R = de;
+        g.ldr = H;
+        g.sR0 = Cg;
+        g.sR1 = (long)T * H;
+        gemm(g);
+    }
+    const int C6 = k.C[k.nconv - 1];
+    if (hp.train_feature) {
+        {  // dWproj = dh0^T fp_y  (per utterance)
+            GemmParams g;
+            gemm_init(g);
+            g.A = dh0;
+            g.ta = 1;
+            g.lda = H;
+            g.B = pl.fp_y;
+            g.ldb = C6;
+            g.C = G + o_pw;
+            g.ldc = C6;
+            g.M = H;
+            g.N = C6;
+            g.K = T;
+            g.Z = B;
+            g.sA1 = (long)T * H;
+            g.sB1 = (long)T * C6;
+            g.sC1 = Pn;
+            gemm(g);
+        }
+        timed(F_NORM, [&] { launch_colsum(dh0, B, T, H, G + o_pb, Pn, pl.lnpart, st); });
+    }
+    {  // d fp_y = dh0 @ Wproj  (per utterance W)
+        GemmParams g;
+        gemm_init(g);
+        g.A = dh0;
+        g.lda = H;
+        g.B = P + o_pw;
+        g.ldb = C6;
+        g.C = pl.dzc;
+        g.ldc = C6;
+        g.M = T;
+        g.N = C6;
+        g.K = H;
+        g.Z = B;
+        g.sA1 = (long)T * H;
+        g.sB1 = Pn;
+        g.sC1 = (long)T * C6;
+        gemm(g);
+    }
+    const int last = k.nconv - 1;
+    // feature-projection LN bwd; in group mode also * gelu'(z_last) => dz_last
+    float* cur = pl.dzc2;
+    timed(F_NORM, [&] {
+        launch_layernorm_bwd(pl.dzc, pl.fp_xhat, pl.fp_rstd, P + o_fpg, P + o_fpb, Pn, T, B, C6, 0,
+                             (!k.layer_mode && hp.train_feature) ? pl.z[last] : nullptr, nullptr, cur, G + o_fpg,
+                             G + o_fpb, Pn, pl.lnpart, st);
+    });
+    if (!hp.train_feature) return;
+    float* other = pl.dzc;
+    for (int i = last; i >= 1; --i) {
+        // cur: group mode -> dz_i ; layer mode -> da_i
+        if (k.layer_mode) {
+            timed(F_NORM, [&] {
+                launch_layernorm_bwd(cur, pl.cxhat[i], pl.crstd[i], P + o_cg[i], P + o_cbeta[i], Pn, pl.Lc[i], B,
+                                     k.C[i], 1, nullptr, nullptr, other, G + o_cg[i], G + o_cbeta[i], Pn, pl.lnpart,
+                                     st);
+            });
+            std::swap(cur, other);
+        }
+        if (k.conv_bias)
+            timed(F_NORM, [&] { launch_colsum(cur, B, pl.Lc[i], k.C[i], G + o_cb[i], Pn, pl.lnpart, st); });
+        {  // dW_i = im2col(a_{i-1})^T dz_i
+            GemmParams g;
+            gemm_init(g);
+            g.A = pl.a[i - 1];
+            g.ta = 1;
+            g.lda = (long)k.S[i] * k.C[i - 1];
+            g.M = k.K[i] * k.C[i - 1];
+            g.K = pl.Lc[i];
+            g.B = cur;
+            g.ldb = k.C[i];
+            g.N = k.C[i];
+            g.C = G + o_cw[i];
+            g.ldc = k.C[i];
+            g.Z = B;
+            g.sA1 = (long)pl.Lc[i - 1] * k.C[i - 1];
+            g.sB1 = (long)pl.Lc[i] * k.C[i];
+            g.sC1 = Pn;
+            gemm(g);
+        }
+        {  // dcol = dz_i W_i^T
+            GemmParams g;
+            gemm_init(g);
+            g.A = cur;
+            g.lda = k.C[i];
+            g.M = pl.Lc[i];
+            g.K = k.C[i];
+            g.B = P + o_cw[i];
+            g.tb = 1;
+            g.ldb = k.C[i];
+            g.N = k.K[i] * k.C[i - 1];
+            g.C = pl.dcol;
+            g.ldc = (long)k.K[i] * k.C[i - 1];
+            g.Z = B;
+            g.sA1 = (long)pl.Lc[i] * k.C[i];
+            g.sB1 = Pn;
+            g.sC1 = (long)pl.Lc[i] * k.K[i] * k.C[i - 1];
+            gemm(g);
+        }
+        const float* zprev = (!k.layer_mode && i - 1 >= 1) ? pl.z[i - 1] : nullptr;
+        timed(F_EW, [&] {
+            launch_col2im(pl.dcol, B, pl.Lc[i], pl.Lc[i - 1], k.C[i - 1], k.K[i], k.S[i], zprev, other, st);
+        });
+        std::swap(cur, other);
+    }
+    // conv0: cur = da0
+    if (!k.layer_mode) {
+        timed(F_NORM, [&] {
+            launch_gn_gelu_bwd(cur, pl.z[0], pl.gn_mean, pl.gn_rstd, P + o_cg[0], P + o_cbeta[0], Pn, other,
+                               G + o_cg[0], G + o_cbeta[0], Pn, B, pl.Lc[0], k.C[0], pl.dpart, st);
+        });
+    } else {
+        timed(F_NORM, [&] {
+            launch_layernorm_bwd(cur, pl.cxhat[0], pl.crstd[0], P + o_cg[0], P + o_cbeta[0], Pn, pl.Lc[0], B, k.C[0], 1,
+                                 nullptr, nullptr, other, G + o_cg[0], G + o_cbeta[0], Pn, pl.lnpart, st);
+        });
+        if (k.conv_bias)
+            timed(F_NORM, [&] { launch_colsum(other, B, pl.Lc[0], k.C[0], G + o_cb[0], Pn, pl.lnpart, st); });
+    }
+    {  // dW0[k][c] = sum_t x[S0 t + k] dz0[t][c]
+        GemmParams g;
+        gemm_init(g);
+        g.A = pl.x;
+        g.ta = 1;
+        g.lda = k.S[0];
+        g.M = k.K[0];
+        g.K = pl.Lc[0];
+        g.B = other;
+        g.ldb = k.C[0];
+        g.N = k.C[0];
+        g.C = G + o_cw[0];
+        g.ldc = k.C[0];
+        g.Z = B;
+        g.sA1 = pl.N;
+        g.sB1 = (long)pl.Lc[0] * k.C[0];
+        g.sC1 = Pn;
+        gemm(g);
+    }
+}
+
+void suta_engine::adam(int B, const suta_hparams& hp) {
+    AdamArgs a{};
+    // Python floats are doubles: recover the decimal the caller meant (0.9f -> 0.9) so the
+    // scalars match torch's double-precision host arithmetic (adam.py:495-510)
+    const double lr = py_double(hp.lr), b1 = py_double(hp.beta1), b2 = py_double(hp.beta2);
+    a.beta1 = (float)b1;
+    a.beta2 = (float)b2;
+    a.omb1 = (float)(1.0 - b1);
+    a.omb2 = (float)(1.0 - b2);
+    a.eps = (float)py_double(hp.adam_eps);
+    a.lr_wd = (float)(lr * py_double(hp.weight_decay));
+    // runs of equal multiplicity over the flat layout
+    a.nruns = 0;
+    int kmax = 0;
+    for (const TP& t : tps) {
+        const int m = multiplicity(t, hp.train_feature, hp.bias_only);
+        kmax = std::max(kmax, m);
+        if (m == 0) continue;
+        if (a.nruns > 0 && a.runs[a.nruns - 1].k == m && a.runs[a.nruns - 1].start + a.runs[a.nruns - 1].len == t.off) {
+            a.runs[a.nruns - 1].len += t.numel;
+        } else {
+            if (a.nruns >= SUTA_MAX_RUNS) throw SutaError(SUTA_ERR_UNSUPPORTED, "too many Adam runs");
+            a.runs[a.nruns++] = AdamRun{t.off, t.numel, m};
+        }
+    }
+    if (kmax > 5) throw SutaError(SUTA_ERR_UNSUPPORTED, "multiplicity > 5");
+    for (int kk = 1; kk <= 5; ++kk)
+        for (int j = 1; j <= kk; ++j) {
+            const double t = (double)(opt_steps * kk + j);
+            const double bc1 = 1.0 - std::pow(b1, t);
+            const double bc2 = 1.0 - std::pow(b2, t);
+            a.step_size[kk - 1][j - 1] = (float)(lr / bc1);
+            a.bc2_sqrt[kk - 1][j - 1] = (float)std::sqrt(bc2);
+        }
+    timed(F_ADAM, [&] { launch_adam(P, G, Mo, Vo, Pn, B, a, st); });
+    opt_steps += 1;
+}
+
+void suta_engine::reset_slots(int B) {
+    for (int b = 0; b < B; ++b)
+        HIPCHK(hipMemcpyAsync(P + (long)b * Pn, P0, Pn * sizeof(float), hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipMemsetAsync(Mo, 0, (size_t)B * Pn * sizeof(float), st));
+    HIPCHK(hipMemsetAsync(Vo, 0, (size_t)B * Pn * sizeof(float), st));
+    opt_steps = 0;
+}
+
+void suta_engine::stage_input(const float* wav, int on_dev, int norm, int B, long N) {
+    HIPCHK(hipMemcpyAsync(plan.xraw, wav, (size_t)B * N * sizeof(float),
+                          on_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
+    if (norm) timed(F_EW, [&] { launch_wave_normalize(plan.xraw, plan.x, B, N, st); });
+    else HIPCHK(hipMemcpyAsync(plan.x, plan.xraw, (size_t)B * N * sizeof(float), hipMemcpyDeviceToDevice, st));
+}
+
+// ==============================================================================================
+// C ABI
+// ==============================================================================================
+namespace {
+
+template <typename Fn>
+int32_t guard(Fn&& fn) {
+    try {
+        fn();
+        return SUTA_OK;
+    } catch (const SutaError& e) {
+        g_err = e.what();
+        return e.code;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return SUTA_ERR_ARG;
+    }
+}
+
+Cfg make_cfg(const suta_model_config* m) {
+    Cfg c{};
+    c.H = m->hidden_size;
+    c.L = m->num_hidden_layers;
+    c.NH = m->num_attention_heads;
+    c.F = m->intermediate_size;
+    c.V = m->vocab_size;
+    c.nconv = m->num_conv_layers;
+    if (c.nconv < 2 || c.nconv > SUTA_MAX_CONV) throw SutaError(SUTA_ERR_ARG, "num_conv_layers out of range");
+    for (int i = 0; i < c.nconv; ++i) {
+        c.C[i] = m->conv_dim[i];
+        c.K[i] = m->conv_kernel[i];
+        c.S[i] = m->conv_stride[i];
+        if (c.C[i] % 4 || c.C[i] <= 0) throw SutaError(SUTA_ERR_UNSUPPORTED, "conv_dim must be a multiple of 4");
+    }
+    if (c.K[0] > 16) throw SutaError(SUTA_ERR_UNSUPPORTED, "conv0 kernel > 16");
+    c.conv_bias = m->conv_bias;
+    c.layer_mode = m->feat_extract_norm_layer;
+    c.stable = m->do_stable_layer_norm;
+    c.posK = m->num_conv_pos_embeddings;
+    c.posG = m->num_conv_pos_embedding_groups;
+    c.eps = m->layer_norm_eps;
+    if (c.H % c.NH || c.H % c.posG) throw SutaError(SUTA_ERR_ARG, "hidden_size not divisible by heads/groups");
+    if ((c.H / c.posG) % 16) throw SutaError(SUTA_ERR_UNSUPPORTED, "pos-conv group width must be a multiple of 16");
+    if (c.V > 64) throw SutaError(SUTA_ERR_UNSUPPORTED, "vocab_size > 64");
+    if (c.H > 1024 || c.C[c.nconv - 1] > 1024) throw SutaError(SUTA_ERR_UNSUPPORTED, "hidden > 1024");
+    return c;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* suta_last_error(void) { return g_err.c_str(); }
+
+int32_t suta_num_frames(const suta_model_config* cfg, int64_t n, int64_t* out) {
+    return guard([&] {
+        long L = n;
+        for (int i = 0; i < cfg->num_conv_layers; ++i) L = (L - cfg->conv_kernel[i]) / cfg->conv_stride[i] + 1;
+        *out = L;
+    });
+}
+
+int32_t suta_create(const suta_model_config* cfg, const char* const* names, const float* const* data,
+                    const int64_t* numels, int32_t n, int32_t device, int32_t max_batch, int64_t max_samples,
+                    suta_engine** out) {
+    return guard([&] {
+        if (!cfg || !out || max_batch < 1) throw SutaError(SUTA_ERR_ARG, "null argument");
+        std::unique_ptr<suta_engine> e(new suta_engine());
+        e->c = make_cfg(cfg);
+        const Cfg& c = e->c;
+        e->device = device;
+        e->max_batch = max_batch;
+        e->max_samples = max_samples;
+        HIPCHK(hipSetDevice(device));
+        HIPCHK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
+        std::map<std::string, std::pair<const float*, long>> w;
+        for (int i = 0; i < n; ++i) w[names[i]] = {data[i], numels[i]};
+        auto get = [&](const std::string& nm, long numel) -> const float* {
+            auto it = w.find(nm);
+            if (it == w.end()) throw SutaError(SUTA_ERR_ARG, "missing weight " + nm);
+            if (it->second.second != numel)
+                throw SutaError(SUTA_ERR_ARG, "size mismatch for " + nm + ": got " + std::to_string(it->second.second) +
+                                                  " expected " + std::to_string(numel));
+            return it->second.first;
+        };
+        auto up = [&](const std::string& nm, long numel) {
+            const float* h = get(nm, numel);
+            float* dptr = e->dalloc(numel);
+            HIPCHK(hipMemcpy(dptr, h, numel * sizeof(float), hipMemcpyHostToDevice));
+            return dptr;
+        };
+        const std::string pfx = "wav2vec2.";
+        const int H = c.H;
+        // ---- trainable layout ----
+        auto add = [&](const std::string& nm, std::vector<long> shape, bool conv_w, bool ln, bool bias, int depth) {
+            TP t;
+            t.name = nm;
+            t.shape = shape;
+            t.numel = 1;
+            for (long s : shape) t.numel *= s;
+            t.conv_w = conv_w;
+            t.ln_member = ln;
+            t.is_bias = bias;
+            t.feat_depth = depth;
+            t.off = rup(e->Pn, 4);
+            e->Pn = t.off + t.numel;
+            e->tpi[nm] = (int)e->tps.size();
+            e->tps.push_back(t);
+            return t.off;
+        };
+        for (int i = 0; i < c.nconv; ++i) {  // conv-layer norms first (layer mode: k = 5)
+            const std::string b = pfx + "feature_extractor.conv_layers." + std::to_string(i) + ".layer_norm.";
+            if (c.layer_mode) {
+                e->o_cg[i] = add(b + "weight", {c.C[i]}, false, true, false, 4);
+                e->o_cbeta[i] = add(b + "bias", {c.C[i]}, false, true, true, 4);
+            } else if (i == 0) {
+                e->o_cg[i] = add(b + "weight", {c.C[i]}, false, false, false, 4);
+                e->o_cbeta[i] = add(b + "bias", {c.C[i]}, false, false, true, 4);
+            } else {
+                e->o_cg[i] = e->o_cbeta[i] = -1;
+            }
+        }
+        for (int i = 0; i < c.nconv; ++i) {
+            const std::string b = pfx + "feature_extractor.conv_layers." + std::to_string(i) + ".conv.";
+            const long cin = i == 0 ? 1 : c.C[i - 1];
+            e->o_cw[i] = add(b + "weight", {c.C[i], cin, c.K[i]}, true, false, false, 4);
+            e->o_cb[i] = c.conv_bias ? add(b + "bias", {c.C[i]}, false, false, true, 4) : -1;
+        }
+        const int C6 = c.C[c.nconv - 1];
+        e->o_fpg = add(pfx + "feature_projection.layer_norm.weight", {C6}, false, true, false, 2);
+        e->o_fpb = add(pfx + "feature_projection.layer_norm.bias", {C6}, false, true, true, 2);
+        e->o_pw = add(pfx + "feature_projection.projection.weight", {H, C6}, false, false, false, 2);
+        e->o_pb = add(pfx + "feature_projection.projection.bias", {H}, false, false, true, 2);
+        e->o_eg = add(pfx + "encoder.layer_norm.weight", {H}, false, true, false, 0);
+        e->o_eb = add(pfx + "encoder.layer_norm.bias", {H}, false, true, true, 0);
+        for (int l = 0; l < c.L; ++l) {
+            const std::string b = pfx + "encoder.layers." + std::to_string(l) + ".";
+            e->o_l1g.push_back(add(b + "layer_norm.weight", {H}, false, true, false, 0));
+            e->o_l1b.push_back(add(b + "layer_norm.bias", {H}, false, true, true, 0));
+            e->o_l2g.push_back(add(b + "final_layer_norm.weight", {H}, false, true, false, 0));
+            e->o_l2b.push_back(add(b + "final_layer_norm.bias", {H}, false, true, true, 0));
+        }
+        e->Pn = rup(e->Pn, 64);
+        std::vector<float> hp0(e->Pn, 0.f);
+        for (const TP& t : e->tps) {
+            const float* src = get(t.name, t.numel);
+            if (t.conv_w) {  // [co][ci][k] -> [k][ci][co]
+                const long co = t.shape[0], ci = t.shape[1], kk = t.shape[2];
+                for (long o = 0; o < co; ++o)
+                    for (long i2 = 0; i2 < ci; ++i2)
+                        for (long q = 0; q < kk; ++q) hp0[t.off + (q * ci + i2) * co + o] = src[(o * ci + i2) * kk + q];
+            } else {
+                std::memcpy(&hp0[t.off], src, t.numel * sizeof(float));
+            }
+        }
+        e->P0 = e->dalloc(e->Pn);
+        HIPCHK(hipMemcpy(e->P0, hp0.data(), e->Pn * sizeof(float), hipMemcpyHostToDevice));
+        e->P = e->dalloc((long)max_batch * e->Pn);
+        e->G = e->dalloc((long)max_batch * e->Pn);
+        e->Mo = e->dalloc((long)max_batch * e->Pn);
+        e->Vo = e->dalloc((long)max_batch * e->Pn);
+        HIPCHK(hipMemset(e->G, 0, (size_t)max_batch * e->Pn * sizeof(float)));
+        // ---- frozen encoder weights ----
+        for (int l = 0; l < c.L; ++l) {
+            const std::string b = pfx + "encoder.layers." + std::to_string(l) + ".";
+            std::vector<float> qkv((size_t)3 * H * H), bq((size_t)3 * H);
+            const char* parts[3] = {"q_proj", "k_proj", "v_proj"};
+            for (int j = 0; j < 3; ++j) {
+                std::memcpy(&qkv[(size_t)j * H * H], get(b + "attention." + parts[j] + ".weight", (long)H * H),
+                            sizeof(float) * H * H);
+                std::memcpy(&bq[(size_t)j * H], get(b + "attention." + parts[j] + ".bias", H), sizeof(float) * H);
+            }
+            float* dq = e->dalloc(3L * H * H);
+            HIPCHK(hipMemcpy(dq, qkv.data(), qkv.size() * 4, hipMemcpyHostToDevice));
+            float* dbq = e->dalloc(3L * H);
+            HIPCHK(hipMemcpy(dbq, bq.data(), bq.size() * 4, hipMemcpyHostToDevice));
+            e->wqkv.push_back(dq);
+            e->bqkv.push_back(dbq);
+            e->wo.push_back(up(b + "attention.out_proj.weight", (long)H * H));
+            e->bo.push_back(up(b + "attention.out_proj.bias", H));
+            e->w1.push_back(up(b + "feed_forward.intermediate_dense.weight", (long)c.F * H));
+            e->b1.push_back(up(b + "feed_forward.intermediate_dense.bias", c.F));
+            e->w2.push_back(up(b + "feed_forward.output_dense.weight", (long)c.F * H));
+            e->b2.push_back(up(b + "feed_forward.output_dense.bias", H));
+        }
+        e->wlm = up("lm_head.weight", (long)c.V * H);
+        e->blm = up("lm_head.bias", c.V);
+        // ---- positional conv: weight norm (dim=2) precomputed, regrouped for the conv-A GEMM ----
+        {
+            const int K = c.posK, G = c.posG, Cg = H / G;
+            const std::string b = pfx + "encoder.pos_conv_embed.conv.";
+            const float* g = get(b + "parametrizations.weight.original0", K);
+            const float* v = get(b + "parametrizations.weight.original1", (long)H * Cg * K);
+            std::vector<double> nrm(K, 0.0);
+            for (long o = 0; o < H; ++o)
+                for (long i2 = 0; i2 < Cg; ++i2)
+                    for (int q = 0; q < K; ++q) {
+                        const double x = v[(o * Cg + i2) * K + q];
+                        nrm[q] += x * x;
+                    }
+            // ATen _weight_norm: w = v * (g / ||v||) in fp32
+            std::vector<float> nf(K);
+            for (int q = 0; q < K; ++q) nf[q] = (float)std::sqrt(nrm[q]);
+            std::vector<float> wf((size_t)G * K * Cg * Cg), wb((size_t)G * K * Cg * Cg);
+            for (int gi = 0; gi < G; ++gi)
+                for (int co = 0; co < Cg; ++co)
+                    for (int ci = 0; ci < Cg; ++ci)
+                        for (int q = 0; q < K; ++q) {
+                            const long o = (long)gi * Cg + co;
+                            const float wv = v[(o * Cg + ci) * K + q] * (g[q] / nf[q]);  // ATen _weight_norm
+                            // fwd B[(q, ci)][co] ; bwd B[(q', co)][ci] with q' = K-1-q
+                            wf[(((size_t)gi * K + q) * Cg + ci) * Cg + co] = wv;
+                            wb[(((size_t)gi * K + (K - 1 - q)) * Cg + co) * Cg + ci] = wv;
+                        }
+            e->wpos_f = e->dalloc((long)wf.size());
+            e->wpos_b = e->dalloc((long)wb.size());
+            HIPCHK(hipMemcpy(e->wpos_f, wf.data(), wf.size() * 4, hipMemcpyHostToDevice));
+            HIPCHK(hipMemcpy(e->wpos_b, wb.data(), wb.size() * 4, hipMemcpyHostToDevice));
+            e->bpos = up(b + "bias", H);
+        }
+        e->reset_slots(max_batch);
+        HIPCHK(hipStreamSynchronize(e->st));
+        *out = e.release();
+    });
+}
+
+int32_t suta_destroy(suta_engine* e) {
+    return guard([&] {
+        if (!e) return;
+        (void)hipStreamSynchronize(e->st);
+        delete e;
+    });
+}
+
+int32_t suta_reset(suta_engine* e) {
+    return guard([&] {
+        e->reset_slots(e->max_batch);
+        HIPCHK(hipStreamSynchronize(e->st));
+    });
+}
+
+static void check_batch(suta_engine* e, int32_t batch, int64_t n) {
+    if (batch < 1 || batch > e->max_batch) throw SutaError(SUTA_ERR_ARG, "batch outside [1, max_batch]");
+    if (n < 1) throw SutaError(SUTA_ERR_ARG, "n_samples < 1");
+}
+
+int32_t suta_forward(suta_engine* e, const float* wav, int32_t on_dev, int32_t norm, int32_t batch, int64_t n,
+                     float* logits_out) {
+    return guard([&] {
+        check_batch(e, batch, n);
+        HIPCHK(hipSetDevice(e->device));
+        e->build_plan(batch, n);
+        e->stage_input(wav, on_dev, norm, batch, n);
+        e->forward(batch);
+        HIPCHK(hipMemcpyAsync(logits_out, e->plan.logits, (size_t)batch * e->plan.T * e->c.V * 4, hipMemcpyDeviceToHost,
+                              e->st));
+        HIPCHK(hipStreamSynchronize(e->st));
+        if (e->timing) e->collect_timing();
+    });
+}
+
+int32_t suta_step(suta_engine* e, const float* wav, int32_t on_dev, int32_t norm, int32_t batch, int64_t n,
+                  const suta_hparams* hp, float* logits_out, float* loss_out) {
+    return guard([&] {
+        check_batch(e, batch, n);
+        HIPCHK(hipSetDevice(e->device));
+        e->build_plan(batch, n);
+        e->stage_input(wav, on_dev, norm, batch, n);
+        e->forward(batch);
+        e->backward(batch, *hp);
+        e->adam(batch, *hp);
+        e->forward(batch);
+        if (loss_out)
+            HIPCHK(hipMemcpyAsync(loss_out, e->plan.loss, (size_t)batch * 4, hipMemcpyDeviceToHost, e->st));
+        HIPCHK(hipMemcpyAsync(logits_out, e->plan.logits, (size_t)batch * e->plan.T * e->c.V * 4, hipMemcpyDeviceToHost,
+                              e->st));
+        HIPCHK(hipStreamSynchronize(e->st));
+        if (e->timing) e->collect_timing();
+    });
+}
+
+int32_t suta_adapt(suta_engine* e, const float* wav, int32_t on_dev, int32_t norm, int32_t batch, int64_t n,
+                   int32_t steps, const suta_hparams* hp, const int32_t* rec, int32_t nrec, float* logits_out,
+                   int32_t logits_on_dev, int32_t* ids_out, int64_t* frames_out) {
+    return guard([&] {
+        check_batch(e, batch, n);
+        if (steps < 0) throw SutaError(SUTA_ERR_ARG, "steps < 0");
+        for (int i = 0; i < nrec; ++i)
+            if (rec[i] < 0 || rec[i] > steps) throw SutaError(SUTA_ERR_ARG, "record step outside [0, steps]");
+        HIPCHK(hipSetDevice(e->device));
+        e->build_plan(batch, n);
+        const int T = e->plan.T, V = e->c.V;
+        if (frames_out) *frames_out = T;
+        const size_t per = (size_t)batch * T * V;
+        e->stage_input(wav, on_dev, norm, batch, n);
+        if (hp->episodic) e->reset_slots(batch);
+        for (int s = 0; s <= steps; ++s) {
+            e->forward(batch);
+            for (int i = 0; i < nrec; ++i) {
+                if (rec[i] != s) continue;
+                if (logits_out)
+                    HIPCHK(hipMemcpyAsync(logits_out + i * per, e->plan.logits, per * 4,
+                                          logits_on_dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, e->st));
+                if (ids_out) {
+                    launch_argmax(e->plan.logits, (long)batch * T, V, e->plan.ids, e->st);
+                    HIPCHK(hipMemcpyAsync(ids_out + (size_t)i * batch * T, e->plan.ids, (size_t)batch * T * 4,
+                                          hipMemcpyDeviceToHost, e->st));
+                }
+            }
+            if (s == steps) break;
+            e->backward(batch, *hp);
+            e->adam(batch, *hp);
+        }
+        HIPCHK(hipStreamSynchronize(e->st));
+        if (e->timing) e->collect_timing();
+    });
+}
+
+int32_t suta_loss_grad(suta_engine* e, const float* logits, int32_t batch, int64_t frames, const suta_hparams* hp,
+                       float* dlogits_out, float* loss_out) {
+    return guard([&] {
+        if (batch < 1 || frames < 1) throw SutaError(SUTA_ERR_ARG, "empty logits");
+        HIPCHK(hipSetDevice(e->device));
+        const int V = e->c.V;
+        const size_t n = (size_t)batch * frames * V;
+        DevBuf buf;
+        buf.alloc((2 * n + (size_t)batch * frames * 66 + 64 + batch) * sizeof(float));
+        float* dl = buf.p;
+        float* dd = dl + n;
+        float* scr = dd + n;
+        float* ls = scr + (size_t)batch * frames * 66 + 64;
+        HIPCHK(hipMemcpyAsync(dl, logits, n * 4, hipMemcpyHostToDevice, e->st));
+        LossHP lh{hp->temp, hp->em_coef, hp->div_coef, hp->reweight, hp->non_blank};
+        launch_suta_loss(dl, batch, (int)frames, V, lh, dd, ls, scr, e->st);
+        HIPCHK(hipMemcpyAsync(dlogits_out, dd, n * 4, hipMemcpyDeviceToHost, e->st));
+        HIPCHK(hipMemcpyAsync(loss_out, ls, (size_t)batch * 4, hipMemcpyDeviceToHost, e->st));
+        HIPCHK(hipStreamSynchronize(e->st));
+    });
+}
+
+int32_t suta_get_param(suta_engine* e, int32_t slot, const char* name, float* out, int64_t numel) {
+    return guard([&] {
+        auto it = e->tpi.find(name);
+        if (it == e->tpi.end()) throw SutaError(SUTA_ERR_ARG, std::string("not a trainable tensor: ") + name);
+        if (slot < 0 || slot >= e->max_batch) throw SutaError(SUTA_ERR_ARG, "slot out of range");
+        const TP& t = e->tps[it->second];
+        if (numel != t.numel) throw SutaError(SUTA_ERR_ARG, "numel mismatch");
+        std::vector<float> h(t.numel);
+        HIPCHK(hipStreamSynchronize(e->st));
+        HIPCHK(hipMemcpy(h.data(), e->P + (long)slot * e->Pn + t.off, t.numel * 4, hipMemcpyDeviceToHost));
+        if (t.conv_w) {
+            const long co = t.shape[0], ci = t.shape[1], kk = t.shape[2];
+            for (long o = 0; o < co; ++o)
+                for (long i2 = 0; i2 < ci; ++i2)
+                    for (long q = 0; q < kk; ++q) out[(o * ci + i2) * kk + q] = h[(q * ci + i2) * co + o];
+        } else {
+            std::memcpy(out, h.data(), t.numel * 4);
+        }
+    });
+}
+
+int32_t suta_param_info(suta_engine* e, const char* name, int32_t train_feature, int32_t bias_only, int32_t* k,
+                        int64_t* numel) {
+    return guard([&] {
+        auto it = e->tpi.find(name);
+        if (it == e->tpi.end()) {
+            *k = 0;
+            *numel = 0;
+            return;
+        }
+        const TP& t = e->tps[it->second];
+        *k = e->multiplicity(t, train_feature, bias_only);
+        *numel = t.numel;
+    });
+}
+
+int32_t suta_sync(suta_engine* e) { return guard([&] { HIPCHK(hipStreamSynchronize(e->st)); }); }
+
+void* suta_stream(suta_engine* e) { return (void*)e->st; }
+
+int32_t suta_set_timing(suta_engine* e, int32_t enable) {
+    return guard([&] {
+        e->timing = enable != 0;
+        for (int i = 0; i < NFAM; ++i) {
+            e->fam_ms[i] = 0;
+            e->fam_n[i] = 0;
+        }
+    });
+}
+
+int32_t suta_get_timing(suta_engine* e, double* ms, int64_t* n) {
+    return guard([&] {
+        e->collect_timing();
+        for (int i = 0; i < NFAM; ++i) {
+            ms[i] = e->fam_ms[i];
+            n[i] = e->fam_n[i];
+        }
+    });
+}
+
+int32_t suta_set_graphs(suta_engine* e, int32_t enable) {
+    return guard([&] { e->use_graphs = enable != 0; });
+}
+
+}  // extern "C"

@@ -1,0 +1,82 @@
+// Launchers for the non-GEMM kernels of the SUTA step (ops.hip).  All tensors are fp32,
+// time-major ([frame][channel]) and packed over the utterances of a batch.
+#pragma once
+#include "common.h"
+
+// HF feature-extractor normalisation (feature_extraction_wav2vec2.py:78-97), per utterance:
+// y = (x - mean) / sqrt(var + 1e-7), population variance.
+void launch_wave_normalize(const float* x, float* y, int B, long N, hipStream_t st);
+
+// conv0: z[b][t][c] = sum_k x[b][s*t + k] * W[b][k][c] (+ bias[b][c]);  W stored [k][c] per utterance.
+void launch_conv0(const float* x, long N, const float* W, const float* bias, long wstride, float* z, int B, int L0,
+                  int C, int K, int S, hipStream_t st);
+
+// Per-utterance column statistics over rows (GroupNorm with one group per channel):
+// mean[b][c], rstd[b][c] = 1/sqrt(var + eps).  part: scratch of >= B * nchunk * C * 2 doubles.
+void launch_col_stats(const float* z, int B, int rows, int C, float eps, double* part, float* mean, float* rstd,
+                      hipStream_t st);
+// a = gelu((z - mean[c]) * rstd[c] * g[c] + beta[c])  (g, beta per utterance at stride pstride)
+void launch_gn_apply_gelu(const float* z, const float* mean, const float* rstd, const float* g, const float* beta,
+                          long pstride, float* a, int B, int rows, int C, hipStream_t st);
+// GroupNorm(+GELU) backward.  da: grad of a.  Writes dz, and dgamma/dbeta into grad buffers
+// (per utterance at gstride).
+void launch_gn_gelu_bwd(const float* da, const float* z, const float* mean, const float* rstd, const float* g,
+                        const float* beta, long pstride, float* dz, float* dgamma, float* dbeta, long gstride, int B,
+                        int rows, int C, double* part, hipStream_t st);
+
+// LayerNorm over the last dim D of `rows` rows; gamma/beta of utterance (row / rows_per_utt)
+// at pstride.  Stores y, xhat, rstd.  gelu_out: y = gelu(LN(x)) (feature-encoder "layer" mode).
+void launch_layernorm_fwd(const float* x, const float* g, const float* beta, long pstride, int rows_per_utt,
+                          float* y, float* xhat, float* rstd, int rows, int D, float eps, int gelu_out,
+                          hipStream_t st);
+// LayerNorm backward.  gin = dy (times gelu'(xhat*g+beta) when gelu_in); dx = LN-bwd(gin)
+// (times gelu'(post_aux) when post_aux) (+ resid).  dgamma/dbeta (may be null) summed per
+// utterance into the grad buffer (gstride per utterance).  part: >= B*ceil(rows_per_utt/32)*2*D floats.
+void launch_layernorm_bwd(const float* dy, const float* xhat, const float* rstd, const float* g, const float* beta,
+                          long pstride, int rows_per_utt, int B, int D, int gelu_in, const float* post_aux,
+                          const float* resid, float* dx, float* dgamma, float* dbeta, long gstride, float* part,
+                          hipStream_t st);
+
+// Column sums per utterance: out[b][c] = sum_{t < rows} x[b][t][c]   (bias gradients).
+void launch_colsum(const float* x, int B, int rows, int C, float* out, long ostride, float* part, hipStream_t st);
+
+// In-place row softmax of `nrows` rows of length T (row stride ld).
+void launch_softmax_rows(float* s, long nrows, int T, long ld, hipStream_t st);
+// In place: dP <- scale * P * (dP - rowsum(dP * P)).
+void launch_softmax_bwd_rows(const float* P, float* dP, long nrows, int T, long ld, float scale, hipStream_t st);
+
+// col2im for a stride-S, kernel-K conv on time-major data: da[b][r][c] = sum_{S t + k = r} dcol[b][t][k*C + c],
+// rows r < Lin; optionally times gelu'(z[b][r][c]).
+void launch_col2im(const float* dcol, int B, int Lout, int Lin, int C, int K, int S, const float* z, float* da,
+                   hipStream_t st);
+
+// out = g * gelu'(z), n elements.
+void launch_dgelu_mul(const float* g, const float* z, float* out, long n, hipStream_t st);
+
+// SUTA loss + dL/dlogits for each utterance (reference main.py:26-60, 181-203).
+struct LossHP {
+    float temp, em_coef, div_coef;
+    int reweight, non_blank;
+};
+void launch_suta_loss(const float* logits, int B, int T, int V, LossHP hp, float* dlogits, float* loss,
+                      float* scratch, hipStream_t st);
+
+// Argmax ids per frame (first max, like torch.argmax), optional copy of logits.
+void launch_argmax(const float* logits, long rows, int V, int* ids, hipStream_t st);
+
+// AdamW single-tensor semantics with per-run multiplicity k (k sub-steps with the same gradient).
+struct AdamRun {
+    long start, len;
+    int k;
+};
+#define SUTA_MAX_RUNS 24
+struct AdamArgs {
+    int nruns;
+    AdamRun runs[SUTA_MAX_RUNS];
+    float beta1, beta2, omb1, omb2, eps, lr_wd;  // omb = (1 - beta) rounded from double; lr_wd = lr * wd
+    // per sub-step j (1-based t = step0*k + j): step_size and sqrt(bias_correction2), indexed [k-1][j-1]
+    float step_size[5][5];
+    float bc2_sqrt[5][5];
+};
+void launch_adam(float* P, const float* G, float* M, float* V, long pstride, int B, const AdamArgs& a,
+                 hipStream_t st);

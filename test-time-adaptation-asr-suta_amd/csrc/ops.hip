@@ -1,0 +1,827 @@
+// Non-GEMM kernels of the SUTA step for gfx950: waveform normalisation, conv0 stencil,
+// GroupNorm / LayerNorm forward+backward with per-utterance affine gradients, attention
+// softmax forward/backward, col2im, the fused entropy+MCC loss-and-grad, and AdamW with
+// duplicate-entry multiplicity.  All reductions are fixed-order (bitwise reproducible).
+#include "ops.h"
+#include <algorithm>
+
+namespace {
+
+inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+
+template <typename T>
+__device__ __forceinline__ T block_sum(T v, T* red) {
+    // 256-thread block reduction (4 waves)
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    __syncthreads();
+    if (lane == 0) red[w] = v;
+    __syncthreads();
+    T s = red[0] + red[1] + red[2] + red[3];
+    __syncthreads();
+    return s;
+}
+
+// ------------------------------------------------------------------------------------------
+// waveform normalisation (one block per utterance)
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void wave_normalize_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                             long N) {
+    __shared__ double red[4];
+    const float* xb = x + (long)blockIdx.x * N;
+    float* yb = y + (long)blockIdx.x * N;
+    double s = 0.0;
+    for (long i = threadIdx.x; i < N; i += 256) s += xb[i];
+    s = block_sum(s, red);
+    const double mean = s / (double)N;
+    double q = 0.0;
+    for (long i = threadIdx.x; i < N; i += 256) {
+        const double d = (double)xb[i] - mean;
+        q += d * d;
+    }
+    q = block_sum(q, red);
+    const float meanf = (float)mean;
+    const float denom = (float)sqrt(q / (double)N + 1e-7);
+    for (long i = threadIdx.x; i < N; i += 256) yb[i] = (xb[i] - meanf) / denom;
+}
+
+// ------------------------------------------------------------------------------------------
+// conv0 (1 -> C channels, kernel K <= 16, stride S): time-major output
+// block: 32 output frames x all channels; x segment staged in LDS
+// ------------------------------------------------------------------------------------------
+constexpr int C0_ROWS = 32;
+__global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x, long N, const float* __restrict__ W,
+                                                    const float* __restrict__ bias, long wstride,
+                                                    float* __restrict__ z, int L0, int C, int K, int S) {
+    __shared__ float xs[C0_ROWS * 16 + 16];
+    const int b = blockIdx.y;
+    const int t0 = blockIdx.x * C0_ROWS;
+    const float* xb = x + (long)b * N;
+    const float* Wb = W + (long)b * wstride;
+    const float* bb = bias ? bias + (long)b * wstride : nullptr;
+    const int nx = (C0_ROWS - 1) * S + K;
+    for (int i = threadIdx.x; i < nx; i += 256) {
+        const long gi = (long)t0 * S + i;
+        xs[i] = gi < N ? xb[gi] : 0.f;
+    }
+    __syncthreads();
+    const int rows = min(C0_ROWS, L0 - t0);
+    float* zb = z + ((long)b * L0 + t0) * C;
+    for (int c = threadIdx.x; c < C; c += 256) {
+        float w[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) w[k] = k < K ? Wb[(long)k * C + c] : 0.f;
+        const float bv = bb ? bb[c] : 0.f;
+        for (int r = 0; r < rows; ++r) {
+            float acc = 0.f;
+            // same summation order as a k-ordered dot product
+            for (int k = 0; k < K; ++k) acc = fmaf(xs[r * S + k], w[k], acc);
+            zb[(long)r * C + c] = acc + bv;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// per-utterance column statistics (GroupNorm with groups == channels), double partials
+// ------------------------------------------------------------------------------------------
+constexpr int CS_ROWS = 128;
+__global__ __launch_bounds__(256) void col_stats_partial(const float* __restrict__ z, int rows, int C,
+                                                         double* __restrict__ part, int nchunk) {
+    const int b = blockIdx.y, ch = blockIdx.x;
+    const int r0 = ch * CS_ROWS, r1 = min(rows, r0 + CS_ROWS);
+    const float* zb = z + (long)b * rows * C;
+    double* pb = part + ((long)b * nchunk + ch) * 2 * C;
+    for (int c = threadIdx.x; c < C; c += 256) {
+        double s = 0.0, q = 0.0;
+        for (int r = r0; r < r1; ++r) {
+            const double v = zb[(long)r * C + c];
+            s += v;
+            q += v * v;
+        }
+        pb[c] = s;
+        pb[C + c] = q;
+    }
+}
+__global__ __launch_bounds__(256) void col_stats_final(const double* __restrict__ part, int nchunk, int rows, int C,
+                                                       float eps, float* __restrict__ mean, float* __restrict__ rstd) {
+    const int b = blockIdx.y;
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= C) return;
+    double s = 0.0, q = 0.0;
+    for (int ch = 0; ch < nchunk; ++ch) {
+        const double* pb = part + ((long)b * nchunk + ch) * 2 * C;
+        s += pb[c];
+        q += pb[C + c];
+    }
+    const double m = s / rows;
+    double var = q / rows - m * m;
+    if (var < 0) var = 0;
+    mean[(long)b * C + c] = (float)m;
+    rstd[(long)b * C + c] = (float)(1.0 / sqrt(var + (double)eps));
+}
+
+__global__ __launch_bounds__(256) void gn_apply_gelu_kernel(const float* __restrict__ z, const float* __restrict__ mean,
+                                                            const float* __restrict__ rstd, const float* __restrict__ g,
+                                                            const float* __restrict__ beta, long pstride,
+                                                            float* __restrict__ a, int rows, int C) {
+    const int b = blockIdx.y;
+    const long n = (long)rows * C;
+    const float* zb = z + (long)b * n;
+    float* ab = a + (long)b * n;
+    const float* mb = mean + (long)b * C;
+    const float* rb = rstd + (long)b * C;
+    const float* gb = g + (long)b * pstride;
+    const float* bb = beta + (long)b * pstride;
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+        const int c = (int)(i % C);
+        const float xh = (zb[i] - mb[c]) * rb[c];
+        ab[i] = gelu_f(xh * gb[c] + bb[c]);
+    }
+}
+
+// partials of sum(dg) and sum(dg * xhat) per column, dg = da * gelu'(xhat*g + beta)
+__global__ __launch_bounds__(256) void gn_bwd_partial(const float* __restrict__ da, const float* __restrict__ z,
+                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                      const float* __restrict__ g, const float* __restrict__ beta,
+                                                      long pstride, int rows, int C, double* __restrict__ part,
+                                                      int nchunk) {
+    const int b = blockIdx.y, ch = blockIdx.x;
+    const int r0 = ch * CS_ROWS, r1 = min(rows, r0 + CS_ROWS);
+    const long off = (long)b * rows * C;
+    double* pb = part + ((long)b * nchunk + ch) * 2 * C;
+    for (int c = threadIdx.x; c < C; c += 256) {
+        const float m = mean[(long)b * C + c], rs = rstd[(long)b * C + c];
+        const float gg = g[(long)b * pstride + c], bt = beta[(long)b * pstride + c];
+        double s = 0.0, q = 0.0;
+        for (int r = r0; r < r1; ++r) {
+            const long i = off + (long)r * C + c;
+            const float xh = (z[i] - m) * rs;
+            const float dg = da[i] * dgelu_f(xh * gg + bt);
+            s += dg;
+            q += (double)dg * xh;
+        }
+        pb[c] = s;
+        pb[C + c] = q;
+    }
+}
+// finalize: dgamma = sum dg*xhat, dbeta = sum dg; also writes coefficients for the dx pass
+__global__ __launch_bounds__(256) void gn_bwd_final(const double* __restrict__ part, int nchunk, int C,
+                                                    float* __restrict__ dgamma, float* __restrict__ dbeta, long gstride,
+                                                    float* __restrict__ coef) {
+    const int b = blockIdx.y;
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= C) return;
+    double s = 0.0, q = 0.0;
+    for (int ch = 0; ch < nchunk; ++ch) {
+        const double* pb = part + ((long)b * nchunk + ch) * 2 * C;
+        s += pb[c];
+        q += pb[C + c];
+    }
+    dgamma[(long)b * gstride + c] = (float)q;
+    dbeta[(long)b * gstride + c] = (float)s;
+    coef[((long)b * C + c) * 2 + 0] = (float)s;
+    coef[((long)b * C + c) * 2 + 1] = (float)q;
+}
+// dz = rstd * gamma * (dg - mean(dg) - xhat * mean(dg*xhat))
+__global__ __launch_bounds__(256) void gn_bwd_dx(const float* __restrict__ da, const float* __restrict__ z,
+                                                 const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                 const float* __restrict__ g, const float* __restrict__ beta,
+                                                 long pstride, const float* __restrict__ coef, float* __restrict__ dz,
+                                                 int rows, int C) {
+    const int b = blockIdx.y;
+    const long n = (long)rows * C;
+    const long off = (long)b * n;
+    const float inv = 1.0f / rows;
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+        const int c = (int)(i % C);
+        const float m = mean[(long)b * C + c], rs = rstd[(long)b * C + c];
+        const float gg = g[(long)b * pstride + c], bt = beta[(long)b * pstride + c];
+        const float xh = (z[off + i] - m) * rs;
+        const float dg = da[off + i] * dgelu_f(xh * gg + bt);
+        const float s = coef[((long)b * C + c) * 2 + 0], q = coef[((long)b * C + c) * 2 + 1];
+        dz[off + i] = rs * gg * (dg - s * inv - xh * (q * inv));
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// LayerNorm over D (<= 1024): one wave per row
+// ------------------------------------------------------------------------------------------
+template <int NPL>  // elements per lane = ceil(D / 64)
+__global__ __launch_bounds__(256) void layernorm_fwd_kernel(const float* __restrict__ x, const float* __restrict__ g,
+                                                            const float* __restrict__ beta, long pstride,
+                                                            int rows_per_utt, float* __restrict__ y,
+                                                            float* __restrict__ xhat, float* __restrict__ rstd,
+                                                            int rows, int D, float eps, int gelu_out) {
+    const int lane = threadIdx.x & 63;
+    const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const int u = (int)(row / rows_per_utt);
+    const float* xr = x + row * D;
+    float v[NPL];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+        const int c = lane + i * 64;
+        v[i] = c < D ? xr[c] : 0.f;
+        s += v[i];
+    }
+    s = wave_sum(s);
+    const float mean = s / D;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+        const int c = lane + i * 64;
+        const float d = c < D ? v[i] - mean : 0.f;
+        q += d * d;
+    }
+    q = wave_sum(q);
+    const float rs = 1.0f / sqrtf(q / D + eps);
+    const float* gu = g + (long)u * pstride;
+    const float* bu = beta + (long)u * pstride;
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+        const int c = lane + i * 64;
+        if (c < D) {
+            const float xh = (v[i] - mean) * rs;
+            xhat[row * D + c] = xh;
+            const float o = xh * gu[c] + bu[c];
+            y[row * D + c] = gelu_out ? gelu_f(o) : o;
+        }
+    }
+    if (lane == 0) rstd[row] = rs;
+}
+
+constexpr int LNB_ROWS = 32;
+template <int NPL>
+__global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ xhat,
+                                                            const float* __restrict__ rstd, const float* __restrict__ g,
+                                                            const float* __restrict__ beta, long pstride,
+                                                            int rows_per_utt, int D, int gelu_in,
+                                                            const float* __restrict__ post_aux,
+                                                            const float* __restrict__ resid, float* __restrict__ dx,
+                                                            float* __restrict__ part, int nchunk) {
+    __shared__ float red[4][2][NPL * 64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int u = blockIdx.y, ch = blockIdx.x;
+    const float* gu = g + (long)u * pstride;
+    const float* bu = beta + (long)u * pstride;
+    float gam[NPL], bet[NPL];
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+        const int c = lane + i * 64;
+        gam[i] = c < D ? gu[c] : 0.f;
+        bet[i] = c < D ? bu[c] : 0.f;
+    }
+    float pg[NPL], pb[NPL];
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) pg[i] = pb[i] = 0.f;
+    const int r0 = ch * LNB_ROWS, r1 = min(rows_per_utt, r0 + LNB_ROWS);
+    for (int r = r0 + w; r < r1; r += 4) {
+        const long row = (long)u * rows_per_utt + r;
+        float gi[NPL], xh[NPL];
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < NPL; ++i) {
+            const int c = lane + i * 64;
+            if (c < D) {
+                xh[i] = xhat[row * D + c];
+                float d = dy[row * D + c];
+                if (gelu_in) d *= dgelu_f(xh[i] * gam[i] + bet[i]);
+                gi[i] = d;
+                pg[i] += d * xh[i];
+                pb[i] += d;
+                const float dg = d * gam[i];
+                s1 += dg;
+                s2 += dg * xh[i];
+            } else {
+                xh[i] = gi[i] = 0.f;
+            }
+        }
+        s1 = wave_sum(s1);
+        s2 = wave_sum(s2);
+        const float rs = rstd[row];
+        const float m1 = s1 / D, m2 = s2 / D;
+#pragma unroll
+        for (int i = 0; i < NPL; ++i) {
+            const int c = lane + i * 64;
+            if (c < D) {
+                float o = rs * (gi[i] * gam[i] - m1 - xh[i] * m2);
+                if (post_aux) o *= dgelu_f(post_aux[row * D + c]);
+                if (resid) o += resid[row * D + c];
+                dx[row * D + c] = o;
+            }
+        }
+    }
+    if (part) {
+#pragma unroll
+        for (int i = 0; i < NPL; ++i) {
+            red[w][0][lane + i * 64] = pg[i];
+            red[w][1][lane + i * 64] = pb[i];
+        }
+        __syncthreads();
+        float* pp = part + ((long)u * nchunk + ch) * 2 * D;
+        for (int c = threadIdx.x; c < D; c += 256) {
+            pp[c] = red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c];
+            pp[D + c] = red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
+        }
+    }
+}
+
+// sum partial slabs [B][nchunk][nvec][D] over chunks in order -> out_v[b*ostride + c]
+__global__ __launch_bounds__(256) void chunk_reduce(const float* __restrict__ part, int nchunk, int nvec, int D,
+                                                    float* __restrict__ out0, float* __restrict__ out1, long ostride) {
+    const int b = blockIdx.y;
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= D) return;
+    for (int v = 0; v < nvec; ++v) {
+        float* out = v == 0 ? out0 : out1;
+        if (!out) continue;
+        float s = 0.f;
+        for (int ch = 0; ch < nchunk; ++ch) s += part[(((long)b * nchunk + ch) * nvec + v) * D + c];
+        out[(long)b * ostride + c] = s;
+    }
+}
+
+__global__ __launch_bounds__(256) void colsum_partial(const float* __restrict__ x, int rows, int C,
+                                                      float* __restrict__ part, int nchunk) {
+    const int b = blockIdx.y, ch = blockIdx.x;
+    const int r0 = ch * CS_ROWS, r1 = min(rows, r0 + CS_ROWS);
+    const float* xb = x + (long)b * rows * C;
+    for (int c = threadIdx.x; c < C; c += 256) {
+        float s = 0.f;
+        for (int r = r0; r < r1; ++r) s += xb[(long)r * C + c];
+        part[((long)b * nchunk + ch) * C + c] = s;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// attention softmax over rows of length T (<= 64*NPL), one wave per row
+// ------------------------------------------------------------------------------------------
+template <int NPL>
+__global__ __launch_bounds__(256) void softmax_rows_kernel(float* __restrict__ s, long nrows, int T, long ld) {
+    const int lane = threadIdx.x & 63;
+    const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= nrows) return;
+    float* r = s + row * ld;
+    float v[NPL];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+        const int c = lane + i * 64;
+        v[i] = c < T ? r[c] : -INFINITY;
+        mx = fmaxf(mx, v[i]);
+    }
+    mx = wave_max(mx);
+    float sum = 0.f;
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+        const int c = lane + i * 64;
+        v[i] = c < T ? expf(v[i] - mx) : 0.f;
+        sum += v[i];
+    }
+    sum = wave_sum(sum);
+    const float inv = 1.0f / sum;
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+        const int c = lane + i * 64;
+        if (c < T) r[c] = v[i] * inv;
+    }
+}
+
+template <int NPL>
+__global__ __launch_bounds__(256) void softmax_bwd_rows_kernel(const float* __restrict__ P, float* __restrict__ dP,
+                                                               long nrows, int T, long ld, float scale) {
+    const int lane = threadIdx.x & 63;
+    const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= nrows) return;
+    const float* p = P + row * ld;
+    float* d = dP + row * ld;
+    float pv[NPL], dv[NPL];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+        const int c = lane + i * 64;
+        pv[i] = c < T ? p[c] : 0.f;
+        dv[i] = c < T ? d[c] : 0.f;
+        s += pv[i] * dv[i];
+    }
+    s = wave_sum(s);
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+        const int c = lane + i * 64;
+        if (c < T) d[c] = scale * (pv[i] * (dv[i] - s));
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// col2im (+ optional gelu') for stride-S kernel-K convs on time-major data
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void col2im_kernel(const float* __restrict__ dcol, int Lout, int Lin, int C, int K,
+                                                     int S, const float* __restrict__ z, float* __restrict__ da) {
+    const int b = blockIdx.y;
+    const long n = (long)Lin * C;
+    const float* dc = dcol + (long)b * Lout * K * C;
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+        const int r = (int)(i / C), c = (int)(i % C);
+        // t in [ceil((r-K+1)/S), floor(r/S)] intersect [0, Lout)
+        int thi = r / S;
+        if (thi > Lout - 1) thi = Lout - 1;
+        int tlo = r - K + 1;
+        tlo = tlo <= 0 ? 0 : (tlo + S - 1) / S;
+        float s = 0.f;
+        for (int t = tlo; t <= thi; ++t) {
+            const int k = r - S * t;
+            s += dc[((long)t * K + k) * C + c];
+        }
+        if (z) s *= dgelu_f(z[(long)b * n + i]);
+        da[(long)b * n + i] = s;
+    }
+}
+
+__global__ __launch_bounds__(256) void dgelu_mul_kernel(const float* __restrict__ g, const float* __restrict__ z,
+                                                        float* __restrict__ out, long n) {
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) out[i] = g[i] * dgelu_f(z[i]);
+}
+
+// ------------------------------------------------------------------------------------------
+// fused SUTA loss + gradient, one 256-thread block per utterance, V <= 64 (lane = class)
+// scratch per utterance: P[T][64], H[T] (floats)
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void suta_loss_kernel(const float* __restrict__ logits, int T, int V, LossHP hp,
+                                                        float* __restrict__ dlogits, float* __restrict__ loss_out,
+                                                        float* __restrict__ scratch) {
+    __shared__ double Cm[64 * 64];
+    __shared__ float Sm[64 * 64];
+    __shared__ double redd[4][4];
+    __shared__ double colsum[4][64];
+    __shared__ double rvec[64], rho[64], clsv[64];
+    __shared__ double scal[8];
+    const int b = blockIdx.x;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const float* L = logits + (long)b * T * V;
+    float* dL = dlogits + (long)b * T * V;
+    float* Ps = scratch + (long)b * T * 66;
+    float* Hs = Ps + (long)T * 64;
+    float* Ws = Hs + T;
+    const bool act = lane < V;
+    const float invt = 1.0f / hp.temp;
+
+    // ---- phase 1: per-row softmax, entropy, argmax ----
+    double kcnt = 0.0, wsum = 0.0, hsum_m = 0.0, hsum_all = 0.0;
+    double cls = 0.0;  // per-lane column sum of raw logits (div loss)
+    for (int t = w; t < T; t += 4) {
+        const float l = act ? L[(long)t * V + lane] : -INFINITY;
+        if (act) cls += l;
+        const float zv = l * invt;
+        const float mx = wave_max(zv);
+        const float e = act ? expf(zv - mx) : 0.f;
+        const float s = wave_sum(e);
+        const float p = e / s;
+        const float lp = zv - mx - logf(s);
+        const float H = -wave_sum(act ? p * lp : 0.f);
+        // argmax of raw logits, first max wins
+        float bv = l;
+        int bi = act ? lane : 1 << 30;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const float ov = __shfl_xor(bv, o, 64);
+            const int oi = __shfl_xor(bi, o, 64);
+            if (ov > bv || (ov == bv && oi < bi)) {
+                bv = ov;
+                bi = oi;
+            }
+        }
+        const bool m = bi != 0;
+        Ps[(long)t * 64 + lane] = p;
+        if (lane == 0) Hs[t] = H;
+        kcnt += m ? 1.0 : 0.0;
+        wsum += 1.0 + exp(-(double)H);
+        hsum_m += m ? (double)H : 0.0;
+        hsum_all += H;
+    }
+    if (lane == 0) {
+        redd[w][0] = kcnt;
+        redd[w][1] = wsum;
+        redd[w][2] = hsum_m;
+        redd[w][3] = hsum_all;
+    }
+    colsum[w][lane] = cls;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int j = 0; j < 4; ++j) scal[j] = redd[0][j] + redd[1][j] + redd[2][j] + redd[3][j];
+    }
+    if (threadIdx.x < 64) clsv[threadIdx.x] = colsum[0][threadIdx.x] + colsum[1][threadIdx.x] +
+                                              colsum[2][threadIdx.x] + colsum[3][threadIdx.x];
+    __syncthreads();
+    const double K = scal[0], Wsum = scal[1];
+    const bool use_mcc = 1.0f - hp.em_coef > 0.f;
+    for (int t = threadIdx.x; t < T; t += 256)
+        Ws[t] = hp.reweight ? (float)((double)T * (1.0 + exp(-(double)Hs[t])) / Wsum) : 1.f;
+    __syncthreads();
+
+    // ---- phase 2: C = P^T diag(w_hat) P ----
+    double mcc = 0.0;
+    if (use_mcc) {
+        for (int idx = threadIdx.x; idx < V * V; idx += 256) {
+            const int a = idx / V, c = idx % V;
+            double acc = 0.0;
+            for (int t = 0; t < T; ++t)
+                acc += (double)Ws[t] * (double)Ps[(long)t * 64 + a] * (double)Ps[(long)t * 64 + c];
+            Cm[a * 64 + c] = acc;
+        }
+        __syncthreads();
+        if (threadIdx.x < V) {  // r_j = sum_k C_jk (torch.sum(C, dim=1))
+            const int j = threadIdx.x;
+            double s = 0.0;
+            for (int k = 0; k < V; ++k) s += Cm[j * 64 + k];
+            rvec[j] = s;
+        }
+        __syncthreads();
+        if (threadIdx.x < V) {  // rho_a = sum_i G_ia C_ia / r_a^2, G = (1 - delta)/V
+            const int a = threadIdx.x;
+            double s = 0.0;
+            for (int i = 0; i < V; ++i)
+                if (i != a) s += Cm[i * 64 + a];
+            rho[a] = s / V / (rvec[a] * rvec[a]);
+        }
+        __syncthreads();
+        double part = 0.0;
+        for (int idx = threadIdx.x; idx < V * V; idx += 256) {
+            const int i = idx / V, j = idx % V;
+            if (i != j) part += Cm[i * 64 + j] / rvec[j];
+        }
+        part = block_sum(part, &redd[0][0]);
+        mcc = part / V;
+        // S = dC + dC^T, dC_ab = G_ab / r_b - rho_a
+        for (int idx = threadIdx.x; idx < V * V; idx += 256) {
+            const int a = idx / V, c = idx % V;
+            const double dab = (a != c ? 1.0 / V / rvec[c] : 0.0) - rho[a];
+            const double dba = (a != c ? 1.0 / V / rvec[a] : 0.0) - rho[c];
+            Sm[a * 64 + c] = (float)(dab + dba);
+        }
+    }
+    // div loss: q = softmax(mean_t logits[1:])
+    double Hq = 0.0;
+    __shared__ float qv[64], lqv[64];
+    if (hp.div_coef > 0.f && threadIdx.x < 64) {
+        const bool a2 = lane >= 1 && lane < V;
+        const float c = a2 ? (float)(clsv[lane] / T) : -INFINITY;
+        const float mx = wave_max(c);
+        const float e = a2 ? expf(c - mx) : 0.f;
+        const float s = wave_sum(e);
+        const float q = e / s;
+        const float lq = c - mx - logf(s);
+        const float h = -wave_sum(a2 ? q * lq : 0.f);
+        qv[lane] = a2 ? q : 0.f;
+        lqv[lane] = a2 ? lq : 0.f;
+        if (lane == 0) scal[4] = h;
+    }
+    __syncthreads();
+    if (hp.div_coef > 0.f) Hq = scal[4];
+
+    // ---- phase 3: gradient rows ----
+    const double Kd = K;
+    const float em = hp.em_coef;
+    for (int t = w; t < T; t += 4) {
+        const float p = act ? Ps[(long)t * 64 + lane] : 0.f;
+        const float H = Hs[t];
+        const float l = act ? L[(long)t * V + lane] : -INFINITY;
+        // recompute mask and log p
+        float bv = l;
+        int bi = act ? lane : 1 << 30;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const float ov = __shfl_xor(bv, o, 64);
+            const int oi = __shfl_xor(bi, o, 64);
+            if (ov > bv || (ov == bv && oi < bi)) {
+                bv = ov;
+                bi = oi;
+            }
+        }
+        const bool m = bi != 0;
+        const float zv = l * invt;
+        const float mx = wave_max(zv);
+        const float e = act ? expf(zv - mx) : 0.f;
+        const float lp = zv - mx - logf(wave_sum(e));
+        float dz = 0.f;
+        if (em > 0.f) {
+            const float dH = act ? -p * (lp + H) : 0.f;
+            if (hp.non_blank) {
+                if (m && Kd > 0) dz += em * (float)(1.0 / Kd) * dH;
+            } else {
+                dz += em * (1.0f / T) * dH;
+            }
+        }
+        if (use_mcc) {
+            const float wt = Ws[t];
+            // dP_j = wt * sum_a p_a S_aj
+            float dp = 0.f;
+            for (int a = 0; a < V; ++a) {
+                const float pa = __shfl(p, a, 64);
+                if (act) dp += pa * Sm[a * 64 + lane];
+            }
+            dp *= wt;
+            const float sd = wave_sum(act ? dp * p : 0.f);
+            dz += (1.0f - em) * (act ? p * (dp - sd) : 0.f);
+        }
+        float g = dz * invt;
+        if (hp.div_coef > 0.f && act && lane >= 1) g += hp.div_coef * qv[lane] * (lqv[lane] + (float)Hq) / T;
+        if (act) dL[(long)t * V + lane] = g;
+    }
+    if (threadIdx.x == 0 && loss_out) {
+        double lv = 0.0;
+        if (em > 0.f) {
+            if (hp.non_blank) lv += em * (K > 0 ? scal[2] / K : NAN);
+            else lv += em * scal[3] / T;
+        }
+        if (use_mcc) lv += (1.0 - em) * mcc;
+        if (hp.div_coef > 0.f) lv += hp.div_coef * (-Hq);
+        loss_out[b] = (float)lv;
+    }
+}
+
+__global__ __launch_bounds__(256) void argmax_kernel(const float* __restrict__ logits, long rows, int V,
+                                                     int* __restrict__ ids) {
+    const long r = (long)blockIdx.x * 256 + threadIdx.x;
+    if (r >= rows) return;
+    const float* l = logits + r * V;
+    float bv = l[0];
+    int bi = 0;
+    for (int j = 1; j < V; ++j)
+        if (l[j] > bv) {
+            bv = l[j];
+            bi = j;
+        }
+    ids[r] = bi;
+}
+
+// ------------------------------------------------------------------------------------------
+// AdamW (torch single-tensor path, decoupled wd) with k sub-steps per element
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ P, const float* __restrict__ G,
+                                                   float* __restrict__ M, float* __restrict__ Vv, long pstride,
+                                                   AdamArgs a, long total) {
+    const int b = blockIdx.y;
+    const long base = (long)b * pstride;
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+        // map i to (run, offset)
+        long rem = i;
+        int run = 0;
+        while (run < a.nruns && rem >= a.runs[run].len) {
+            rem -= a.runs[run].len;
+            ++run;
+        }
+        if (run >= a.nruns) continue;
+        const long idx = base + a.runs[run].start + rem;
+        const int k = a.runs[run].k;
+        const float g = G[idx];
+        float p = P[idx], m = M[idx], v = Vv[idx];
+        for (int j = 0; j < k; ++j) {
+            if (a.lr_wd != 0.f) p *= 1.0f - a.lr_wd;
+            m = m + a.omb1 * (g - m);                 // lerp_(g, 1-beta1), weight < 0.5 form
+            v = v * a.beta2 + a.omb2 * (g * g);        // mul_(beta2).addcmul_(g, g, 1-beta2)
+            const float denom = sqrtf(v) / a.bc2_sqrt[k - 1][j] + a.eps;
+            p = p + (-a.step_size[k - 1][j]) * (m / denom);      // addcdiv_(m, denom, -step_size)
+        }
+        P[idx] = p;
+        M[idx] = m;
+        Vv[idx] = v;
+    }
+}
+
+}  // namespace
+
+// ==========================================================================================
+// launchers
+// ==========================================================================================
+void launch_wave_normalize(const float* x, float* y, int B, long N, hipStream_t st) {
+    hipLaunchKernelGGL(wave_normalize_kernel, dim3(B), dim3(256), 0, st, x, y, N);
+}
+
+void launch_conv0(const float* x, long N, const float* W, const float* bias, long wstride, float* z, int B, int L0,
+                  int C, int K, int S, hipStream_t st) {
+    hipLaunchKernelGGL(conv0_kernel, dim3(cdiv(L0, C0_ROWS), B), dim3(256), 0, st, x, N, W, bias, wstride, z, L0, C,
+                       K, S);
+}
+
+void launch_col_stats(const float* z, int B, int rows, int C, float eps, double* part, float* mean, float* rstd,
+                      hipStream_t st) {
+    const int nchunk = cdiv(rows, CS_ROWS);
+    hipLaunchKernelGGL(col_stats_partial, dim3(nchunk, B), dim3(256), 0, st, z, rows, C, part, nchunk);
+    hipLaunchKernelGGL(col_stats_final, dim3(cdiv(C, 256), B), dim3(256), 0, st, part, nchunk, rows, C, eps, mean,
+                       rstd);
+}
+
+static int ew_grid(long n) { return (int)std::min<long>(2048, std::max<long>(1, (n + 255) / 256)); }
+
+void launch_gn_apply_gelu(const float* z, const float* mean, const float* rstd, const float* g, const float* beta,
+                          long pstride, float* a, int B, int rows, int C, hipStream_t st) {
+    const long n = (long)rows * C;
+    hipLaunchKernelGGL(gn_apply_gelu_kernel, dim3(std::max(1, ew_grid(n) / std::max(1, B / 2)), B), dim3(256), 0, st,
+                       z, mean, rstd, g, beta, pstride, a, rows, C);
+}
+
+void launch_gn_gelu_bwd(const float* da, const float* z, const float* mean, const float* rstd, const float* g,
+                        const float* beta, long pstride, float* dz, float* dgamma, float* dbeta, long gstride, int B,
+                        int rows, int C, double* part, hipStream_t st) {
+    const int nchunk = cdiv(rows, CS_ROWS);
+    hipLaunchKernelGGL(gn_bwd_partial, dim3(nchunk, B), dim3(256), 0, st, da, z, mean, rstd, g, beta, pstride, rows,
+                       C, part, nchunk);
+    float* coef = reinterpret_cast<float*>(part + (long)B * nchunk * 2 * C);
+    hipLaunchKernelGGL(gn_bwd_final, dim3(cdiv(C, 256), B), dim3(256), 0, st, part, nchunk, C, dgamma, dbeta, gstride,
+                       coef);
+    const long n = (long)rows * C;
+    hipLaunchKernelGGL(gn_bwd_dx, dim3(std::max(1, ew_grid(n) / std::max(1, B / 2)), B), dim3(256), 0, st, da, z,
+                       mean, rstd, g, beta, pstride, coef, dz, rows, C);
+}
+
+void launch_layernorm_fwd(const float* x, const float* g, const float* beta, long pstride, int rows_per_utt,
+                          float* y, float* xhat, float* rstd, int rows, int D, float eps, int gelu_out,
+                          hipStream_t st) {
+    dim3 grid(cdiv(rows, 4));
+    if (D <= 256)
+        hipLaunchKernelGGL(layernorm_fwd_kernel<4>, grid, dim3(256), 0, st, x, g, beta, pstride, rows_per_utt, y, xhat,
+                           rstd, rows, D, eps, gelu_out);
+    else if (D <= 512)
+        hipLaunchKernelGGL(layernorm_fwd_kernel<8>, grid, dim3(256), 0, st, x, g, beta, pstride, rows_per_utt, y, xhat,
+                           rstd, rows, D, eps, gelu_out);
+    else
+        hipLaunchKernelGGL(layernorm_fwd_kernel<16>, grid, dim3(256), 0, st, x, g, beta, pstride, rows_per_utt, y,
+                           xhat, rstd, rows, D, eps, gelu_out);
+}
+
+void launch_layernorm_bwd(const float* dy, const float* xhat, const float* rstd, const float* g, const float* beta,
+                          long pstride, int rows_per_utt, int B, int D, int gelu_in, const float* post_aux,
+                          const float* resid, float* dx, float* dgamma, float* dbeta, long gstride, float* part,
+                          hipStream_t st) {
+    const int nchunk = cdiv(rows_per_utt, LNB_ROWS);
+    float* pp = (dgamma || dbeta) ? part : nullptr;
+    dim3 grid(nchunk, B);
+    if (D <= 256)
+        hipLaunchKernelGGL(layernorm_bwd_kernel<4>, grid, dim3(256), 0, st, dy, xhat, rstd, g, beta, pstride,
+                           rows_per_utt, D, gelu_in, post_aux, resid, dx, pp, nchunk);
+    else if (D <= 512)
+        hipLaunchKernelGGL(layernorm_bwd_kernel<8>, grid, dim3(256), 0, st, dy, xhat, rstd, g, beta, pstride,
+                           rows_per_utt, D, gelu_in, post_aux, resid, dx, pp, nchunk);
+    else
+        hipLaunchKernelGGL(layernorm_bwd_kernel<16>, grid, dim3(256), 0, st, dy, xhat, rstd, g, beta, pstride,
+                           rows_per_utt, D, gelu_in, post_aux, resid, dx, pp, nchunk);
+    if (pp)
+        hipLaunchKernelGGL(chunk_reduce, dim3(cdiv(D, 256), B), dim3(256), 0, st, pp, nchunk, 2, D, dgamma, dbeta,
+                           gstride);
+}
+
+void launch_colsum(const float* x, int B, int rows, int C, float* out, long ostride, float* part, hipStream_t st) {
+    const int nchunk = cdiv(rows, CS_ROWS);
+    hipLaunchKernelGGL(colsum_partial, dim3(nchunk, B), dim3(256), 0, st, x, rows, C, part, nchunk);
+    hipLaunchKernelGGL(chunk_reduce, dim3(cdiv(C, 256), B), dim3(256), 0, st, part, nchunk, 1, C, out, (float*)nullptr,
+                       ostride);
+}
+
+void launch_softmax_rows(float* s, long nrows, int T, long ld, hipStream_t st) {
+    dim3 grid((unsigned)((nrows + 3) / 4));
+    if (T <= 256) hipLaunchKernelGGL(softmax_rows_kernel<4>, grid, dim3(256), 0, st, s, nrows, T, ld);
+    else if (T <= 512) hipLaunchKernelGGL(softmax_rows_kernel<8>, grid, dim3(256), 0, st, s, nrows, T, ld);
+    else if (T <= 1024) hipLaunchKernelGGL(softmax_rows_kernel<16>, grid, dim3(256), 0, st, s, nrows, T, ld);
+    else hipLaunchKernelGGL(softmax_rows_kernel<32>, grid, dim3(256), 0, st, s, nrows, T, ld);
+}
+
+void launch_softmax_bwd_rows(const float* P, float* dP, long nrows, int T, long ld, float scale, hipStream_t st) {
+    dim3 grid((unsigned)((nrows + 3) / 4));
+    if (T <= 256) hipLaunchKernelGGL(softmax_bwd_rows_kernel<4>, grid, dim3(256), 0, st, P, dP, nrows, T, ld, scale);
+    else if (T <= 512)
+        hipLaunchKernelGGL(softmax_bwd_rows_kernel<8>, grid, dim3(256), 0, st, P, dP, nrows, T, ld, scale);
+    else if (T <= 1024)
+        hipLaunchKernelGGL(softmax_bwd_rows_kernel<16>, grid, dim3(256), 0, st, P, dP, nrows, T, ld, scale);
+    else hipLaunchKernelGGL(softmax_bwd_rows_kernel<32>, grid, dim3(256), 0, st, P, dP, nrows, T, ld, scale);
+}
+
+void launch_col2im(const float* dcol, int B, int Lout, int Lin, int C, int K, int S, const float* z, float* da,
+                   hipStream_t st) {
+    const long n = (long)Lin * C;
+    hipLaunchKernelGGL(col2im_kernel, dim3(std::max(1, ew_grid(n) / std::max(1, B / 2)), B), dim3(256), 0, st, dcol,
+                       Lout, Lin, C, K, S, z, da);
+}
+
+void launch_dgelu_mul(const float* g, const float* z, float* out, long n, hipStream_t st) {
+    hipLaunchKernelGGL(dgelu_mul_kernel, dim3(ew_grid(n)), dim3(256), 0, st, g, z, out, n);
+}
+
+void launch_suta_loss(const float* logits, int B, int T, int V, LossHP hp, float* dlogits, float* loss,
+                      float* scratch, hipStream_t st) {
+    hipLaunchKernelGGL(suta_loss_kernel, dim3(B), dim3(256), 0, st, logits, T, V, hp, dlogits, loss, scratch);
+}
+
+void launch_argmax(const float* logits, long rows, int V, int* ids, hipStream_t st) {
+    hipLaunchKernelGGL(argmax_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, st, logits, rows, V, ids);
+}
+
+void launch_adam(float* P, const float* G, float* M, float* V, long pstride, int B, const AdamArgs& a,
+                 hipStream_t st) {
+    long total = 0;
+    for (int r = 0; r < a.nruns; ++r) total += a.runs[r].len;
+    if (total == 0) return;
+    const int gx = (int)std::min<long>(std::max<long>(1, 4096 / std::max(1, B)), (total + 255) / 256);
+    hipLaunchKernelGGL(adam_kernel, dim3(gx, B), dim3(256), 0, st, P, G, M, V, pstride, a, total);
+}

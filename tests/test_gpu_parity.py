@@ -1,0 +1,180 @@
+"""GPU tier: libsuta (HIP, gfx950) against the committed reference goldens and the CPU oracle.
+
+Every call goes through the C ABI (include/suta.h) via the ctypes binding.
+Tolerances (stated per test):
+  * fused loss-and-grad vs reference autograd (float64 golden): |d| <= 2e-6 * max|g| + 1e-9
+  * adapted logits vs reference: tests/parity.logits_tol(lr) = 2e-5 + 0.2*lr absolute
+  * adapted tensors: tests/parity.assert_params_close (Adam sign-flip budget)
+"""
+import ast
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from suta_amd import synth
+from suta_amd.config import get_config
+from suta_amd.engine import SutaEngine, SutaHParams
+from suta_amd.weights import synth_weights
+from tests.parity import assert_params_close, logits_tol
+
+pytestmark = pytest.mark.gpu
+
+G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+_ENGINES = {}
+
+
+def engine(preset, max_batch=4, blank_bias=1.0):
+    key = (preset, max_batch, blank_bias)
+    if key not in _ENGINES:
+        cfg = get_config(preset)
+        _ENGINES[key] = (SutaEngine(cfg, synth_weights(cfg, blank_bias=blank_bias), max_batch=max_batch), cfg)
+    return _ENGINES[key]
+
+
+def _load(name):
+    return np.load(os.path.join(G, name), allow_pickle=False)
+
+
+def test_loss_kernel_matches_reference_autograd():
+    eng, _ = engine("tiny-group")
+    z = _load("g1_loss_grad.npz")
+    for case in z["cases"]:
+        L = z[f"{case}/logits"]
+        temp, em, rw, nb, div = z[f"{case}/hp"]
+        hp = SutaHParams(temp=float(temp), em_coef=float(em), reweight=bool(rw), non_blank=bool(nb), div_coef=float(div))
+        d, loss = eng.loss_grad(L, hp)
+        ref = z[f"{case}/grad_f64"]
+        np.testing.assert_allclose(d[0], ref, rtol=0, atol=2e-6 * np.abs(ref).max() + 1e-9, err_msg=str(case))
+        rl = float(z[f"{case}/loss_f64"])
+        if np.isnan(rl):
+            assert np.isnan(loss[0]), case
+        else:
+            assert abs(loss[0] - rl) <= 1e-5 * max(1.0, abs(rl)), (case, loss[0], rl)
+
+
+@pytest.mark.parametrize("variant", ["group", "group_lr5e-4", "layer", "layer_lr5e-4", "group_lnonly",
+                                     "group_biasonly", "group_em1"])
+def test_tiny_suta_matches_reference(variant):
+    z = _load(f"g3_tiny_{variant}.npz")
+    preset = "tiny-group" if variant.startswith("group") else "tiny-layer"
+    eng, cfg = engine(preset)
+    h = ast.literal_eval(str(z["hp_json"]))
+    hp = SutaHParams(lr=h["lr"], temp=h["temp"], em_coef=h["em"], reweight=h["rw"], non_blank=h["nb"],
+                     div_coef=h["div"], train_feature=h["train_feature"], bias_only=h["bias_only"])
+    for n in (8000, 12345):
+        x = z[f"N{n}/x"]
+        logits, ids, T = eng.adapt(x, 10, hp, record=list(range(11)))
+        ref = z[f"N{n}/logits"]
+        for i in range(11):
+            np.testing.assert_allclose(logits[i][0], ref[i], rtol=0, atol=logits_tol(h["lr"]),
+                                       err_msg=f"{variant} N{n} step {i}")
+            np.testing.assert_array_equal(ids[i][0], logits[i][0].argmax(-1))
+        for key in z.files:
+            if key.startswith(f"N{n}/final/"):
+                name = key[len(f"N{n}/final/"):]
+                assert_params_close(eng.get_param(0, name), z[key], h["lr"], 10, name=name)
+
+
+@pytest.mark.parametrize("n", [16000, 32000])
+def test_base_suta_matches_reference(n):
+    z = _load(f"g4_base_{n}.npz")
+    eng, cfg = engine("wav2vec2-base")
+    x = synth.wave(n, 0 if n == 16000 else 1)
+    steps = [int(s) for s in z["steps"]]
+    logits, ids, T = eng.adapt(x, 10, SutaHParams(), record=steps)
+    for j, s in enumerate(steps):
+        np.testing.assert_allclose(logits[s][0], z["logits"][j], rtol=0, atol=5e-5, err_msg=f"step {s}")
+    for key in z.files:
+        if key.startswith("final/") and key.endswith("/idx"):
+            name = key[len("final/"):-len("/idx")]
+            got = eng.get_param(0, name).reshape(-1)[z[key]]
+            assert_params_close(got, z[f"final/{name}/val"], 2e-5, 10, max_frac=0.05, name=name)
+
+
+def test_base_forward_matches_oracle_8s():
+    """Vanilla logits at the bench length (8 s, T = 399) against the CPU oracle."""
+    from oracle import w2v2_cpu as W
+    eng, cfg = engine("wav2vec2-base")
+    x = synth.wave(128000, 3)
+    eng.reset()
+    got = eng.forward(x)[0]
+    sd = synth_weights(cfg)
+    with torch.no_grad():
+        ref = W.forward({k: torch.from_numpy(v) for k, v in sd.items()}, cfg, torch.from_numpy(x)[None])[0].numpy()
+    np.testing.assert_allclose(got, ref, rtol=0, atol=5e-5)
+
+
+def test_raw_wave_normalisation_on_device():
+    eng, cfg = engine("tiny-group")
+    raw = synth.raw_wave(9000, 5)
+    eng.reset()
+    a = eng.forward(raw, normalize=True)
+    b = eng.forward(synth.normalize(raw), normalize=False)
+    np.testing.assert_allclose(a, b, rtol=0, atol=2e-5)
+
+
+def test_step_api_equals_adapt_schedule():
+    """Reference schedule (suta_step: 2 forwards/step) == minimal schedule (suta_adapt)."""
+    eng, cfg = engine("tiny-group")
+    x = synth.wave(10000, 7)
+    hp = SutaHParams(lr=5e-4)
+    logits, _, _ = eng.adapt(x, 3, hp, record=[3])
+    eng.reset()
+    for _ in range(3):
+        out, loss = eng.step(x, hp)
+    np.testing.assert_allclose(out[0], logits[3][0], rtol=0, atol=1e-6)
+    assert np.isfinite(loss).all()
+
+
+def test_batch_equals_independent_runs():
+    eng, cfg = engine("tiny-group", max_batch=4)
+    xs = synth.batch(11000, 3, start=20)
+    hp = SutaHParams(lr=5e-4)
+    lb, ib, _ = eng.adapt(xs, 5, hp, record=[0, 5])
+    for b in range(3):
+        l1, _, _ = eng.adapt(xs[b], 5, hp, record=[0, 5])
+        np.testing.assert_allclose(lb[5][b], l1[5][0], rtol=0, atol=logits_tol(5e-4))
+        np.testing.assert_allclose(lb[0][b], l1[0][0], rtol=0, atol=1e-5)
+
+
+def test_bitwise_deterministic():
+    eng, cfg = engine("wav2vec2-base")
+    x = synth.wave(32000, 9)
+    a, _, _ = eng.adapt(x, 3, SutaHParams(), record=[3])
+    b, _, _ = eng.adapt(x, 3, SutaHParams(), record=[3])
+    assert np.array_equal(a[3], b[3])
+
+
+def test_episodic_reset_restores_pristine_tensors():
+    eng, cfg = engine("tiny-layer")
+    sd = synth_weights(cfg)
+    eng.adapt(synth.wave(9000, 1), 2, SutaHParams(lr=1e-3), record=[])
+    eng.reset()
+    for name in eng.trainable_names():
+        assert np.array_equal(eng.get_param(0, name), sd[name]), name
+
+
+@pytest.mark.parametrize("preset", ["wav2vec2-base", "tiny-layer"])
+@pytest.mark.parametrize("tf,bo", [(True, False), (False, False), (True, True)])
+def test_multiplicity_matches_collect_params(preset, tf, bo):
+    from oracle import w2v2_cpu as W
+    eng, cfg = engine(preset)
+    mult = W.multiplicity(W.trainable_entries(cfg, bias_only=bo, train_feature=tf))
+    for name in eng.trainable_names():
+        assert eng.param_info(name, tf, bo)[0] == mult.get(name, 0), name
+    for name in mult:
+        assert eng.param_info(name, tf, bo)[0] == mult[name], name
+
+
+def test_all_blank_utterance_keeps_finite_params():
+    """K = 0 non-blank frames: reference loss is NaN but the gradient stays finite."""
+    eng, cfg = engine("tiny-group", blank_bias=60.0)
+    x = synth.wave(8000, 2)
+    logits, ids, _ = eng.adapt(x, 2, SutaHParams(lr=5e-4), record=[0, 2])
+    assert (ids[0] == 0).all()
+    out, loss = eng.step(x, SutaHParams(lr=5e-4))
+    assert np.isnan(loss).all()
+    for name in eng.trainable_names():
+        assert np.isfinite(eng.get_param(0, name)).all(), name
