@@ -1,0 +1,153 @@
+"""Bench: adapted utterances/sec, 10-step SUTA on wav2vec2-base shapes (BASELINE.json config 2).
+
+One bench "step" = one libsuta `suta_adapt` call over a batch of `--batch` synthetic 8 s
+utterances (N = 128000 samples, T = 399 frames), each adapted for 10 SUTA steps with the
+scripts/LS.sh flags (episodic reset, vanilla forward, greedy ids recorded at steps 0/1/3/5/10).
+Waveforms are resident in HBM before the timed region.  Seeded random weights of the
+w2v2-base architecture (no checkpoints offline).
+
+Multi-GPU: one process per GPU (torchrun); every rank adapts its own utterances (no data-path
+collective, weak scaling); a barrier + device sync brackets the timed region and the max
+elapsed time over ranks is used.  value = utterances of all ranks / that time.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+import suta_loader  # noqa: E402
+
+suta_loader.load()
+import torch  # noqa: E402
+
+from suta_amd import synth  # noqa: E402
+from suta_amd.config import get_config, num_frames  # noqa: E402
+from suta_amd.engine import SutaEngine, SutaHParams  # noqa: E402
+from suta_amd.flops import suta_flops  # noqa: E402
+from suta_amd.weights import synth_weights  # noqa: E402
+
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
+RECORD = [0, 1, 3, 5, 10]
+
+
+def cpu_baseline(cfg, n_samples, suta_steps, budget_s=25.0):
+    """The oracle (PyTorch-CPU restatement of the reference loop) on host cores, bounded sample."""
+    from oracle import w2v2_cpu as W
+    cores = min(16, len(os.sched_getaffinity(0)))
+    torch.set_num_threads(cores)
+    sd = {k: torch.from_numpy(v) for k, v in synth_weights(cfg).items()}
+    W.run_suta(sd, cfg, torch.from_numpy(synth.wave(16000, 999))[None], 1)          # warm-up
+    done, t0 = 0, time.perf_counter()
+    while True:
+        x = torch.from_numpy(synth.wave(n_samples, 1000 + done))[None]
+        W.run_suta(sd, cfg, x, suta_steps, record=[0, suta_steps])
+        done += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or done >= 4:
+            break
+    return {"value": done / el, "unit": "utt/s", "cores": cores, "kind": "port",
+            "sample": f"{done} utterance(s) of {n_samples} samples, {suta_steps} SUTA steps each, oracle/w2v2_cpu.py "
+                      f"run_suta (torch {torch.__version__} CPU, {cores} threads), {el:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=4)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=16, help="utterances in flight per GPU (engine slots)")
+    ap.add_argument("--n-samples", type=int, default=128000)
+    ap.add_argument("--suta-steps", type=int, default=10)
+    ap.add_argument("--model", default="wav2vec2-base")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP-event timing")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.cuda.current_device()
+
+    cfg = get_config(args.model)
+    B, N, S = args.batch, args.n_samples, args.suta_steps
+    eng = SutaEngine(cfg, synth_weights(cfg), device=dev, max_batch=B, max_samples=N)
+    hp = SutaHParams()  # scripts/LS.sh flags
+    nbatches = args.warmup + args.steps
+    # inputs resident in HBM before timing: distinct utterances per rank and batch
+    waves = [torch.from_numpy(synth.batch(N, B, start=(rank * nbatches + i) * B)).to(f"cuda:{dev}")
+             for i in range(nbatches)]
+    torch.cuda.synchronize()
+
+    for i in range(args.warmup):
+        eng.adapt(waves[i], S, hp, record=RECORD, want_logits=False)
+    if not args.no_timing:
+        eng.set_timing(True)
+
+    def barrier():
+        if dist:
+            tdist.barrier()
+        torch.cuda.synchronize()
+        eng.sync()
+
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        eng.adapt(waves[args.warmup + i], S, hp, record=RECORD, want_logits=False)
+    eng.sync()
+    barrier()
+    el = time.perf_counter() - t0
+    timing = eng.get_timing() if not args.no_timing else None
+    if dist:
+        t = torch.tensor([el], device=f"cuda:{dev}")
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        el = float(t.item())
+
+    utts = B * args.steps * world
+    value = utts / el
+    flops_utt = suta_flops(cfg, N, S)
+    out = {
+        "metric": "adapted utterances/sec (whole node) at 10 SUTA steps, w2v2-base; WER parity",
+        "value": round(value, 4), "unit": "utt/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(1000 * el / args.steps, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": f"{args.model} SUTA {S} steps on {N}-sample (8 s) utterances, {B} utterances "
+                               f"per GPU per step, scripts/LS.sh flags",
+                   "model": args.model, "global_batch": B * world, "seq_len": num_frames(cfg, N),
+                   "n_samples": N, "suta_steps": S, "parallelism": f"utterance-sharded x{world}"},
+        "algorithmic_tflops": round(flops_utt * utts / el / 1e12, 3),
+    }
+    if timing:
+        gms, gn = timing["gemm"]
+        # dominant kernel family: the fp32 MFMA GEMM (every conv/linear/attention product)
+        gemm_flops = flops_utt * B * args.steps  # per-rank algorithmic GEMM-shaped FLOPs
+        achieved = gemm_flops / (gms / 1000.0) / 1e12 if gms > 0 else None
+        out["roofline"] = {"bound": "mfma", "achieved": round(achieved, 3) if achieved else None,
+                           "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                           "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4) if achieved else None,
+                           "traffic": None,
+                           "kernel": "gemm_f32_kernel (all launches)",
+                           "launches": int(gn), "avg_launch_ms": round(gms / max(1, gn), 5)}
+        out["time_breakdown_ms"] = {k: round(v[0], 2) for k, v in timing.items()}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(cfg, N, S)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if dist:
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
