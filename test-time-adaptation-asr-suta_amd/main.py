@@ -1,0 +1,211 @@
+"""main.py-compatible driver (reference main.py:217-454) on the libsuta engine.
+
+Same flags, same stdout lines ("original WER:", "adapt-k WER:", "TTA-k WER:"), same log
+file `log_dir/exp_name` and CSV.  Differences, all deliberate:
+  * the adapt loop runs in libsuta (HIP) with the minimal schedule: the logits recorded after
+    step k equal the reference's re-inference output of step k;
+  * utterances are adapted one per engine call (the reference's batch_size > 1 pads without
+    a mask and breaks mcc_loss, main.py:32);
+  * under torchrun, utterances are LPT-sharded over ranks and WER counts are all_reduce'd;
+  * pretrained weights load from a local checkpoint directory or the local HF cache (no
+    network); `--synthetic_weights` uses the seeded generator instead;
+  * when --steps < 10 the CSV is written with empty WERR (the reference raises there).
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+from typing import Dict, List
+
+import numpy as np
+
+SAMPLE_RATE = 16000
+CHECKPOINTS = (1, 3, 5, 10, 20, 40)
+
+
+def build_parser():
+    p = argparse.ArgumentParser(description="TTA ASR")
+    p.add_argument("--asr", type=str, default="facebook/wav2vec2-base-960h")
+    p.add_argument("--steps", type=int, default=40)
+    p.add_argument("--episodic", action="store_true")
+    p.add_argument("--div_coef", type=float, default=0.0)
+    p.add_argument("--opt", type=str, default="AdamW")
+    p.add_argument("--dataset_name", type=str, default="librispeech")
+    p.add_argument("--dataset_dir", type=str, default="/home/daniel094144/data/LibriSpeech")
+    p.add_argument("--split", default=["test-other"])
+    p.add_argument("--lr", type=float, default=1e-4)
+    p.add_argument("--em_coef", type=float, default=1.0)
+    p.add_argument("--reweight", action="store_true")
+    p.add_argument("--bias_only", action="store_true")
+    p.add_argument("--train_feature", action="store_true")
+    p.add_argument("--train_all", action="store_true")
+    p.add_argument("--batch_size", type=int, default=1)
+    p.add_argument("--temp", type=float, default=2.5)
+    p.add_argument("--non_blank", action="store_true")
+    p.add_argument("--log_dir", type=str, default="./exps")
+    p.add_argument("--extra_noise", type=float, default=0.0)
+    p.add_argument("--scheduler", default=None)
+    # engine-only options
+    p.add_argument("--synthetic_weights", action="store_true", help="seeded random weights (no checkpoint)")
+    p.add_argument("--device", type=int, default=None)
+    return p
+
+
+def exp_name_of(a) -> str:
+    """main.py:267."""
+    return (a.dataset_name + "_" + str(a.em_coef) + "_" + str(a.steps) + "_" + str(a.temp) + "_" +
+            a.asr.split("/")[-1] + "_" + "non_blank" + str(a.non_blank) + "_noise_" + str(a.extra_noise) + "_rew_" +
+            str(a.reweight) + "_div_" + str(a.div_coef) + "_bias_" + str(a.bias_only) + "_feat_" +
+            str(a.train_feature) + "_all_" + str(a.train_all) + "_LN_" + str(True))
+
+
+def load_model(asr: str, synthetic: bool):
+    from .config import get_config
+    from .weights import load_hf_checkpoint, synth_weights
+    if os.path.isdir(asr):
+        return get_config(asr), load_hf_checkpoint(asr)
+    try:
+        from huggingface_hub import snapshot_download
+        d = snapshot_download(asr, local_files_only=True)
+        return get_config(d), load_hf_checkpoint(d)
+    except Exception:
+        if not synthetic:
+            raise RuntimeError(f"no local checkpoint for '{asr}' (offline); pass a checkpoint directory or "
+                               "--synthetic_weights")
+    cfg = get_config(asr)
+    return cfg, synth_weights(cfg)
+
+
+def main(argv=None):
+    a = build_parser().parse_args(argv)
+    if a.opt not in ("AdamW", "Adam"):
+        raise SystemExit(f"--opt {a.opt}: only AdamW/Adam are implemented by the engine")
+    if a.scheduler is not None:
+        raise SystemExit("--scheduler: learning-rate schedulers are not implemented by the engine")
+    if a.train_all:
+        raise SystemExit("--train_all: full-model adaptation is outside the engine's scope")
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    if world > 1:
+        import torch.distributed as tdist
+        if torch.cuda.is_available():
+            torch.cuda.set_device(local)
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            tdist.init_process_group("gloo")
+    device = a.device if a.device is not None else local
+    say = print if rank == 0 else (lambda *x, **k: None)
+
+    from .data import load_dataset
+    from .decode import batch_decode, wer, wer_counts
+    from .dist import gather_objects, lpt_shard, reduce_counts, utterance_cost
+    from .engine import SutaEngine, SutaHParams
+    from .synth import normalize
+
+    exp_name = exp_name_of(a)
+    dataset = load_dataset(a.split, a.dataset_name, a.dataset_dir, a.batch_size, a.extra_noise)
+    say("------------------------------------")
+    say(f"exp: {exp_name}")
+    for line in (f"eposidic? {a.episodic}", f"lr = {a.lr}", f"optim = {a.opt}", f"step = {a.steps}",
+                 f"em_coef = {a.em_coef}", f"reweight = {a.reweight}", f"batch size = {a.batch_size}",
+                 f"temperature = {a.temp}", f"non_blank = {str(a.non_blank)}", f"extra_noise = {a.extra_noise}",
+                 f"scheduler = {str(a.scheduler)}", f"div_coef = {str(a.div_coef)}", f"bias_only = {a.bias_only}",
+                 f"train_feature = {a.train_feature}", f"train_all = {a.train_all}", f"train_LN = {True}"):
+        say(line)
+
+    cfg, weights = load_model(a.asr, a.synthetic_weights)
+    engine = SutaEngine(cfg, weights, device=device, max_batch=1)
+    hp = SutaHParams(lr=a.lr, temp=a.temp, em_coef=a.em_coef, div_coef=a.div_coef, reweight=a.reweight,
+                     non_blank=a.non_blank, train_feature=a.train_feature, bias_only=a.bias_only,
+                     episodic=a.episodic)
+    record = [0] + ([c for c in CHECKPOINTS if c <= a.steps] if a.episodic else [])
+    if not a.episodic:
+        record = sorted(set([0, a.steps]))
+
+    # shard batches over ranks by estimated cost (file size ~ duration)
+    batches = dataset.raw_batches()
+    if world > 1:
+        costs = [sum(utterance_cost(max(1, os.path.getsize(str(f)) // 2), cfg, a.steps) for f, _ in b)
+                 for b in batches]
+        mine = lpt_shard(costs, world)[rank]
+    else:
+        mine = list(range(len(batches)))
+
+    results = []
+    start = time.time()
+    for bi in mine:
+        lens, wavs, texts, files = dataset.collate(batches[bi])
+        for wav, text in zip(wavs, texts):
+            x = normalize(wav)
+            _, ids, T = engine.adapt(x, a.steps, hp, record=record, want_logits=False)
+            rec = {"idx": bi, "text": text, "duration": len(x) / SAMPLE_RATE, "hyp": {}}
+            ori = batch_decode(ids[0])
+            rec["hyp"][0] = ori[0]
+            ori_wer = wer([text], ori)
+            print("original WER: ", ori_wer)
+            if a.episodic:
+                for c in CHECKPOINTS:
+                    if c <= a.steps:
+                        h = batch_decode(ids[c])
+                        rec["hyp"][c] = h[0]
+                        ada = wer([text], h)
+                        print(f"adapt-{c} WER: " + (" " if c < 10 else ""), ada)
+                        if c == 10:
+                            rec["werr"] = ori_wer - ada
+            results.append(rec)
+    elapsed = time.time() - start
+
+    allres = [r for part in gather_objects(results) for r in part]
+    allres.sort(key=lambda r: r["idx"])
+    # corpus WER counts, reduced over ranks (the one data collective)
+    local_counts = {}
+    for key in [0] + list(CHECKPOINTS):
+        sel = [r for r in results if key in r["hyp"]]
+        local_counts[str(key)] = wer_counts([r["text"] for r in sel], [r["hyp"][key] for r in sel]) if sel else (0, 0)
+    counts = reduce_counts(local_counts)
+    if rank == 0:
+        def cw(k):
+            e, w = counts[str(k)]
+            return e / w if w else float("nan")
+        lines = [f"original WER: {cw(0)}"]
+        if a.steps >= 10:
+            lines += [f"TTA-{k} WER: {cw(k)}" for k in (1, 3, 5, 10)]
+        if a.steps >= 20:
+            lines.append(f"TTA-20 WER: {cw(20)}")
+        if a.steps >= 40:
+            lines.append(f"TTA-40 WER: {cw(40)}")
+        print("asr:", a.asr)
+        print("non-adapted count = 0")
+        print(f"dataset num = {len(batches)}")
+        for ln in lines:
+            print(ln)
+        print("------------------------------------")
+        print(f"[suta_amd] adapted {len(allres)} utterances in {elapsed:.1f} s on rank 0's shard, {world} rank(s)")
+        os.makedirs(a.log_dir, exist_ok=True)
+        with open(os.path.join(a.log_dir, exp_name), "w") as f:
+            for ln in lines:
+                f.write(ln + "\n")
+            for ln in (f"eposidic? {a.episodic}", f"lr = {a.lr}", f"optim = {a.opt}", f"step = {a.steps}",
+                       f"em_coef = {a.em_coef}", f"reweight = {a.reweight}", f"batch size = {a.batch_size}",
+                       f"temperature = {a.temp}", f"non_blank = {str(a.non_blank)}", f"extra_noise = {a.extra_noise}",
+                       f"scheduler = {str(a.scheduler)}", f"div_coef = {str(a.div_coef)}",
+                       f"bias_only = {str(a.bias_only)}", f"train_feature = {str(a.train_feature)}",
+                       f"train_all = {str(a.train_all)}", f"train_LN = {str(True)}"):
+                f.write(ln + "\n")
+        import pandas as pd
+        durations = [r["duration"] for r in allres]
+        werrs = [r.get("werr", np.nan) for r in allres]
+        pd.DataFrame({"duration": durations, "WERR": werrs}).to_csv(os.path.join(a.log_dir, exp_name + ".csv"))
+    engine.close()
+    if world > 1:
+        import torch.distributed as tdist
+        tdist.destroy_process_group()
+    return counts
+
+
+if __name__ == "__main__":
+    main()

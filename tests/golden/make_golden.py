@@ -203,9 +203,27 @@ def g4(ref):
         print("g4", n, "done")
 
 
+def g5(ref):
+    """CTC decode of random id sequences by HF Wav2Vec2CTCTokenizer on the reference vocab.json."""
+    import json
+    from transformers import Wav2Vec2CTCTokenizer
+    tok = Wav2Vec2CTCTokenizer(os.path.join(REF, "vocab.json"))
+    rng = np.random.default_rng(5)
+    cases = []
+    for i in range(200):
+        T = int(rng.integers(0, 60))
+        p_blank = rng.uniform(0.2, 0.9)
+        ids = [0 if rng.uniform() < p_blank else int(rng.integers(1, 32)) for _ in range(T)]
+        if i % 7 == 0:  # long repeats and delimiter runs
+            ids = [int(v) for v in np.repeat(rng.integers(0, 8, size=max(1, T // 4)), 4)]
+        cases.append({"ids": ids, "text": tok.batch_decode([ids])[0] if ids else tok.decode([])})
+    with open(os.path.join(HERE, "g5_ctc_decode.json"), "w") as f:
+        json.dump(cases, f)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
     ref = import_reference()
-    which = sys.argv[1:] or ["g1", "g2", "g3", "g4"]
+    which = sys.argv[1:] or ["g1", "g2", "g3", "g4", "g5"]
     for w in which:
         globals()[w](ref)

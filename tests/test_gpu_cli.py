@@ -1,0 +1,66 @@
+"""GPU tier: the main.py-compatible driver end to end on a synthetic CHiME-layout corpus.
+
+Transcripts and WER are checked against the CPU oracle run on the same normalised audio.
+"""
+import os
+import wave
+
+import numpy as np
+import pytest
+import torch
+
+from suta_amd import main as M
+from suta_amd.config import get_config
+from suta_amd.data import AudioReader
+from suta_amd.decode import batch_decode, wer_counts
+from suta_amd.synth import normalize
+from suta_amd.weights import synth_weights
+
+pytestmark = pytest.mark.gpu
+
+
+def _corpus(root, n=4):
+    apath = root / "data/audio/16kHz/enhanced/et05_bus_real"
+    tpath = root / "data/transcriptions/et05_bus_real"
+    apath.mkdir(parents=True)
+    tpath.mkdir(parents=True)
+    rng = np.random.default_rng(11)
+    words = ["HELLO", "WORLD", "THE", "CAT", "SAT", "ON", "A", "MAT"]
+    for i in range(n):
+        x = rng.standard_normal(6000 + 1500 * i) * 0.1
+        with wave.open(str(apath / f"U{i}.wav"), "wb") as f:
+            f.setnchannels(1)
+            f.setsampwidth(2)
+            f.setframerate(16000)
+            f.writeframes((np.clip(x, -1, 1) * 32767).astype("<i2").tobytes())
+        (tpath / f"U{i}.trn").write_text(f"U{i} " + " ".join(rng.choice(words, size=3 + i)) + "\n")
+
+
+def test_cli_end_to_end_matches_oracle(tmp_path, capsys):
+    from oracle import w2v2_cpu as W
+    _corpus(tmp_path)
+    args = (f"--asr tiny-group --synthetic_weights --steps 10 --dataset_name chime --dataset_dir {tmp_path} "
+            f"--temp 2.5 --episodic --em_coef 0.3 --reweight --log_dir {tmp_path}/exps --lr 5e-4 --non_blank "
+            f"--train_feature --extra_noise 0").split()
+    counts = M.main(args)
+    out = capsys.readouterr().out
+    assert "original WER: " in out and "adapt-10 WER: " in out and "TTA-10 WER:" in out
+    a = M.build_parser().parse_args(args)
+    log = open(os.path.join(a.log_dir, M.exp_name_of(a))).read().splitlines()
+    assert log[0].startswith("original WER: ") and log[4].startswith("TTA-10 WER: ")
+    assert os.path.exists(os.path.join(a.log_dir, M.exp_name_of(a) + ".csv"))
+
+    # oracle: same audio, same flags
+    cfg = get_config("tiny-group")
+    sd = {k: torch.from_numpy(v) for k, v in synth_weights(cfg).items()}
+    from suta_amd.data import CHiMEDataset
+    ds = CHiMEDataset(None, 1, str(tmp_path))
+    reader = AudioReader(0.0)
+    hyps = {k: [] for k in (0, 1, 3, 5, 10)}
+    for f, t in zip(ds.file_list, ds.text):
+        x = torch.from_numpy(normalize(reader(str(f))))[None]
+        lg, _ = W.run_suta(sd, cfg, x, 10, lr=5e-4, record=[0, 1, 3, 5, 10])
+        for k in hyps:
+            hyps[k].append(batch_decode(lg[k].argmax(-1).numpy())[0])
+    for k in hyps:
+        assert tuple(counts[str(k)]) == wer_counts(list(ds.text), hyps[k]), k
