@@ -60,7 +60,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=16, help="utterances in flight per GPU (engine slots)")
+    ap.add_argument("--batch", type=int, default=64, help="utterances in flight per GPU (engine slots)")
     ap.add_argument("--n-samples", type=int, default=128000)
     ap.add_argument("--suta-steps", type=int, default=10)
     ap.add_argument("--model", default="wav2vec2-base")

@@ -82,3 +82,5 @@ struct GemmParams {
 void gemm_init(GemmParams& p);
 // Launch; ws/ws_floats: scratch for split-K (may be null -> no split).
 void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats);
+// Benchmark/test override: tile (-1 auto, 0 128x128, 1 128x64, 2 64x128, 3 64x64), LDS buffers (1|2).
+void gemm_set_variant(int tile, int nbuf);

@@ -6,60 +6,64 @@
 // matrix a plain matrix with lda = stride*C), their weight gradients (TN, split-K over
 // time), and the grouped positional conv through the conv-A (segmented K) loader.
 //
-// Block = 256 threads = 4 waves (WM x WN), block tile BM x BN, K-step 16 staged through
-// LDS in a k-contiguous layout [row][16 + 4 pad] so every MFMA operand is read with
-// ds_read_b128 (row stride 20 dwords: conflict-free over the b128 lane groups).
-// The MFMA k-pair (lane half h) takes tile-k h*8 + 4q + e, q<2, e<4, so each lane's four
-// consecutive k come from one 16-B LDS read.  Global->register prefetch of stage s+1
-// overlaps the MFMAs of stage s.
+// Block = 256 threads = 4 waves (2 x 2), block tile BM x BN, K-step 32.  Each operand is
+// staged through LDS in the layout its global source makes conflict-free:
+//   k-contiguous source  -> LDS [row][32 + 4]  (16-B writes; 16-B fragment reads, row stride
+//                           36 dwords: conflict-free over the ds_read_b128 lane groups)
+//   row-contiguous source -> LDS [k][ROWS]    (16-B writes; 4-B fragment reads by 32
+//                           consecutive rows: conflict-free)
+// The MFMA k-pair (lane half h) takes tile-k h*16 + 4q + e, so a k-contiguous fragment is
+// one 16-B read per 4 MFMA k-steps.  Global->register prefetch of stage s+1 overlaps the
+// MFMAs of stage s; with two LDS buffers there is one barrier per K-step.
 #include "common.h"
 #include <algorithm>
 
 namespace {
 
-constexpr int BK = 16;
+constexpr int BK = 32;
 constexpr int LDK = BK + 4;
 
 template <int ROWS>
-struct Stage {
-    static constexpr int LOADS = ROWS * BK / 4 / 256;  // float4 per thread
+struct Op {
+    static constexpr int LOADS = ROWS * BK / 4 / 256;  // float4 per thread per stage
+    static constexpr int KC_FLOATS = ROWS * LDK;
+    static constexpr int MN_FLOATS = BK * ROWS;
 };
 
+template <int ROWS, bool KC>
+constexpr int lds_floats() {
+    return KC ? Op<ROWS>::KC_FLOATS : Op<ROWS>::MN_FLOATS;
+}
+
 // Load one BK-deep stage of an operand into registers.
-//   KC = true : source is k-contiguous (A with ta=0, B with tb=1): element (row, k) at row*ld + k
-//   KC = false: source is row-contiguous (A with ta=1, B with tb=0): element (row, k) at k*ld + row
+//   KC = true : element (row, k) at row*ld + k   (A with ta=0, B with tb=1)
+//   KC = false: element (row, k) at k*ld + row   (A with ta=1, B with tb=0)
 template <int ROWS, bool KC, bool CONV>
-__device__ __forceinline__ void load_stage(f32x4 (&r)[Stage<ROWS>::LOADS], const float* __restrict__ src,
-                                           long ld, int row0, int nrows, int k0, int kend, bool vec,
-                                           int segK, int pad, int Mvalid) {
+__device__ __forceinline__ void load_stage(f32x4 (&r)[Op<ROWS>::LOADS], const float* __restrict__ src, long ld,
+                                           int row0, int nrows, int k0, int kend, bool vec, int segK, int pad,
+                                           int Mvalid) {
     const int tid = threadIdx.x;
 #pragma unroll
-    for (int i = 0; i < Stage<ROWS>::LOADS; ++i) {
+    for (int i = 0; i < Op<ROWS>::LOADS; ++i) {
         const int f = tid + i * 256;
         f32x4 v = {0.f, 0.f, 0.f, 0.f};
         if (KC) {
-            const int row = f >> 2;
-            const int kq = (f & 3) * 4;
+            const int row = f >> 3;
+            const int kq = (f & 7) * 4;
             const int gr = row0 + row;
             const int gk = k0 + kq;
-            if (gr < nrows) {
+            if (gr < nrows && gk < kend) {
+                const float* s;
+                bool ok = true;
                 if (CONV) {
                     const int seg = gk / segK;
-                    const int rr = gk - seg * segK;
                     const int srow = gr + seg - pad;
-                    if (gk < kend && srow >= 0 && srow < Mvalid) {
-                        // segK % 4 == 0 and gk % 4 == 0: the 4 elements stay in one segment
-                        const float* s = src + (long)srow * ld + rr;
-                        if (vec && gk + 3 < kend) {
-                            v = *reinterpret_cast<const f32x4*>(s);
-                        } else {
-#pragma unroll
-                            for (int e = 0; e < 4; ++e)
-                                if (gk + e < kend) v[e] = s[e];
-                        }
-                    }
+                    ok = srow >= 0 && srow < Mvalid;
+                    s = src + (long)srow * ld + (gk - seg * segK);  // segK % 4 == 0: one segment
                 } else {
-                    const float* s = src + (long)gr * ld + gk;
+                    s = src + (long)gr * ld + gk;
+                }
+                if (ok) {
                     if (vec && gk + 3 < kend) {
                         v = *reinterpret_cast<const f32x4*>(s);
                     } else {
@@ -75,7 +79,7 @@ __device__ __forceinline__ void load_stage(f32x4 (&r)[Stage<ROWS>::LOADS], const
             const int rq = (f % RQ) * 4;
             const int gk = k0 + k;
             const int gr = row0 + rq;
-            if (gk < kend) {
+            if (gk < kend && gr < nrows) {
                 const float* s = src + (long)gk * ld + gr;
                 if (vec && gr + 3 < nrows) {
                     v = *reinterpret_cast<const f32x4*>(s);
@@ -90,24 +94,47 @@ __device__ __forceinline__ void load_stage(f32x4 (&r)[Stage<ROWS>::LOADS], const
     }
 }
 
+// Interior fast path: the whole ROWS x BK stage is in bounds and 16-B aligned (no predicates).
 template <int ROWS, bool KC>
-__device__ __forceinline__ void store_stage(float* __restrict__ lds, const f32x4 (&r)[Stage<ROWS>::LOADS]) {
+__device__ __forceinline__ void load_stage_full(f32x4 (&r)[Op<ROWS>::LOADS], const float* __restrict__ src, long ld,
+                                                int row0, int k0) {
     const int tid = threadIdx.x;
 #pragma unroll
-    for (int i = 0; i < Stage<ROWS>::LOADS; ++i) {
+    for (int i = 0; i < Op<ROWS>::LOADS; ++i) {
         const int f = tid + i * 256;
         if (KC) {
-            const int row = f >> 2;
-            const int kq = (f & 3) * 4;
-            *reinterpret_cast<f32x4*>(lds + row * LDK + kq) = r[i];
+            r[i] = *reinterpret_cast<const f32x4*>(src + (long)(row0 + (f >> 3)) * ld + k0 + (f & 7) * 4);
         } else {
             constexpr int RQ = ROWS / 4;
-            const int k = f / RQ;
-            const int rq = (f % RQ) * 4;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) lds[(rq + e) * LDK + k] = r[i][e];
+            r[i] = *reinterpret_cast<const f32x4*>(src + (long)(k0 + f / RQ) * ld + row0 + (f % RQ) * 4);
         }
     }
+}
+
+template <int ROWS, bool KC>
+__device__ __forceinline__ void store_stage(float* __restrict__ lds, const f32x4 (&r)[Op<ROWS>::LOADS]) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < Op<ROWS>::LOADS; ++i) {
+        const int f = tid + i * 256;
+        if (KC) {
+            *reinterpret_cast<f32x4*>(lds + (f >> 3) * LDK + (f & 7) * 4) = r[i];
+        } else {
+            constexpr int RQ = ROWS / 4;
+            *reinterpret_cast<f32x4*>(lds + (f / RQ) * ROWS + (f % RQ) * 4) = r[i];
+        }
+    }
+}
+
+// fragment of 4 consecutive MFMA k-steps (tile k = h*16 + 4q + e, e < 4) for MFMA row `row`
+template <int ROWS, bool KC>
+__device__ __forceinline__ f32x4 read_frag(const float* __restrict__ lds, int row, int h, int q) {
+    if (KC) return *reinterpret_cast<const f32x4*>(lds + row * LDK + h * 16 + q * 4);
+    f32x4 v;
+    const int k = h * 16 + q * 4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = lds[(k + e) * ROWS + row];
+    return v;
 }
 
 __device__ __forceinline__ float epi_value(const GemmParams& p, float acc, long row, long col, const float* bias,
@@ -122,14 +149,14 @@ __device__ __forceinline__ float epi_value(const GemmParams& p, float acc, long 
     return v;
 }
 
-template <int BM, int BN, int WM, int WN, bool TA, bool TB, bool CONV>
+template <int BM, int BN, bool TA, bool TB, bool CONV, int NBUF>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
-    constexpr int WTM = BM / WM, WTN = BN / WN;
+    constexpr int WTM = BM / 2, WTN = BN / 2;
     constexpr int RM = WTM / 32, RN = WTN / 32;
-    static_assert(WM * WN == 4, "4 waves");
+    constexpr bool AKC = !TA, BKC = TB;
+    constexpr int A_FL = lds_floats<BM, AKC>(), B_FL = lds_floats<BN, BKC>();
     static_assert(RM >= 1 && RN >= 1, "wave tile >= 32x32");
-    __shared__ __attribute__((aligned(16))) float As[BM * LDK];
-    __shared__ __attribute__((aligned(16))) float Bs[BN * LDK];
+    __shared__ __attribute__((aligned(16))) float smem[NBUF * (A_FL + B_FL)];
 
     int zz = blockIdx.z;
     int split = 0;
@@ -148,7 +175,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
 
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
-    const int wm = wid / WN, wn = wid % WN;
+    const int wm = wid >> 1, wn = wid & 1;
     const int h = lane >> 5, l32 = lane & 31;
 
     f32x16 acc[RM][RN];
@@ -159,31 +186,51 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    f32x4 ra[Stage<BM>::LOADS];
-    f32x4 rb[Stage<BN>::LOADS];
+    f32x4 ra[Op<BM>::LOADS];
+    f32x4 rb[Op<BN>::LOADS];
     const bool va = p.va != 0, vb = p.vb != 0;
 
-    load_stage<BM, !TA, CONV>(ra, A, p.lda, m0, p.M, kbeg, kend, va, p.segK, p.pad, p.Mvalid);
-    load_stage<BN, TB, false>(rb, B, p.ldb, n0, p.N, kbeg, kend, vb, 0, 0, 0);
+    // block-uniform: interior tiles take the unpredicated 16-B loader for every full K-step
+    const bool fullA = !CONV && va && m0 + BM <= p.M;
+    const bool fullB = vb && n0 + BN <= p.N;
+    auto stageA = [&](int k) {
+        if (fullA && k + BK <= kend) load_stage_full<BM, AKC>(ra, A, p.lda, m0, k);
+        else load_stage<BM, AKC, CONV>(ra, A, p.lda, m0, p.M, k, kend, va, p.segK, p.pad, p.Mvalid);
+    };
+    auto stageB = [&](int k) {
+        if (fullB && k + BK <= kend) load_stage_full<BN, BKC>(rb, B, p.ldb, n0, k);
+        else load_stage<BN, BKC, false>(rb, B, p.ldb, n0, p.N, k, kend, vb, 0, 0, 0);
+    };
+    stageA(kbeg);
+    stageB(kbeg);
 
+    int buf = 0;
+    if (NBUF == 2) {
+        store_stage<BM, AKC>(smem, ra);
+        store_stage<BN, BKC>(smem + A_FL, rb);
+        __syncthreads();
+    }
     for (int k0 = kbeg; k0 < kend; k0 += BK) {
-        __syncthreads();
-        store_stage<BM, !TA>(As, ra);
-        store_stage<BN, TB>(Bs, rb);
-        __syncthreads();
-        if (k0 + BK < kend) {
-            load_stage<BM, !TA, CONV>(ra, A, p.lda, m0, p.M, k0 + BK, kend, va, p.segK, p.pad, p.Mvalid);
-            load_stage<BN, TB, false>(rb, B, p.ldb, n0, p.N, k0 + BK, kend, vb, 0, 0, 0);
+        const bool more = k0 + BK < kend;
+        if (NBUF == 1) {
+            __syncthreads();
+            store_stage<BM, AKC>(smem, ra);
+            store_stage<BN, BKC>(smem + A_FL, rb);
+            __syncthreads();
         }
+        if (more) {
+            stageA(k0 + BK);
+            stageB(k0 + BK);
+        }
+        const float* As = smem + buf * (A_FL + B_FL);
+        const float* Bs = As + A_FL;
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
+        for (int q = 0; q < 4; ++q) {
             f32x4 af[RM], bf[RN];
 #pragma unroll
-            for (int i = 0; i < RM; ++i)
-                af[i] = *reinterpret_cast<const f32x4*>(As + (wm * WTM + i * 32 + l32) * LDK + h * 8 + q * 4);
+            for (int i = 0; i < RM; ++i) af[i] = read_frag<BM, AKC>(As, wm * WTM + i * 32 + l32, h, q);
 #pragma unroll
-            for (int j = 0; j < RN; ++j)
-                bf[j] = *reinterpret_cast<const f32x4*>(Bs + (wn * WTN + j * 32 + l32) * LDK + h * 8 + q * 4);
+            for (int j = 0; j < RN; ++j) bf[j] = read_frag<BN, BKC>(Bs, wn * WTN + j * 32 + l32, h, q);
 #pragma unroll
             for (int e = 0; e < 4; ++e)
 #pragma unroll
@@ -191,6 +238,14 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
 #pragma unroll
                     for (int j = 0; j < RN; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][e], bf[j][e], acc[i][j], 0, 0, 0);
+        }
+        if (NBUF == 2 && more) {
+            // the other buffer was last read before the previous barrier
+            float* nxt = smem + (buf ^ 1) * (A_FL + B_FL);
+            store_stage<BM, AKC>(nxt, ra);
+            store_stage<BN, BKC>(nxt + A_FL, rb);
+            __syncthreads();
+            buf ^= 1;
         }
     }
 
@@ -246,25 +301,33 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmParams p) {
     }
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int NBUF>
 void launch_tile(const GemmParams& p, dim3 grid, hipStream_t st) {
     if (p.segK > 0) {
-        hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, false, false, true>), grid, dim3(256), 0, st, p);
+        hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, false, false, true, NBUF>), grid, dim3(256), 0, st, p);
         return;
     }
     if (!p.ta && !p.tb)
-        hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, false, false, false>), grid, dim3(256), 0, st, p);
+        hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, false, false, false, NBUF>), grid, dim3(256), 0, st, p);
     else if (!p.ta && p.tb)
-        hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, false, true, false>), grid, dim3(256), 0, st, p);
+        hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, false, true, false, NBUF>), grid, dim3(256), 0, st, p);
     else if (p.ta && !p.tb)
-        hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, true, false, false>), grid, dim3(256), 0, st, p);
+        hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, true, false, false, NBUF>), grid, dim3(256), 0, st, p);
     else
-        hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, true, true, false>), grid, dim3(256), 0, st, p);
+        hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, true, true, false, NBUF>), grid, dim3(256), 0, st, p);
 }
 
 bool aligned16(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; }
 
+int g_force_tile = -1;  // test/bench override: 0=128x128 1=128x64 2=64x128 3=64x64
+int g_nbuf = 1;
+
 }  // namespace
+
+void gemm_set_variant(int tile, int nbuf) {
+    g_force_tile = tile;
+    g_nbuf = nbuf;
+}
 
 void gemm_init(GemmParams& p) {
     p = GemmParams{};
@@ -274,41 +337,66 @@ void gemm_init(GemmParams& p) {
     p.splits = 1;
 }
 
+// Tile choice: a CU finishes its share of tiles at ~ceil(tiles / 256) x per-tile time, and a
+// tile's time scales with its area over its relative MFMA efficiency (smaller tiles re-read more
+// operand bytes per MFMA and pay the prologue/epilogue more often).
+static int choose_tile(long M, long N, long Z, long K) {
+    struct Cand {
+        int bm, bn;
+        double eff;
+    } cands[4] = {{128, 128, 1.0}, {128, 64, 0.9}, {64, 128, 0.9}, {64, 64, 0.75}};
+    int best = 0;
+    double bt = 1e300;
+    for (int c = 0; c < 4; ++c) {
+        const long tiles = ((M + cands[c].bm - 1) / cands[c].bm) * ((N + cands[c].bn - 1) / cands[c].bn) * Z;
+        const double per_cu = std::ceil((double)tiles / 256.0);
+        const double t = per_cu * cands[c].bm * cands[c].bn / cands[c].eff;
+        if (t < bt * 0.999) {
+            bt = t;
+            best = c;
+        }
+    }
+    (void)K;
+    return best;
+}
+
 void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
     if (p.M <= 0 || p.N <= 0 || p.Z <= 0) return;
-    // vector loads need 16-B aligned rows (and batch strides) along the contiguous axis
     auto vec_ok = [](const float* base, long ld, long s0, long s1) {
         return aligned16(base) && (ld % 4 == 0) && (s0 % 4 == 0) && (s1 % 4 == 0);
     };
     p.va = vec_ok(p.A, p.lda, p.sA0, p.sA1) && (p.segK == 0 || p.segK % 4 == 0);
     p.vb = vec_ok(p.B, p.ldb, p.sB0, p.sB1);
 
-    int BM = p.M > 64 ? 128 : 64;
-    int BN = p.N > 64 ? 128 : 64;
-    // small grids: prefer 64-row tiles to raise the block count
-    const long tiles128 = (long)((p.M + 127) / 128) * ((p.N + BN - 1) / BN) * p.Z;
-    if (BM == 128 && tiles128 < 512) BM = 64;
+    const int tile = g_force_tile >= 0 ? g_force_tile : choose_tile(p.M, p.N, p.Z, p.K);
+    const int BM = (tile == 0 || tile == 1) ? 128 : 64;
+    const int BN = (tile == 0 || tile == 2) ? 128 : 64;
     const int gx = (p.N + BN - 1) / BN, gy = (p.M + BM - 1) / BM;
     const long blocks = (long)gx * gy * p.Z;
 
-    // split-K when the grid is too small to fill 256 CUs and K is long
+    // split-K when the grid cannot fill 256 CUs and K is long
     int splits = 1;
     if (ws && p.K >= 1024 && blocks < 256) {
         splits = (int)std::min<long>(16, (512 + blocks - 1) / blocks);
         while (splits > 1 && (long)splits * p.Z * p.M * (long)p.N > ws_floats) --splits;
-        const int maxs = (p.K + 255) / 256;  // keep >= 256 K per split
-        splits = std::min(splits, std::max(1, maxs));
+        splits = std::min(splits, std::max(1, (p.K + 255) / 256));  // >= 256 K per split
     }
-    p.splits = splits;
     p.kchunk = splits > 1 ? (((p.K + splits - 1) / splits + BK - 1) / BK) * BK : p.K;
     if (splits > 1) splits = (p.K + p.kchunk - 1) / p.kchunk;
     p.splits = splits;
     p.ws = ws;
     dim3 grid(gx, gy, p.Z * splits);
-    if (BM == 128 && BN == 128) launch_tile<128, 128, 2, 2>(p, grid, st);
-    else if (BM == 128 && BN == 64) launch_tile<128, 64, 2, 2>(p, grid, st);
-    else if (BM == 64 && BN == 128) launch_tile<64, 128, 2, 2>(p, grid, st);
-    else launch_tile<64, 64, 2, 2>(p, grid, st);
+    if (g_nbuf == 1) {
+        if (tile == 0) launch_tile<128, 128, 1>(p, grid, st);
+        else if (tile == 1) launch_tile<128, 64, 1>(p, grid, st);
+        else if (tile == 2) launch_tile<64, 128, 1>(p, grid, st);
+        else launch_tile<64, 64, 1>(p, grid, st);
+    } else {
+        if (tile == 0) launch_tile<128, 128, 2>(p, grid, st);
+        else if (tile == 1) launch_tile<128, 64, 2>(p, grid, st);
+        else if (tile == 2) launch_tile<64, 128, 2>(p, grid, st);
+        else launch_tile<64, 64, 2>(p, grid, st);
+    }
     if (splits > 1) {
         const long MN = (long)p.M * p.N;
         const int gxr = (int)std::min<long>(1024, (MN + 255) / 256);
