@@ -38,7 +38,8 @@ __device__ __forceinline__ float wave_max(float v) {
 // GEMM:  C[z](m,n) = epi( sum_k A[z](m,k) * B[z](k,n) )         (fp32 in, fp32 MFMA accumulate)
 //   A(m,k) = A[m*lda + k]   (ta = 0)   or A[k*lda + m]   (ta = 1)
 //   conv A mode (ta = 0, segK > 0): k = seg*segK + r, A(m,k) = A[(m + seg - pad)*lda + r],
-//        zero unless 0 <= m + seg - pad < Mvalid   (implicit grouped/positional conv)
+//        zero unless 0 <= m + seg - pad < Mvalid   (implicit grouped/positional conv, conv dX)
+//   segmented B (segB, tb = 1): B(k,n) = B[n*ldb + seg*sBseg + r]   (per-tap weight slices)
 //   B(k,n) = B[k*ldb + n]   (tb = 0)   or B[n*ldb + k]   (tb = 1)
 //   batch z in [0, Z): pointer += (z / zdiv) * s?1 + (z % zdiv) * s?0
 // epilogue flags, applied in this order:  v = alpha*acc; +bias[n]; +C(acc) ; C2 = v (store pre);
@@ -63,6 +64,8 @@ struct GemmParams {
     long sA0, sA1, sB0, sB1, sC0, sC1;
     int ta, tb;
     int segK, pad, Mvalid;  // conv-A mode when segK > 0
+    int segB;               // with segK > 0 and tb: B(k, n) = B[n*ldb + (k/segK)*sBseg + k%segK]
+    long sBseg;
     const float* bias;
     long sBias0, sBias1;
     const float* R;

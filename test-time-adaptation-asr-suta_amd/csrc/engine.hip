@@ -123,7 +123,7 @@ struct Plan {
     std::vector<LayerBufs> lay;
     float *ctx, *gu, *rtmp, *logits;
     // backward
-    float *dlogits, *d1, *d2, *d3, *dqkv, *dP, *du, *dzc, *dzc2, *dcol, *lnpart, *loss, *loss_scratch;
+    float *dlogits, *d1, *d2, *d3, *dqkv, *dP, *du, *dzc, *dzc2, *lnpart, *loss, *loss_scratch;
     double* dpart;
     int* ids;
     float* splitws;
@@ -255,11 +255,8 @@ void suta_engine::build_plan(int B, long N) {
     pl.Tp = (int)rup(pl.T, 4);
     if (pl.T > 2048) throw SutaError(SUTA_ERR_UNSUPPORTED, "T > 2048 frames (max 600000 samples in the reference)");
     const long T = pl.T, H = k.H, BT = (long)B * T;
-    long maxLC = 0, maxcol = 0;
-    for (int i = 0; i < k.nconv; ++i) {
-        maxLC = std::max(maxLC, (long)pl.Lc[i] * k.C[i]);
-        if (i > 0) maxcol = std::max(maxcol, (long)pl.Lc[i] * k.K[i] * k.C[i - 1]);
-    }
+    long maxLC = 0;
+    for (int i = 0; i < k.nconv; ++i) maxLC = std::max(maxLC, (long)pl.Lc[i] * k.C[i]);
     for (int pass = 0; pass < 2; ++pass) {
         Arena ar;
         ar.dry = pass == 0;
@@ -322,7 +319,6 @@ void suta_engine::build_plan(int B, long N) {
         pl.du = ar.take<float>(BT * k.F);
         pl.dzc = ar.take<float>((size_t)B * maxLC);
         pl.dzc2 = ar.take<float>((size_t)B * maxLC);
-        pl.dcol = ar.take<float>((size_t)B * std::max(maxcol, 1L));
         const long lnrows = std::max<long>(pl.Lc[0], T);
         pl.lnpart = ar.take<float>((size_t)B * ((lnrows + 31) / 32) * 2 * std::max<long>(H, maxLC / pl.Lc[0] + 1) + 64);
         pl.dpart = ar.take<double>((size_t)B * ((pl.Lc[0] + 127) / 128 + 2) * 2 * k.C[0] + (size_t)B * k.C[0] * 2);
@@ -960,29 +956,46 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
             g.sC1 = Pn;
             gemm(g);
         }
-        {  // dcol = dz_i W_i^T
-            GemmParams g;
-            gemm_init(g);
-            g.A = cur;
-            g.lda = k.C[i];
-            g.M = pl.Lc[i];
-            g.K = k.C[i];
-            g.B = P + o_cw[i];
-            g.tb = 1;
-            g.ldb = k.C[i];
-            g.N = k.K[i] * k.C[i - 1];
-            g.C = pl.dcol;
-            g.ldc = (long)k.K[i] * k.C[i - 1];
-            g.Z = B;
-            g.sA1 = (long)pl.Lc[i] * k.C[i];
-            g.sB1 = Pn;
-            g.sC1 = (long)pl.Lc[i] * k.K[i] * k.C[i - 1];
-            gemm(g);
+        {  // da_{i-1} = conv_i^T(dz_i): one GEMM per output-row residue rho (rows S*m + rho), whose K
+           // runs over the taps k = rho + S*j (segment seg = nj-1-j reads dz row m - j and weight tap k)
+            const int S_ = k.S[i], Kt = k.K[i], Cin = k.C[i - 1], Cout = k.C[i];
+            const int Lin = pl.Lc[i - 1], Lout = pl.Lc[i];
+            const float* zprev = (!k.layer_mode && i - 1 >= 1) ? pl.z[i - 1] : nullptr;
+            for (int rho = 0; rho < S_; ++rho) {
+                const int Mrows = (Lin - rho + S_ - 1) / S_;
+                const int nj = (Kt - rho + S_ - 1) / S_;
+                if (Mrows <= 0) continue;
+                if (nj <= 0) throw SutaError(SUTA_ERR_UNSUPPORTED, "conv stride > kernel");
+                GemmParams g;
+                gemm_init(g);
+                g.A = cur;
+                g.lda = Cout;
+                g.segK = Cout;
+                g.pad = nj - 1;
+                g.Mvalid = Lout;
+                g.M = Mrows;
+                g.K = nj * Cout;
+                g.N = Cin;
+                g.B = P + o_cw[i] + (long)(rho + S_ * (nj - 1)) * Cin * Cout;
+                g.tb = 1;
+                g.ldb = Cout;
+                g.segB = 1;
+                g.sBseg = -(long)S_ * Cin * Cout;
+                g.C = other + (long)rho * Cin;
+                g.ldc = (long)S_ * Cin;
+                g.Z = B;
+                g.sA1 = (long)Lout * Cout;
+                g.sB1 = Pn;
+                g.sC1 = (long)Lin * Cin;
+                if (zprev) {
+                    g.epi = EPI_DGELU;
+                    g.aux = zprev + (long)rho * Cin;
+                    g.ldaux = (long)S_ * Cin;
+                    g.sAux1 = (long)Lin * Cin;
+                }
+                gemm(g);
+            }
         }
-        const float* zprev = (!k.layer_mode && i - 1 >= 1) ? pl.z[i - 1] : nullptr;
-        timed(F_EW, [&] {
-            launch_col2im(pl.dcol, B, pl.Lc[i], pl.Lc[i - 1], k.C[i - 1], k.K[i], k.S[i], zprev, other, st);
-        });
         std::swap(cur, other);
     }
     // conv0: cur = da0

@@ -38,10 +38,12 @@ constexpr int lds_floats() {
 // Load one BK-deep stage of an operand into registers.
 //   KC = true : element (row, k) at row*ld + k   (A with ta=0, B with tb=1)
 //   KC = false: element (row, k) at k*ld + row   (A with ta=1, B with tb=0)
-template <int ROWS, bool KC, bool CONV>
+// MODE 0: plain; 1: conv-A (segment shifts the source row by seg - pad, rows outside
+// [0, Mvalid) read as zero); 2: segmented B (segment offsets the source by seg * sseg).
+template <int ROWS, bool KC, int MODE>
 __device__ __forceinline__ void load_stage(f32x4 (&r)[Op<ROWS>::LOADS], const float* __restrict__ src, long ld,
                                            int row0, int nrows, int k0, int kend, bool vec, int segK, int pad,
-                                           int Mvalid) {
+                                           int Mvalid, long sseg) {
     const int tid = threadIdx.x;
 #pragma unroll
     for (int i = 0; i < Op<ROWS>::LOADS; ++i) {
@@ -55,11 +57,14 @@ __device__ __forceinline__ void load_stage(f32x4 (&r)[Op<ROWS>::LOADS], const fl
             if (gr < nrows && gk < kend) {
                 const float* s;
                 bool ok = true;
-                if (CONV) {
+                if (MODE == 1) {
                     const int seg = gk / segK;
                     const int srow = gr + seg - pad;
                     ok = srow >= 0 && srow < Mvalid;
                     s = src + (long)srow * ld + (gk - seg * segK);  // segK % 4 == 0: one segment
+                } else if (MODE == 2) {
+                    const int seg = gk / segK;
+                    s = src + (long)gr * ld + seg * sseg + (gk - seg * segK);
                 } else {
                     s = src + (long)gr * ld + gk;
                 }
@@ -149,7 +154,7 @@ __device__ __forceinline__ float epi_value(const GemmParams& p, float acc, long 
     return v;
 }
 
-template <int BM, int BN, bool TA, bool TB, bool CONV, int NBUF>
+template <int BM, int BN, bool TA, bool TB, bool CONV, bool SEGB, int NBUF>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
     constexpr int WTM = BM / 2, WTN = BN / 2;
     constexpr int RM = WTM / 32, RN = WTN / 32;
@@ -190,16 +195,35 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
     f32x4 rb[Op<BN>::LOADS];
     const bool va = p.va != 0, vb = p.vb != 0;
 
-    // block-uniform: interior tiles take the unpredicated 16-B loader for every full K-step
-    const bool fullA = !CONV && va && m0 + BM <= p.M;
-    const bool fullB = vb && n0 + BN <= p.N;
+    // block-uniform: interior tiles take the unpredicated 16-B loader for every full K-step;
+    // segmented operands qualify when a K-step stays inside one segment (segK % BK == 0)
+    const bool segAligned = p.segK > 0 && p.segK % BK == 0;
     auto stageA = [&](int k) {
-        if (fullA && k + BK <= kend) load_stage_full<BM, AKC>(ra, A, p.lda, m0, k);
-        else load_stage<BM, AKC, CONV>(ra, A, p.lda, m0, p.M, k, kend, va, p.segK, p.pad, p.Mvalid);
+        bool full = va && m0 + BM <= p.M && k + BK <= kend;
+        const float* base = A;
+        int kk = k;
+        if (CONV) {
+            const int seg = segAligned ? k / p.segK : 0;
+            const int sh = seg - p.pad;
+            full = full && segAligned && m0 + sh >= 0 && m0 + BM + sh <= p.Mvalid;
+            base = A + (long)sh * p.lda;
+            kk = k - seg * p.segK;
+        }
+        if (full) load_stage_full<BM, AKC>(ra, base, p.lda, m0, kk);
+        else load_stage<BM, AKC, CONV ? 1 : 0>(ra, A, p.lda, m0, p.M, k, kend, va, p.segK, p.pad, p.Mvalid, 0);
     };
     auto stageB = [&](int k) {
-        if (fullB && k + BK <= kend) load_stage_full<BN, BKC>(rb, B, p.ldb, n0, k);
-        else load_stage<BN, BKC, false>(rb, B, p.ldb, n0, p.N, k, kend, vb, 0, 0, 0);
+        bool full = vb && n0 + BN <= p.N && k + BK <= kend;
+        const float* base = B;
+        int kk = k;
+        if (SEGB) {
+            const int seg = segAligned ? k / p.segK : 0;
+            full = full && segAligned;
+            base = B + seg * p.sBseg;
+            kk = k - seg * p.segK;
+        }
+        if (full) load_stage_full<BN, BKC>(rb, base, p.ldb, n0, kk);
+        else load_stage<BN, BKC, SEGB ? 2 : 0>(rb, B, p.ldb, n0, p.N, k, kend, vb, p.segK, 0, 0, p.sBseg);
     };
     stageA(kbeg);
     stageB(kbeg);
@@ -304,17 +328,20 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmParams p) {
 template <int BM, int BN, int NBUF>
 void launch_tile(const GemmParams& p, dim3 grid, hipStream_t st) {
     if (p.segK > 0) {
-        hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, false, false, true, NBUF>), grid, dim3(256), 0, st, p);
+        if (p.segB)
+            hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, false, true, true, true, NBUF>), grid, dim3(256), 0, st, p);
+        else
+            hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, false, false, true, false, NBUF>), grid, dim3(256), 0, st, p);
         return;
     }
     if (!p.ta && !p.tb)
-        hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, false, false, false, NBUF>), grid, dim3(256), 0, st, p);
+        hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, false, false, false, false, NBUF>), grid, dim3(256), 0, st, p);
     else if (!p.ta && p.tb)
-        hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, false, true, false, NBUF>), grid, dim3(256), 0, st, p);
+        hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, false, true, false, false, NBUF>), grid, dim3(256), 0, st, p);
     else if (p.ta && !p.tb)
-        hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, true, false, false, NBUF>), grid, dim3(256), 0, st, p);
+        hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, true, false, false, false, NBUF>), grid, dim3(256), 0, st, p);
     else
-        hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, true, true, false, NBUF>), grid, dim3(256), 0, st, p);
+        hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, true, true, false, false, NBUF>), grid, dim3(256), 0, st, p);
 }
 
 bool aligned16(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; }
@@ -366,7 +393,7 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
         return aligned16(base) && (ld % 4 == 0) && (s0 % 4 == 0) && (s1 % 4 == 0);
     };
     p.va = vec_ok(p.A, p.lda, p.sA0, p.sA1) && (p.segK == 0 || p.segK % 4 == 0);
-    p.vb = vec_ok(p.B, p.ldb, p.sB0, p.sB1);
+    p.vb = vec_ok(p.B, p.ldb, p.sB0, p.sB1) && (!p.segB || (p.sBseg % 4 == 0 && p.segK % 4 == 0));
 
     const int tile = g_force_tile >= 0 ? g_force_tile : choose_tile(p.M, p.N, p.Z, p.K);
     const int BM = (tile == 0 || tile == 1) ? 128 : 64;

@@ -45,11 +45,6 @@ void launch_softmax_rows(float* s, long nrows, int T, long ld, hipStream_t st);
 // In place: dP <- scale * P * (dP - rowsum(dP * P)).
 void launch_softmax_bwd_rows(const float* P, float* dP, long nrows, int T, long ld, float scale, hipStream_t st);
 
-// col2im for a stride-S, kernel-K conv on time-major data: da[b][r][c] = sum_{S t + k = r} dcol[b][t][k*C + c],
-// rows r < Lin; optionally times gelu'(z[b][r][c]).
-void launch_col2im(const float* dcol, int B, int Lout, int Lin, int C, int K, int S, const float* z, float* da,
-                   hipStream_t st);
-
 // out = g * gelu'(z), n elements.
 void launch_dgelu_mul(const float* g, const float* z, float* out, long n, hipStream_t st);
 

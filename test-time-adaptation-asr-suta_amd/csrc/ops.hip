@@ -1,6 +1,6 @@
 // Non-GEMM kernels of the SUTA step for gfx950: waveform normalisation, conv0 stencil,
 // GroupNorm / LayerNorm forward+backward with per-utterance affine gradients, attention
-// softmax forward/backward, col2im, the fused entropy+MCC loss-and-grad, and AdamW with
+// softmax forward/backward, the fused entropy+MCC loss-and-grad, and AdamW with
 // duplicate-entry multiplicity.  All reductions are fixed-order (bitwise reproducible).
 #include "ops.h"
 #include <algorithm>
@@ -414,31 +414,6 @@ __global__ __launch_bounds__(256) void softmax_bwd_rows_kernel(const float* __re
     }
 }
 
-// ------------------------------------------------------------------------------------------
-// col2im (+ optional gelu') for stride-S kernel-K convs on time-major data
-// ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void col2im_kernel(const float* __restrict__ dcol, int Lout, int Lin, int C, int K,
-                                                     int S, const float* __restrict__ z, float* __restrict__ da) {
-    const int b = blockIdx.y;
-    const long n = (long)Lin * C;
-    const float* dc = dcol + (long)b * Lout * K * C;
-    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
-        const int r = (int)(i / C), c = (int)(i % C);
-        // t in [ceil((r-K+1)/S), floor(r/S)] intersect [0, Lout)
-        int thi = r / S;
-        if (thi > Lout - 1) thi = Lout - 1;
-        int tlo = r - K + 1;
-        tlo = tlo <= 0 ? 0 : (tlo + S - 1) / S;
-        float s = 0.f;
-        for (int t = tlo; t <= thi; ++t) {
-            const int k = r - S * t;
-            s += dc[((long)t * K + k) * C + c];
-        }
-        if (z) s *= dgelu_f(z[(long)b * n + i]);
-        da[(long)b * n + i] = s;
-    }
-}
-
 __global__ __launch_bounds__(256) void dgelu_mul_kernel(const float* __restrict__ g, const float* __restrict__ z,
                                                         float* __restrict__ out, long n) {
     for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) out[i] = g[i] * dgelu_f(z[i]);
@@ -795,13 +770,6 @@ void launch_softmax_bwd_rows(const float* P, float* dP, long nrows, int T, long 
     else if (T <= 1024)
         hipLaunchKernelGGL(softmax_bwd_rows_kernel<16>, grid, dim3(256), 0, st, P, dP, nrows, T, ld, scale);
     else hipLaunchKernelGGL(softmax_bwd_rows_kernel<32>, grid, dim3(256), 0, st, P, dP, nrows, T, ld, scale);
-}
-
-void launch_col2im(const float* dcol, int B, int Lout, int Lin, int C, int K, int S, const float* z, float* da,
-                   hipStream_t st) {
-    const long n = (long)Lin * C;
-    hipLaunchKernelGGL(col2im_kernel, dim3(std::max(1, ew_grid(n) / std::max(1, B / 2)), B), dim3(256), 0, st, dcol,
-                       Lout, Lin, C, K, S, z, da);
 }
 
 void launch_dgelu_mul(const float* g, const float* z, float* out, long n, hipStream_t st) {
