@@ -32,6 +32,7 @@ from suta_amd.flops import suta_flops  # noqa: E402
 from suta_amd.weights import synth_weights  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
+BF16_SPLIT_PEAK_TFLOPS = 2500.0 / 6  # bf16 dense MFMA peak / 6 products per fp32-equivalent MAC
 RECORD = [0, 1, 3, 5, 10]
 
 
@@ -66,6 +67,10 @@ def main():
     ap.add_argument("--model", default="wav2vec2-base")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP-event timing")
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "fp32-split-bf16"],
+                    help="GEMM arithmetic: exact fp32 MFMA, or fp32-accurate 3-way bf16 split")
+    ap.add_argument("--no-split", dest="also_split", action="store_false",
+                    help="do not also time the fp32-accurate split-bf16 GEMM mode")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -83,6 +88,7 @@ def main():
     cfg = get_config(args.model)
     B, N, S = args.batch, args.n_samples, args.suta_steps
     eng = SutaEngine(cfg, synth_weights(cfg), device=dev, max_batch=B, max_samples=N)
+    eng.set_precision(args.precision)
     hp = SutaHParams()  # scripts/LS.sh flags
     nbatches = args.warmup + args.steps
     # inputs resident in HBM before timing: distinct utterances per rank and batch
@@ -121,7 +127,7 @@ def main():
         "metric": "adapted utterances/sec (whole node) at 10 SUTA steps, w2v2-base; WER parity",
         "value": round(value, 4), "unit": "utt/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(1000 * el / args.steps, 3), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "vs_baseline": None, "dtype": "f32", "data": "synthetic", "precision": args.precision,
         "config": {"workload": f"{args.model} SUTA {S} steps on {N}-sample (8 s) utterances, {B} utterances "
                                f"per GPU per step, scripts/LS.sh flags",
                    "model": args.model, "global_batch": B * world, "seq_len": num_frames(cfg, N),
@@ -140,6 +146,35 @@ def main():
                            "kernel": "gemm_f32_kernel (all launches)",
                            "launches": int(gn), "avg_launch_ms": round(gms / max(1, gn), 5)}
         out["time_breakdown_ms"] = {k: round(v[0], 2) for k, v in timing.items()}
+    if args.also_split and args.precision == "fp32":
+        # same workload with the fp32-accurate split-bf16 GEMMs (reported beside the headline)
+        eng.set_precision("fp32-split-bf16")
+        eng.set_timing(False)
+        eng.adapt(waves[0], S, hp, record=RECORD, want_logits=False)
+        if not args.no_timing:
+            eng.set_timing(True)
+        barrier()
+        t1 = time.perf_counter()
+        for i in range(args.steps):
+            eng.adapt(waves[args.warmup + i], S, hp, record=RECORD, want_logits=False)
+        eng.sync()
+        barrier()
+        el2 = time.perf_counter() - t1
+        if dist:
+            t = torch.tensor([el2], device=f"cuda:{dev}")
+            tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+            el2 = float(t.item())
+        split = {"precision": "fp32-split-bf16", "value": round(utts / el2, 4),
+                 "ms_per_step": round(1000 * el2 / args.steps, 3)}
+        if not args.no_timing:
+            t2 = eng.get_timing()
+            gms2 = t2["gemm"][0]
+            ach2 = flops_utt * B * args.steps / (gms2 / 1000.0) / 1e12
+            split["roofline"] = {"bound": "mfma", "achieved": round(ach2, 3), "peak": BF16_SPLIT_PEAK_TFLOPS,
+                                 "unit": "TFLOP/s (fp32-equivalent)", "frac": round(ach2 / BF16_SPLIT_PEAK_TFLOPS, 4),
+                                 "note": "6 bf16 MFMA products per fp32 MAC: peak = 2500 TF bf16 dense / 6"}
+        out["fp32_split_bf16"] = split
+        eng.set_precision("fp32")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cfg, N, S)
     if rank == 0:

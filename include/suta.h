@@ -149,6 +149,15 @@ void* suta_stream(suta_engine* e);
 int32_t suta_set_timing(suta_engine* e, int32_t enable);
 int32_t suta_get_timing(suta_engine* e, double* ms_out /*[6]*/, int64_t* launches_out /*[6]*/);
 
+/* GEMM arithmetic.  Both are fp32-accurate; results agree to fp32 rounding (tests/test_gpu_parity.py):
+ *   SUTA_PRECISION_FP32_MFMA        v_mfma_f32_32x32x2_f32: exact fp32 products, fp32 accumulation
+ *   SUTA_PRECISION_FP32_SPLIT_BF16  each fp32 operand split exactly into 3 bf16 terms; the 6 products
+ *                                   of order <= 2 on v_mfma_f32_32x32x16_bf16, fp32 accumulation
+ *                                   (dropped terms <= 2^-24 |ab|: the size of one fp32 rounding) */
+#define SUTA_PRECISION_FP32_MFMA 0
+#define SUTA_PRECISION_FP32_SPLIT_BF16 1
+int32_t suta_set_precision(suta_engine* e, int32_t mode);
+
 /* Use hipGraph capture/replay for suta_adapt (default on). */
 int32_t suta_set_graphs(suta_engine* e, int32_t enable);
 

@@ -162,6 +162,7 @@ struct suta_engine {
     std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
     std::vector<hipEvent_t> evpool;
     bool use_graphs = true;
+    int gemm_mode = 0;  // SUTA_PRECISION_*
     std::vector<float*> owned;
 
     ~suta_engine();
@@ -207,7 +208,9 @@ struct suta_engine {
         }
         pending.clear();
     }
-    void gemm(const GemmParams& p) {
+    void gemm(const GemmParams& p0) {
+        GemmParams p = p0;
+        p.mode = gemm_mode;
         timed(F_GEMM, [&] { gemm_launch(p, st, plan.splitws, plan.splitws_floats); });
     }
 
@@ -1483,6 +1486,14 @@ int32_t suta_get_timing(suta_engine* e, double* ms, int64_t* n) {
             ms[i] = e->fam_ms[i];
             n[i] = e->fam_n[i];
         }
+    });
+}
+
+int32_t suta_set_precision(suta_engine* e, int32_t mode) {
+    return guard([&] {
+        if (mode != SUTA_PRECISION_FP32_MFMA && mode != SUTA_PRECISION_FP32_SPLIT_BF16)
+            throw SutaError(SUTA_ERR_ARG, "unknown precision mode");
+        e->gemm_mode = mode;
     });
 }
 

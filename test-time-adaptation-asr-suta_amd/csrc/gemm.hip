@@ -306,6 +306,291 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
             }
 }
 
+// ============================================================================================
+// fp32-accurate GEMM on the bf16 matrix cores ("x6"): every fp32 operand is split exactly into
+// three bf16 terms x = x_h + x_m + x_l (24 = 3 x 8 significand bits, each residual exact in fp32),
+// and A*B is accumulated in fp32 from the six products whose order is <= 2 (h*h, h*m, m*h, h*l,
+// m*m, l*h); the dropped terms are <= 2^-24 |a b|, the size of one fp32 rounding, so the result
+// carries the error of an fp32 GEMM (tools/split_accuracy + tests) at 16/6 = 2.7x the fp32-MFMA
+// rate.  The split happens once per element when the stage is written to LDS: three bf16 planes
+// per operand, rows of 32 k (64 B) with the 16-B chunk XOR-swizzled by (row >> 2) & 3 so the
+// ds_read_b128 fragment reads are conflict-free without padding.
+// ============================================================================================
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+template <int ROWS>
+struct X6 {
+    static constexpr int LOADS = ROWS * BK / 4 / 256;  // float4 per thread per stage (4 | 2)
+    static constexpr int PLANE = ROWS * BK;            // bf16 per plane
+    static constexpr int KPT = LOADS;                  // MN mapping: k per thread (4 rows each)
+    static constexpr int JN = BK / KPT;                // MN mapping: threads along k
+};
+
+__device__ __forceinline__ int x6_idx(int row, int k) {  // swizzled bf16 index inside a plane
+    return row * BK + ((((k >> 3) ^ (row >> 2)) & 3) << 3) + (k & 7);
+}
+
+__device__ __forceinline__ void split3(float x, __bf16& h, __bf16& m, __bf16& l) {
+    h = (__bf16)x;
+    const float r = x - (float)h;
+    m = (__bf16)r;
+    l = (__bf16)(r - (float)m);
+}
+
+// MN (row-contiguous) source, block mapping: thread -> rows 4i..4i+3, k = KPT*j + c.
+template <int ROWS, bool FULL>
+__device__ __forceinline__ void x6_load_mn(f32x4 (&r)[X6<ROWS>::LOADS], const float* __restrict__ src, long ld,
+                                           int row0, int nrows, int k0, int kend, bool vec) {
+    const int f = threadIdx.x;
+    const int i = f / X6<ROWS>::JN, j = f % X6<ROWS>::JN;
+#pragma unroll
+    for (int c = 0; c < X6<ROWS>::KPT; ++c) {
+        const int gk = k0 + X6<ROWS>::KPT * j + c;
+        const int gr = row0 + 4 * i;
+        const float* s = src + (long)gk * ld + gr;
+        if (FULL) {
+            r[c] = *reinterpret_cast<const f32x4*>(s);
+        } else {
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if (gk < kend && gr < nrows) {
+                if (vec && gr + 3 < nrows) {
+                    v = *reinterpret_cast<const f32x4*>(s);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (gr + e < nrows) v[e] = s[e];
+                }
+            }
+            r[c] = v;
+        }
+    }
+}
+
+template <int ROWS, bool KC>
+__device__ __forceinline__ void x6_store(__bf16* __restrict__ lds, const f32x4 (&r)[X6<ROWS>::LOADS]) {
+    const int f = threadIdx.x;
+    if (KC) {
+#pragma unroll
+        for (int i = 0; i < X6<ROWS>::LOADS; ++i) {
+            const int idx = f + i * 256;
+            const int row = idx >> 3, kq = (idx & 7) * 4;
+            bf16x4 hh, mm, ll;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                __bf16 a, b, c;
+                split3(r[i][e], a, b, c);
+                hh[e] = a;
+                mm[e] = b;
+                ll[e] = c;
+            }
+            const int o = x6_idx(row, kq);
+            *reinterpret_cast<bf16x4*>(lds + o) = hh;
+            *reinterpret_cast<bf16x4*>(lds + X6<ROWS>::PLANE + o) = mm;
+            *reinterpret_cast<bf16x4*>(lds + 2 * X6<ROWS>::PLANE + o) = ll;
+        }
+    } else {
+        constexpr int KPT = X6<ROWS>::KPT;
+        const int i = f / X6<ROWS>::JN, j = f % X6<ROWS>::JN;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+            const int row = 4 * i + rr, k = KPT * j;
+            const int o = x6_idx(row, k);
+            if (KPT == 4) {
+                bf16x4 hh, mm, ll;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    __bf16 a, b, cc;
+                    split3(r[c][rr], a, b, cc);
+                    hh[c] = a;
+                    mm[c] = b;
+                    ll[c] = cc;
+                }
+                *reinterpret_cast<bf16x4*>(lds + o) = hh;
+                *reinterpret_cast<bf16x4*>(lds + X6<ROWS>::PLANE + o) = mm;
+                *reinterpret_cast<bf16x4*>(lds + 2 * X6<ROWS>::PLANE + o) = ll;
+            } else {
+                bf16x2 hh, mm, ll;
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    __bf16 a, b, cc;
+                    split3(r[c][rr], a, b, cc);
+                    hh[c] = a;
+                    mm[c] = b;
+                    ll[c] = cc;
+                }
+                *reinterpret_cast<bf16x2*>(lds + o) = hh;
+                *reinterpret_cast<bf16x2*>(lds + X6<ROWS>::PLANE + o) = mm;
+                *reinterpret_cast<bf16x2*>(lds + 2 * X6<ROWS>::PLANE + o) = ll;
+            }
+        }
+    }
+}
+
+template <int BM, int BN, bool TA, bool TB, bool CONV, bool SEGB>
+__global__ __launch_bounds__(256, 3) void gemm_x6_kernel(GemmParams p) {
+    constexpr int WTM = BM / 2, WTN = BN / 2;
+    constexpr int RM = WTM / 32, RN = WTN / 32;
+    constexpr bool AKC = !TA, BKC = TB;
+    static_assert(RM >= 1 && RN >= 1, "wave tile >= 32x32");
+    __shared__ __attribute__((aligned(16))) __bf16 smem[3 * (X6<BM>::PLANE + X6<BN>::PLANE)];
+    __bf16* As = smem;
+    __bf16* Bs = smem + 3 * X6<BM>::PLANE;
+
+    int zz = blockIdx.z;
+    int split = 0;
+    if (p.splits > 1) {
+        split = zz % p.splits;
+        zz /= p.splits;
+    }
+    const int z1 = zz / p.zdiv, z0 = zz % p.zdiv;
+    const float* A = p.A + z1 * p.sA1 + z0 * p.sA0;
+    const float* B = p.B + z1 * p.sB1 + z0 * p.sB0;
+    const int m0 = blockIdx.y * BM;
+    const int n0 = blockIdx.x * BN;
+    const int kbeg = split * p.kchunk;
+    const int kend = min(p.K, kbeg + p.kchunk);
+    const int lane = threadIdx.x & 63;
+    const int wid = threadIdx.x >> 6;
+    const int wm = wid >> 1, wn = wid & 1;
+    const int h = lane >> 5, l32 = lane & 31;
+
+    f32x16 acc[RM][RN];
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    f32x4 ra[X6<BM>::LOADS];
+    f32x4 rb[X6<BN>::LOADS];
+    const bool va = p.va != 0, vb = p.vb != 0;
+    const bool segAligned = p.segK > 0 && p.segK % BK == 0;
+    auto stageA = [&](int k) {
+        bool full = va && m0 + BM <= p.M && k + BK <= kend;
+        const float* base = A;
+        int kk = k;
+        if (CONV) {
+            const int seg = segAligned ? k / p.segK : 0;
+            const int sh = seg - p.pad;
+            full = full && segAligned && m0 + sh >= 0 && m0 + BM + sh <= p.Mvalid;
+            base = A + (long)sh * p.lda;
+            kk = k - seg * p.segK;
+        }
+        if (AKC) {
+            if (full) load_stage_full<BM, true>(ra, base, p.lda, m0, kk);
+            else load_stage<BM, true, CONV ? 1 : 0>(ra, A, p.lda, m0, p.M, k, kend, va, p.segK, p.pad, p.Mvalid, 0);
+        } else {
+            if (full) x6_load_mn<BM, true>(ra, A, p.lda, m0, p.M, k, kend, va);
+            else x6_load_mn<BM, false>(ra, A, p.lda, m0, p.M, k, kend, va);
+        }
+    };
+    auto stageB = [&](int k) {
+        bool full = vb && n0 + BN <= p.N && k + BK <= kend;
+        const float* base = B;
+        int kk = k;
+        if (SEGB) {
+            const int seg = segAligned ? k / p.segK : 0;
+            full = full && segAligned;
+            base = B + seg * p.sBseg;
+            kk = k - seg * p.segK;
+        }
+        if (BKC) {
+            if (full) load_stage_full<BN, true>(rb, base, p.ldb, n0, kk);
+            else load_stage<BN, true, SEGB ? 2 : 0>(rb, B, p.ldb, n0, p.N, k, kend, vb, p.segK, 0, 0, p.sBseg);
+        } else {
+            if (full) x6_load_mn<BN, true>(rb, B, p.ldb, n0, p.N, k, kend, vb);
+            else x6_load_mn<BN, false>(rb, B, p.ldb, n0, p.N, k, kend, vb);
+        }
+    };
+    stageA(kbeg);
+    stageB(kbeg);
+    for (int k0 = kbeg; k0 < kend; k0 += BK) {
+        __syncthreads();
+        x6_store<BM, AKC>(As, ra);
+        x6_store<BN, BKC>(Bs, rb);
+        __syncthreads();
+        if (k0 + BK < kend) {
+            stageA(k0 + BK);
+            stageB(k0 + BK);
+        }
+#pragma unroll
+        for (int kc = 0; kc < 2; ++kc) {
+            bf16x8 af[RM][3], bf[RN][3];
+            const int k = kc * 16 + h * 8;
+#pragma unroll
+            for (int i = 0; i < RM; ++i) {
+                const int o = x6_idx(wm * WTM + i * 32 + l32, k);
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) af[i][pl] = *reinterpret_cast<const bf16x8*>(As + pl * X6<BM>::PLANE + o);
+            }
+#pragma unroll
+            for (int j = 0; j < RN; ++j) {
+                const int o = x6_idx(wn * WTN + j * 32 + l32, k);
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) bf[j][pl] = *reinterpret_cast<const bf16x8*>(Bs + pl * X6<BN>::PLANE + o);
+            }
+            // small terms first, the h*h product last
+#pragma unroll
+            for (int t = 0; t < 6; ++t) {
+                constexpr int pa[6] = {0, 1, 2, 0, 1, 0};
+                constexpr int pb[6] = {2, 1, 0, 1, 0, 0};
+#pragma unroll
+                for (int i = 0; i < RM; ++i)
+#pragma unroll
+                    for (int j = 0; j < RN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][pa[t]], bf[j][pb[t]], acc[i][j], 0, 0, 0);
+            }
+        }
+    }
+
+    if (p.splits > 1) {
+        float* W = p.ws + ((long)blockIdx.z) * p.M * (long)p.N;
+#pragma unroll
+        for (int i = 0; i < RM; ++i)
+#pragma unroll
+            for (int j = 0; j < RN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int row = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    const int col = n0 + wn * WTN + j * 32 + l32;
+                    if (row < p.M && col < p.N) W[(long)row * p.N + col] = acc[i][j][r];
+                }
+        return;
+    }
+    float* C = p.C + z1 * p.sC1 + z0 * p.sC0;
+    const float* bias = p.bias ? p.bias + z1 * p.sBias1 + z0 * p.sBias0 : nullptr;
+    const float* R = p.R ? p.R + z1 * p.sR1 + z0 * p.sR0 : nullptr;
+    const float* aux = p.aux ? p.aux + z1 * p.sAux1 + z0 * p.sAux0 : nullptr;
+    float* C2 = p.C2 ? p.C2 + z1 * p.sC21 + z0 * p.sC20 : nullptr;
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                const int col = n0 + wn * WTN + j * 32 + l32;
+                if (row < p.M && col < p.N)
+                    C[(long)row * p.ldc + col] = epi_value(p, acc[i][j][r], row, col, bias, R, aux, C2, C);
+            }
+}
+
+template <int BM, int BN>
+void launch_x6(const GemmParams& p, dim3 grid, hipStream_t st) {
+    if (p.segK > 0) {
+        if (p.segB) hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, false, true, true, true>), grid, dim3(256), 0, st, p);
+        else hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, false, false, true, false>), grid, dim3(256), 0, st, p);
+        return;
+    }
+    if (!p.ta && !p.tb) hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, false, false, false, false>), grid, dim3(256), 0, st, p);
+    else if (!p.ta && p.tb) hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, false, true, false, false>), grid, dim3(256), 0, st, p);
+    else if (p.ta && !p.tb) hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, true, false, false, false>), grid, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, true, true, false, false>), grid, dim3(256), 0, st, p);
+}
+
 // Sum split-K partials in split order (deterministic) and apply the epilogue.
 __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmParams p) {
     const long MN = (long)p.M * p.N;
@@ -348,6 +633,7 @@ bool aligned16(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 
 
 int g_force_tile = -1;  // test/bench override: 0=128x128 1=128x64 2=64x128 3=64x64
 int g_nbuf = 1;
+int g_mode = 0;  // 0 = exact fp32 MFMA, 1 = x6 (fp32-accurate bf16 split)
 
 }  // namespace
 
@@ -356,12 +642,16 @@ void gemm_set_variant(int tile, int nbuf) {
     g_nbuf = nbuf;
 }
 
+void gemm_set_mode(int mode) { g_mode = mode; }
+int gemm_get_mode() { return g_mode; }
+
 void gemm_init(GemmParams& p) {
     p = GemmParams{};
     p.Z = 1;
     p.zdiv = 1;
     p.alpha = 1.f;
     p.splits = 1;
+    p.mode = g_mode;
 }
 
 // Tile choice: a CU finishes its share of tiles at ~ceil(tiles / 256) x per-tile time, and a
@@ -413,7 +703,12 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
     p.splits = splits;
     p.ws = ws;
     dim3 grid(gx, gy, p.Z * splits);
-    if (g_nbuf == 1) {
+    if (p.mode == 1) {
+        if (tile == 0) launch_x6<128, 128>(p, grid, st);
+        else if (tile == 1) launch_x6<128, 64>(p, grid, st);
+        else if (tile == 2) launch_x6<64, 128>(p, grid, st);
+        else launch_x6<64, 64>(p, grid, st);
+    } else if (g_nbuf == 1) {
         if (tile == 0) launch_tile<128, 128, 1>(p, grid, st);
         else if (tile == 1) launch_tile<128, 64, 1>(p, grid, st);
         else if (tile == 2) launch_tile<64, 128, 1>(p, grid, st);

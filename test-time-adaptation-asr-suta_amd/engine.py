@@ -20,7 +20,7 @@ MAX_CONV = 8
 # exported symbols (kept in sync with include/suta.h; tests/test_abi.py checks both)
 EXPORTS = ("suta_create", "suta_destroy", "suta_reset", "suta_num_frames", "suta_forward", "suta_step",
            "suta_adapt", "suta_loss_grad", "suta_get_param", "suta_param_info", "suta_sync", "suta_stream", "suta_set_timing",
-           "suta_get_timing", "suta_set_graphs", "suta_last_error")
+           "suta_get_timing", "suta_set_precision", "suta_set_graphs", "suta_last_error")
 
 
 class ModelConfigC(C.Structure):
@@ -95,6 +95,7 @@ def load_library(path: str = LIB_PATH):
     lib.suta_set_timing.argtypes = [C.c_void_p, C.c_int32]
     lib.suta_get_timing.argtypes = [C.c_void_p, P(C.c_double), i64p]
     lib.suta_set_graphs.argtypes = [C.c_void_p, C.c_int32]
+    lib.suta_set_precision.argtypes = [C.c_void_p, C.c_int32]
     lib.suta_last_error.restype = C.c_char_p
     for name in EXPORTS:
         if name != "suta_stream" and name != "suta_last_error":
@@ -268,6 +269,12 @@ class SutaEngine:
         _check(self.lib.suta_get_timing(self.handle, ms, n))
         fams = ("gemm", "softmax", "norm", "elementwise", "loss", "adam")
         return {f: (ms[i], n[i]) for i, f in enumerate(fams)}
+
+    PRECISIONS = {"fp32": 0, "fp32-split-bf16": 1}
+
+    def set_precision(self, mode: str):
+        """'fp32' (exact fp32 MFMA) or 'fp32-split-bf16' (fp32-accurate 3-way bf16 split)."""
+        _check(self.lib.suta_set_precision(self.handle, self.PRECISIONS[mode]))
 
     def set_graphs(self, enable: bool):
         _check(self.lib.suta_set_graphs(self.handle, int(enable)))

@@ -25,11 +25,15 @@ G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 _ENGINES = {}
 
 
-def engine(preset, max_batch=4, blank_bias=1.0):
+PRECISIONS = ["fp32", "fp32-split-bf16"]
+
+
+def engine(preset, max_batch=4, blank_bias=1.0, precision="fp32"):
     key = (preset, max_batch, blank_bias)
     if key not in _ENGINES:
         cfg = get_config(preset)
         _ENGINES[key] = (SutaEngine(cfg, synth_weights(cfg, blank_bias=blank_bias), max_batch=max_batch), cfg)
+    _ENGINES[key][0].set_precision(precision)
     return _ENGINES[key]
 
 
@@ -54,12 +58,13 @@ def test_loss_kernel_matches_reference_autograd():
             assert abs(loss[0] - rl) <= 1e-5 * max(1.0, abs(rl)), (case, loss[0], rl)
 
 
+@pytest.mark.parametrize("precision", PRECISIONS)
 @pytest.mark.parametrize("variant", ["group", "group_lr5e-4", "layer", "layer_lr5e-4", "group_lnonly",
                                      "group_biasonly", "group_em1"])
-def test_tiny_suta_matches_reference(variant):
+def test_tiny_suta_matches_reference(variant, precision):
     z = _load(f"g3_tiny_{variant}.npz")
     preset = "tiny-group" if variant.startswith("group") else "tiny-layer"
-    eng, cfg = engine(preset)
+    eng, cfg = engine(preset, precision=precision)
     h = ast.literal_eval(str(z["hp_json"]))
     hp = SutaHParams(lr=h["lr"], temp=h["temp"], em_coef=h["em"], reweight=h["rw"], non_blank=h["nb"],
                      div_coef=h["div"], train_feature=h["train_feature"], bias_only=h["bias_only"])
@@ -77,10 +82,11 @@ def test_tiny_suta_matches_reference(variant):
                 assert_params_close(eng.get_param(0, name), z[key], h["lr"], 10, name=name)
 
 
+@pytest.mark.parametrize("precision", PRECISIONS)
 @pytest.mark.parametrize("n", [16000, 32000])
-def test_base_suta_matches_reference(n):
+def test_base_suta_matches_reference(n, precision):
     z = _load(f"g4_base_{n}.npz")
-    eng, cfg = engine("wav2vec2-base")
+    eng, cfg = engine("wav2vec2-base", precision=precision)
     x = synth.wave(n, 0 if n == 16000 else 1)
     steps = [int(s) for s in z["steps"]]
     logits, ids, T = eng.adapt(x, 10, SutaHParams(), record=steps)
@@ -93,10 +99,11 @@ def test_base_suta_matches_reference(n):
             assert_params_close(got, z[f"final/{name}/val"], 2e-5, 10, max_frac=0.05, name=name)
 
 
-def test_base_forward_matches_oracle_8s():
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_base_forward_matches_oracle_8s(precision):
     """Vanilla logits at the bench length (8 s, T = 399) against the CPU oracle."""
     from oracle import w2v2_cpu as W
-    eng, cfg = engine("wav2vec2-base")
+    eng, cfg = engine("wav2vec2-base", precision=precision)
     x = synth.wave(128000, 3)
     eng.reset()
     got = eng.forward(x)[0]
@@ -139,8 +146,21 @@ def test_batch_equals_independent_runs():
         np.testing.assert_allclose(lb[0][b], l1[0][0], rtol=0, atol=1e-5)
 
 
-def test_bitwise_deterministic():
+def test_split_precision_tracks_exact_fp32_8s():
+    """Both GEMM modes are fp32-accurate: 10-step adapted logits agree to fp32 noise."""
     eng, cfg = engine("wav2vec2-base")
+    x = synth.wave(128000, 4)
+    a, _, _ = eng.adapt(x, 10, SutaHParams(), record=[0, 10])
+    eng.set_precision("fp32-split-bf16")
+    b, _, _ = eng.adapt(x, 10, SutaHParams(), record=[0, 10])
+    eng.set_precision("fp32")
+    for r in (0, 10):
+        np.testing.assert_allclose(b[r], a[r], rtol=0, atol=5e-5)
+
+
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_bitwise_deterministic(precision):
+    eng, cfg = engine("wav2vec2-base", precision=precision)
     x = synth.wave(32000, 9)
     a, _, _ = eng.adapt(x, 3, SutaHParams(), record=[3])
     b, _, _ = eng.adapt(x, 3, SutaHParams(), record=[3])

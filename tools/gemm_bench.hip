@@ -94,6 +94,9 @@ int main(int argc, char** argv) {
     bool check = argc < 2 || atoi(argv[1]) != 0;
     int only_v = argc >= 3 ? atoi(argv[2]) : -1;
     int only_s = argc >= 4 ? atoi(argv[3]) : -1;
+    int mode = argc >= 5 ? atoi(argv[4]) : 0;
+    gemm_set_mode(mode);
+    printf("GEMM mode %d (%s)\n", mode, mode ? "x6 bf16-split" : "exact fp32 MFMA");
     {
         const int iters = 20000, blocks = 256 * 4;
         hipLaunchKernelGGL(mfma_peak, dim3(blocks), dim3(256), 0, st, C, 100, 0.001f);
