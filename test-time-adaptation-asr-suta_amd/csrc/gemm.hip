@@ -320,47 +320,104 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
-template <int ROWS>
+template <int ROWS, int BKX>
 struct X6 {
-    static constexpr int LOADS = ROWS * BK / 4 / 256;  // float4 per thread per stage (4 | 2)
-    static constexpr int PLANE = ROWS * BK;            // bf16 per plane
-    static constexpr int KPT = LOADS;                  // MN mapping: k per thread (4 rows each)
-    static constexpr int JN = BK / KPT;                // MN mapping: threads along k
+    static constexpr int LOADS = ROWS * BKX / 4 / 256;  // float4 per thread per stage
+    static constexpr int PLANE = ROWS * BKX;            // bf16 per plane
+    static constexpr int KPT = LOADS;                   // MN mapping: k per thread (4 rows each)
+    static constexpr int JN = BKX / KPT;                // MN mapping: threads along k
+    static constexpr int KQ = BKX / 4;                  // KC mapping: float4 per row
 };
 
-__device__ __forceinline__ int x6_idx(int row, int k) {  // swizzled bf16 index inside a plane
-    return row * BK + ((((k >> 3) ^ (row >> 2)) & 3) << 3) + (k & 7);
+// swizzled bf16 index inside a plane: rows of BKX bf16, 16-B chunks XORed so that the
+// ds_read_b128 lane groups (rows {0-3,12-15,20-27}+...) hit distinct bank slots
+template <int BKX>
+__device__ __forceinline__ int x6_idx(int row, int k) {
+    if (BKX == 32) return row * 32 + ((((k >> 3) ^ (row >> 2)) & 3) << 3) + (k & 7);
+    return row * 16 + ((((k >> 3) ^ (row >> 3)) & 1) << 3) + (k & 7);
 }
 
+#ifndef X6_ABLATE
+#define X6_ABLATE 0  // benchmark-only ablations: 1 = no split VALU, 2 = one MFMA product instead of six
+#endif
 __device__ __forceinline__ void split3(float x, __bf16& h, __bf16& m, __bf16& l) {
     h = (__bf16)x;
+#if X6_ABLATE == 1
+    m = h;
+    l = h;
+#else
     const float r = x - (float)h;
     m = (__bf16)r;
     l = (__bf16)(r - (float)m);
+#endif
+}
+
+// KC (k-contiguous) source: thread -> float4 (row idx / KQ, k 4*(idx % KQ)); MODE as load_stage.
+template <int ROWS, int BKX, int MODE, bool FULL>
+__device__ __forceinline__ void x6_load_kc(f32x4 (&r)[(X6<ROWS, BKX>::LOADS)], const float* __restrict__ src, long ld,
+                                           int row0, int nrows, int k0, int kend, bool vec, int segK, int pad,
+                                           int Mvalid, long sseg) {
+    constexpr int KQ = X6<ROWS, BKX>::KQ;
+#pragma unroll
+    for (int i = 0; i < X6<ROWS, BKX>::LOADS; ++i) {
+        const int f = threadIdx.x + i * 256;
+        const int row = f / KQ, kq = (f % KQ) * 4;
+        if (FULL) {
+            r[i] = *reinterpret_cast<const f32x4*>(src + (long)(row0 + row) * ld + k0 + kq);
+            continue;
+        }
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        const int gr = row0 + row, gk = k0 + kq;
+        if (gr < nrows && gk < kend) {
+            const float* sp;
+            bool ok = true;
+            if (MODE == 1) {
+                const int seg = gk / segK;
+                const int srow = gr + seg - pad;
+                ok = srow >= 0 && srow < Mvalid;
+                sp = src + (long)srow * ld + (gk - seg * segK);
+            } else if (MODE == 2) {
+                const int seg = gk / segK;
+                sp = src + (long)gr * ld + seg * sseg + (gk - seg * segK);
+            } else {
+                sp = src + (long)gr * ld + gk;
+            }
+            if (ok) {
+                if (vec && gk + 3 < kend) {
+                    v = *reinterpret_cast<const f32x4*>(sp);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (gk + e < kend) v[e] = sp[e];
+                }
+            }
+        }
+        r[i] = v;
+    }
 }
 
 // MN (row-contiguous) source, block mapping: thread -> rows 4i..4i+3, k = KPT*j + c.
-template <int ROWS, bool FULL>
-__device__ __forceinline__ void x6_load_mn(f32x4 (&r)[X6<ROWS>::LOADS], const float* __restrict__ src, long ld,
+template <int ROWS, int BKX, bool FULL>
+__device__ __forceinline__ void x6_load_mn(f32x4 (&r)[(X6<ROWS, BKX>::LOADS)], const float* __restrict__ src, long ld,
                                            int row0, int nrows, int k0, int kend, bool vec) {
     const int f = threadIdx.x;
-    const int i = f / X6<ROWS>::JN, j = f % X6<ROWS>::JN;
+    const int i = f / X6<ROWS, BKX>::JN, j = f % X6<ROWS, BKX>::JN;
 #pragma unroll
-    for (int c = 0; c < X6<ROWS>::KPT; ++c) {
-        const int gk = k0 + X6<ROWS>::KPT * j + c;
+    for (int c = 0; c < X6<ROWS, BKX>::KPT; ++c) {
+        const int gk = k0 + X6<ROWS, BKX>::KPT * j + c;
         const int gr = row0 + 4 * i;
-        const float* s = src + (long)gk * ld + gr;
+        const float* sp = src + (long)gk * ld + gr;
         if (FULL) {
-            r[c] = *reinterpret_cast<const f32x4*>(s);
+            r[c] = *reinterpret_cast<const f32x4*>(sp);
         } else {
             f32x4 v = {0.f, 0.f, 0.f, 0.f};
             if (gk < kend && gr < nrows) {
                 if (vec && gr + 3 < nrows) {
-                    v = *reinterpret_cast<const f32x4*>(s);
+                    v = *reinterpret_cast<const f32x4*>(sp);
                 } else {
 #pragma unroll
                     for (int e = 0; e < 4; ++e)
-                        if (gr + e < nrows) v[e] = s[e];
+                        if (gr + e < nrows) v[e] = sp[e];
                 }
             }
             r[c] = v;
@@ -368,14 +425,27 @@ __device__ __forceinline__ void x6_load_mn(f32x4 (&r)[X6<ROWS>::LOADS], const fl
     }
 }
 
-template <int ROWS, bool KC>
-__device__ __forceinline__ void x6_store(__bf16* __restrict__ lds, const f32x4 (&r)[X6<ROWS>::LOADS]) {
+template <int N>
+struct bfvec;
+template <>
+struct bfvec<4> {
+    typedef bf16x4 T;
+};
+template <>
+struct bfvec<2> {
+    typedef bf16x2 T;
+};
+
+template <int ROWS, int BKX, bool KC>
+__device__ __forceinline__ void x6_store(__bf16* __restrict__ lds, const f32x4 (&r)[(X6<ROWS, BKX>::LOADS)]) {
+    constexpr int PL = X6<ROWS, BKX>::PLANE;
     const int f = threadIdx.x;
     if (KC) {
+        constexpr int KQ = X6<ROWS, BKX>::KQ;
 #pragma unroll
-        for (int i = 0; i < X6<ROWS>::LOADS; ++i) {
+        for (int i = 0; i < X6<ROWS, BKX>::LOADS; ++i) {
             const int idx = f + i * 256;
-            const int row = idx >> 3, kq = (idx & 7) * 4;
+            const int row = idx / KQ, kq = (idx % KQ) * 4;
             bf16x4 hh, mm, ll;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -385,58 +455,54 @@ __device__ __forceinline__ void x6_store(__bf16* __restrict__ lds, const f32x4 (
                 mm[e] = b;
                 ll[e] = c;
             }
-            const int o = x6_idx(row, kq);
+            const int o = x6_idx<BKX>(row, kq);
             *reinterpret_cast<bf16x4*>(lds + o) = hh;
-            *reinterpret_cast<bf16x4*>(lds + X6<ROWS>::PLANE + o) = mm;
-            *reinterpret_cast<bf16x4*>(lds + 2 * X6<ROWS>::PLANE + o) = ll;
+            *reinterpret_cast<bf16x4*>(lds + PL + o) = mm;
+            *reinterpret_cast<bf16x4*>(lds + 2 * PL + o) = ll;
         }
-    } else {
-        constexpr int KPT = X6<ROWS>::KPT;
-        const int i = f / X6<ROWS>::JN, j = f % X6<ROWS>::JN;
+    } else if (X6<ROWS, BKX>::KPT == 1) {
+        const int i = f / X6<ROWS, BKX>::JN, j = f % X6<ROWS, BKX>::JN;
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
-            const int row = 4 * i + rr, k = KPT * j;
-            const int o = x6_idx(row, k);
-            if (KPT == 4) {
-                bf16x4 hh, mm, ll;
+            const int o = x6_idx<BKX>(4 * i + rr, j);
+            __bf16 a, b, cc;
+            split3(r[0][rr], a, b, cc);
+            lds[o] = a;
+            lds[PL + o] = b;
+            lds[2 * PL + o] = cc;
+        }
+    } else {
+        constexpr int KPT = X6<ROWS, BKX>::KPT > 1 ? X6<ROWS, BKX>::KPT : 2;
+        typedef typename bfvec<KPT>::T V;
+        const int i = f / X6<ROWS, BKX>::JN, j = f % X6<ROWS, BKX>::JN;
 #pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    __bf16 a, b, cc;
-                    split3(r[c][rr], a, b, cc);
-                    hh[c] = a;
-                    mm[c] = b;
-                    ll[c] = cc;
-                }
-                *reinterpret_cast<bf16x4*>(lds + o) = hh;
-                *reinterpret_cast<bf16x4*>(lds + X6<ROWS>::PLANE + o) = mm;
-                *reinterpret_cast<bf16x4*>(lds + 2 * X6<ROWS>::PLANE + o) = ll;
-            } else {
-                bf16x2 hh, mm, ll;
+        for (int rr = 0; rr < 4; ++rr) {
+            const int o = x6_idx<BKX>(4 * i + rr, KPT * j);
+            V hh, mm, ll;
 #pragma unroll
-                for (int c = 0; c < 2; ++c) {
-                    __bf16 a, b, cc;
-                    split3(r[c][rr], a, b, cc);
-                    hh[c] = a;
-                    mm[c] = b;
-                    ll[c] = cc;
-                }
-                *reinterpret_cast<bf16x2*>(lds + o) = hh;
-                *reinterpret_cast<bf16x2*>(lds + X6<ROWS>::PLANE + o) = mm;
-                *reinterpret_cast<bf16x2*>(lds + 2 * X6<ROWS>::PLANE + o) = ll;
+            for (int c = 0; c < KPT; ++c) {
+                __bf16 a, b, cc;
+                split3(r[c][rr], a, b, cc);
+                hh[c] = a;
+                mm[c] = b;
+                ll[c] = cc;
             }
+            *reinterpret_cast<V*>(lds + o) = hh;
+            *reinterpret_cast<V*>(lds + PL + o) = mm;
+            *reinterpret_cast<V*>(lds + 2 * PL + o) = ll;
         }
     }
 }
 
-template <int BM, int BN, bool TA, bool TB, bool CONV, bool SEGB>
+template <int BM, int BN, bool TA, bool TB, bool CONV, bool SEGB, int BKX, int NBUF>
 __global__ __launch_bounds__(256, 3) void gemm_x6_kernel(GemmParams p) {
     constexpr int WTM = BM / 2, WTN = BN / 2;
     constexpr int RM = WTM / 32, RN = WTN / 32;
     constexpr bool AKC = !TA, BKC = TB;
+    constexpr int PA = X6<BM, BKX>::PLANE, PB = X6<BN, BKX>::PLANE;
+    constexpr int STAGE = 3 * (PA + PB);
     static_assert(RM >= 1 && RN >= 1, "wave tile >= 32x32");
-    __shared__ __attribute__((aligned(16))) __bf16 smem[3 * (X6<BM>::PLANE + X6<BN>::PLANE)];
-    __bf16* As = smem;
-    __bf16* Bs = smem + 3 * X6<BM>::PLANE;
+    __shared__ __attribute__((aligned(16))) __bf16 smem[NBUF * STAGE];
 
     int zz = blockIdx.z;
     int split = 0;
@@ -464,12 +530,12 @@ __global__ __launch_bounds__(256, 3) void gemm_x6_kernel(GemmParams p) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    f32x4 ra[X6<BM>::LOADS];
-    f32x4 rb[X6<BN>::LOADS];
+    f32x4 ra[X6<BM, BKX>::LOADS];
+    f32x4 rb[X6<BN, BKX>::LOADS];
     const bool va = p.va != 0, vb = p.vb != 0;
-    const bool segAligned = p.segK > 0 && p.segK % BK == 0;
+    const bool segAligned = p.segK > 0 && p.segK % BKX == 0;
     auto stageA = [&](int k) {
-        bool full = va && m0 + BM <= p.M && k + BK <= kend;
+        bool full = va && m0 + BM <= p.M && k + BKX <= kend;
         const float* base = A;
         int kk = k;
         if (CONV) {
@@ -480,15 +546,15 @@ __global__ __launch_bounds__(256, 3) void gemm_x6_kernel(GemmParams p) {
             kk = k - seg * p.segK;
         }
         if (AKC) {
-            if (full) load_stage_full<BM, true>(ra, base, p.lda, m0, kk);
-            else load_stage<BM, true, CONV ? 1 : 0>(ra, A, p.lda, m0, p.M, k, kend, va, p.segK, p.pad, p.Mvalid, 0);
+            if (full) x6_load_kc<BM, BKX, 0, true>(ra, base, p.lda, m0, p.M, kk, kend, va, 0, 0, 0, 0);
+            else x6_load_kc<BM, BKX, CONV ? 1 : 0, false>(ra, A, p.lda, m0, p.M, k, kend, va, p.segK, p.pad, p.Mvalid, 0);
         } else {
-            if (full) x6_load_mn<BM, true>(ra, A, p.lda, m0, p.M, k, kend, va);
-            else x6_load_mn<BM, false>(ra, A, p.lda, m0, p.M, k, kend, va);
+            if (full) x6_load_mn<BM, BKX, true>(ra, A, p.lda, m0, p.M, k, kend, va);
+            else x6_load_mn<BM, BKX, false>(ra, A, p.lda, m0, p.M, k, kend, va);
         }
     };
     auto stageB = [&](int k) {
-        bool full = vb && n0 + BN <= p.N && k + BK <= kend;
+        bool full = vb && n0 + BN <= p.N && k + BKX <= kend;
         const float* base = B;
         int kk = k;
         if (SEGB) {
@@ -498,43 +564,33 @@ __global__ __launch_bounds__(256, 3) void gemm_x6_kernel(GemmParams p) {
             kk = k - seg * p.segK;
         }
         if (BKC) {
-            if (full) load_stage_full<BN, true>(rb, base, p.ldb, n0, kk);
-            else load_stage<BN, true, SEGB ? 2 : 0>(rb, B, p.ldb, n0, p.N, k, kend, vb, p.segK, 0, 0, p.sBseg);
+            if (full) x6_load_kc<BN, BKX, 0, true>(rb, base, p.ldb, n0, p.N, kk, kend, vb, 0, 0, 0, 0);
+            else x6_load_kc<BN, BKX, SEGB ? 2 : 0, false>(rb, B, p.ldb, n0, p.N, k, kend, vb, p.segK, 0, 0, p.sBseg);
         } else {
-            if (full) x6_load_mn<BN, true>(rb, B, p.ldb, n0, p.N, k, kend, vb);
-            else x6_load_mn<BN, false>(rb, B, p.ldb, n0, p.N, k, kend, vb);
+            if (full) x6_load_mn<BN, BKX, true>(rb, B, p.ldb, n0, p.N, k, kend, vb);
+            else x6_load_mn<BN, BKX, false>(rb, B, p.ldb, n0, p.N, k, kend, vb);
         }
     };
-    stageA(kbeg);
-    stageB(kbeg);
-    for (int k0 = kbeg; k0 < kend; k0 += BK) {
-        __syncthreads();
-        x6_store<BM, AKC>(As, ra);
-        x6_store<BN, BKC>(Bs, rb);
-        __syncthreads();
-        if (k0 + BK < kend) {
-            stageA(k0 + BK);
-            stageB(k0 + BK);
-        }
+    auto mfma_stage = [&](const __bf16* As, const __bf16* Bs) {
 #pragma unroll
-        for (int kc = 0; kc < 2; ++kc) {
+        for (int kc = 0; kc < BKX / 16; ++kc) {
             bf16x8 af[RM][3], bf[RN][3];
             const int k = kc * 16 + h * 8;
 #pragma unroll
             for (int i = 0; i < RM; ++i) {
-                const int o = x6_idx(wm * WTM + i * 32 + l32, k);
+                const int o = x6_idx<BKX>(wm * WTM + i * 32 + l32, k);
 #pragma unroll
-                for (int pl = 0; pl < 3; ++pl) af[i][pl] = *reinterpret_cast<const bf16x8*>(As + pl * X6<BM>::PLANE + o);
+                for (int pl = 0; pl < 3; ++pl) af[i][pl] = *reinterpret_cast<const bf16x8*>(As + pl * PA + o);
             }
 #pragma unroll
             for (int j = 0; j < RN; ++j) {
-                const int o = x6_idx(wn * WTN + j * 32 + l32, k);
+                const int o = x6_idx<BKX>(wn * WTN + j * 32 + l32, k);
 #pragma unroll
-                for (int pl = 0; pl < 3; ++pl) bf[j][pl] = *reinterpret_cast<const bf16x8*>(Bs + pl * X6<BN>::PLANE + o);
+                for (int pl = 0; pl < 3; ++pl) bf[j][pl] = *reinterpret_cast<const bf16x8*>(Bs + pl * PB + o);
             }
             // small terms first, the h*h product last
 #pragma unroll
-            for (int t = 0; t < 6; ++t) {
+            for (int t = (X6_ABLATE == 2 ? 5 : 0); t < 6; ++t) {
                 constexpr int pa[6] = {0, 1, 2, 0, 1, 0};
                 constexpr int pb[6] = {2, 1, 0, 1, 0, 0};
 #pragma unroll
@@ -542,6 +598,48 @@ __global__ __launch_bounds__(256, 3) void gemm_x6_kernel(GemmParams p) {
 #pragma unroll
                     for (int j = 0; j < RN; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][pa[t]], bf[j][pb[t]], acc[i][j], 0, 0, 0);
+            }
+        }
+    };
+
+    stageA(kbeg);
+    stageB(kbeg);
+    if (NBUF == 1) {
+        for (int k0 = kbeg; k0 < kend; k0 += BKX) {
+            __syncthreads();
+            x6_store<BM, BKX, AKC>(smem, ra);
+            x6_store<BN, BKX, BKC>(smem + 3 * PA, rb);
+            __syncthreads();
+            if (k0 + BKX < kend) {
+                stageA(k0 + BKX);
+                stageB(k0 + BKX);
+            }
+            mfma_stage(smem, smem + 3 * PA);
+        }
+    } else {
+        // two LDS stages: while the MFMAs read stage s, the registers holding stage s+1 are split
+        // into the other buffer (last read before the previous barrier) and stage s+2 is loaded
+        x6_store<BM, BKX, AKC>(smem, ra);
+        x6_store<BN, BKX, BKC>(smem + 3 * PA, rb);
+        if (kbeg + BKX < kend) {
+            stageA(kbeg + BKX);
+            stageB(kbeg + BKX);
+        }
+        __syncthreads();
+        int buf = 0;
+        for (int k0 = kbeg; k0 < kend; k0 += BKX) {
+            const __bf16* As = smem + buf * STAGE;
+            mfma_stage(As, As + 3 * PA);
+            if (k0 + BKX < kend) {
+                __bf16* nxt = smem + (buf ^ 1) * STAGE;
+                x6_store<BM, BKX, AKC>(nxt, ra);
+                x6_store<BN, BKX, BKC>(nxt + 3 * PA, rb);
+                if (k0 + 2 * BKX < kend) {
+                    stageA(k0 + 2 * BKX);
+                    stageB(k0 + 2 * BKX);
+                }
+                __syncthreads();
+                buf ^= 1;
             }
         }
     }
@@ -578,17 +676,19 @@ __global__ __launch_bounds__(256, 3) void gemm_x6_kernel(GemmParams p) {
             }
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int BKX, int NB>
 void launch_x6(const GemmParams& p, dim3 grid, hipStream_t st) {
+#define X6K(TA_, TB_, CV_, SB_) gemm_x6_kernel<BM, BN, TA_, TB_, CV_, SB_, BKX, NB>
     if (p.segK > 0) {
-        if (p.segB) hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, false, true, true, true>), grid, dim3(256), 0, st, p);
-        else hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, false, false, true, false>), grid, dim3(256), 0, st, p);
+        if (p.segB) hipLaunchKernelGGL((X6K(false, true, true, true)), grid, dim3(256), 0, st, p);
+        else hipLaunchKernelGGL((X6K(false, false, true, false)), grid, dim3(256), 0, st, p);
         return;
     }
-    if (!p.ta && !p.tb) hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, false, false, false, false>), grid, dim3(256), 0, st, p);
-    else if (!p.ta && p.tb) hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, false, true, false, false>), grid, dim3(256), 0, st, p);
-    else if (p.ta && !p.tb) hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, true, false, false, false>), grid, dim3(256), 0, st, p);
-    else hipLaunchKernelGGL((gemm_x6_kernel<BM, BN, true, true, false, false>), grid, dim3(256), 0, st, p);
+    if (!p.ta && !p.tb) hipLaunchKernelGGL((X6K(false, false, false, false)), grid, dim3(256), 0, st, p);
+    else if (!p.ta && p.tb) hipLaunchKernelGGL((X6K(false, true, false, false)), grid, dim3(256), 0, st, p);
+    else if (p.ta && !p.tb) hipLaunchKernelGGL((X6K(true, false, false, false)), grid, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((X6K(true, true, false, false)), grid, dim3(256), 0, st, p);
+#undef X6K
 }
 
 // Sum split-K partials in split order (deterministic) and apply the epilogue.
@@ -704,10 +804,18 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
     p.ws = ws;
     dim3 grid(gx, gy, p.Z * splits);
     if (p.mode == 1) {
-        if (tile == 0) launch_x6<128, 128>(p, grid, st);
-        else if (tile == 1) launch_x6<128, 64>(p, grid, st);
-        else if (tile == 2) launch_x6<64, 128>(p, grid, st);
-        else launch_x6<64, 64>(p, grid, st);
+        // x6 variants: g_nbuf 1 -> BK 32 single LDS stage; 2 -> BK 16 double-buffered
+        if (g_nbuf == 2) {
+            if (tile == 0) launch_x6<128, 128, 16, 2>(p, grid, st);
+            else if (tile == 1) launch_x6<128, 64, 16, 2>(p, grid, st);
+            else if (tile == 2) launch_x6<64, 128, 16, 2>(p, grid, st);
+            else launch_x6<64, 64, 16, 2>(p, grid, st);
+        } else {
+            if (tile == 0) launch_x6<128, 128, 32, 1>(p, grid, st);
+            else if (tile == 1) launch_x6<128, 64, 32, 1>(p, grid, st);
+            else if (tile == 2) launch_x6<64, 128, 32, 1>(p, grid, st);
+            else launch_x6<64, 64, 32, 1>(p, grid, st);
+        }
     } else if (g_nbuf == 1) {
         if (tile == 0) launch_tile<128, 128, 1>(p, grid, st);
         else if (tile == 1) launch_tile<128, 64, 1>(p, grid, st);
