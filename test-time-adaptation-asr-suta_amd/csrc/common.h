@@ -52,6 +52,7 @@ enum {
     EPI_STORE_PRE = 8,
     EPI_DGELU = 16,
     EPI_ACCUM = 32,
+    EPI_SMBWD = 64,  // softmax backward: v = alpha * aux(m,n) * (acc - rowv[m])  (dS from dP, P, delta)
 };
 
 struct GemmParams {
@@ -74,6 +75,8 @@ struct GemmParams {
     long ldaux, sAux0, sAux1;
     float* C2;
     long ldc2, sC20, sC21;
+    const float* rowv;  // per-row vector (EPI_SMBWD), batch strides as the others
+    long sRow0, sRow1;
     float alpha;
     int epi;
     // internal

@@ -107,7 +107,7 @@ struct Arena {
 };
 
 struct LayerBufs {
-    float *x_in, *xhat1, *rstd1, *y1, *qkv, *P, *hmid, *xhat2, *rstd2, *y2, *u, *x_out;
+    float *x_in, *xhat1, *rstd1, *y1, *qkv, *P, *ctx, *hmid, *xhat2, *rstd2, *y2, *u, *x_out;
 };
 
 struct Plan {
@@ -123,7 +123,7 @@ struct Plan {
     std::vector<LayerBufs> lay;
     float *ctx, *gu, *rtmp, *logits;
     // backward
-    float *dlogits, *d1, *d2, *d3, *dqkv, *dP, *du, *dzc, *dzc2, *lnpart, *loss, *loss_scratch;
+    float *dlogits, *d1, *d2, *d3, *dqkv, *dP, *du, *dzc, *dzc2, *lnpart, *loss, *loss_scratch, *c0part, *delta;
     double* dpart;
     int* ids;
     float* splitws;
@@ -268,7 +268,7 @@ void suta_engine::build_plan(int B, long N) {
         pl.x = ar.take<float>((size_t)B * N);
         for (int i = 0; i < k.nconv; ++i) {
             const long n = (long)B * pl.Lc[i] * k.C[i];
-            pl.z[i] = ar.take<float>(n);
+            pl.z[i] = (i == 0 && !k.layer_mode) ? nullptr : ar.take<float>(n);  // group-mode conv0 is recomputed
             pl.a[i] = ar.take<float>(n);
             if (k.layer_mode) {
                 pl.cxhat[i] = ar.take<float>(n);
@@ -298,6 +298,7 @@ void suta_engine::build_plan(int B, long N) {
             lb.y1 = ar.take<float>(BT * H);
             lb.qkv = ar.take<float>(BT * 3 * H);
             lb.P = ar.take<float>(Psz);
+            lb.ctx = ar.take<float>(BT * H);
             lb.hmid = k.stable ? ar.take<float>(BT * H) : nullptr;
             lb.xhat2 = ar.take<float>(BT * H);
             lb.rstd2 = ar.take<float>(BT);
@@ -319,12 +320,14 @@ void suta_engine::build_plan(int B, long N) {
         pl.d3 = ar.take<float>(BT * H);
         pl.dqkv = ar.take<float>(BT * 3 * H);
         pl.dP = ar.take<float>(Psz);
+        pl.delta = ar.take<float>((size_t)B * k.NH * T);
         pl.du = ar.take<float>(BT * k.F);
         pl.dzc = ar.take<float>((size_t)B * maxLC);
         pl.dzc2 = ar.take<float>((size_t)B * maxLC);
         const long lnrows = std::max<long>(pl.Lc[0], T);
         pl.lnpart = ar.take<float>((size_t)B * ((lnrows + 31) / 32) * 2 * std::max<long>(H, maxLC / pl.Lc[0] + 1) + 64);
         pl.dpart = ar.take<double>((size_t)B * ((pl.Lc[0] + 127) / 128 + 2) * 2 * k.C[0] + (size_t)B * k.C[0] * 2);
+        pl.c0part = ar.take<float>((size_t)B * ((pl.Lc[0] + 127) / 128) * k.K[0] * k.C[0] + 64);
         pl.loss = ar.take<float>(B);
         pl.loss_scratch = ar.take<float>((size_t)B * T * 66 + 64);
         pl.ids = ar.take<int>((size_t)BT);
@@ -344,18 +347,18 @@ void suta_engine::forward(int B) {
     Plan& pl = plan;
     const int T = pl.T, H = k.H, NH = k.NH, d = H / NH;
     const long BT = (long)B * T;
-    // conv0
-    timed(F_EW, [&] {
-        launch_conv0(pl.x, pl.N, P + o_cw[0], k.conv_bias ? P + o_cb[0] : nullptr, Pn, pl.z[0], B, pl.Lc[0], k.C[0],
-                     k.K[0], k.S[0], st);
-    });
     if (!k.layer_mode) {
+        // conv0 + GroupNorm + GELU, conv0 recomputed in each pass (never stored)
         timed(F_NORM, [&] {
-            launch_col_stats(pl.z[0], B, pl.Lc[0], k.C[0], 1e-5f, pl.dpart, pl.gn_mean, pl.gn_rstd, st);
-            launch_gn_apply_gelu(pl.z[0], pl.gn_mean, pl.gn_rstd, P + o_cg[0], P + o_cbeta[0], Pn, pl.a[0], B,
-                                 pl.Lc[0], k.C[0], st);
+            launch_front_gn_fwd(pl.x, pl.N, P + o_cw[0], k.conv_bias ? P + o_cb[0] : nullptr, Pn, B, pl.Lc[0], k.C[0],
+                                k.K[0], k.S[0], P + o_cg[0], P + o_cbeta[0], pl.gn_mean, pl.gn_rstd, pl.a[0],
+                                pl.dpart, st);
         });
     } else {
+        timed(F_EW, [&] {
+            launch_conv0(pl.x, pl.N, P + o_cw[0], k.conv_bias ? P + o_cb[0] : nullptr, Pn, pl.z[0], B, pl.Lc[0],
+                         k.C[0], k.K[0], k.S[0], st);
+        });
         timed(F_NORM, [&] {
             launch_layernorm_fwd(pl.z[0], P + o_cg[0], P + o_cbeta[0], Pn, pl.Lc[0], pl.a[0], pl.cxhat[0],
                                  pl.crstd[0], B * pl.Lc[0], k.C[0], 1e-5f, 1, st);
@@ -528,7 +531,7 @@ void suta_engine::forward(int B) {
             g.lda = pl.Tp;
             g.B = lb.qkv + 2 * H;
             g.ldb = 3 * H;
-            g.C = pl.ctx;
+            g.C = lb.ctx;
             g.ldc = H;
             g.M = T;
             g.N = d;
@@ -546,7 +549,7 @@ void suta_engine::forward(int B) {
         {  // out projection + residual
             GemmParams g;
             gemm_init(g);
-            g.A = pl.ctx;
+            g.A = lb.ctx;
             g.lda = H;
             g.B = wo[l];
             g.tb = 1;
@@ -729,7 +732,9 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
         }
         // dctx = dhres @ Wo
         nn_gemm(dhres, H, wo[l], H, pl.ctx, H, (int)BT, H, H, 0, nullptr, 0, nullptr, 0);
-        {  // dP = dctx_h @ V_h^T
+        // softmax-backward row term delta = rowsum(dctx * ctx) per head, fused into the dP epilogue
+        timed(F_SOFTMAX, [&] { launch_attn_delta(pl.ctx, lb.ctx, pl.delta, B, T, NH, d, st); });
+        {  // dS = scale * P * (dctx_h @ V_h^T - delta)
             GemmParams g;
             gemm_init(g);
             g.A = pl.ctx;
@@ -750,9 +755,17 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
             g.sB1 = (long)T * 3 * H;
             g.sC0 = (long)T * pl.Tp;
             g.sC1 = (long)NH * T * pl.Tp;
+            g.epi = EPI_SMBWD;
+            g.alpha = scale;
+            g.aux = lb.P;
+            g.ldaux = pl.Tp;
+            g.sAux0 = (long)T * pl.Tp;
+            g.sAux1 = (long)NH * T * pl.Tp;
+            g.rowv = pl.delta;
+            g.sRow0 = T;
+            g.sRow1 = (long)NH * T;
             gemm(g);
         }
-        timed(F_SOFTMAX, [&] { launch_softmax_bwd_rows(lb.P, pl.dP, (long)B * NH * T, T, pl.Tp, scale, st); });
         {  // dQ = dS K_h
             GemmParams g;
             gemm_init(g);
@@ -1004,17 +1017,18 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
     // conv0: cur = da0
     if (!k.layer_mode) {
         timed(F_NORM, [&] {
-            launch_gn_gelu_bwd(cur, pl.z[0], pl.gn_mean, pl.gn_rstd, P + o_cg[0], P + o_cbeta[0], Pn, other,
-                               G + o_cg[0], G + o_cbeta[0], Pn, B, pl.Lc[0], k.C[0], pl.dpart, st);
+            launch_front_gn_bwd(pl.x, pl.N, P + o_cw[0], k.conv_bias ? P + o_cb[0] : nullptr, Pn, B, pl.Lc[0], k.C[0],
+                                k.K[0], k.S[0], P + o_cg[0], P + o_cbeta[0], pl.gn_mean, pl.gn_rstd, cur, G + o_cg[0],
+                                G + o_cbeta[0], G + o_cw[0], Pn, pl.dpart, pl.c0part, st);
         });
-    } else {
-        timed(F_NORM, [&] {
-            launch_layernorm_bwd(cur, pl.cxhat[0], pl.crstd[0], P + o_cg[0], P + o_cbeta[0], Pn, pl.Lc[0], B, k.C[0], 1,
-                                 nullptr, nullptr, other, G + o_cg[0], G + o_cbeta[0], Pn, pl.lnpart, st);
-        });
-        if (k.conv_bias)
-            timed(F_NORM, [&] { launch_colsum(other, B, pl.Lc[0], k.C[0], G + o_cb[0], Pn, pl.lnpart, st); });
+        return;
     }
+    timed(F_NORM, [&] {
+        launch_layernorm_bwd(cur, pl.cxhat[0], pl.crstd[0], P + o_cg[0], P + o_cbeta[0], Pn, pl.Lc[0], B, k.C[0], 1,
+                             nullptr, nullptr, other, G + o_cg[0], G + o_cbeta[0], Pn, pl.lnpart, st);
+    });
+    if (k.conv_bias)
+        timed(F_NORM, [&] { launch_colsum(other, B, pl.Lc[0], k.C[0], G + o_cb[0], Pn, pl.lnpart, st); });
     {  // dW0[k][c] = sum_t x[S0 t + k] dz0[t][c]
         GemmParams g;
         gemm_init(g);

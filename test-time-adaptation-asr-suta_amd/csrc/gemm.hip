@@ -17,6 +17,7 @@
 // MFMAs of stage s; with two LDS buffers there is one barrier per K-step.
 #include "common.h"
 #include <algorithm>
+#include <stdexcept>
 
 namespace {
 
@@ -142,20 +143,152 @@ __device__ __forceinline__ f32x4 read_frag(const float* __restrict__ lds, int ro
     return v;
 }
 
-__device__ __forceinline__ float epi_value(const GemmParams& p, float acc, long row, long col, const float* bias,
-                                           const float* R, const float* aux, float* C2, const float* Cold) {
-    float v = acc * p.alpha;
-    if (p.epi & EPI_BIAS) v += bias[col];
-    if (p.epi & EPI_ACCUM) v += Cold[row * p.ldc + col];
-    if (p.epi & EPI_STORE_PRE) C2[row * p.ldc2 + col] = v;
-    if (p.epi & EPI_GELU) v = gelu_f(v);
-    if (p.epi & EPI_DGELU) v *= dgelu_f(aux[row * p.ldaux + col]);
-    if (p.epi & EPI_RESID) v += R[row * p.ldr + col];
+// Epilogue arithmetic on operands already in registers (xa = aux, xr = R, xc = old C, xw = rowv).
+__device__ __forceinline__ float epi_apply(int epi, float alpha, float acc, float bj, float xa, float xr, float xc,
+                                           float xw, float* c2) {
+    if (epi & EPI_SMBWD) return alpha * (xa * (acc - xw));
+    float v = acc * alpha;
+    if (epi & EPI_BIAS) v += bj;
+    if (epi & EPI_ACCUM) v += xc;
+    if (epi & EPI_STORE_PRE) *c2 = v;
+    if (epi & EPI_GELU) v = gelu_f(v);
+    if (epi & EPI_DGELU) v *= dgelu_f(xa);
+    if (epi & EPI_RESID) v += xr;
     return v;
 }
 
+__device__ __forceinline__ float epi_value(const GemmParams& p, float acc, long row, long col, const float* bias,
+                                           const float* R, const float* aux, float* C2, const float* Cold,
+                                           const float* rowv) {
+    const int e = p.epi;
+    return epi_apply(e, p.alpha, acc, (e & EPI_BIAS) ? bias[col] : 0.f,
+                     (e & (EPI_DGELU | EPI_SMBWD)) ? aux[row * p.ldaux + col] : 0.f,
+                     (e & EPI_RESID) ? R[row * p.ldr + col] : 0.f, (e & EPI_ACCUM) ? Cold[row * p.ldc + col] : 0.f,
+                     (e & EPI_SMBWD) ? rowv[row] : 0.f, C2 ? C2 + row * p.ldc2 + col : nullptr);
+}
+
+// Store the wave's RM x RN 32x32 accumulator fragments (MFMA 32x32 output layout: lane -> column,
+// register r -> row (r&3) + 8(r>>2) + 4h).  Flags are block-uniform, so each epilogue step is one
+// uniform branch per fragment rather than per element; operand loads use clamped (always valid)
+// indices so they are unpredicated, and every operand of a fragment is in registers before its first
+// store (C may alias aux / R in place).  Only the stores are predicated, and only on edge tiles.
+// gemm_launch guarantees RESID, ACCUM and SMBWD are mutually exclusive (they share xq).
+template <int RM, int RN>
+__device__ __forceinline__ void gemm_epilogue(const GemmParams& p, const f32x16 (&acc)[RM][RN], int z1, int z0,
+                                              int rbase, int cbase, int h, int l32, bool interior) {
+    if (p.splits > 1) {
+        float* W = p.ws + ((long)blockIdx.z) * p.M * (long)p.N;
+#pragma unroll
+        for (int i = 0; i < RM; ++i)
+#pragma unroll
+            for (int j = 0; j < RN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int row = rbase + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    const int col = cbase + j * 32 + l32;
+                    if (interior || (row < p.M && col < p.N)) W[(long)row * p.N + col] = acc[i][j][r];
+                }
+        return;
+    }
+    const int e = p.epi;
+    float* C = p.C + z1 * p.sC1 + z0 * p.sC0;
+    const float* bias = p.bias ? p.bias + z1 * p.sBias1 + z0 * p.sBias0 : nullptr;
+    const float* aux = p.aux ? p.aux + z1 * p.sAux1 + z0 * p.sAux0 : nullptr;
+    float* C2 = p.C2 ? p.C2 + z1 * p.sC21 + z0 * p.sC20 : nullptr;
+    // second operand: R (RESID), old C (ACCUM) or the row vector (SMBWD)
+    const float* Q = nullptr;
+    long ldq = 0, colq = 1;
+    if (e & EPI_RESID) {
+        Q = p.R + z1 * p.sR1 + z0 * p.sR0;
+        ldq = p.ldr;
+    } else if (e & EPI_ACCUM) {
+        Q = C;
+        ldq = p.ldc;
+    } else if (e & EPI_SMBWD) {
+        Q = p.rowv + z1 * p.sRow1 + z0 * p.sRow0;
+        ldq = 1;
+        colq = 0;
+    }
+    const float alpha = p.alpha;
+#ifndef GEMM_EPI_CH
+#define GEMM_EPI_CH 8
+#endif
+    constexpr int CH = GEMM_EPI_CH;  // elements per epilogue chunk (bounds the extra live registers to 3 x CH)
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+#pragma unroll
+            for (int r0 = 0; r0 < 16; r0 += CH) {
+                const int col = cbase + j * 32 + l32;
+                const long colc = min(col, p.N - 1);
+                float v[CH], xa[CH], xq[CH];
+                if (e & (EPI_DGELU | EPI_SMBWD)) {
+#pragma unroll
+                    for (int r = 0; r < CH; ++r) {
+                        const int rr = r0 + r;
+                        const long row = min(rbase + i * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * h, p.M - 1);
+                        xa[r] = aux[row * p.ldaux + colc];
+                    }
+                }
+                if (Q) {
+#pragma unroll
+                    for (int r = 0; r < CH; ++r) {
+                        const int rr = r0 + r;
+                        const long row = min(rbase + i * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * h, p.M - 1);
+                        xq[r] = Q[row * ldq + colc * colq];
+                    }
+                }
+                if (e & EPI_SMBWD) {
+#pragma unroll
+                    for (int r = 0; r < CH; ++r) v[r] = alpha * (xa[r] * (acc[i][j][r0 + r] - xq[r]));
+                } else {
+#pragma unroll
+                    for (int r = 0; r < CH; ++r) v[r] = acc[i][j][r0 + r] * alpha;
+                    if (e & EPI_BIAS) {
+                        const float bj = bias[colc];
+#pragma unroll
+                        for (int r = 0; r < CH; ++r) v[r] += bj;
+                    }
+                    if (e & EPI_ACCUM) {
+#pragma unroll
+                        for (int r = 0; r < CH; ++r) v[r] += xq[r];
+                    }
+                    if (e & EPI_STORE_PRE) {
+#pragma unroll
+                        for (int r = 0; r < CH; ++r) {
+                            const int rr = r0 + r;
+                            const int row = rbase + i * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * h;
+                            if (interior || (row < p.M && col < p.N)) C2[(long)row * p.ldc2 + col] = v[r];
+                        }
+                    }
+                    if (e & EPI_GELU) {
+#pragma unroll
+                        for (int r = 0; r < CH; ++r) v[r] = gelu_f(v[r]);
+                    }
+                    if (e & EPI_DGELU) {
+#pragma unroll
+                        for (int r = 0; r < CH; ++r) v[r] *= dgelu_f(xa[r]);
+                    }
+                    if (e & EPI_RESID) {
+#pragma unroll
+                        for (int r = 0; r < CH; ++r) v[r] += xq[r];
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < CH; ++r) {
+                    const int rr = r0 + r;
+                    const int row = rbase + i * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * h;
+                    if (interior || (row < p.M && col < p.N)) C[(long)row * p.ldc + col] = v[r];
+                }
+            }
+}
+
 template <int BM, int BN, bool TA, bool TB, bool CONV, bool SEGB, int NBUF>
-__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
+#ifndef GEMM_F32_MINB
+#define GEMM_F32_MINB 3
+#endif
+__global__ __launch_bounds__(256, GEMM_F32_MINB) void gemm_f32_kernel(GemmParams p) {
     constexpr int WTM = BM / 2, WTN = BN / 2;
     constexpr int RM = WTM / 32, RN = WTN / 32;
     constexpr bool AKC = !TA, BKC = TB;
@@ -273,37 +406,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
         }
     }
 
-    // ---- epilogue ----
-    if (p.splits > 1) {
-        float* W = p.ws + ((long)blockIdx.z) * p.M * (long)p.N;
-#pragma unroll
-        for (int i = 0; i < RM; ++i)
-#pragma unroll
-            for (int j = 0; j < RN; ++j)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int row = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                    const int col = n0 + wn * WTN + j * 32 + l32;
-                    if (row < p.M && col < p.N) W[(long)row * p.N + col] = acc[i][j][r];
-                }
-        return;
-    }
-    float* C = p.C + z1 * p.sC1 + z0 * p.sC0;
-    const float* bias = p.bias ? p.bias + z1 * p.sBias1 + z0 * p.sBias0 : nullptr;
-    const float* R = p.R ? p.R + z1 * p.sR1 + z0 * p.sR0 : nullptr;
-    const float* aux = p.aux ? p.aux + z1 * p.sAux1 + z0 * p.sAux0 : nullptr;
-    float* C2 = p.C2 ? p.C2 + z1 * p.sC21 + z0 * p.sC20 : nullptr;
-#pragma unroll
-    for (int i = 0; i < RM; ++i)
-#pragma unroll
-        for (int j = 0; j < RN; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int row = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                const int col = n0 + wn * WTN + j * 32 + l32;
-                if (row < p.M && col < p.N)
-                    C[(long)row * p.ldc + col] = epi_value(p, acc[i][j][r], row, col, bias, R, aux, C2, C);
-            }
+    gemm_epilogue<RM, RN>(p, acc, z1, z0, m0 + wm * WTM, n0 + wn * WTN, h, l32, m0 + BM <= p.M && n0 + BN <= p.N);
 }
 
 // ============================================================================================
@@ -644,36 +747,8 @@ __global__ __launch_bounds__(256, 3) void gemm_x6_kernel(GemmParams p) {
         }
     }
 
-    if (p.splits > 1) {
-        float* W = p.ws + ((long)blockIdx.z) * p.M * (long)p.N;
-#pragma unroll
-        for (int i = 0; i < RM; ++i)
-#pragma unroll
-            for (int j = 0; j < RN; ++j)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int row = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                    const int col = n0 + wn * WTN + j * 32 + l32;
-                    if (row < p.M && col < p.N) W[(long)row * p.N + col] = acc[i][j][r];
-                }
-        return;
-    }
-    float* C = p.C + z1 * p.sC1 + z0 * p.sC0;
-    const float* bias = p.bias ? p.bias + z1 * p.sBias1 + z0 * p.sBias0 : nullptr;
-    const float* R = p.R ? p.R + z1 * p.sR1 + z0 * p.sR0 : nullptr;
-    const float* aux = p.aux ? p.aux + z1 * p.sAux1 + z0 * p.sAux0 : nullptr;
-    float* C2 = p.C2 ? p.C2 + z1 * p.sC21 + z0 * p.sC20 : nullptr;
-#pragma unroll
-    for (int i = 0; i < RM; ++i)
-#pragma unroll
-        for (int j = 0; j < RN; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int row = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                const int col = n0 + wn * WTN + j * 32 + l32;
-                if (row < p.M && col < p.N)
-                    C[(long)row * p.ldc + col] = epi_value(p, acc[i][j][r], row, col, bias, R, aux, C2, C);
-            }
+
+    gemm_epilogue<RM, RN>(p, acc, z1, z0, m0 + wm * WTM, n0 + wn * WTN, h, l32, m0 + BM <= p.M && n0 + BN <= p.N);
 }
 
 template <int BM, int BN, int BKX, int NB>
@@ -701,12 +776,13 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmParams p) {
     const float* R = p.R ? p.R + z1 * p.sR1 + z0 * p.sR0 : nullptr;
     const float* aux = p.aux ? p.aux + z1 * p.sAux1 + z0 * p.sAux0 : nullptr;
     float* C2 = p.C2 ? p.C2 + z1 * p.sC21 + z0 * p.sC20 : nullptr;
+    const float* rowv = p.rowv ? p.rowv + z1 * p.sRow1 + z0 * p.sRow0 : nullptr;
     const float* W = p.ws + (long)zz * p.splits * MN;
     for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < MN; idx += (long)gridDim.x * blockDim.x) {
         float s = 0.f;
         for (int sp = 0; sp < p.splits; ++sp) s += W[sp * MN + idx];
         const long row = idx / p.N, col = idx % p.N;
-        C[row * p.ldc + col] = epi_value(p, s, row, col, bias, R, aux, C2, C);
+        C[row * p.ldc + col] = epi_value(p, s, row, col, bias, R, aux, C2, C, rowv);
     }
 }
 
@@ -779,6 +855,9 @@ static int choose_tile(long M, long N, long Z, long K) {
 
 void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
     if (p.M <= 0 || p.N <= 0 || p.Z <= 0) return;
+    const int second = ((p.epi & EPI_RESID) != 0) + ((p.epi & EPI_ACCUM) != 0) + ((p.epi & EPI_SMBWD) != 0);
+    if (second > 1 || ((p.epi & EPI_SMBWD) && p.epi != EPI_SMBWD))
+        throw std::invalid_argument("gemm epilogue: RESID / ACCUM / SMBWD are mutually exclusive");
     auto vec_ok = [](const float* base, long ld, long s0, long s1) {
         return aligned16(base) && (ld % 4 == 0) && (s0 % 4 == 0) && (s1 % 4 == 0);
     };

@@ -11,18 +11,17 @@ void launch_wave_normalize(const float* x, float* y, int B, long N, hipStream_t 
 void launch_conv0(const float* x, long N, const float* W, const float* bias, long wstride, float* z, int B, int L0,
                   int C, int K, int S, hipStream_t st);
 
-// Per-utterance column statistics over rows (GroupNorm with one group per channel):
-// mean[b][c], rstd[b][c] = 1/sqrt(var + eps).  part: scratch of >= B * nchunk * C * 2 doubles.
-void launch_col_stats(const float* z, int B, int rows, int C, float eps, double* part, float* mean, float* rstd,
-                      hipStream_t st);
-// a = gelu((z - mean[c]) * rstd[c] * g[c] + beta[c])  (g, beta per utterance at stride pstride)
-void launch_gn_apply_gelu(const float* z, const float* mean, const float* rstd, const float* g, const float* beta,
-                          long pstride, float* a, int B, int rows, int C, hipStream_t st);
-// GroupNorm(+GELU) backward.  da: grad of a.  Writes dz, and dgamma/dbeta into grad buffers
-// (per utterance at gstride).
-void launch_gn_gelu_bwd(const float* da, const float* z, const float* mean, const float* rstd, const float* g,
-                        const float* beta, long pstride, float* dz, float* dgamma, float* dbeta, long gstride, int B,
-                        int rows, int C, double* part, hipStream_t st);
+// Fused conv0 + GroupNorm + GELU (group mode): conv0 is recomputed from the waveform in each pass.
+// fwd: mean/rstd per (utterance, channel) and a = gelu(GN(conv0(x))).  dpart: >= B*ceil(L0/128)*2*C + B*C doubles.
+void launch_front_gn_fwd(const float* x, long N, const float* W, const float* bias, long wstride, int B, int L0, int C,
+                         int K, int S, const float* g, const float* beta, float* mean, float* rstd, float* a,
+                         double* dpart, hipStream_t st);
+// bwd: da (overwritten with dg) -> dgamma, dbeta and the conv0 weight gradient dW[k][c] (gstride per
+// utterance).  fpart: >= B*ceil(L0/128)*K*C floats.
+void launch_front_gn_bwd(const float* x, long N, const float* W, const float* bias, long wstride, int B, int L0, int C,
+                         int K, int S, const float* g, const float* beta, const float* mean, const float* rstd,
+                         float* da, float* dgamma, float* dbeta, float* dW, long gstride, double* dpart, float* fpart,
+                         hipStream_t st);
 
 // LayerNorm over the last dim D of `rows` rows; gamma/beta of utterance (row / rows_per_utt)
 // at pstride.  Stores y, xhat, rstd.  gelu_out: y = gelu(LN(x)) (feature-encoder "layer" mode).
@@ -42,8 +41,9 @@ void launch_colsum(const float* x, int B, int rows, int C, float* out, long ostr
 
 // In-place row softmax of `nrows` rows of length T (row stride ld).
 void launch_softmax_rows(float* s, long nrows, int T, long ld, hipStream_t st);
-// In place: dP <- scale * P * (dP - rowsum(dP * P)).
-void launch_softmax_bwd_rows(const float* P, float* dP, long nrows, int T, long ld, float scale, hipStream_t st);
+
+// delta[b][h][t] = dot(dO[b][t][head h], O[b][t][head h]): the softmax-backward row term sum_j P_ij dP_ij.
+void launch_attn_delta(const float* dO, const float* O, float* delta, int B, int T, int NH, int dh, hipStream_t st);
 
 // out = g * gelu'(z), n elements.
 void launch_dgelu_mul(const float* g, const float* z, float* out, long n, hipStream_t st);

@@ -86,23 +86,6 @@ __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x,
 // per-utterance column statistics (GroupNorm with groups == channels), double partials
 // ------------------------------------------------------------------------------------------
 constexpr int CS_ROWS = 128;
-__global__ __launch_bounds__(256) void col_stats_partial(const float* __restrict__ z, int rows, int C,
-                                                         double* __restrict__ part, int nchunk) {
-    const int b = blockIdx.y, ch = blockIdx.x;
-    const int r0 = ch * CS_ROWS, r1 = min(rows, r0 + CS_ROWS);
-    const float* zb = z + (long)b * rows * C;
-    double* pb = part + ((long)b * nchunk + ch) * 2 * C;
-    for (int c = threadIdx.x; c < C; c += 256) {
-        double s = 0.0, q = 0.0;
-        for (int r = r0; r < r1; ++r) {
-            const double v = zb[(long)r * C + c];
-            s += v;
-            q += v * v;
-        }
-        pb[c] = s;
-        pb[C + c] = q;
-    }
-}
 __global__ __launch_bounds__(256) void col_stats_final(const double* __restrict__ part, int nchunk, int rows, int C,
                                                        float eps, float* __restrict__ mean, float* __restrict__ rstd) {
     const int b = blockIdx.y;
@@ -121,50 +104,6 @@ __global__ __launch_bounds__(256) void col_stats_final(const double* __restrict_
     rstd[(long)b * C + c] = (float)(1.0 / sqrt(var + (double)eps));
 }
 
-__global__ __launch_bounds__(256) void gn_apply_gelu_kernel(const float* __restrict__ z, const float* __restrict__ mean,
-                                                            const float* __restrict__ rstd, const float* __restrict__ g,
-                                                            const float* __restrict__ beta, long pstride,
-                                                            float* __restrict__ a, int rows, int C) {
-    const int b = blockIdx.y;
-    const long n = (long)rows * C;
-    const float* zb = z + (long)b * n;
-    float* ab = a + (long)b * n;
-    const float* mb = mean + (long)b * C;
-    const float* rb = rstd + (long)b * C;
-    const float* gb = g + (long)b * pstride;
-    const float* bb = beta + (long)b * pstride;
-    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
-        const int c = (int)(i % C);
-        const float xh = (zb[i] - mb[c]) * rb[c];
-        ab[i] = gelu_f(xh * gb[c] + bb[c]);
-    }
-}
-
-// partials of sum(dg) and sum(dg * xhat) per column, dg = da * gelu'(xhat*g + beta)
-__global__ __launch_bounds__(256) void gn_bwd_partial(const float* __restrict__ da, const float* __restrict__ z,
-                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
-                                                      const float* __restrict__ g, const float* __restrict__ beta,
-                                                      long pstride, int rows, int C, double* __restrict__ part,
-                                                      int nchunk) {
-    const int b = blockIdx.y, ch = blockIdx.x;
-    const int r0 = ch * CS_ROWS, r1 = min(rows, r0 + CS_ROWS);
-    const long off = (long)b * rows * C;
-    double* pb = part + ((long)b * nchunk + ch) * 2 * C;
-    for (int c = threadIdx.x; c < C; c += 256) {
-        const float m = mean[(long)b * C + c], rs = rstd[(long)b * C + c];
-        const float gg = g[(long)b * pstride + c], bt = beta[(long)b * pstride + c];
-        double s = 0.0, q = 0.0;
-        for (int r = r0; r < r1; ++r) {
-            const long i = off + (long)r * C + c;
-            const float xh = (z[i] - m) * rs;
-            const float dg = da[i] * dgelu_f(xh * gg + bt);
-            s += dg;
-            q += (double)dg * xh;
-        }
-        pb[c] = s;
-        pb[C + c] = q;
-    }
-}
 // finalize: dgamma = sum dg*xhat, dbeta = sum dg; also writes coefficients for the dx pass
 __global__ __launch_bounds__(256) void gn_bwd_final(const double* __restrict__ part, int nchunk, int C,
                                                     float* __restrict__ dgamma, float* __restrict__ dbeta, long gstride,
@@ -183,25 +122,117 @@ __global__ __launch_bounds__(256) void gn_bwd_final(const double* __restrict__ p
     coef[((long)b * C + c) * 2 + 0] = (float)s;
     coef[((long)b * C + c) * 2 + 1] = (float)q;
 }
-// dz = rstd * gamma * (dg - mean(dg) - xhat * mean(dg*xhat))
-__global__ __launch_bounds__(256) void gn_bwd_dx(const float* __restrict__ da, const float* __restrict__ z,
-                                                 const float* __restrict__ mean, const float* __restrict__ rstd,
-                                                 const float* __restrict__ g, const float* __restrict__ beta,
-                                                 long pstride, const float* __restrict__ coef, float* __restrict__ dz,
-                                                 int rows, int C) {
-    const int b = blockIdx.y;
-    const long n = (long)rows * C;
-    const long off = (long)b * n;
-    const float inv = 1.0f / rows;
-    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
-        const int c = (int)(i % C);
-        const float m = mean[(long)b * C + c], rs = rstd[(long)b * C + c];
-        const float gg = g[(long)b * pstride + c], bt = beta[(long)b * pstride + c];
-        const float xh = (z[off + i] - m) * rs;
-        const float dg = da[off + i] * dgelu_f(xh * gg + bt);
-        const float s = coef[((long)b * C + c) * 2 + 0], q = coef[((long)b * C + c) * 2 + 1];
-        dz[off + i] = rs * gg * (dg - s * inv - xh * (q * inv));
+// ------------------------------------------------------------------------------------------
+// Fused conv0 + GroupNorm(+GELU) front-end (feat_extract_norm "group").  conv0 (K <= 16 taps,
+// 1 input channel) is recomputed from the waveform in every pass instead of being stored, so the
+// front-end moves the 512-channel activation through HBM only as a0 (written once) and da0/dg
+// (read/written in the backward).  Block: F0_ROWS frames x all channels, waveform segment in LDS.
+//   MODE 0: per-channel partial sum / sum of squares of z (double)          -> part
+//   MODE 1: a = gelu(((z - mean) * rstd) * g + beta)                         -> a
+//   MODE 2: dg = da * gelu'(xhat * g + beta) (in place), partial sum(dg), sum(dg * xhat)
+//   MODE 3: dz = rstd*g*(dg - S/L - xhat*Q/L); partial dW[k][c] = sum_t dz[t][c] x[s t + k]
+// ------------------------------------------------------------------------------------------
+constexpr int F0_ROWS = 128;
+// KT/ST: compile-time taps/stride (every wav2vec2 conv0 is K = 10, S = 5) -- keeps the filter in
+// statically indexed registers and lets the tap loop unroll; KT = 0 is the generic (K <= 16) path.
+template <int MODE, int KT, int ST>
+__global__ __launch_bounds__(256) void conv0_gn_kernel(const float* __restrict__ x, long N, const float* __restrict__ W,
+                                                       const float* __restrict__ bias, long wstride, int L0, int C,
+                                                       int K, int S, const float* __restrict__ mean,
+                                                       const float* __restrict__ rstd, const float* __restrict__ g,
+                                                       const float* __restrict__ beta, float* __restrict__ io,
+                                                       const float* __restrict__ coef, double* __restrict__ dpart,
+                                                       float* __restrict__ fpart, int nchunk) {
+    __shared__ float xs[F0_ROWS * 16 + 16];
+    if (KT > 0) {
+        K = KT;
+        S = ST;
     }
+    const int b = blockIdx.y, ch = blockIdx.x;
+    const int t0 = ch * F0_ROWS;
+    const float* xb = x + (long)b * N;
+    const int nx = (F0_ROWS - 1) * S + K;
+    for (int i = threadIdx.x; i < nx; i += 256) {
+        const long gi = (long)t0 * S + i;
+        xs[i] = gi < N ? xb[gi] : 0.f;
+    }
+    __syncthreads();
+    const int rows = min(F0_ROWS, L0 - t0);
+    const float* Wb = W + (long)b * wstride;
+    const float* bb = bias ? bias + (long)b * wstride : nullptr;
+    float* iob = io ? io + ((long)b * L0 + t0) * C : nullptr;
+    const float invL = 1.0f / L0;
+    for (int c = threadIdx.x; c < C; c += 256) {
+        float w[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) w[k] = k < K ? Wb[(long)k * C + c] : 0.f;
+        const float bv = bb ? bb[c] : 0.f;
+        float mu = 0.f, rs = 0.f, gg = 0.f, bt = 0.f, sS = 0.f, sQ = 0.f;
+        if (MODE >= 1) {
+            mu = mean[(long)b * C + c];
+            rs = rstd[(long)b * C + c];
+            gg = g[(long)b * wstride + c];
+            bt = beta[(long)b * wstride + c];
+        }
+        if (MODE == 3) {
+            sS = coef[((long)b * C + c) * 2 + 0] * invL;
+            sQ = coef[((long)b * C + c) * 2 + 1] * invL;
+        }
+        double a0 = 0.0, a1 = 0.0;
+        float dw[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) dw[k] = 0.f;
+#pragma unroll 2
+        for (int r = 0; r < rows; ++r) {
+            float z = 0.f;
+#pragma unroll
+            for (int k = 0; k < (KT > 0 ? KT : 16); ++k)  // same order as conv0_kernel
+                if (KT > 0 || k < K) z = fmaf(xs[r * S + k], w[k], z);
+            z += bv;
+            if (MODE == 0) {
+                a0 += z;
+                a1 += (double)z * z;
+            } else {
+                const float xh = (z - mu) * rs;
+                const long o = (long)r * C + c;
+                if (MODE == 1) {
+                    iob[o] = gelu_f(xh * gg + bt);
+                } else if (MODE == 2) {
+                    const float dg = iob[o] * dgelu_f(xh * gg + bt);
+                    iob[o] = dg;
+                    a0 += dg;
+                    a1 += (double)dg * xh;
+                } else {
+                    const float dz = rs * gg * (iob[o] - sS - xh * sQ);
+#pragma unroll
+                    for (int k = 0; k < (KT > 0 ? KT : 16); ++k)
+                        if (KT > 0 || k < K) dw[k] = fmaf(dz, xs[r * S + k], dw[k]);
+                }
+            }
+        }
+        if (MODE == 0 || MODE == 2) {
+            double* pb = dpart + ((long)b * nchunk + ch) * 2 * C;
+            pb[c] = a0;
+            pb[C + c] = a1;
+        }
+        if (MODE == 3) {
+            float* pf = fpart + ((long)b * nchunk + ch) * K * (long)C;
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                if (k < K) pf[(long)k * C + c] = dw[k];
+        }
+    }
+}
+
+// dW[b][k][c] = sum over chunks (fixed order) of the MODE-3 partials
+__global__ __launch_bounds__(256) void conv0_dw_reduce(const float* __restrict__ fpart, int nchunk, int KC,
+                                                       float* __restrict__ dW, long gstride) {
+    const int b = blockIdx.y;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= KC) return;
+    double s = 0.0;
+    for (int ch = 0; ch < nchunk; ++ch) s += fpart[((long)b * nchunk + ch) * KC + i];
+    dW[(long)b * gstride + i] = (float)s;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -389,29 +420,39 @@ __global__ __launch_bounds__(256) void softmax_rows_kernel(float* __restrict__ s
     }
 }
 
-template <int NPL>
-__global__ __launch_bounds__(256) void softmax_bwd_rows_kernel(const float* __restrict__ P, float* __restrict__ dP,
-                                                               long nrows, int T, long ld, float scale) {
-    const int lane = threadIdx.x & 63;
-    const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (row >= nrows) return;
-    const float* p = P + row * ld;
-    float* d = dP + row * ld;
-    float pv[NPL], dv[NPL];
+// delta[b][h][t] = sum_d dO[b][t][h*dh + d] * O[b][t][h*dh + d]   (= rowsum(P * dP) of the softmax backward)
+// delta[b][h][t] = sum_d dctx[b,t,h,d] * ctx[b,t,h,d].  Items (row, head) are dh contiguous floats, so
+// G = dh/4 lanes each load one 16-B vector of an item and reduce over their lane group (coalesced).
+template <int G>
+__global__ __launch_bounds__(256) void attn_delta_kernel(const f32x4* __restrict__ dO, const f32x4* __restrict__ O,
+                                                         float* __restrict__ delta, long items, int T, int NH) {
+    const long g = (long)blockIdx.x * 256 + threadIdx.x;
+    const long item = g / G;
     float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < NPL; ++i) {
-        const int c = lane + i * 64;
-        pv[i] = c < T ? p[c] : 0.f;
-        dv[i] = c < T ? d[c] : 0.f;
-        s += pv[i] * dv[i];
+    if (item < items) {
+        const f32x4 a = dO[g], c = O[g];
+        s = a[0] * c[0] + a[1] * c[1] + a[2] * c[2] + a[3] * c[3];
     }
-    s = wave_sum(s);
 #pragma unroll
-    for (int i = 0; i < NPL; ++i) {
-        const int c = lane + i * 64;
-        if (c < T) d[c] = scale * (pv[i] * (dv[i] - s));
+    for (int o = G / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if (item < items && (g % G) == 0) {
+        const long row = item / NH;
+        const int hh = (int)(item % NH);
+        const long b = row / T, t = row % T;
+        delta[(b * NH + hh) * T + t] = s;
     }
+}
+
+__global__ __launch_bounds__(256) void attn_delta_scalar(const float* __restrict__ dO, const float* __restrict__ O,
+                                                         float* __restrict__ delta, long items, int T, int NH,
+                                                         int dh) {
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= items) return;
+    float s = 0.f;
+    for (int d = 0; d < dh; ++d) s = fmaf(dO[i * dh + d], O[i * dh + d], s);
+    const long row = i / NH;
+    const long b = row / T, t = row % T;
+    delta[(b * NH + i % NH) * T + t] = s;
 }
 
 __global__ __launch_bounds__(256) void dgelu_mul_kernel(const float* __restrict__ g, const float* __restrict__ z,
@@ -680,36 +721,7 @@ void launch_conv0(const float* x, long N, const float* W, const float* bias, lon
                        K, S);
 }
 
-void launch_col_stats(const float* z, int B, int rows, int C, float eps, double* part, float* mean, float* rstd,
-                      hipStream_t st) {
-    const int nchunk = cdiv(rows, CS_ROWS);
-    hipLaunchKernelGGL(col_stats_partial, dim3(nchunk, B), dim3(256), 0, st, z, rows, C, part, nchunk);
-    hipLaunchKernelGGL(col_stats_final, dim3(cdiv(C, 256), B), dim3(256), 0, st, part, nchunk, rows, C, eps, mean,
-                       rstd);
-}
-
 static int ew_grid(long n) { return (int)std::min<long>(2048, std::max<long>(1, (n + 255) / 256)); }
-
-void launch_gn_apply_gelu(const float* z, const float* mean, const float* rstd, const float* g, const float* beta,
-                          long pstride, float* a, int B, int rows, int C, hipStream_t st) {
-    const long n = (long)rows * C;
-    hipLaunchKernelGGL(gn_apply_gelu_kernel, dim3(std::max(1, ew_grid(n) / std::max(1, B / 2)), B), dim3(256), 0, st,
-                       z, mean, rstd, g, beta, pstride, a, rows, C);
-}
-
-void launch_gn_gelu_bwd(const float* da, const float* z, const float* mean, const float* rstd, const float* g,
-                        const float* beta, long pstride, float* dz, float* dgamma, float* dbeta, long gstride, int B,
-                        int rows, int C, double* part, hipStream_t st) {
-    const int nchunk = cdiv(rows, CS_ROWS);
-    hipLaunchKernelGGL(gn_bwd_partial, dim3(nchunk, B), dim3(256), 0, st, da, z, mean, rstd, g, beta, pstride, rows,
-                       C, part, nchunk);
-    float* coef = reinterpret_cast<float*>(part + (long)B * nchunk * 2 * C);
-    hipLaunchKernelGGL(gn_bwd_final, dim3(cdiv(C, 256), B), dim3(256), 0, st, part, nchunk, C, dgamma, dbeta, gstride,
-                       coef);
-    const long n = (long)rows * C;
-    hipLaunchKernelGGL(gn_bwd_dx, dim3(std::max(1, ew_grid(n) / std::max(1, B / 2)), B), dim3(256), 0, st, da, z,
-                       mean, rstd, g, beta, pstride, coef, dz, rows, C);
-}
 
 void launch_layernorm_fwd(const float* x, const float* g, const float* beta, long pstride, int rows_per_utt,
                           float* y, float* xhat, float* rstd, int rows, int D, float eps, int gelu_out,
@@ -762,16 +774,6 @@ void launch_softmax_rows(float* s, long nrows, int T, long ld, hipStream_t st) {
     else hipLaunchKernelGGL(softmax_rows_kernel<32>, grid, dim3(256), 0, st, s, nrows, T, ld);
 }
 
-void launch_softmax_bwd_rows(const float* P, float* dP, long nrows, int T, long ld, float scale, hipStream_t st) {
-    dim3 grid((unsigned)((nrows + 3) / 4));
-    if (T <= 256) hipLaunchKernelGGL(softmax_bwd_rows_kernel<4>, grid, dim3(256), 0, st, P, dP, nrows, T, ld, scale);
-    else if (T <= 512)
-        hipLaunchKernelGGL(softmax_bwd_rows_kernel<8>, grid, dim3(256), 0, st, P, dP, nrows, T, ld, scale);
-    else if (T <= 1024)
-        hipLaunchKernelGGL(softmax_bwd_rows_kernel<16>, grid, dim3(256), 0, st, P, dP, nrows, T, ld, scale);
-    else hipLaunchKernelGGL(softmax_bwd_rows_kernel<32>, grid, dim3(256), 0, st, P, dP, nrows, T, ld, scale);
-}
-
 void launch_dgelu_mul(const float* g, const float* z, float* out, long n, hipStream_t st) {
     hipLaunchKernelGGL(dgelu_mul_kernel, dim3(ew_grid(n)), dim3(256), 0, st, g, z, out, n);
 }
@@ -792,4 +794,58 @@ void launch_adam(float* P, const float* G, float* M, float* V, long pstride, int
     if (total == 0) return;
     const int gx = (int)std::min<long>(std::max<long>(1, 4096 / std::max(1, B)), (total + 255) / 256);
     hipLaunchKernelGGL(adam_kernel, dim3(gx, B), dim3(256), 0, st, P, G, M, V, pstride, a, total);
+}
+
+template <int MODE, typename... Args>
+static void launch_conv0_gn(dim3 grid, hipStream_t st, int K, int S, Args... args) {
+    if (K == 10 && S == 5)
+        hipLaunchKernelGGL((conv0_gn_kernel<MODE, 10, 5>), grid, dim3(256), 0, st, args...);
+    else
+        hipLaunchKernelGGL((conv0_gn_kernel<MODE, 0, 0>), grid, dim3(256), 0, st, args...);
+}
+
+void launch_front_gn_fwd(const float* x, long N, const float* W, const float* bias, long wstride, int B, int L0, int C,
+                         int K, int S, const float* g, const float* beta, float* mean, float* rstd, float* a,
+                         double* dpart, hipStream_t st) {
+    const int nchunk = cdiv(L0, F0_ROWS);
+    launch_conv0_gn<0>(dim3(nchunk, B), st, K, S, x, N, W, bias, wstride, L0, C, K, S,
+                       (const float*)nullptr, (const float*)nullptr, (const float*)nullptr, (const float*)nullptr,
+                       (float*)nullptr, (const float*)nullptr, dpart, (float*)nullptr, nchunk);
+    hipLaunchKernelGGL(col_stats_final, dim3(cdiv(C, 256), B), dim3(256), 0, st, dpart, nchunk, L0, C, 1e-5f, mean,
+                       rstd);
+    launch_conv0_gn<1>(dim3(nchunk, B), st, K, S, x, N, W, bias, wstride, L0, C, K, S,
+                       mean, rstd, g, beta, a, (const float*)nullptr, (double*)nullptr, (float*)nullptr, nchunk);
+}
+
+void launch_front_gn_bwd(const float* x, long N, const float* W, const float* bias, long wstride, int B, int L0, int C,
+                         int K, int S, const float* g, const float* beta, const float* mean, const float* rstd,
+                         float* da, float* dgamma, float* dbeta, float* dW, long gstride, double* dpart, float* fpart,
+                         hipStream_t st) {
+    const int nchunk = cdiv(L0, F0_ROWS);
+    launch_conv0_gn<2>(dim3(nchunk, B), st, K, S, x, N, W, bias, wstride, L0, C, K, S,
+                       mean, rstd, g, beta, da, (const float*)nullptr, dpart, (float*)nullptr, nchunk);
+    float* coef = reinterpret_cast<float*>(dpart + (long)B * nchunk * 2 * C);
+    hipLaunchKernelGGL(gn_bwd_final, dim3(cdiv(C, 256), B), dim3(256), 0, st, dpart, nchunk, C, dgamma, dbeta, gstride,
+                       coef);
+    launch_conv0_gn<3>(dim3(nchunk, B), st, K, S, x, N, W, bias, wstride, L0, C, K, S,
+                       mean, rstd, g, beta, da, coef, (double*)nullptr, fpart, nchunk);
+    hipLaunchKernelGGL(conv0_dw_reduce, dim3(cdiv((long)K * C, 256), B), dim3(256), 0, st, fpart, nchunk, K * C, dW,
+                       gstride);
+}
+
+void launch_attn_delta(const float* dO, const float* O, float* delta, int B, int T, int NH, int dh, hipStream_t st) {
+    const long items = (long)B * T * NH;
+    const long vec = items * (dh / 4);
+    const dim3 grid((unsigned)((vec + 255) / 256));
+    const f32x4* a = reinterpret_cast<const f32x4*>(dO);
+    const f32x4* c = reinterpret_cast<const f32x4*>(O);
+    switch (dh) {
+        case 16: hipLaunchKernelGGL(attn_delta_kernel<4>, grid, dim3(256), 0, st, a, c, delta, items, T, NH); return;
+        case 32: hipLaunchKernelGGL(attn_delta_kernel<8>, grid, dim3(256), 0, st, a, c, delta, items, T, NH); return;
+        case 64: hipLaunchKernelGGL(attn_delta_kernel<16>, grid, dim3(256), 0, st, a, c, delta, items, T, NH); return;
+        case 128: hipLaunchKernelGGL(attn_delta_kernel<32>, grid, dim3(256), 0, st, a, c, delta, items, T, NH); return;
+        default:
+            hipLaunchKernelGGL(attn_delta_scalar, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, st, dO, O, delta,
+                               items, T, NH, dh);
+    }
 }

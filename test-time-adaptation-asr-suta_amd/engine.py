@@ -14,7 +14,7 @@ import numpy as np
 
 from .config import param_shapes
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsuta.so")
+LIB_PATH = os.environ.get("SUTA_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsuta.so")
 MAX_CONV = 8
 
 # exported symbols (kept in sync with include/suta.h; tests/test_abi.py checks both)

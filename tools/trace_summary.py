@@ -1,17 +1,43 @@
-"""Summarise a rocprofv3 kernel-trace CSV: time per kernel family and per GEMM grid."""
-import collections, csv, sys
-r = list(csv.DictReader(open(sys.argv[1])))
-fam = collections.defaultdict(float); g = collections.defaultdict(lambda: [0, 0.0])
-for x in r:
-    n = x['Kernel_Name']; t = (int(x['End_Timestamp']) - int(x['Start_Timestamp'])) / 1e6
-    base = n.replace('void ', '').replace('(anonymous namespace)::', '')
-    fam[base.split('(')[0].split('<')[0]] += t
-    if 'gemm_f32_kernel' in n:
-        k = (n[n.find('<') + 1:n.find('>')], int(x['Grid_Size_X']) // 256, int(x['Grid_Size_Y']), int(x['Grid_Size_Z']))
-        g[k][0] += 1; g[k][1] += t
-tot = sum(fam.values())
-print(f"total kernel ms {tot:.1f}")
-for k, v in sorted(fam.items(), key=lambda kv: -kv[1])[:25]: print(f"  {v:9.2f} ms {100*v/tot:5.1f}%  {k}")
-print("GEMM by template/grid:")
-for k, v in sorted(g.items(), key=lambda kv: -kv[1][1])[:int(sys.argv[2]) if len(sys.argv) > 2 else 30]:
-    print(f"  {v[1]:9.2f} ms {v[0]:5d} calls {v[1]/v[0]:.4f} ms/call  {k}")
+"""Summarise a rocprofv3 kernel trace (CSV `*_kernel_trace.csv` or rocpd `*_results.db`):
+time per kernel family, per GEMM template/grid, and VGPR counts of the GEMM kernels."""
+import collections, csv, sqlite3, sys
+
+
+def rows(path):
+    """Yield (name, ms, grid_x, grid_y, grid_z, vgpr) per dispatch."""
+    if path.endswith('.db'):
+        c = sqlite3.connect(path)
+        for n, d, gx, gy, gz, vg in c.execute(
+                "select name, duration, grid_x, grid_y, grid_z, vgpr_count from kernels"):
+            yield n, d / 1e6, gx, gy, gz, vg
+    else:
+        for x in csv.DictReader(open(path)):
+            yield (x['Kernel_Name'], (int(x['End_Timestamp']) - int(x['Start_Timestamp'])) / 1e6,
+                   int(x['Grid_Size_X']), int(x['Grid_Size_Y']), int(x['Grid_Size_Z']), int(x.get('VGPR_Count', 0) or 0))
+
+
+def main():
+    fam = collections.defaultdict(float)
+    g = collections.defaultdict(lambda: [0, 0.0])
+    vg = {}
+    for n, t, gx, gy, gz, v in rows(sys.argv[1]):
+        base = n.replace('void ', '').replace('(anonymous namespace)::', '')
+        fam[base.split('(')[0].split('<')[0]] += t
+        if 'gemm_f32_kernel' in n or 'gemm_x6_kernel' in n:
+            tmpl = n[n.find('<') + 1:n.find('>')]
+            k = (tmpl, gx // 256, gy, gz)
+            g[k][0] += 1
+            g[k][1] += t
+            vg[tmpl] = v
+    tot = sum(fam.values())
+    print(f"total kernel ms {tot:.1f}")
+    for k, v in sorted(fam.items(), key=lambda kv: -kv[1])[:25]:
+        print(f"  {v:9.2f} ms {100*v/tot:5.1f}%  {k}")
+    print("GEMM by template/grid:")
+    for k, v in sorted(g.items(), key=lambda kv: -kv[1][1])[:int(sys.argv[2]) if len(sys.argv) > 2 else 30]:
+        print(f"  {v[1]:9.2f} ms {v[0]:5d} calls {v[1]/v[0]:.4f} ms/call  {k}")
+    print("GEMM VGPRs:", {k: v for k, v in vg.items()})
+
+
+if __name__ == '__main__':
+    main()
