@@ -167,6 +167,21 @@ __device__ __forceinline__ float epi_value(const GemmParams& p, float acc, long 
                      (e & EPI_SMBWD) ? rowv[row] : 0.f, C2 ? C2 + row * p.ldc2 + col : nullptr);
 }
 
+// XCD-aware tile order (cdna_hip_programming.md T1, bijective form): blocks are dealt round-robin over
+// the 8 XCDs, so block b is renumbered to give every XCD one contiguous range of tiles (n fastest, then
+// m, then batch/split) -- the tiles that share an A row panel run on one L2.  Speed only.
+struct TileId {
+    int x, y, z;
+};
+__device__ __forceinline__ TileId xcd_tile() {
+    const int gx = gridDim.x, gy = gridDim.y;
+    const int nwg = gx * gy * gridDim.z;
+    const int orig = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+    const int id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+    return TileId{id % gx, (id / gx) % gy, id / (gx * gy)};
+}
+
 // Store the wave's RM x RN 32x32 accumulator fragments (MFMA 32x32 output layout: lane -> column,
 // register r -> row (r&3) + 8(r>>2) + 4h).  Flags are block-uniform, so each epilogue step is one
 // uniform branch per fragment rather than per element; operand loads use clamped (always valid)
@@ -175,9 +190,9 @@ __device__ __forceinline__ float epi_value(const GemmParams& p, float acc, long 
 // gemm_launch guarantees RESID, ACCUM and SMBWD are mutually exclusive (they share xq).
 template <int RM, int RN>
 __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, const f32x16 (&acc)[RM][RN], int z1, int z0,
-                                              int rbase, int cbase, int h, int l32, bool interior) {
+                                              int rbase, int cbase, int h, int l32, bool interior, int tz) {
     if (p.splits > 1) {
-        float* W = p.ws + ((long)blockIdx.z) * p.M * (long)p.N;
+        float* W = p.ws + ((long)tz) * p.M * (long)p.N;
 #pragma unroll
         for (int i = 0; i < RM; ++i)
 #pragma unroll
@@ -285,6 +300,9 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, const f32x16 
 }
 
 template <int BM, int BN, bool TA, bool TB, bool CONV, bool SEGB, int NBUF>
+#ifndef GEMM_ABL
+#define GEMM_ABL 0  // benchmark-only ablations (wrong results): 1 no global loads, 2 1/4 LDS reads, 4 no barriers
+#endif
 #ifndef GEMM_F32_MINB
 #define GEMM_F32_MINB 3
 #endif
@@ -296,7 +314,8 @@ __global__ __launch_bounds__(256, GEMM_F32_MINB) void gemm_f32_kernel(GemmParams
     static_assert(RM >= 1 && RN >= 1, "wave tile >= 32x32");
     __shared__ __attribute__((aligned(16))) float smem[NBUF * (A_FL + B_FL)];
 
-    int zz = blockIdx.z;
+    const TileId tid = xcd_tile();
+    int zz = tid.z;
     int split = 0;
     if (p.splits > 1) {
         split = zz % p.splits;
@@ -306,8 +325,8 @@ __global__ __launch_bounds__(256, GEMM_F32_MINB) void gemm_f32_kernel(GemmParams
     const float* A = p.A + z1 * p.sA1 + z0 * p.sA0;
     const float* B = p.B + z1 * p.sB1 + z0 * p.sB0;
 
-    const int m0 = blockIdx.y * BM;
-    const int n0 = blockIdx.x * BN;
+    const int m0 = tid.y * BM;
+    const int n0 = tid.x * BN;
     const int kbeg = split * p.kchunk;
     const int kend = min(p.K, kbeg + p.kchunk);
 
@@ -369,13 +388,13 @@ __global__ __launch_bounds__(256, GEMM_F32_MINB) void gemm_f32_kernel(GemmParams
     }
     for (int k0 = kbeg; k0 < kend; k0 += BK) {
         const bool more = k0 + BK < kend;
-        if (NBUF == 1) {
+        if (NBUF == 1 && !(GEMM_ABL & 4)) {
             __syncthreads();
             store_stage<BM, AKC>(smem, ra);
             store_stage<BN, BKC>(smem + A_FL, rb);
             __syncthreads();
         }
-        if (more) {
+        if (more && !(GEMM_ABL & 1)) {
             stageA(k0 + BK);
             stageB(k0 + BK);
         }
@@ -384,10 +403,11 @@ __global__ __launch_bounds__(256, GEMM_F32_MINB) void gemm_f32_kernel(GemmParams
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             f32x4 af[RM], bf[RN];
+            const int qq = (GEMM_ABL & 2) ? 0 : q;  // benchmark ablation: one fragment read per K-step
 #pragma unroll
-            for (int i = 0; i < RM; ++i) af[i] = read_frag<BM, AKC>(As, wm * WTM + i * 32 + l32, h, q);
+            for (int i = 0; i < RM; ++i) af[i] = read_frag<BM, AKC>(As, wm * WTM + i * 32 + l32, h, qq);
 #pragma unroll
-            for (int j = 0; j < RN; ++j) bf[j] = read_frag<BN, BKC>(Bs, wn * WTN + j * 32 + l32, h, q);
+            for (int j = 0; j < RN; ++j) bf[j] = read_frag<BN, BKC>(Bs, wn * WTN + j * 32 + l32, h, qq);
 #pragma unroll
             for (int e = 0; e < 4; ++e)
 #pragma unroll
@@ -406,7 +426,7 @@ __global__ __launch_bounds__(256, GEMM_F32_MINB) void gemm_f32_kernel(GemmParams
         }
     }
 
-    gemm_epilogue<RM, RN>(p, acc, z1, z0, m0 + wm * WTM, n0 + wn * WTN, h, l32, m0 + BM <= p.M && n0 + BN <= p.N);
+    gemm_epilogue<RM, RN>(p, acc, z1, z0, m0 + wm * WTM, n0 + wn * WTN, h, l32, m0 + BM <= p.M && n0 + BN <= p.N, tid.z);
 }
 
 // ============================================================================================
@@ -607,7 +627,8 @@ __global__ __launch_bounds__(256, 3) void gemm_x6_kernel(GemmParams p) {
     static_assert(RM >= 1 && RN >= 1, "wave tile >= 32x32");
     __shared__ __attribute__((aligned(16))) __bf16 smem[NBUF * STAGE];
 
-    int zz = blockIdx.z;
+    const TileId tid = xcd_tile();
+    int zz = tid.z;
     int split = 0;
     if (p.splits > 1) {
         split = zz % p.splits;
@@ -616,8 +637,8 @@ __global__ __launch_bounds__(256, 3) void gemm_x6_kernel(GemmParams p) {
     const int z1 = zz / p.zdiv, z0 = zz % p.zdiv;
     const float* A = p.A + z1 * p.sA1 + z0 * p.sA0;
     const float* B = p.B + z1 * p.sB1 + z0 * p.sB0;
-    const int m0 = blockIdx.y * BM;
-    const int n0 = blockIdx.x * BN;
+    const int m0 = tid.y * BM;
+    const int n0 = tid.x * BN;
     const int kbeg = split * p.kchunk;
     const int kend = min(p.K, kbeg + p.kchunk);
     const int lane = threadIdx.x & 63;
@@ -748,7 +769,7 @@ __global__ __launch_bounds__(256, 3) void gemm_x6_kernel(GemmParams p) {
     }
 
 
-    gemm_epilogue<RM, RN>(p, acc, z1, z0, m0 + wm * WTM, n0 + wn * WTN, h, l32, m0 + BM <= p.M && n0 + BN <= p.N);
+    gemm_epilogue<RM, RN>(p, acc, z1, z0, m0 + wm * WTM, n0 + wn * WTN, h, l32, m0 + BM <= p.M && n0 + BN <= p.N, tid.z);
 }
 
 template <int BM, int BN, int BKX, int NB>
@@ -786,6 +807,165 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmParams p) {
     }
 }
 
+// ============================================================================================
+// fp32 GEMM with LDS-DMA staging ("glds"): global_load_lds_dwordx4 moves each K-step of both
+// operands straight into LDS (no VGPR staging, no ds_write), two LDS stages, ONE barrier per K-step:
+//   wait(stage s landed) + barrier -> issue DMA of stage s+1 into the other buffer -> MFMAs on stage s
+// so the next stage's loads are in flight for the whole compute phase.  LDS-DMA writes are
+// lane-linear (1 KiB per wave-instruction), so:
+//   k-contiguous operand: LDS [row][32] (128-B rows) with the 16-B chunk c of row r stored in slot
+//       c ^ ((r >> 1) & 7) -- the swizzle is applied to the per-lane SOURCE address; fragment reads
+//       (16 lanes = 16 consecutive rows, same chunk) hit 16 distinct 4-bank groups: conflict-free
+//   row-contiguous operand: LDS [k][ROWS] linear; 4-B fragment reads by consecutive rows.
+// Lanes outside the operand (M/N edge rows, K tail, conv padding rows) read a zero page, so no
+// predicates reach LDS.  Preconditions (checked by the dispatcher): 16-B aligned operands, leading
+// dimensions and batch strides multiples of 4, K % 4 == 0 for k-contiguous operands.
+// ============================================================================================
+__device__ __attribute__((aligned(16))) float g_zero16[4];
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+constexpr int GBK = 32;
+
+__device__ __forceinline__ int glds_swz(int row) { return (row >> 1) & 7; }
+
+// Issue the LDS-DMA of one GBK-deep stage of an operand tile (ROWS rows) into `dst` (wave-uniform).
+//   KC = true : element (row, k) at src[row*ld + k]     (MODE 1: conv-A row shift, MODE 2: segmented)
+//   KC = false: element (row, k) at src[k*ld + row]
+template <int ROWS, bool KC, int MODE>
+__device__ __forceinline__ void glds_stage(float* dst, const float* __restrict__ src, long ld, int row0, int nrows,
+                                           int k0, int kend, int segK, int pad, int Mvalid, long sseg, int w,
+                                           int lane) {
+    constexpr int NI = ROWS / 32;  // wave-instructions per wave (ROWS * 128 B / 1 KiB / 4 waves)
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+        const int ci = i * 4 + w;  // 1-KiB piece of the stage image
+        const float* g = g_zero16;
+        if (KC) {
+            const int row = ci * 8 + (lane >> 3);
+            const int c = (lane & 7) ^ glds_swz(row);
+            const int gr = row0 + row, gk = k0 + c * 4;
+            if (gr < nrows && gk < kend) {
+                if (MODE == 1) {
+                    const int seg = gk / segK;
+                    const int srow = gr + seg - pad;
+                    if (srow >= 0 && srow < Mvalid) g = src + (long)srow * ld + (gk - seg * segK);
+                } else if (MODE == 2) {
+                    const int seg = gk / segK;
+                    g = src + (long)gr * ld + seg * sseg + (gk - seg * segK);
+                } else {
+                    g = src + (long)gr * ld + gk;
+                }
+            }
+        } else {
+            const int f = ci * 256 + lane * 4;
+            const int k = f / ROWS, m = f % ROWS;
+            const int gk = k0 + k, gm = row0 + m;
+            if (gk < kend && gm < nrows) g = src + (long)gk * ld + gm;
+        }
+        __builtin_amdgcn_global_load_lds(g, (lds_ptr_t)(dst + ci * 256), 16, 0, 0);
+    }
+}
+
+template <int ROWS, bool KC>
+__device__ __forceinline__ f32x4 glds_frag(const float* __restrict__ lds, int row, int h, int q) {
+    if (KC) return *reinterpret_cast<const f32x4*>(lds + row * GBK + (((h * 4 + q) ^ glds_swz(row)) * 4));
+    f32x4 v;
+    const int k = h * 16 + q * 4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = lds[(k + e) * ROWS + row];
+    return v;
+}
+
+template <int BM, int BN, bool TA, bool TB, bool CONV, bool SEGB>
+__global__ __launch_bounds__(256, 2) void gemm_glds_kernel(GemmParams p) {
+    constexpr int WTM = BM / 2, WTN = BN / 2;
+    constexpr int RM = WTM / 32, RN = WTN / 32;
+    constexpr bool AKC = !TA, BKC = TB;
+    constexpr int STAGE = (BM + BN) * GBK;  // floats per LDS stage
+    __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+
+    const TileId tid = xcd_tile();
+    int zz = tid.z;
+    int split = 0;
+    if (p.splits > 1) {
+        split = zz % p.splits;
+        zz /= p.splits;
+    }
+    const int z1 = zz / p.zdiv, z0 = zz % p.zdiv;
+    const float* A = p.A + z1 * p.sA1 + z0 * p.sA0;
+    const float* B = p.B + z1 * p.sB1 + z0 * p.sB0;
+    const int m0 = tid.y * BM;
+    const int n0 = tid.x * BN;
+    const int kbeg = split * p.kchunk;
+    const int kend = min(p.K, kbeg + p.kchunk);
+    const int nst = (kend - kbeg + GBK - 1) / GBK;
+
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wid >> 1, wn = wid & 1;
+    const int h = lane >> 5, l32 = lane & 31;
+
+    f32x16 acc[RM][RN];
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    auto issue = [&](int s) {
+        float* st = smem + (s & 1) * STAGE;
+        const int k = kbeg + s * GBK;
+        glds_stage<BM, AKC, CONV ? 1 : 0>(st, A, p.lda, m0, p.M, k, kend, p.segK, p.pad, p.Mvalid, 0, wid, lane);
+        glds_stage<BN, BKC, SEGB ? 2 : 0>(st + BM * GBK, B, p.ldb, n0, p.N, k, kend, p.segK, 0, 0, p.sBseg, wid,
+                                          lane);
+    };
+    auto compute = [&](int s) {
+        const float* As = smem + (s & 1) * STAGE;
+        const float* Bs = As + BM * GBK;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            f32x4 af[RM], bf[RN];
+#pragma unroll
+            for (int i = 0; i < RM; ++i) af[i] = glds_frag<BM, AKC>(As, wm * WTM + i * 32 + l32, h, q);
+#pragma unroll
+            for (int j = 0; j < RN; ++j) bf[j] = glds_frag<BN, BKC>(Bs, wn * WTN + j * 32 + l32, h, q);
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int i = 0; i < RM; ++i)
+#pragma unroll
+                    for (int j = 0; j < RN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][e], bf[j][e], acc[i][j], 0, 0, 0);
+        }
+    };
+
+    if (nst > 0) issue(0);
+    for (int s = 0; s < nst; ++s) {
+        __syncthreads();  // s_waitcnt vmcnt(0): stage s landed; all waves are done reading stage s-1's buffer
+        if (s + 1 < nst) issue(s + 1);
+        compute(s);
+    }
+    gemm_epilogue<RM, RN>(p, acc, z1, z0, m0 + wm * WTM, n0 + wn * WTN, h, l32, m0 + BM <= p.M && n0 + BN <= p.N,
+                          tid.z);
+}
+
+template <int BM, int BN>
+void launch_glds(const GemmParams& p, dim3 grid, hipStream_t st) {
+#define GK(TA_, TB_, CV_, SB_) gemm_glds_kernel<BM, BN, TA_, TB_, CV_, SB_>
+    if (p.segK > 0) {
+        if (p.segB) hipLaunchKernelGGL((GK(false, true, true, true)), grid, dim3(256), 0, st, p);
+        else hipLaunchKernelGGL((GK(false, false, true, false)), grid, dim3(256), 0, st, p);
+        return;
+    }
+    if (!p.ta && !p.tb) hipLaunchKernelGGL((GK(false, false, false, false)), grid, dim3(256), 0, st, p);
+    else if (!p.ta && p.tb) hipLaunchKernelGGL((GK(false, true, false, false)), grid, dim3(256), 0, st, p);
+    else if (p.ta && !p.tb) hipLaunchKernelGGL((GK(true, false, false, false)), grid, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((GK(true, true, false, false)), grid, dim3(256), 0, st, p);
+#undef GK
+}
+
 template <int BM, int BN, int NBUF>
 void launch_tile(const GemmParams& p, dim3 grid, hipStream_t st) {
     if (p.segK > 0) {
@@ -808,7 +988,7 @@ void launch_tile(const GemmParams& p, dim3 grid, hipStream_t st) {
 bool aligned16(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; }
 
 int g_force_tile = -1;  // test/bench override: 0=128x128 1=128x64 2=64x128 3=64x64
-int g_nbuf = 1;
+int g_nbuf = 3;  // 3 = LDS-DMA kernel where its preconditions hold (else the register-staged one)
 int g_mode = 0;  // 0 = exact fp32 MFMA, 1 = x6 (fp32-accurate bf16 split)
 
 }  // namespace
@@ -830,20 +1010,24 @@ void gemm_init(GemmParams& p) {
     p.mode = g_mode;
 }
 
-// Tile choice: a CU finishes its share of tiles at ~ceil(tiles / 256) x per-tile time, and a
-// tile's time scales with its area over its relative MFMA efficiency (smaller tiles re-read more
-// operand bytes per MFMA and pay the prologue/epilogue more often).
-static int choose_tile(long M, long N, long Z, long K) {
+// Tile choice: a CU runs `conc` tiles at once (LDS/VGPR-limited residency), so a launch takes
+// ceil(tiles / (256 conc)) rounds of conc x area / eff, eff being the tile's relative MFMA
+// efficiency (measured with tools/gemm_bench on the SUTA shapes; smaller tiles re-read more operand
+// bytes per MFMA and pay the prologue/epilogue more often).
+static int choose_tile(long M, long N, long Z, long K, int mode) {
     struct Cand {
-        int bm, bn;
+        int bm, bn, conc;
         double eff;
-    } cands[4] = {{128, 128, 1.0}, {128, 64, 0.9}, {64, 128, 0.9}, {64, 64, 0.75}};
+    };
+    static const Cand glds[4] = {{128, 128, 2, 1.0}, {128, 64, 3, 0.95}, {64, 128, 3, 0.94}, {64, 64, 4, 0.88}};
+    static const Cand x6[4] = {{128, 128, 1, 1.0}, {128, 64, 1, 0.9}, {64, 128, 1, 0.9}, {64, 64, 1, 0.75}};
+    const Cand* cands = mode == 1 ? x6 : glds;
     int best = 0;
     double bt = 1e300;
     for (int c = 0; c < 4; ++c) {
         const long tiles = ((M + cands[c].bm - 1) / cands[c].bm) * ((N + cands[c].bn - 1) / cands[c].bn) * Z;
-        const double per_cu = std::ceil((double)tiles / 256.0);
-        const double t = per_cu * cands[c].bm * cands[c].bn / cands[c].eff;
+        const double rounds = std::ceil((double)tiles / (256.0 * cands[c].conc));
+        const double t = rounds * cands[c].conc * cands[c].bm * cands[c].bn / cands[c].eff;
         if (t < bt * 0.999) {
             bt = t;
             best = c;
@@ -864,7 +1048,7 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
     p.va = vec_ok(p.A, p.lda, p.sA0, p.sA1) && (p.segK == 0 || p.segK % 4 == 0);
     p.vb = vec_ok(p.B, p.ldb, p.sB0, p.sB1) && (!p.segB || (p.sBseg % 4 == 0 && p.segK % 4 == 0));
 
-    const int tile = g_force_tile >= 0 ? g_force_tile : choose_tile(p.M, p.N, p.Z, p.K);
+    const int tile = g_force_tile >= 0 ? g_force_tile : choose_tile(p.M, p.N, p.Z, p.K, p.mode);
     const int BM = (tile == 0 || tile == 1) ? 128 : 64;
     const int BN = (tile == 0 || tile == 2) ? 128 : 64;
     const int gx = (p.N + BN - 1) / BN, gy = (p.M + BM - 1) / BM;
@@ -895,7 +1079,12 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
             else if (tile == 2) launch_x6<64, 128, 32, 1>(p, grid, st);
             else launch_x6<64, 64, 32, 1>(p, grid, st);
         }
-    } else if (g_nbuf == 1) {
+    } else if (g_nbuf == 3 && p.va && p.vb && (p.ta || p.K % 4 == 0) && (!p.tb || p.K % 4 == 0)) {
+        if (tile == 0) launch_glds<128, 128>(p, grid, st);
+        else if (tile == 1) launch_glds<128, 64>(p, grid, st);
+        else if (tile == 2) launch_glds<64, 128>(p, grid, st);
+        else launch_glds<64, 64>(p, grid, st);
+    } else if (g_nbuf == 1 || g_nbuf == 3) {
         if (tile == 0) launch_tile<128, 128, 1>(p, grid, st);
         else if (tile == 1) launch_tile<128, 64, 1>(p, grid, st);
         else if (tile == 2) launch_tile<64, 128, 1>(p, grid, st);

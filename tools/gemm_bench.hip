@@ -56,7 +56,7 @@ struct Shape { const char* name; int M, N, K, Z, zdiv; int ta, tb; long lda, ldb
                long Asz, Bsz, Csz; int segK, pad, Mvalid; double flops_scale; };
 
 int main(int argc, char** argv) {
-    const int Bu = 16, T = 399, Tp = 400, H = 768, F = 3072, L1 = 12799, L0 = 25599, NH = 12;
+    const int Bu = 64, T = 399, Tp = 400, H = 768, F = 3072, L1 = 12799, L0 = 25599, NH = 12;
     std::vector<Shape> S = {
         {"ffn1_fwd NT", Bu*T, F, H, 1, 1, 0, 1, H, H, F, 0,0,0,0,0,0, (long)Bu*T*H, (long)F*H, (long)Bu*T*F, 0,0,0, 1},
         {"qkv_fwd NT", Bu*T, 3*H, H, 1, 1, 0, 1, H, H, 3*H, 0,0,0,0,0,0, (long)Bu*T*H, 3L*H*H, (long)Bu*T*3*H, 0,0,0, 1},
@@ -89,8 +89,12 @@ int main(int argc, char** argv) {
     hipLaunchKernelGGL(fill, dim3((maxB + 255) / 256), dim3(256), 0, 0, B, maxB, 2u);
     hipStream_t st; CK(hipStreamCreate(&st));
     hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-    const int variants[][2] = {{-1, 2}, {-1, 1}, {0, 2}, {1, 2}, {2, 2}, {3, 2}};
-    const char* vname[] = {"auto/2buf", "auto/1buf", "128x128/2", "128x64/2", "64x128/2", "64x64/2"};
+    const int variants[][2] = {{-1, 2}, {-1, 1}, {0, 2}, {1, 2}, {2, 2}, {3, 2},
+                               {-1, 3}, {0, 3}, {1, 3}, {2, 3}, {3, 3}, {0, 1}, {1, 1}, {2, 1}, {3, 1}};
+    const char* vname[] = {"auto/2buf", "auto/1buf", "128x128/2", "128x64/2", "64x128/2", "64x64/2",
+                           "auto/glds", "128x128/g", "128x64/g", "64x128/g", "64x64/g",
+                           "128x128/1", "128x64/1", "64x128/1", "64x64/1"};
+    const int NV = 15;
     bool check = argc < 2 || atoi(argv[1]) != 0;
     int only_v = argc >= 3 ? atoi(argv[2]) : -1;
     int only_s = argc >= 4 ? atoi(argv[3]) : -1;
@@ -124,7 +128,7 @@ int main(int argc, char** argv) {
             long n = (long)s.M * s.N * s.Z;
             hipLaunchKernelGGL(ref_gemm, dim3((n + 255) / 256), dim3(256), 0, st, p, ref);
         }
-        for (int v = 0; v < 6; ++v) {
+        for (int v = 0; v < NV; ++v) {
             if (only_v >= 0 && v != only_v) continue;
             gemm_set_variant(variants[v][0], variants[v][1]);
             CK(hipMemsetAsync(C, 0, s.Csz * 4, st));

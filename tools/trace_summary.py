@@ -23,8 +23,8 @@ def main():
     for n, t, gx, gy, gz, v in rows(sys.argv[1]):
         base = n.replace('void ', '').replace('(anonymous namespace)::', '')
         fam[base.split('(')[0].split('<')[0]] += t
-        if 'gemm_f32_kernel' in n or 'gemm_x6_kernel' in n:
-            tmpl = n[n.find('<') + 1:n.find('>')]
+        if 'gemm_f32_kernel' in n or 'gemm_x6_kernel' in n or 'gemm_glds_kernel' in n:
+            tmpl = base.split("<")[0][5:9] + ":" + n[n.find('<') + 1:n.find('>')]
             k = (tmpl, gx // 256, gy, gz)
             g[k][0] += 1
             g[k][1] += t
