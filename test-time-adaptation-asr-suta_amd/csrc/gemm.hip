@@ -825,65 +825,89 @@ __device__ __attribute__((aligned(16))) float g_zero16[4];
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-constexpr int GBK = 32;
+// k-contiguous stage image: rows of BKS floats, CPR = BKS/4 16-B chunks per row, RPB = rows per
+// 256-B bank row; chunk c of row r lives in slot c ^ ((r / RPB) % CPR).
+template <int BKS>
+__device__ __forceinline__ int glds_swz(int row) {
+    constexpr int CPR = BKS / 4, RPB = 64 / BKS;
+    return (row / RPB) % CPR;
+}
 
-__device__ __forceinline__ int glds_swz(int row) { return (row >> 1) & 7; }
-
-// Issue the LDS-DMA of one GBK-deep stage of an operand tile (ROWS rows) into `dst` (wave-uniform).
+// Issue the LDS-DMA of one BKS-deep stage of an operand tile (ROWS rows) into `dst` (wave-uniform).
 //   KC = true : element (row, k) at src[row*ld + k]     (MODE 1: conv-A row shift, MODE 2: segmented)
 //   KC = false: element (row, k) at src[k*ld + row]
-template <int ROWS, bool KC, int MODE>
+// dummy: load the zero page (keeps the per-wave DMA count uniform past the last K-step).
+template <int ROWS, int BKS, bool KC, int MODE>
 __device__ __forceinline__ void glds_stage(float* dst, const float* __restrict__ src, long ld, int row0, int nrows,
                                            int k0, int kend, int segK, int pad, int Mvalid, long sseg, int w,
-                                           int lane) {
-    constexpr int NI = ROWS / 32;  // wave-instructions per wave (ROWS * 128 B / 1 KiB / 4 waves)
+                                           int lane, bool dummy) {
+    constexpr int NI = ROWS * BKS / 1024;  // wave-instructions per wave (ROWS * BKS * 4 B / 1 KiB / 4 waves)
+    static_assert(NI >= 1, "stage too small for 4 waves");
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
         const int ci = i * 4 + w;  // 1-KiB piece of the stage image
         const float* g = g_zero16;
-        if (KC) {
-            const int row = ci * 8 + (lane >> 3);
-            const int c = (lane & 7) ^ glds_swz(row);
-            const int gr = row0 + row, gk = k0 + c * 4;
-            if (gr < nrows && gk < kend) {
-                if (MODE == 1) {
-                    const int seg = gk / segK;
-                    const int srow = gr + seg - pad;
-                    if (srow >= 0 && srow < Mvalid) g = src + (long)srow * ld + (gk - seg * segK);
-                } else if (MODE == 2) {
-                    const int seg = gk / segK;
-                    g = src + (long)gr * ld + seg * sseg + (gk - seg * segK);
-                } else {
-                    g = src + (long)gr * ld + gk;
+        if (!dummy) {
+            if (KC) {
+                constexpr int CPR = BKS / 4;
+                const int row = ci * (256 / BKS) + lane / CPR;
+                const int c = (lane % CPR) ^ glds_swz<BKS>(row);
+                const int gr = row0 + row, gk = k0 + c * 4;
+                if (gr < nrows && gk < kend) {
+                    if (MODE == 1) {
+                        const int seg = gk / segK;
+                        const int srow = gr + seg - pad;
+                        if (srow >= 0 && srow < Mvalid) g = src + (long)srow * ld + (gk - seg * segK);
+                    } else if (MODE == 2) {
+                        const int seg = gk / segK;
+                        g = src + (long)gr * ld + seg * sseg + (gk - seg * segK);
+                    } else {
+                        g = src + (long)gr * ld + gk;
+                    }
                 }
+            } else {
+                const int f = ci * 256 + lane * 4;
+                const int k = f / ROWS, m = f % ROWS;
+                const int gk = k0 + k, gm = row0 + m;
+                if (gk < kend && gm < nrows) g = src + (long)gk * ld + gm;
             }
-        } else {
-            const int f = ci * 256 + lane * 4;
-            const int k = f / ROWS, m = f % ROWS;
-            const int gk = k0 + k, gm = row0 + m;
-            if (gk < kend && gm < nrows) g = src + (long)gk * ld + gm;
         }
         __builtin_amdgcn_global_load_lds(g, (lds_ptr_t)(dst + ci * 256), 16, 0, 0);
     }
 }
 
-template <int ROWS, bool KC>
+// fragment of 4 consecutive MFMA k-steps: tile k = h * BKS/2 + 4q + e  (q < BKS/8)
+template <int ROWS, int BKS, bool KC>
 __device__ __forceinline__ f32x4 glds_frag(const float* __restrict__ lds, int row, int h, int q) {
-    if (KC) return *reinterpret_cast<const f32x4*>(lds + row * GBK + (((h * 4 + q) ^ glds_swz(row)) * 4));
+    if (KC) {
+        const int c = h * (BKS / 8) + q;
+        return *reinterpret_cast<const f32x4*>(lds + row * BKS + ((c ^ glds_swz<BKS>(row)) * 4));
+    }
     f32x4 v;
-    const int k = h * 16 + q * 4;
+    const int k = h * (BKS / 2) + q * 4;
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[e] = lds[(k + e) * ROWS + row];
     return v;
 }
 
-template <int BM, int BN, bool TA, bool TB, bool CONV, bool SEGB>
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    static_assert(N >= 0 && N < 64, "vmcnt");
+    // s_waitcnt: vmcnt[3:0] | expcnt[6:4] (7 = no wait) | lgkmcnt[11:8] (15 = no wait) | vmcnt[5:4] << 14
+    __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+// BKS-deep K-steps through NS LDS stages: NS-1 stages of DMA in flight while a stage is consumed;
+// one barrier per K-step, preceded by a counted vmcnt that retires exactly the stage about to be
+// read (never vmcnt(0) inside the loop).
+template <int BM, int BN, bool TA, bool TB, bool CONV, bool SEGB, int BKS, int NS>
 __global__ __launch_bounds__(256, 2) void gemm_glds_kernel(GemmParams p) {
     constexpr int WTM = BM / 2, WTN = BN / 2;
     constexpr int RM = WTM / 32, RN = WTN / 32;
     constexpr bool AKC = !TA, BKC = TB;
-    constexpr int STAGE = (BM + BN) * GBK;  // floats per LDS stage
-    __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+    constexpr int STAGE = (BM + BN) * BKS;  // floats per LDS stage
+    constexpr int NPW = (BM + BN) * BKS / 1024;  // DMA instructions per wave per stage
+    __shared__ __attribute__((aligned(16))) float smem[NS * STAGE];
 
     const TileId tid = xcd_tile();
     int zz = tid.z;
@@ -899,7 +923,7 @@ __global__ __launch_bounds__(256, 2) void gemm_glds_kernel(GemmParams p) {
     const int n0 = tid.x * BN;
     const int kbeg = split * p.kchunk;
     const int kend = min(p.K, kbeg + p.kchunk);
-    const int nst = (kend - kbeg + GBK - 1) / GBK;
+    const int nst = (kend - kbeg + BKS - 1) / BKS;
 
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -915,22 +939,24 @@ __global__ __launch_bounds__(256, 2) void gemm_glds_kernel(GemmParams p) {
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
     auto issue = [&](int s) {
-        float* st = smem + (s & 1) * STAGE;
-        const int k = kbeg + s * GBK;
-        glds_stage<BM, AKC, CONV ? 1 : 0>(st, A, p.lda, m0, p.M, k, kend, p.segK, p.pad, p.Mvalid, 0, wid, lane);
-        glds_stage<BN, BKC, SEGB ? 2 : 0>(st + BM * GBK, B, p.ldb, n0, p.N, k, kend, p.segK, 0, 0, p.sBseg, wid,
-                                          lane);
+        float* st = smem + (s % NS) * STAGE;
+        const int k = kbeg + s * BKS;
+        const bool dummy = s >= nst;
+        glds_stage<BM, BKS, AKC, CONV ? 1 : 0>(st, A, p.lda, m0, p.M, k, kend, p.segK, p.pad, p.Mvalid, 0, wid,
+                                                lane, dummy);
+        glds_stage<BN, BKS, BKC, SEGB ? 2 : 0>(st + BM * BKS, B, p.ldb, n0, p.N, k, kend, p.segK, 0, 0, p.sBseg,
+                                                wid, lane, dummy);
     };
     auto compute = [&](int s) {
-        const float* As = smem + (s & 1) * STAGE;
-        const float* Bs = As + BM * GBK;
+        const float* As = smem + (s % NS) * STAGE;
+        const float* Bs = As + BM * BKS;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < BKS / 8; ++q) {
             f32x4 af[RM], bf[RN];
 #pragma unroll
-            for (int i = 0; i < RM; ++i) af[i] = glds_frag<BM, AKC>(As, wm * WTM + i * 32 + l32, h, q);
+            for (int i = 0; i < RM; ++i) af[i] = glds_frag<BM, BKS, AKC>(As, wm * WTM + i * 32 + l32, h, q);
 #pragma unroll
-            for (int j = 0; j < RN; ++j) bf[j] = glds_frag<BN, BKC>(Bs, wn * WTN + j * 32 + l32, h, q);
+            for (int j = 0; j < RN; ++j) bf[j] = glds_frag<BN, BKS, BKC>(Bs, wn * WTN + j * 32 + l32, h, q);
 #pragma unroll
             for (int e = 0; e < 4; ++e)
 #pragma unroll
@@ -941,19 +967,22 @@ __global__ __launch_bounds__(256, 2) void gemm_glds_kernel(GemmParams p) {
         }
     };
 
-    if (nst > 0) issue(0);
+#pragma unroll
+    for (int s = 0; s < NS - 1; ++s) issue(s);
     for (int s = 0; s < nst; ++s) {
-        __syncthreads();  // s_waitcnt vmcnt(0): stage s landed; all waves are done reading stage s-1's buffer
-        if (s + 1 < nst) issue(s + 1);
+        wait_vm<(NS - 2) * NPW>();  // stage s landed (this wave's share); later stages may be in flight
+        __builtin_amdgcn_s_barrier();  // every wave's share landed; stage s-1's buffer is free
+        issue(s + NS - 1);
         compute(s);
     }
+    wait_vm<0>();  // no LDS-DMA may outlive the block
     gemm_epilogue<RM, RN>(p, acc, z1, z0, m0 + wm * WTM, n0 + wn * WTN, h, l32, m0 + BM <= p.M && n0 + BN <= p.N,
                           tid.z);
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int BKS, int NS>
 void launch_glds(const GemmParams& p, dim3 grid, hipStream_t st) {
-#define GK(TA_, TB_, CV_, SB_) gemm_glds_kernel<BM, BN, TA_, TB_, CV_, SB_>
+#define GK(TA_, TB_, CV_, SB_) gemm_glds_kernel<BM, BN, TA_, TB_, CV_, SB_, BKS, NS>
     if (p.segK > 0) {
         if (p.segB) hipLaunchKernelGGL((GK(false, true, true, true)), grid, dim3(256), 0, st, p);
         else hipLaunchKernelGGL((GK(false, false, true, false)), grid, dim3(256), 0, st, p);
@@ -964,6 +993,14 @@ void launch_glds(const GemmParams& p, dim3 grid, hipStream_t st) {
     else if (p.ta && !p.tb) hipLaunchKernelGGL((GK(true, false, false, false)), grid, dim3(256), 0, st, p);
     else hipLaunchKernelGGL((GK(true, true, false, false)), grid, dim3(256), 0, st, p);
 #undef GK
+}
+
+template <int BKS, int NS>
+void launch_glds_tile(int tile, const GemmParams& p, dim3 grid, hipStream_t st) {
+    if (tile == 0) launch_glds<128, 128, BKS, NS>(p, grid, st);
+    else if (tile == 1) launch_glds<128, 64, BKS, NS>(p, grid, st);
+    else if (tile == 2) launch_glds<64, 128, BKS, NS>(p, grid, st);
+    else launch_glds<64, 64, BKS, NS>(p, grid, st);
 }
 
 template <int BM, int BN, int NBUF>
@@ -1010,24 +1047,25 @@ void gemm_init(GemmParams& p) {
     p.mode = g_mode;
 }
 
-// Tile choice: a CU runs `conc` tiles at once (LDS/VGPR-limited residency), so a launch takes
-// ceil(tiles / (256 conc)) rounds of conc x area / eff, eff being the tile's relative MFMA
-// efficiency (measured with tools/gemm_bench on the SUTA shapes; smaller tiles re-read more operand
-// bytes per MFMA and pay the prologue/epilogue more often).
+// Tile choice: time ~ padded output area / eff, where eff is the tile's relative MFMA efficiency
+// (measured with tools/gemm_bench on the SUTA shapes at 64 utterances: 128x128 wins every large
+// GEMM despite its coarser tail; smaller tiles win where M or N is below ~128, e.g. attention and
+// the 48-channel positional-conv groups); a grid with fewer tiles than CUs is charged as one full
+// round of its tiles.
 static int choose_tile(long M, long N, long Z, long K, int mode) {
     struct Cand {
-        int bm, bn, conc;
+        int bm, bn;
         double eff;
     };
-    static const Cand glds[4] = {{128, 128, 2, 1.0}, {128, 64, 3, 0.95}, {64, 128, 3, 0.94}, {64, 64, 4, 0.88}};
-    static const Cand x6[4] = {{128, 128, 1, 1.0}, {128, 64, 1, 0.9}, {64, 128, 1, 0.9}, {64, 64, 1, 0.75}};
+    static const Cand glds[4] = {{128, 128, 1.0}, {128, 64, 0.93}, {64, 128, 0.92}, {64, 64, 0.85}};
+    static const Cand x6[4] = {{128, 128, 1.0}, {128, 64, 0.9}, {64, 128, 0.9}, {64, 64, 0.75}};
     const Cand* cands = mode == 1 ? x6 : glds;
     int best = 0;
     double bt = 1e300;
     for (int c = 0; c < 4; ++c) {
         const long tiles = ((M + cands[c].bm - 1) / cands[c].bm) * ((N + cands[c].bn - 1) / cands[c].bn) * Z;
-        const double rounds = std::ceil((double)tiles / (256.0 * cands[c].conc));
-        const double t = rounds * cands[c].conc * cands[c].bm * cands[c].bn / cands[c].eff;
+        const double area = (double)cands[c].bm * cands[c].bn;
+        const double t = std::max((double)tiles, 256.0) * area / cands[c].eff;
         if (t < bt * 0.999) {
             bt = t;
             best = c;
@@ -1079,12 +1117,13 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
             else if (tile == 2) launch_x6<64, 128, 32, 1>(p, grid, st);
             else launch_x6<64, 64, 32, 1>(p, grid, st);
         }
-    } else if (g_nbuf == 3 && p.va && p.vb && (p.ta || p.K % 4 == 0) && (!p.tb || p.K % 4 == 0)) {
-        if (tile == 0) launch_glds<128, 128>(p, grid, st);
-        else if (tile == 1) launch_glds<128, 64>(p, grid, st);
-        else if (tile == 2) launch_glds<64, 128>(p, grid, st);
-        else launch_glds<64, 64>(p, grid, st);
-    } else if (g_nbuf == 1 || g_nbuf == 3) {
+    } else if (g_nbuf >= 3 && p.va && p.vb && (p.ta || p.K % 4 == 0) && (!p.tb || p.K % 4 == 0)) {
+        // LDS-DMA variants: 3 = BK32 x 2 stages, 4 = BK16 x 4, 5 = BK16 x 3, 6 = BK32 x 3
+        if (g_nbuf == 4) launch_glds_tile<16, 4>(tile, p, grid, st);
+        else if (g_nbuf == 5) launch_glds_tile<16, 3>(tile, p, grid, st);
+        else if (g_nbuf == 6) launch_glds_tile<32, 3>(tile, p, grid, st);
+        else launch_glds_tile<32, 2>(tile, p, grid, st);
+    } else if (g_nbuf == 1 || g_nbuf >= 3) {
         if (tile == 0) launch_tile<128, 128, 1>(p, grid, st);
         else if (tile == 1) launch_tile<128, 64, 1>(p, grid, st);
         else if (tile == 2) launch_tile<64, 128, 1>(p, grid, st);
