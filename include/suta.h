@@ -15,6 +15,7 @@
  *   suta_adapt           the per-utterance loop: vanilla forward + `steps` x forward_and_adapt
  *                        with recorded checkpoints (main.py:327-398), minimal schedule
  *                        ((S+1) forwards + S backwards), batched over utterances
+ *   suta_adapt_varlen    the same over utterances of different lengths in one batch
  *   suta_loss_grad       softmax_entropy + mcc_loss (+ div_loss) and loss.backward() w.r.t. the
  *                        logits (main.py:26-60, 181-205): the fused loss kernel alone
  *   suta_get_param       model.state_dict()[name] of an adapted slot (main.py:139)
@@ -122,6 +123,18 @@ int32_t suta_adapt(suta_engine* e, const float* wav, int32_t wav_on_device, int3
                    int32_t batch, int64_t n_samples, int32_t steps, const suta_hparams* hp,
                    const int32_t* record_steps, int32_t n_record, float* logits_out,
                    int32_t logits_on_device, int32_t* ids_out, int64_t* frames_out);
+
+/* suta_adapt over a ragged batch: utterance b has n_samples[b] samples at wav + b*stride
+ * (stride >= max n_samples), and is adapted exactly as if it were run alone (the reference
+ * processes one utterance per forward_and_adapt, main.py:327-398; no padding enters any
+ * statistic, softmax or gradient).  frames_out receives `batch` frame counts T_b.  logits_out /
+ * ids_out use the layout of the longest utterance: [n_record][batch][Tmax][vocab] / [..][Tmax],
+ * Tmax = max T_b; rows t >= T_b of utterance b are padding. */
+int32_t suta_adapt_varlen(suta_engine* e, const float* wav, int32_t wav_on_device, int32_t normalize,
+                          int32_t batch, const int64_t* n_samples, int64_t stride, int32_t steps,
+                          const suta_hparams* hp, const int32_t* record_steps, int32_t n_record,
+                          float* logits_out, int32_t logits_on_device, int32_t* ids_out,
+                          int64_t* frames_out);
 
 /* The fused entropy+MCC loss-and-gradient kernel alone (softmax_entropy / mcc_loss / div_loss and
  * the loss assembly of main.py:26-60, 181-203) on `batch` host logit blocks of T x vocab.

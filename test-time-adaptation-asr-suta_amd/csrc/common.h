@@ -53,6 +53,7 @@ enum {
     EPI_DGELU = 16,
     EPI_ACCUM = 32,
     EPI_SMBWD = 64,  // softmax backward: v = alpha * aux(m,n) * (acc - rowv[m])  (dS from dP, P, delta)
+    EPI_ROWMASK = 128,  // ragged batch: rows >= zrows[z / zdiv] are stored as 0
 };
 
 struct GemmParams {
@@ -77,6 +78,10 @@ struct GemmParams {
     long ldc2, sC20, sC21;
     const float* rowv;  // per-row vector (EPI_SMBWD), batch strides as the others
     long sRow0, sRow1;
+    // ragged batch (per utterance z1 = z / zdiv): valid output rows (EPI_ROWMASK) and the conv-A
+    // Mvalid (rows outside [0, zmvalid[z1]) read as zero); null = uniform
+    const int* zrows;
+    const int* zmvalid;
     float alpha;
     int epi;
     // internal

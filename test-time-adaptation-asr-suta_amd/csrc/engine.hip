@@ -80,13 +80,15 @@ enum Fam { F_GEMM = 0, F_SOFTMAX = 1, F_NORM = 2, F_EW = 3, F_LOSS = 4, F_ADAM =
 struct DevBuf {
     float* p = nullptr;
     size_t bytes = 0;
-    void alloc(size_t b) {
-        if (b <= bytes) return;
+    // returns true when (re)allocated
+    bool alloc(size_t b) {
+        if (b <= bytes) return false;
         if (p) HIPCHK(hipFree(p));
         p = nullptr;
         bytes = 0;
         HIPCHK(hipMalloc(&p, b));
         bytes = b;
+        return true;
     }
     ~DevBuf() {
         if (p) (void)hipFree(p);
@@ -115,6 +117,11 @@ struct Plan {
     long N = 0;
     int Lc[SUTA_MAX_CONV];
     int T = 0, Tp = 0;
+    // ragged batch: utterance b has n[b] <= N samples, L0[b] conv0 frames and T[b] <= T frames
+    // (device copies); the layout (strides) stays that of the longest utterance, N
+    bool ragged = false;
+    int *len_n = nullptr, *len_L0 = nullptr, *len_T = nullptr;
+    std::vector<int> h_n, h_T;
     // forward
     float *xraw, *x;
     float *z[SUTA_MAX_CONV], *a[SUTA_MAX_CONV], *cxhat[SUTA_MAX_CONV], *crstd[SUTA_MAX_CONV];
@@ -222,11 +229,15 @@ struct suta_engine {
     }
 
     void build_plan(int B, long N);
+    void set_lengths(int B, const int64_t* ns);
+    const int* rN() const { return plan.ragged ? plan.len_n : nullptr; }
+    const int* rL0() const { return plan.ragged ? plan.len_L0 : nullptr; }
+    const int* rT() const { return plan.ragged ? plan.len_T : nullptr; }
     void forward(int B);
     void backward(int B, const suta_hparams& hp);
     void adam(int B, const suta_hparams& hp);
     void reset_slots(int B);
-    void stage_input(const float* wav, int on_dev, int norm, int B, long N);
+    void stage_input(const float* wav, int on_dev, int norm, int B, long N, long stride = 0);
 };
 
 suta_engine::~suta_engine() {
@@ -331,12 +342,44 @@ void suta_engine::build_plan(int B, long N) {
         pl.loss = ar.take<float>(B);
         pl.loss_scratch = ar.take<float>((size_t)B * T * 66 + 64);
         pl.ids = ar.take<int>((size_t)BT);
+        pl.len_n = ar.take<int>((size_t)B);
+        pl.len_L0 = ar.take<int>((size_t)B);
+        pl.len_T = ar.take<int>((size_t)B);
         pl.splitws_floats = 32L << 20;
         pl.splitws = ar.take<float>(pl.splitws_floats);
         pl.bytes = ar.off;
-        if (pass == 0) ws.alloc(ar.off + 256);
+        // a fresh workspace starts zeroed (on the engine stream, ordered before any use): the padding
+        // frames of ragged batches must hold finite values
+        if (pass == 0 && ws.alloc(ar.off + 256)) HIPCHK(hipMemsetAsync(ws.p, 0, ws.bytes, st));
     }
     plan = pl;
+}
+
+// Per-utterance lengths of a ragged batch (null: every utterance has the layout length plan.N).
+void suta_engine::set_lengths(int B, const int64_t* ns) {
+    Plan& pl = plan;
+    pl.ragged = false;
+    pl.h_n.assign(B, (int)pl.N);
+    pl.h_T.assign(B, pl.T);
+    if (!ns) return;
+    std::vector<int> l0(B);
+    for (int b = 0; b < B; ++b) {
+        if (ns[b] < 1 || ns[b] > pl.N) throw SutaError(SUTA_ERR_ARG, "n_samples[b] outside [1, layout length]");
+        long L = ns[b];
+        for (int i = 0; i < c.nconv; ++i) {
+            L = (L - c.K[i]) / c.S[i] + 1;
+            if (L < 1) throw SutaError(SUTA_ERR_ARG, "utterance too short for the conv feature encoder");
+            if (i == 0) l0[b] = (int)L;
+        }
+        pl.h_n[b] = (int)ns[b];
+        pl.h_T[b] = (int)L;
+        if (ns[b] != pl.N) pl.ragged = true;
+    }
+    if (!pl.ragged) return;
+    HIPCHK(hipMemcpyAsync(pl.len_n, pl.h_n.data(), B * sizeof(int), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(pl.len_L0, l0.data(), B * sizeof(int), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(pl.len_T, pl.h_T.data(), B * sizeof(int), hipMemcpyHostToDevice, st));
+    HIPCHK(hipStreamSynchronize(st));  // host vectors are pageable and reused
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -352,7 +395,7 @@ void suta_engine::forward(int B) {
         timed(F_NORM, [&] {
             launch_front_gn_fwd(pl.x, pl.N, P + o_cw[0], k.conv_bias ? P + o_cb[0] : nullptr, Pn, B, pl.Lc[0], k.C[0],
                                 k.K[0], k.S[0], P + o_cg[0], P + o_cbeta[0], pl.gn_mean, pl.gn_rstd, pl.a[0],
-                                pl.dpart, st);
+                                pl.dpart, rL0(), st);
         });
     } else {
         timed(F_EW, [&] {
@@ -438,6 +481,7 @@ void suta_engine::forward(int B) {
         g.segK = Cg;
         g.pad = k.posK / 2;
         g.Mvalid = T;
+        g.zmvalid = rT();  // zero padding at each utterance's own end
         g.M = T;
         g.N = Cg;
         g.K = k.posK * Cg;
@@ -523,7 +567,7 @@ void suta_engine::forward(int B) {
             g.alpha = scale;
             gemm(g);
         }
-        timed(F_SOFTMAX, [&] { launch_softmax_rows(lb.P, (long)B * NH * T, T, pl.Tp, st); });
+        timed(F_SOFTMAX, [&] { launch_softmax_rows(lb.P, (long)B * NH * T, T, pl.Tp, rT(), (long)NH * T, st); });
         {  // ctx = P V
             GemmParams g;
             gemm_init(g);
@@ -667,7 +711,8 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
     const long BT = (long)B * T;
     const float scale = 1.0f / std::sqrt((float)d);
     LossHP lh{hp.temp, hp.em_coef, hp.div_coef, hp.reweight, hp.non_blank};
-    timed(F_LOSS, [&] { launch_suta_loss(pl.logits, B, T, k.V, lh, pl.dlogits, pl.loss, pl.loss_scratch, st); });
+    timed(F_LOSS,
+          [&] { launch_suta_loss(pl.logits, B, T, k.V, lh, rT(), pl.dlogits, pl.loss, pl.loss_scratch, st); });
 
     auto nn_gemm = [&](const float* A, int lda, const float* Bm, int ldb, float* C, int ldc, int M, int N, int K,
                        int epi, const float* R, int ldr, const float* aux, int ldaux) {
@@ -869,6 +914,7 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
         g.segK = Cg;
         g.pad = k.posK - 1 - k.posK / 2;
         g.Mvalid = T;
+        g.zmvalid = rT();
         g.M = T;
         g.N = Cg;
         g.K = k.posK * Cg;
@@ -888,6 +934,10 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
         g.ldr = H;
         g.sR0 = Cg;
         g.sR1 = (long)T * H;
+        if (plan.ragged) {  // padding frames receive conv gradient from valid ones: keep them at 0
+            g.epi |= EPI_ROWMASK;
+            g.zrows = rT();
+        }
         gemm(g);
     }
     const int C6 = k.C[k.nconv - 1];
@@ -1019,7 +1069,7 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
         timed(F_NORM, [&] {
             launch_front_gn_bwd(pl.x, pl.N, P + o_cw[0], k.conv_bias ? P + o_cb[0] : nullptr, Pn, B, pl.Lc[0], k.C[0],
                                 k.K[0], k.S[0], P + o_cg[0], P + o_cbeta[0], pl.gn_mean, pl.gn_rstd, cur, G + o_cg[0],
-                                G + o_cbeta[0], G + o_cw[0], Pn, pl.dpart, pl.c0part, st);
+                                G + o_cbeta[0], G + o_cw[0], Pn, pl.dpart, pl.c0part, rL0(), st);
         });
         return;
     }
@@ -1096,10 +1146,17 @@ void suta_engine::reset_slots(int B) {
     opt_steps = 0;
 }
 
-void suta_engine::stage_input(const float* wav, int on_dev, int norm, int B, long N) {
-    HIPCHK(hipMemcpyAsync(plan.xraw, wav, (size_t)B * N * sizeof(float),
-                          on_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
-    if (norm) timed(F_EW, [&] { launch_wave_normalize(plan.xraw, plan.x, B, N, st); });
+void suta_engine::stage_input(const float* wav, int on_dev, int norm, int B, long N, long stride) {
+    const hipMemcpyKind kind = on_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    if (!plan.ragged) {
+        HIPCHK(hipMemcpyAsync(plan.xraw, wav, (size_t)B * N * sizeof(float), kind, st));
+    } else {  // utterance b: n[b] samples at wav + b * stride -> slot b of the N-stride layout, zero padded
+        HIPCHK(hipMemsetAsync(plan.xraw, 0, (size_t)B * N * sizeof(float), st));
+        for (int b = 0; b < B; ++b)
+            HIPCHK(hipMemcpyAsync(plan.xraw + (long)b * N, wav + (long)b * stride, (size_t)plan.h_n[b] * sizeof(float),
+                                  kind, st));
+    }
+    if (norm) timed(F_EW, [&] { launch_wave_normalize(plan.xraw, plan.x, B, N, rN(), st); });
     else HIPCHK(hipMemcpyAsync(plan.x, plan.xraw, (size_t)B * N * sizeof(float), hipMemcpyDeviceToDevice, st));
 }
 
@@ -1355,6 +1412,7 @@ int32_t suta_forward(suta_engine* e, const float* wav, int32_t on_dev, int32_t n
         check_batch(e, batch, n);
         HIPCHK(hipSetDevice(e->device));
         e->build_plan(batch, n);
+        e->set_lengths(batch, nullptr);
         e->stage_input(wav, on_dev, norm, batch, n);
         e->forward(batch);
         HIPCHK(hipMemcpyAsync(logits_out, e->plan.logits, (size_t)batch * e->plan.T * e->c.V * 4, hipMemcpyDeviceToHost,
@@ -1370,6 +1428,7 @@ int32_t suta_step(suta_engine* e, const float* wav, int32_t on_dev, int32_t norm
         check_batch(e, batch, n);
         HIPCHK(hipSetDevice(e->device));
         e->build_plan(batch, n);
+        e->set_lengths(batch, nullptr);
         e->stage_input(wav, on_dev, norm, batch, n);
         e->forward(batch);
         e->backward(batch, *hp);
@@ -1384,40 +1443,70 @@ int32_t suta_step(suta_engine* e, const float* wav, int32_t on_dev, int32_t norm
     });
 }
 
+}  // extern "C"
+
+// suta_adapt / suta_adapt_varlen body: ns == null -> every utterance has n samples (stride n)
+static void adapt_impl(suta_engine* e, const float* wav, int32_t on_dev, int32_t norm, int32_t batch, int64_t n,
+                       const int64_t* ns, int64_t stride, int32_t steps, const suta_hparams* hp, const int32_t* rec,
+                       int32_t nrec, float* logits_out, int32_t logits_on_dev, int32_t* ids_out, int64_t* frames_out) {
+    check_batch(e, batch, n);
+    if (steps < 0) throw SutaError(SUTA_ERR_ARG, "steps < 0");
+    for (int i = 0; i < nrec; ++i)
+        if (rec[i] < 0 || rec[i] > steps) throw SutaError(SUTA_ERR_ARG, "record step outside [0, steps]");
+    HIPCHK(hipSetDevice(e->device));
+    e->build_plan(batch, n);
+    e->set_lengths(batch, ns);
+    const int T = e->plan.T, V = e->c.V;
+    if (frames_out) {
+        if (ns) for (int b = 0; b < batch; ++b) frames_out[b] = e->plan.h_T[b];
+        else *frames_out = T;
+    }
+    const size_t per = (size_t)batch * T * V;
+    e->stage_input(wav, on_dev, norm, batch, n, stride);
+    if (hp->episodic) e->reset_slots(batch);
+    for (int s = 0; s <= steps; ++s) {
+        e->forward(batch);
+        for (int i = 0; i < nrec; ++i) {
+            if (rec[i] != s) continue;
+            if (logits_out)
+                HIPCHK(hipMemcpyAsync(logits_out + i * per, e->plan.logits, per * 4,
+                                      logits_on_dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, e->st));
+            if (ids_out) {
+                launch_argmax(e->plan.logits, (long)batch * T, V, e->plan.ids, e->st);
+                HIPCHK(hipMemcpyAsync(ids_out + (size_t)i * batch * T, e->plan.ids, (size_t)batch * T * 4,
+                                      hipMemcpyDeviceToHost, e->st));
+            }
+        }
+        if (s == steps) break;
+        e->backward(batch, *hp);
+        e->adam(batch, *hp);
+    }
+    HIPCHK(hipStreamSynchronize(e->st));
+    if (e->timing) e->collect_timing();
+}
+
+extern "C" {
+
 int32_t suta_adapt(suta_engine* e, const float* wav, int32_t on_dev, int32_t norm, int32_t batch, int64_t n,
                    int32_t steps, const suta_hparams* hp, const int32_t* rec, int32_t nrec, float* logits_out,
                    int32_t logits_on_dev, int32_t* ids_out, int64_t* frames_out) {
     return guard([&] {
-        check_batch(e, batch, n);
-        if (steps < 0) throw SutaError(SUTA_ERR_ARG, "steps < 0");
-        for (int i = 0; i < nrec; ++i)
-            if (rec[i] < 0 || rec[i] > steps) throw SutaError(SUTA_ERR_ARG, "record step outside [0, steps]");
-        HIPCHK(hipSetDevice(e->device));
-        e->build_plan(batch, n);
-        const int T = e->plan.T, V = e->c.V;
-        if (frames_out) *frames_out = T;
-        const size_t per = (size_t)batch * T * V;
-        e->stage_input(wav, on_dev, norm, batch, n);
-        if (hp->episodic) e->reset_slots(batch);
-        for (int s = 0; s <= steps; ++s) {
-            e->forward(batch);
-            for (int i = 0; i < nrec; ++i) {
-                if (rec[i] != s) continue;
-                if (logits_out)
-                    HIPCHK(hipMemcpyAsync(logits_out + i * per, e->plan.logits, per * 4,
-                                          logits_on_dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, e->st));
-                if (ids_out) {
-                    launch_argmax(e->plan.logits, (long)batch * T, V, e->plan.ids, e->st);
-                    HIPCHK(hipMemcpyAsync(ids_out + (size_t)i * batch * T, e->plan.ids, (size_t)batch * T * 4,
-                                          hipMemcpyDeviceToHost, e->st));
-                }
-            }
-            if (s == steps) break;
-            e->backward(batch, *hp);
-            e->adam(batch, *hp);
-        }
-        HIPCHK(hipStreamSynchronize(e->st));
-        if (e->timing) e->collect_timing();
+        adapt_impl(e, wav, on_dev, norm, batch, n, nullptr, n, steps, hp, rec, nrec, logits_out, logits_on_dev,
+                   ids_out, frames_out);
+    });
+}
+
+int32_t suta_adapt_varlen(suta_engine* e, const float* wav, int32_t on_dev, int32_t norm, int32_t batch,
+                          const int64_t* n_samples, int64_t stride, int32_t steps, const suta_hparams* hp,
+                          const int32_t* rec, int32_t nrec, float* logits_out, int32_t logits_on_dev, int32_t* ids_out,
+                          int64_t* frames_out) {
+    return guard([&] {
+        if (!n_samples || batch < 1) throw SutaError(SUTA_ERR_ARG, "n_samples is null or batch < 1");
+        int64_t nmax = 0;
+        for (int b = 0; b < batch; ++b) nmax = std::max<int64_t>(nmax, n_samples[b]);
+        if (stride < nmax) throw SutaError(SUTA_ERR_ARG, "stride < max(n_samples)");
+        adapt_impl(e, wav, on_dev, norm, batch, nmax, n_samples, stride, steps, hp, rec, nrec, logits_out,
+                   logits_on_dev, ids_out, frames_out);
     });
 }
 
@@ -1436,7 +1525,7 @@ int32_t suta_loss_grad(suta_engine* e, const float* logits, int32_t batch, int64
         float* ls = scr + (size_t)batch * frames * 66 + 64;
         HIPCHK(hipMemcpyAsync(dl, logits, n * 4, hipMemcpyHostToDevice, e->st));
         LossHP lh{hp->temp, hp->em_coef, hp->div_coef, hp->reweight, hp->non_blank};
-        launch_suta_loss(dl, batch, (int)frames, V, lh, dd, ls, scr, e->st);
+        launch_suta_loss(dl, batch, (int)frames, V, lh, nullptr, dd, ls, scr, e->st);
         HIPCHK(hipMemcpyAsync(dlogits_out, dd, n * 4, hipMemcpyDeviceToHost, e->st));
         HIPCHK(hipMemcpyAsync(loss_out, ls, (size_t)batch * 4, hipMemcpyDeviceToHost, e->st));
         HIPCHK(hipStreamSynchronize(e->st));

@@ -209,6 +209,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, const f32x16 
     float* C = p.C + z1 * p.sC1 + z0 * p.sC0;
     const float* bias = p.bias ? p.bias + z1 * p.sBias1 + z0 * p.sBias0 : nullptr;
     const float* aux = p.aux ? p.aux + z1 * p.sAux1 + z0 * p.sAux0 : nullptr;
+    const int rlim = (e & EPI_ROWMASK) ? p.zrows[z1] : p.M;
     float* C2 = p.C2 ? p.C2 + z1 * p.sC21 + z0 * p.sC20 : nullptr;
     // second operand: R (RESID), old C (ACCUM) or the row vector (SMBWD)
     const float* Q = nullptr;
@@ -294,7 +295,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, const f32x16 
                 for (int r = 0; r < CH; ++r) {
                     const int rr = r0 + r;
                     const int row = rbase + i * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * h;
-                    if (interior || (row < p.M && col < p.N)) C[(long)row * p.ldc + col] = v[r];
+                    if (interior || (row < p.M && col < p.N)) C[(long)row * p.ldc + col] = row < rlim ? v[r] : 0.f;
                 }
             }
 }
@@ -322,6 +323,7 @@ __global__ __launch_bounds__(256, GEMM_F32_MINB) void gemm_f32_kernel(GemmParams
         zz /= p.splits;
     }
     const int z1 = zz / p.zdiv, z0 = zz % p.zdiv;
+    const int Mv = p.zmvalid ? p.zmvalid[z1] : p.Mvalid;  // conv-A valid source rows
     const float* A = p.A + z1 * p.sA1 + z0 * p.sA0;
     const float* B = p.B + z1 * p.sB1 + z0 * p.sB0;
 
@@ -357,12 +359,12 @@ __global__ __launch_bounds__(256, GEMM_F32_MINB) void gemm_f32_kernel(GemmParams
         if (CONV) {
             const int seg = segAligned ? k / p.segK : 0;
             const int sh = seg - p.pad;
-            full = full && segAligned && m0 + sh >= 0 && m0 + BM + sh <= p.Mvalid;
+            full = full && segAligned && m0 + sh >= 0 && m0 + BM + sh <= Mv;
             base = A + (long)sh * p.lda;
             kk = k - seg * p.segK;
         }
         if (full) load_stage_full<BM, AKC>(ra, base, p.lda, m0, kk);
-        else load_stage<BM, AKC, CONV ? 1 : 0>(ra, A, p.lda, m0, p.M, k, kend, va, p.segK, p.pad, p.Mvalid, 0);
+        else load_stage<BM, AKC, CONV ? 1 : 0>(ra, A, p.lda, m0, p.M, k, kend, va, p.segK, p.pad, Mv, 0);
     };
     auto stageB = [&](int k) {
         bool full = vb && n0 + BN <= p.N && k + BK <= kend;
@@ -635,6 +637,7 @@ __global__ __launch_bounds__(256, 3) void gemm_x6_kernel(GemmParams p) {
         zz /= p.splits;
     }
     const int z1 = zz / p.zdiv, z0 = zz % p.zdiv;
+    const int Mv = p.zmvalid ? p.zmvalid[z1] : p.Mvalid;  // conv-A valid source rows
     const float* A = p.A + z1 * p.sA1 + z0 * p.sA0;
     const float* B = p.B + z1 * p.sB1 + z0 * p.sB0;
     const int m0 = tid.y * BM;
@@ -665,13 +668,13 @@ __global__ __launch_bounds__(256, 3) void gemm_x6_kernel(GemmParams p) {
         if (CONV) {
             const int seg = segAligned ? k / p.segK : 0;
             const int sh = seg - p.pad;
-            full = full && segAligned && m0 + sh >= 0 && m0 + BM + sh <= p.Mvalid;
+            full = full && segAligned && m0 + sh >= 0 && m0 + BM + sh <= Mv;
             base = A + (long)sh * p.lda;
             kk = k - seg * p.segK;
         }
         if (AKC) {
             if (full) x6_load_kc<BM, BKX, 0, true>(ra, base, p.lda, m0, p.M, kk, kend, va, 0, 0, 0, 0);
-            else x6_load_kc<BM, BKX, CONV ? 1 : 0, false>(ra, A, p.lda, m0, p.M, k, kend, va, p.segK, p.pad, p.Mvalid, 0);
+            else x6_load_kc<BM, BKX, CONV ? 1 : 0, false>(ra, A, p.lda, m0, p.M, k, kend, va, p.segK, p.pad, Mv, 0);
         } else {
             if (full) x6_load_mn<BM, BKX, true>(ra, A, p.lda, m0, p.M, k, kend, va);
             else x6_load_mn<BM, BKX, false>(ra, A, p.lda, m0, p.M, k, kend, va);
@@ -803,7 +806,8 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmParams p) {
         float s = 0.f;
         for (int sp = 0; sp < p.splits; ++sp) s += W[sp * MN + idx];
         const long row = idx / p.N, col = idx % p.N;
-        C[row * p.ldc + col] = epi_value(p, s, row, col, bias, R, aux, C2, C, rowv);
+        const float v = epi_value(p, s, row, col, bias, R, aux, C2, C, rowv);
+        C[row * p.ldc + col] = ((p.epi & EPI_ROWMASK) && row >= p.zrows[z1]) ? 0.f : v;
     }
 }
 
@@ -917,6 +921,7 @@ __global__ __launch_bounds__(256, 2) void gemm_glds_kernel(GemmParams p) {
         zz /= p.splits;
     }
     const int z1 = zz / p.zdiv, z0 = zz % p.zdiv;
+    const int Mv = p.zmvalid ? p.zmvalid[z1] : p.Mvalid;  // conv-A valid source rows
     const float* A = p.A + z1 * p.sA1 + z0 * p.sA0;
     const float* B = p.B + z1 * p.sB1 + z0 * p.sB0;
     const int m0 = tid.y * BM;
@@ -942,7 +947,7 @@ __global__ __launch_bounds__(256, 2) void gemm_glds_kernel(GemmParams p) {
         float* st = smem + (s % NS) * STAGE;
         const int k = kbeg + s * BKS;
         const bool dummy = s >= nst;
-        glds_stage<BM, BKS, AKC, CONV ? 1 : 0>(st, A, p.lda, m0, p.M, k, kend, p.segK, p.pad, p.Mvalid, 0, wid,
+        glds_stage<BM, BKS, AKC, CONV ? 1 : 0>(st, A, p.lda, m0, p.M, k, kend, p.segK, p.pad, Mv, 0, wid,
                                                 lane, dummy);
         glds_stage<BN, BKS, BKC, SEGB ? 2 : 0>(st + BM * BKS, B, p.ldb, n0, p.N, k, kend, p.segK, 0, 0, p.sBseg,
                                                 wid, lane, dummy);

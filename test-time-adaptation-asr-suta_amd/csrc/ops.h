@@ -4,8 +4,9 @@
 #include "common.h"
 
 // HF feature-extractor normalisation (feature_extraction_wav2vec2.py:78-97), per utterance:
-// y = (x - mean) / sqrt(var + 1e-7), population variance.
-void launch_wave_normalize(const float* x, float* y, int B, long N, hipStream_t st);
+// y = (x - mean) / sqrt(var + 1e-7), population variance.  lens (device, may be null): ragged batch,
+// utterance b has lens[b] <= N samples at stride N; its padding samples are written as 0.
+void launch_wave_normalize(const float* x, float* y, int B, long N, const int* lens, hipStream_t st);
 
 // conv0: z[b][t][c] = sum_k x[b][s*t + k] * W[b][k][c] (+ bias[b][c]);  W stored [k][c] per utterance.
 void launch_conv0(const float* x, long N, const float* W, const float* bias, long wstride, float* z, int B, int L0,
@@ -13,15 +14,17 @@ void launch_conv0(const float* x, long N, const float* W, const float* bias, lon
 
 // Fused conv0 + GroupNorm + GELU (group mode): conv0 is recomputed from the waveform in each pass.
 // fwd: mean/rstd per (utterance, channel) and a = gelu(GN(conv0(x))).  dpart: >= B*ceil(L0/128)*2*C + B*C doubles.
+// L0s (device, may be null): ragged batch, utterance b has L0s[b] <= L0 valid frames (statistics and
+// gradients over those only).
 void launch_front_gn_fwd(const float* x, long N, const float* W, const float* bias, long wstride, int B, int L0, int C,
                          int K, int S, const float* g, const float* beta, float* mean, float* rstd, float* a,
-                         double* dpart, hipStream_t st);
+                         double* dpart, const int* L0s, hipStream_t st);
 // bwd: da (overwritten with dg) -> dgamma, dbeta and the conv0 weight gradient dW[k][c] (gstride per
 // utterance).  fpart: >= B*ceil(L0/128)*K*C floats.
 void launch_front_gn_bwd(const float* x, long N, const float* W, const float* bias, long wstride, int B, int L0, int C,
                          int K, int S, const float* g, const float* beta, const float* mean, const float* rstd,
                          float* da, float* dgamma, float* dbeta, float* dW, long gstride, double* dpart, float* fpart,
-                         hipStream_t st);
+                         const int* L0s, hipStream_t st);
 
 // LayerNorm over the last dim D of `rows` rows; gamma/beta of utterance (row / rows_per_utt)
 // at pstride.  Stores y, xhat, rstd.  gelu_out: y = gelu(LN(x)) (feature-encoder "layer" mode).
@@ -39,8 +42,9 @@ void launch_layernorm_bwd(const float* dy, const float* xhat, const float* rstd,
 // Column sums per utterance: out[b][c] = sum_{t < rows} x[b][t][c]   (bias gradients).
 void launch_colsum(const float* x, int B, int rows, int C, float* out, long ostride, float* part, hipStream_t st);
 
-// In-place row softmax of `nrows` rows of length T (row stride ld).
-void launch_softmax_rows(float* s, long nrows, int T, long ld, hipStream_t st);
+// In-place row softmax of `nrows` rows of length T (row stride ld).  tlen (device, may be null):
+// ragged batch, rows of utterance row / rows_per_utt use their first tlen[u] keys; the rest get 0.
+void launch_softmax_rows(float* s, long nrows, int T, long ld, const int* tlen, long rows_per_utt, hipStream_t st);
 
 // delta[b][h][t] = dot(dO[b][t][head h], O[b][t][head h]): the softmax-backward row term sum_j P_ij dP_ij.
 void launch_attn_delta(const float* dO, const float* O, float* delta, int B, int T, int NH, int dh, hipStream_t st);
@@ -53,7 +57,9 @@ struct LossHP {
     float temp, em_coef, div_coef;
     int reweight, non_blank;
 };
-void launch_suta_loss(const float* logits, int B, int T, int V, LossHP hp, float* dlogits, float* loss,
+// tlen (device, may be null): ragged batch, utterance b has tlen[b] <= T frames at stride T; the
+// gradient of its padding frames is written as 0.
+void launch_suta_loss(const float* logits, int B, int T, int V, LossHP hp, const int* tlen, float* dlogits, float* loss,
                       float* scratch, hipStream_t st);
 
 // Argmax ids per frame (first max, like torch.argmax), optional copy of logits.

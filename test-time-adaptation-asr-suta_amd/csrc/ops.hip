@@ -27,23 +27,24 @@ __device__ __forceinline__ T block_sum(T v, T* red) {
 // waveform normalisation (one block per utterance)
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void wave_normalize_kernel(const float* __restrict__ x, float* __restrict__ y,
-                                                             long N) {
+                                                             long N, const int* __restrict__ lens) {
     __shared__ double red[4];
     const float* xb = x + (long)blockIdx.x * N;
     float* yb = y + (long)blockIdx.x * N;
+    const long n = lens ? lens[blockIdx.x] : N;  // ragged batch: utterance length within the N stride
     double s = 0.0;
-    for (long i = threadIdx.x; i < N; i += 256) s += xb[i];
+    for (long i = threadIdx.x; i < n; i += 256) s += xb[i];
     s = block_sum(s, red);
-    const double mean = s / (double)N;
+    const double mean = s / (double)n;
     double q = 0.0;
-    for (long i = threadIdx.x; i < N; i += 256) {
+    for (long i = threadIdx.x; i < n; i += 256) {
         const double d = (double)xb[i] - mean;
         q += d * d;
     }
     q = block_sum(q, red);
     const float meanf = (float)mean;
-    const float denom = (float)sqrt(q / (double)N + 1e-7);
-    for (long i = threadIdx.x; i < N; i += 256) yb[i] = (xb[i] - meanf) / denom;
+    const float denom = (float)sqrt(q / (double)n + 1e-7);
+    for (long i = threadIdx.x; i < N; i += 256) yb[i] = i < n ? (xb[i] - meanf) / denom : 0.f;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -87,8 +88,10 @@ __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x,
 // ------------------------------------------------------------------------------------------
 constexpr int CS_ROWS = 128;
 __global__ __launch_bounds__(256) void col_stats_final(const double* __restrict__ part, int nchunk, int rows, int C,
-                                                       float eps, float* __restrict__ mean, float* __restrict__ rstd) {
+                                                       float eps, float* __restrict__ mean, float* __restrict__ rstd,
+                                                       const int* __restrict__ rows_b) {
     const int b = blockIdx.y;
+    if (rows_b) rows = rows_b[b];
     const int c = blockIdx.x * 256 + threadIdx.x;
     if (c >= C) return;
     double s = 0.0, q = 0.0;
@@ -142,7 +145,8 @@ __global__ __launch_bounds__(256) void conv0_gn_kernel(const float* __restrict__
                                                        const float* __restrict__ rstd, const float* __restrict__ g,
                                                        const float* __restrict__ beta, float* __restrict__ io,
                                                        const float* __restrict__ coef, double* __restrict__ dpart,
-                                                       float* __restrict__ fpart, int nchunk) {
+                                                       float* __restrict__ fpart, int nchunk,
+                                                       const int* __restrict__ L0s) {
     __shared__ float xs[F0_ROWS * 16 + 16];
     if (KT > 0) {
         K = KT;
@@ -157,11 +161,14 @@ __global__ __launch_bounds__(256) void conv0_gn_kernel(const float* __restrict__
         xs[i] = gi < N ? xb[gi] : 0.f;
     }
     __syncthreads();
-    const int rows = min(F0_ROWS, L0 - t0);
+    // ragged batch: statistics and gradients over the utterance's Lb valid frames; MODE 1 also
+    // fills the padding frames of the layout (finite values, never read as data)
+    const int Lb = L0s ? L0s[b] : L0;
+    const int rows = MODE == 1 ? min(F0_ROWS, L0 - t0) : min(F0_ROWS, Lb - t0);
     const float* Wb = W + (long)b * wstride;
     const float* bb = bias ? bias + (long)b * wstride : nullptr;
     float* iob = io ? io + ((long)b * L0 + t0) * C : nullptr;
-    const float invL = 1.0f / L0;
+    const float invL = 1.0f / Lb;
     for (int c = threadIdx.x; c < C; c += 256) {
         float w[16];
 #pragma unroll
@@ -390,11 +397,14 @@ __global__ __launch_bounds__(256) void colsum_partial(const float* __restrict__ 
 // attention softmax over rows of length T (<= 64*NPL), one wave per row
 // ------------------------------------------------------------------------------------------
 template <int NPL>
-__global__ __launch_bounds__(256) void softmax_rows_kernel(float* __restrict__ s, long nrows, int T, long ld) {
+__global__ __launch_bounds__(256) void softmax_rows_kernel(float* __restrict__ s, long nrows, int T, long ld,
+                                                           const int* __restrict__ tlen, long rows_per_utt) {
     const int lane = threadIdx.x & 63;
     const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= nrows) return;
     float* r = s + row * ld;
+    const int Tl = T;  // layout width; keys >= the utterance's length get probability 0
+    if (tlen) T = tlen[row / rows_per_utt];
     float v[NPL];
     float mx = -INFINITY;
 #pragma unroll
@@ -416,7 +426,7 @@ __global__ __launch_bounds__(256) void softmax_rows_kernel(float* __restrict__ s
 #pragma unroll
     for (int i = 0; i < NPL; ++i) {
         const int c = lane + i * 64;
-        if (c < T) r[c] = v[i] * inv;
+        if (c < Tl) r[c] = c < T ? v[i] * inv : 0.f;
     }
 }
 
@@ -466,7 +476,7 @@ __global__ __launch_bounds__(256) void dgelu_mul_kernel(const float* __restrict_
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void suta_loss_kernel(const float* __restrict__ logits, int T, int V, LossHP hp,
                                                         float* __restrict__ dlogits, float* __restrict__ loss_out,
-                                                        float* __restrict__ scratch) {
+                                                        float* __restrict__ scratch, const int* __restrict__ tlen) {
     __shared__ double Cm[64 * 64];
     __shared__ float Sm[64 * 64];
     __shared__ double redd[4][4];
@@ -475,11 +485,16 @@ __global__ __launch_bounds__(256) void suta_loss_kernel(const float* __restrict_
     __shared__ double scal[8];
     const int b = blockIdx.x;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const float* L = logits + (long)b * T * V;
-    float* dL = dlogits + (long)b * T * V;
-    float* Ps = scratch + (long)b * T * 66;
-    float* Hs = Ps + (long)T * 64;
-    float* Ws = Hs + T;
+    const int Tl = T;  // layout stride (frames); the utterance has T <= Tl valid frames
+    const float* L = logits + (long)b * Tl * V;
+    float* dL = dlogits + (long)b * Tl * V;
+    float* Ps = scratch + (long)b * Tl * 66;
+    float* Hs = Ps + (long)Tl * 64;
+    if (tlen) {
+        T = tlen[b];
+        for (long i = (long)T * V + threadIdx.x; i < (long)Tl * V; i += 256) dL[i] = 0.f;  // padding frames
+    }
+    float* Ws = Hs + Tl;
     const bool act = lane < V;
     const float invt = 1.0f / hp.temp;
 
@@ -711,8 +726,8 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ P, const 
 // ==========================================================================================
 // launchers
 // ==========================================================================================
-void launch_wave_normalize(const float* x, float* y, int B, long N, hipStream_t st) {
-    hipLaunchKernelGGL(wave_normalize_kernel, dim3(B), dim3(256), 0, st, x, y, N);
+void launch_wave_normalize(const float* x, float* y, int B, long N, const int* lens, hipStream_t st) {
+    hipLaunchKernelGGL(wave_normalize_kernel, dim3(B), dim3(256), 0, st, x, y, N, lens);
 }
 
 void launch_conv0(const float* x, long N, const float* W, const float* bias, long wstride, float* z, int B, int L0,
@@ -766,21 +781,25 @@ void launch_colsum(const float* x, int B, int rows, int C, float* out, long ostr
                        ostride);
 }
 
-void launch_softmax_rows(float* s, long nrows, int T, long ld, hipStream_t st) {
+void launch_softmax_rows(float* s, long nrows, int T, long ld, const int* tlen, long rows_per_utt, hipStream_t st) {
     dim3 grid((unsigned)((nrows + 3) / 4));
-    if (T <= 256) hipLaunchKernelGGL(softmax_rows_kernel<4>, grid, dim3(256), 0, st, s, nrows, T, ld);
-    else if (T <= 512) hipLaunchKernelGGL(softmax_rows_kernel<8>, grid, dim3(256), 0, st, s, nrows, T, ld);
-    else if (T <= 1024) hipLaunchKernelGGL(softmax_rows_kernel<16>, grid, dim3(256), 0, st, s, nrows, T, ld);
-    else hipLaunchKernelGGL(softmax_rows_kernel<32>, grid, dim3(256), 0, st, s, nrows, T, ld);
+    if (T <= 256) hipLaunchKernelGGL(softmax_rows_kernel<4>, grid, dim3(256), 0, st, s, nrows, T, ld, tlen,
+                                    rows_per_utt);
+    else if (T <= 512) hipLaunchKernelGGL(softmax_rows_kernel<8>, grid, dim3(256), 0, st, s, nrows, T, ld, tlen,
+                                    rows_per_utt);
+    else if (T <= 1024) hipLaunchKernelGGL(softmax_rows_kernel<16>, grid, dim3(256), 0, st, s, nrows, T, ld, tlen,
+                                    rows_per_utt);
+    else hipLaunchKernelGGL(softmax_rows_kernel<32>, grid, dim3(256), 0, st, s, nrows, T, ld, tlen,
+                                    rows_per_utt);
 }
 
 void launch_dgelu_mul(const float* g, const float* z, float* out, long n, hipStream_t st) {
     hipLaunchKernelGGL(dgelu_mul_kernel, dim3(ew_grid(n)), dim3(256), 0, st, g, z, out, n);
 }
 
-void launch_suta_loss(const float* logits, int B, int T, int V, LossHP hp, float* dlogits, float* loss,
+void launch_suta_loss(const float* logits, int B, int T, int V, LossHP hp, const int* tlen, float* dlogits, float* loss,
                       float* scratch, hipStream_t st) {
-    hipLaunchKernelGGL(suta_loss_kernel, dim3(B), dim3(256), 0, st, logits, T, V, hp, dlogits, loss, scratch);
+    hipLaunchKernelGGL(suta_loss_kernel, dim3(B), dim3(256), 0, st, logits, T, V, hp, dlogits, loss, scratch, tlen);
 }
 
 void launch_argmax(const float* logits, long rows, int V, int* ids, hipStream_t st) {
@@ -806,29 +825,29 @@ static void launch_conv0_gn(dim3 grid, hipStream_t st, int K, int S, Args... arg
 
 void launch_front_gn_fwd(const float* x, long N, const float* W, const float* bias, long wstride, int B, int L0, int C,
                          int K, int S, const float* g, const float* beta, float* mean, float* rstd, float* a,
-                         double* dpart, hipStream_t st) {
+                         double* dpart, const int* L0s, hipStream_t st) {
     const int nchunk = cdiv(L0, F0_ROWS);
     launch_conv0_gn<0>(dim3(nchunk, B), st, K, S, x, N, W, bias, wstride, L0, C, K, S,
                        (const float*)nullptr, (const float*)nullptr, (const float*)nullptr, (const float*)nullptr,
-                       (float*)nullptr, (const float*)nullptr, dpart, (float*)nullptr, nchunk);
+                       (float*)nullptr, (const float*)nullptr, dpart, (float*)nullptr, nchunk, L0s);
     hipLaunchKernelGGL(col_stats_final, dim3(cdiv(C, 256), B), dim3(256), 0, st, dpart, nchunk, L0, C, 1e-5f, mean,
-                       rstd);
+                       rstd, L0s);
     launch_conv0_gn<1>(dim3(nchunk, B), st, K, S, x, N, W, bias, wstride, L0, C, K, S,
-                       mean, rstd, g, beta, a, (const float*)nullptr, (double*)nullptr, (float*)nullptr, nchunk);
+                       mean, rstd, g, beta, a, (const float*)nullptr, (double*)nullptr, (float*)nullptr, nchunk, L0s);
 }
 
 void launch_front_gn_bwd(const float* x, long N, const float* W, const float* bias, long wstride, int B, int L0, int C,
                          int K, int S, const float* g, const float* beta, const float* mean, const float* rstd,
                          float* da, float* dgamma, float* dbeta, float* dW, long gstride, double* dpart, float* fpart,
-                         hipStream_t st) {
+                         const int* L0s, hipStream_t st) {
     const int nchunk = cdiv(L0, F0_ROWS);
     launch_conv0_gn<2>(dim3(nchunk, B), st, K, S, x, N, W, bias, wstride, L0, C, K, S,
-                       mean, rstd, g, beta, da, (const float*)nullptr, dpart, (float*)nullptr, nchunk);
+                       mean, rstd, g, beta, da, (const float*)nullptr, dpart, (float*)nullptr, nchunk, L0s);
     float* coef = reinterpret_cast<float*>(dpart + (long)B * nchunk * 2 * C);
     hipLaunchKernelGGL(gn_bwd_final, dim3(cdiv(C, 256), B), dim3(256), 0, st, dpart, nchunk, C, dgamma, dbeta, gstride,
                        coef);
     launch_conv0_gn<3>(dim3(nchunk, B), st, K, S, x, N, W, bias, wstride, L0, C, K, S,
-                       mean, rstd, g, beta, da, coef, (double*)nullptr, fpart, nchunk);
+                       mean, rstd, g, beta, da, coef, (double*)nullptr, fpart, nchunk, L0s);
     hipLaunchKernelGGL(conv0_dw_reduce, dim3(cdiv((long)K * C, 256), B), dim3(256), 0, st, fpart, nchunk, K * C, dW,
                        gstride);
 }

@@ -19,7 +19,7 @@ MAX_CONV = 8
 
 # exported symbols (kept in sync with include/suta.h; tests/test_abi.py checks both)
 EXPORTS = ("suta_create", "suta_destroy", "suta_reset", "suta_num_frames", "suta_forward", "suta_step",
-           "suta_adapt", "suta_loss_grad", "suta_get_param", "suta_param_info", "suta_sync", "suta_stream", "suta_set_timing",
+           "suta_adapt", "suta_adapt_varlen", "suta_loss_grad", "suta_get_param", "suta_param_info", "suta_sync", "suta_stream", "suta_set_timing",
            "suta_get_timing", "suta_set_precision", "suta_set_graphs", "suta_last_error")
 
 
@@ -92,13 +92,17 @@ def load_library(path: str = LIB_PATH):
     lib.suta_sync.argtypes = [C.c_void_p]
     lib.suta_stream.argtypes = [C.c_void_p]
     lib.suta_stream.restype = C.c_void_p
+    if hasattr(lib, "suta_adapt_varlen"):  # (tools may load an older library build for A/B runs)
+        lib.suta_adapt_varlen.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, i64p, C.c_int64,
+                                          C.c_int32, P(HParamsC), i32p, C.c_int32, C.c_void_p, C.c_int32,
+                                          C.c_void_p, i64p]
     lib.suta_set_timing.argtypes = [C.c_void_p, C.c_int32]
     lib.suta_get_timing.argtypes = [C.c_void_p, P(C.c_double), i64p]
     lib.suta_set_graphs.argtypes = [C.c_void_p, C.c_int32]
     lib.suta_set_precision.argtypes = [C.c_void_p, C.c_int32]
     lib.suta_last_error.restype = C.c_char_p
     for name in EXPORTS:
-        if name != "suta_stream" and name != "suta_last_error":
+        if name != "suta_stream" and name != "suta_last_error" and hasattr(lib, name):
             getattr(lib, name).restype = C.c_int32
     _lib = lib
     return lib
@@ -226,6 +230,36 @@ class SutaEngine:
                                    len(rec), lp, ldev, _ptr(ids) if rec else None, C.byref(frames)))
         lg = {r: logits[i] for i, r in enumerate(rec)} if logits is not None else None
         return lg, {r: ids[i] for i, r in enumerate(rec)}, frames.value
+
+    def adapt_varlen(self, wavs, steps: int, hp: SutaHParams, record: Sequence[int] = (), normalize: bool = False,
+                     want_logits: bool = True, lengths: Optional[Sequence[int]] = None):
+        """Ragged batch (suta_adapt_varlen): `wavs` is a list of 1-D waveforms, or a padded (B, stride)
+        array / tensor with `lengths`.  Each utterance is adapted as if alone.  Returns
+        (logits {r: [ (T_b, V) ]} or None, ids {r: [ (T_b,) ]}, [T_b])."""
+        if lengths is None:
+            arrs = [np.ascontiguousarray(w.detach().cpu().numpy() if hasattr(w, "detach") else w,
+                                         dtype=np.float32).reshape(-1) for w in wavs]
+            lengths = [a.size for a in arrs]
+            pad = np.zeros((len(arrs), max(lengths)), np.float32)
+            for b, a in enumerate(arrs):
+                pad[b, :a.size] = a
+            wavs = pad
+        p, dev, B, stride, keep = self._wav(wavs)
+        ns = (C.c_int64 * B)(*[int(n) for n in lengths])
+        T = self.num_frames(max(lengths))
+        rec = list(record)
+        crec = (C.c_int32 * max(1, len(rec)))(*rec)
+        ids = np.empty((max(1, len(rec)), B, T), np.int32)
+        frames = (C.c_int64 * B)()
+        logits = np.empty((len(rec), B, T, self.V), np.float32) if (want_logits and rec) else None
+        _check(self.lib.suta_adapt_varlen(self.handle, p, dev, int(normalize), B, ns, stride, steps,
+                                          C.byref(hp.to_c()), crec, len(rec),
+                                          _ptr(logits) if logits is not None else None, 0,
+                                          _ptr(ids) if rec else None, frames))
+        tb = [int(frames[b]) for b in range(B)]
+        lg = ({r: [logits[i, b, :tb[b]] for b in range(B)] for i, r in enumerate(rec)}
+              if logits is not None else None)
+        return lg, {r: [ids[i, b, :tb[b]] for b in range(B)] for i, r in enumerate(rec)}, tb
 
     def loss_grad(self, logits: np.ndarray, hp: SutaHParams):
         """Fused loss-and-grad kernel on logits of shape (B, T, V): returns (dlogits, loss)."""

@@ -1,0 +1,45 @@
+"""HBM traffic per launch from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE), per kernel family.
+
+gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports half the bytes of wide
+(16 B/lane) coalesced reads -> doubled here; WRITE_SIZE is exact for 16-B/lane stores.  Both are in KB.
+usage: python tools/pmc_traffic.py FETCH_counter_collection.csv WRITE_counter_collection.csv [out.json]
+"""
+import collections
+import csv
+import json
+import sys
+
+
+def load(path, counter):
+    per = collections.defaultdict(lambda: [0, 0.0])
+    seen = set()
+    for r in csv.DictReader(open(path)):
+        if r.get("Counter_Name") != counter:
+            continue
+        key = (r.get("Dispatch_Id"), r.get("Counter_Name"))
+        name = r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0].split("<")[0]
+        v = float(r["Counter_Value"])
+        if key not in seen:
+            seen.add(key)
+            per[name][0] += 1
+        per[name][1] += v
+    return per
+
+
+def main():
+    fetch = load(sys.argv[1], "FETCH_SIZE")
+    write = load(sys.argv[2], "WRITE_SIZE")
+    out = {}
+    for k in sorted(set(fetch) | set(write)):
+        n = max(fetch[k][0], write[k][0])
+        rd = 2.0 * fetch[k][1] * 1024 / max(1, fetch[k][0])
+        wr = write[k][1] * 1024 / max(1, write[k][0])
+        out[k] = {"launches": n, "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
+                  "hbm_bytes_per_launch": rd + wr}
+        print(f"{k:28s} {n:6d} launches  read {rd/1e6:9.2f} MB  write {wr/1e6:9.2f} MB per launch")
+    if len(sys.argv) > 3:
+        json.dump(out, open(sys.argv[3], "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
