@@ -4,8 +4,11 @@ Same flags, same stdout lines ("original WER:", "adapt-k WER:", "TTA-k WER:"), s
 file `log_dir/exp_name` and CSV.  Differences, all deliberate:
   * the adapt loop runs in libsuta (HIP) with the minimal schedule: the logits recorded after
     step k equal the reference's re-inference output of step k;
-  * utterances are adapted one per engine call (the reference's batch_size > 1 pads without
-    a mask and breaks mcc_loss, main.py:32);
+  * episodic runs adapt up to --gpu_batch utterances per engine call as a ragged batch
+    (suta_adapt_varlen: every utterance at its own length, results equal to running it alone;
+    utterances are length-sorted inside windows of 8 batches to keep padding low, and the
+    per-utterance lines are printed in dataset order).  The reference's own --batch_size > 1
+    pads without a mask and breaks mcc_loss (main.py:32); it is only used for loading here;
   * under torchrun, utterances are LPT-sharded over ranks and WER counts are all_reduce'd;
   * pretrained weights load from a local checkpoint directory or the local HF cache (no
     network); `--synthetic_weights` uses the seeded generator instead;
@@ -50,6 +53,8 @@ def build_parser():
     # engine-only options
     p.add_argument("--synthetic_weights", action="store_true", help="seeded random weights (no checkpoint)")
     p.add_argument("--device", type=int, default=None)
+    p.add_argument("--gpu_batch", type=int, default=16,
+                   help="utterances adapted together as one ragged batch (episodic runs; 1 = one per call)")
     return p
 
 
@@ -118,7 +123,8 @@ def main(argv=None):
         say(line)
 
     cfg, weights = load_model(a.asr, a.synthetic_weights)
-    engine = SutaEngine(cfg, weights, device=device, max_batch=1)
+    gb = max(1, a.gpu_batch) if a.episodic else 1  # non-episodic adaptation is sequential
+    engine = SutaEngine(cfg, weights, device=device, max_batch=gb)
     hp = SutaHParams(lr=a.lr, temp=a.temp, em_coef=a.em_coef, div_coef=a.div_coef, reweight=a.reweight,
                      non_blank=a.non_blank, train_feature=a.train_feature, bias_only=a.bias_only,
                      episodic=a.episodic)
@@ -135,28 +141,52 @@ def main(argv=None):
     else:
         mine = list(range(len(batches)))
 
+    def adapt_window(items):
+        """ids {record step: (T,)} per item, adapting length-sorted groups of gb as ragged batches."""
+        order = sorted(range(len(items)), key=lambda i: len(items[i][1])) if gb > 1 else list(range(len(items)))
+        out = [None] * len(items)
+        for s0 in range(0, len(order), gb):
+            grp = order[s0:s0 + gb]
+            if len(grp) == 1:
+                _, ids, _ = engine.adapt(items[grp[0]][1], a.steps, hp, record=record, want_logits=False)
+                out[grp[0]] = {r: ids[r][0] for r in record}
+            else:
+                _, ids, _ = engine.adapt_varlen([items[i][1] for i in grp], a.steps, hp, record=record,
+                                                want_logits=False)
+                for j, i in enumerate(grp):
+                    out[i] = {r: ids[r][j] for r in record}
+        return out
+
     results = []
     start = time.time()
-    for bi in mine:
-        lens, wavs, texts, files = dataset.collate(batches[bi])
-        for wav, text in zip(wavs, texts):
-            x = normalize(wav)
-            _, ids, T = engine.adapt(x, a.steps, hp, record=record, want_logits=False)
+    window: List = []
+
+    def flush():
+        for (bi, x, text), ids in zip(window, adapt_window(window)):
             rec = {"idx": bi, "text": text, "duration": len(x) / SAMPLE_RATE, "hyp": {}}
-            ori = batch_decode(ids[0])
+            ori = batch_decode(ids[0][None])
             rec["hyp"][0] = ori[0]
             ori_wer = wer([text], ori)
             print("original WER: ", ori_wer)
             if a.episodic:
                 for c in CHECKPOINTS:
                     if c <= a.steps:
-                        h = batch_decode(ids[c])
+                        h = batch_decode(ids[c][None])
                         rec["hyp"][c] = h[0]
                         ada = wer([text], h)
                         print(f"adapt-{c} WER: " + (" " if c < 10 else ""), ada)
                         if c == 10:
                             rec["werr"] = ori_wer - ada
             results.append(rec)
+        window.clear()
+
+    for bi in mine:
+        lens, wavs, texts, files = dataset.collate(batches[bi])
+        for wav, text in zip(wavs, texts):
+            window.append((bi, normalize(wav), text))
+        if len(window) >= 8 * gb:
+            flush()
+    flush()
     elapsed = time.time() - start
 
     allres = [r for part in gather_objects(results) for r in part]
