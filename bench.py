@@ -34,6 +34,20 @@ from suta_amd.weights import synth_weights  # noqa: E402
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
 BF16_SPLIT_PEAK_TFLOPS = 2500.0 / 6  # bf16 dense MFMA peak / 6 products per fp32-equivalent MAC
 RECORD = [0, 1, 3, 5, 10]
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r1", "pmc_traffic.json")
+GEMM_KERNELS = ("gemm_glds_kernel", "gemm_f32_kernel")
+
+
+def gemm_traffic(args):
+    """HBM bytes per GEMM launch from the committed rocprofv3 PMC passes of this same workload
+    (profiles/r1/README.md); None for other workloads."""
+    if not (args.model == "wav2vec2-base" and args.batch == 64 and args.n_samples == 128000 and args.suta_steps == 10
+            and os.path.exists(PMC_TRAFFIC)):
+        return None
+    d = json.load(open(PMC_TRAFFIC))
+    n = sum(d[k]["launches"] for k in GEMM_KERNELS if k in d)
+    b = sum(d[k]["launches"] * d[k]["hbm_bytes_per_launch"] for k in GEMM_KERNELS if k in d)
+    return round(b / n) if n else None
 
 
 def cpu_baseline(cfg, n_samples, suta_steps, budget_s=25.0):
@@ -139,11 +153,15 @@ def main():
         # dominant kernel family: the fp32 MFMA GEMM (every conv/linear/attention product)
         gemm_flops = flops_utt * B * args.steps  # per-rank algorithmic GEMM-shaped FLOPs
         achieved = gemm_flops / (gms / 1000.0) / 1e12 if gms > 0 else None
+        traffic = gemm_traffic(args)
         out["roofline"] = {"bound": "mfma", "achieved": round(achieved, 3) if achieved else None,
                            "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                            "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4) if achieved else None,
-                           "traffic": None,
-                           "kernel": "gemm_f32_kernel (all launches)",
+                           "traffic": traffic,
+                           "traffic_unit": "HBM bytes per GEMM launch",
+                           "traffic_source": "profiles/r1/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE "
+                                             "passes of this workload)" if traffic else None,
+                           "kernel": "fp32 MFMA GEMM family: gemm_glds_kernel + gemm_f32_kernel (all launches)",
                            "launches": int(gn), "avg_launch_ms": round(gms / max(1, gn), 5)}
         out["time_breakdown_ms"] = {k: round(v[0], 2) for k, v in timing.items()}
     if args.also_split and args.precision == "fp32":
