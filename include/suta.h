@@ -83,6 +83,8 @@ typedef struct suta_hparams {
     int32_t train_feature;/* --train_feature */
     int32_t bias_only;    /* --bias_only */
     int32_t episodic;     /* --episodic: reset every slot before adapting */
+    float pl_coef;        /* SDPL (main_SDPL.py:143-209): loss = (1 - pl_coef) * SUTA + pl_coef *
+                             pseudo-label CTC; 0 = SUTA only (main.py); main_SDPL's driver passes 1 */
 } suta_hparams;
 
 /* Weights: `n` tensors named by their HF state_dict key (e.g.

@@ -19,6 +19,8 @@ PyTorch-CPU functional restatement of the reference's SUTA adapt loop:
                                per `optimizer.step()` with the same gradient
   * episodic adapt loop      — reference main.py:319-402 (vanilla forward,
                                then `steps` x forward_and_adapt main.py:172-215)
+  * SDPL pseudo-label loss   — reference main_SDPL.py:143-209 (torch CPU CTCLoss
+                               on the time-log-softmax; target = greedy transcript)
 
 Parameters are a dict keyed by the HF `state_dict()` names; the config is a dict
 with HF `Wav2Vec2Config` key names.
@@ -230,6 +232,48 @@ def suta_loss(logits: torch.Tensor, em_coef: float, reweight: bool, temp: float,
 
 
 # ----------------------------------------------------------------------------------------------
+# SDPL objective (reference main_SDPL.py:143-209)
+# ----------------------------------------------------------------------------------------------
+SPECIAL_IDS = (1, 2, 3)  # <s>, </s>, <unk>: decoded as several characters -> the reference's vocab lookup raises
+
+
+def pseudo_label_target(ids: Sequence[int]) -> List[int]:
+    """processor.batch_decode(argmax)[0] mapped back through vocab.json (main_SDPL.py:194-200): collapse
+    repeats, drop blank 0, '|' (4) <-> ' ', strip() -> leading/trailing delimiters dropped."""
+    out, prev = [], None
+    for i in ids:
+        i = int(i)
+        if i == prev:
+            continue
+        prev = i
+        if i != 0:
+            out.append(i)
+    while out and out[0] == 4:
+        out.pop(0)
+    while out and out[-1] == 4:
+        out.pop()
+    if any(i in SPECIAL_IDS for i in out):
+        raise KeyError("special token in the pseudo-label transcript (reference vocab lookup fails)")
+    return out
+
+
+def pseudo_labeling_loss(logits: torch.Tensor) -> torch.Tensor:
+    """nn.CTCLoss(blank=0)(outputs.log_softmax(1).transpose(1, 0), target) (main_SDPL.py:192-209): the
+    log-softmax is over TIME (dim 1 of (1, T, V)); reduction 'mean' divides by the target length."""
+    target = pseudo_label_target(logits.argmax(-1)[0].tolist())
+    logp = logits.log_softmax(1).transpose(1, 0)                                 # (T, 1, V)
+    return F.ctc_loss(logp, torch.tensor(target, dtype=torch.int32), torch.tensor([logp.shape[0]]),
+                      torch.tensor([len(target)]), blank=0, reduction="mean", zero_infinity=False)
+
+
+def sdpl_loss(logits: torch.Tensor, em_coef: float, reweight: bool, temp: float, non_blank: bool,
+              pl_coef: float, div_coef: float = 0.0) -> torch.Tensor:
+    """loss * (1 - pl_coef) + pseudo_labeling_loss * pl_coef (main_SDPL.py:180)."""
+    return suta_loss(logits, em_coef, reweight, temp, non_blank, div_coef) * (1 - pl_coef) + \
+        pseudo_labeling_loss(logits) * pl_coef
+
+
+# ----------------------------------------------------------------------------------------------
 # AdamW single-tensor path with duplicate-entry multiplicity
 # ----------------------------------------------------------------------------------------------
 class AdamState:
@@ -269,7 +313,7 @@ def adam_step(params: Dict[str, torch.Tensor], grads: Dict[str, torch.Tensor], s
 # ----------------------------------------------------------------------------------------------
 def run_suta(params0: Dict[str, torch.Tensor], cfg: dict, x: torch.Tensor, steps: int, *, lr=2e-5, temp=2.5,
              em_coef=0.3, reweight=True, non_blank=True, div_coef=0.0, train_feature=True, bias_only=False,
-             record: Sequence[int] = None) -> Tuple[Dict[int, torch.Tensor], Dict[str, torch.Tensor]]:
+             record: Sequence[int] = None, pl_coef: float = 0.0) -> Tuple[Dict[int, torch.Tensor], Dict[str, torch.Tensor]]:
     """Returns ({r: logits after r updates} for r in record (0 = vanilla), final trainable tensors).
 
     Uses the minimal schedule (S+1 forwards, S backwards): the re-inference forward of
@@ -290,7 +334,10 @@ def run_suta(params0: Dict[str, torch.Tensor], cfg: dict, x: torch.Tensor, steps
             out[i] = logits.detach().clone()
         if i == steps:
             break
-        loss = suta_loss(logits, em_coef, reweight, temp, non_blank, div_coef)
+        if pl_coef > 0:  # SDPL (main_SDPL.py:143-186)
+            loss = sdpl_loss(logits, em_coef, reweight, temp, non_blank, pl_coef, div_coef)
+        else:
+            loss = suta_loss(logits, em_coef, reweight, temp, non_blank, div_coef)
         grads = torch.autograd.grad(loss, [params[n] for n in uniq])
         adam_step(params, dict(zip(uniq, grads)), state, entries, lr)
     return out, {n: params[n].detach().clone() for n in uniq}

@@ -162,6 +162,21 @@ struct suta_engine {
     // workspace
     DevBuf ws;
     Plan plan;
+    DevBuf sdpl_ws;  // SDPL CTC scratch (+ error flag), allocated on first use
+    bool sdpl_used = false;
+    int* sdpl_err = nullptr;
+    // after a call that ran the SDPL objective: a pseudo-label transcript held <s>, </s> or <unk>
+    void check_sdpl() {
+        if (!sdpl_used) return;
+        int e = 0;
+        HIPCHK(hipMemcpy(&e, sdpl_err, sizeof(int), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemset(sdpl_err, 0, sizeof(int)));
+        sdpl_used = false;
+        if (e)
+            throw SutaError(SUTA_ERR_UNSUPPORTED,
+                            "SDPL pseudo label contains a special token (<s>, </s>, <unk>): the reference's "
+                            "vocab lookup raises KeyError (main_SDPL.py:196-200)");
+    }
     // timing
     bool timing = false;
     double fam_ms[NFAM] = {0};
@@ -713,6 +728,19 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
     LossHP lh{hp.temp, hp.em_coef, hp.div_coef, hp.reweight, hp.non_blank};
     timed(F_LOSS,
           [&] { launch_suta_loss(pl.logits, B, T, k.V, lh, rT(), pl.dlogits, pl.loss, pl.loss_scratch, st); });
+    if (hp.pl_coef > 0.f) {  // SDPL: (1 - pl) * SUTA + pl * pseudo-label CTC (main_SDPL.py:143-209)
+        if (k.V > 32) throw SutaError(SUTA_ERR_UNSUPPORTED, "SDPL objective needs vocab_size <= 32");
+        const long per = sdpl_scratch_floats(T);
+        // [error flag | 63 pad | B x per-utterance scratch]: the flag stays at a fixed offset
+        if (sdpl_ws.alloc(((size_t)B * per + 64) * sizeof(float)))
+            HIPCHK(hipMemsetAsync(sdpl_ws.p, 0, sdpl_ws.bytes, st));
+        int* err = reinterpret_cast<int*>(sdpl_ws.p);
+        timed(F_LOSS, [&] {
+            launch_sdpl_loss(pl.logits, B, T, k.V, hp.pl_coef, rT(), pl.dlogits, pl.loss, sdpl_ws.p + 64, err, st);
+        });
+        sdpl_used = true;
+        sdpl_err = err;
+    }
 
     auto nn_gemm = [&](const float* A, int lda, const float* Bm, int ldb, float* C, int ldc, int M, int N, int K,
                        int epi, const float* R, int ldr, const float* aux, int ldaux) {
@@ -1419,6 +1447,7 @@ int32_t suta_forward(suta_engine* e, const float* wav, int32_t on_dev, int32_t n
                               e->st));
         HIPCHK(hipStreamSynchronize(e->st));
         if (e->timing) e->collect_timing();
+        e->check_sdpl();
     });
 }
 
@@ -1440,6 +1469,7 @@ int32_t suta_step(suta_engine* e, const float* wav, int32_t on_dev, int32_t norm
                               e->st));
         HIPCHK(hipStreamSynchronize(e->st));
         if (e->timing) e->collect_timing();
+        e->check_sdpl();
     });
 }
 
@@ -1483,6 +1513,7 @@ static void adapt_impl(suta_engine* e, const float* wav, int32_t on_dev, int32_t
     }
     HIPCHK(hipStreamSynchronize(e->st));
     if (e->timing) e->collect_timing();
+    e->check_sdpl();
 }
 
 extern "C" {
@@ -1526,9 +1557,22 @@ int32_t suta_loss_grad(suta_engine* e, const float* logits, int32_t batch, int64
         HIPCHK(hipMemcpyAsync(dl, logits, n * 4, hipMemcpyHostToDevice, e->st));
         LossHP lh{hp->temp, hp->em_coef, hp->div_coef, hp->reweight, hp->non_blank};
         launch_suta_loss(dl, batch, (int)frames, V, lh, nullptr, dd, ls, scr, e->st);
+        DevBuf sbuf;
+        if (hp->pl_coef > 0.f) {
+            if (V > 32) throw SutaError(SUTA_ERR_UNSUPPORTED, "SDPL objective needs vocab_size <= 32");
+            if (frames > 2048) throw SutaError(SUTA_ERR_UNSUPPORTED, "T > 2048 frames");
+            const long per = sdpl_scratch_floats((int)frames);
+            sbuf.alloc(((size_t)batch * per + 64) * sizeof(float));
+            HIPCHK(hipMemsetAsync(sbuf.p, 0, sbuf.bytes, e->st));
+            int* err = reinterpret_cast<int*>(sbuf.p);
+            launch_sdpl_loss(dl, batch, (int)frames, V, hp->pl_coef, nullptr, dd, ls, sbuf.p + 64, err, e->st);
+            e->sdpl_used = true;
+            e->sdpl_err = err;
+        }
         HIPCHK(hipMemcpyAsync(dlogits_out, dd, n * 4, hipMemcpyDeviceToHost, e->st));
         HIPCHK(hipMemcpyAsync(loss_out, ls, (size_t)batch * 4, hipMemcpyDeviceToHost, e->st));
         HIPCHK(hipStreamSynchronize(e->st));
+        e->check_sdpl();
     });
 }
 

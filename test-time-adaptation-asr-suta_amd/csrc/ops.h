@@ -62,6 +62,13 @@ struct LossHP {
 void launch_suta_loss(const float* logits, int B, int T, int V, LossHP hp, const int* tlen, float* dlogits, float* loss,
                       float* scratch, hipStream_t st);
 
+// SDPL pseudo-label CTC objective (main_SDPL.py:143-209; sdpl.hip): mixes pl_coef * L_ctc into the
+// SUTA loss / gradient already in loss / dlogits (V <= 32).  scratch: B * sdpl_scratch_floats(T)
+// floats; *err |= 1 when a pseudo-label transcript holds a special token (the reference raises).
+long sdpl_scratch_floats(int T);
+void launch_sdpl_loss(const float* logits, int B, int T, int V, float pl_coef, const int* tlen, float* dlogits,
+                      float* loss, float* scratch, int* err, hipStream_t st);
+
 // Argmax ids per frame (first max, like torch.argmax), optional copy of logits.
 void launch_argmax(const float* logits, long rows, int V, int* ids, hipStream_t st);
 

@@ -37,7 +37,7 @@ class HParamsC(C.Structure):
     _fields_ = [("lr", C.c_float), ("temp", C.c_float), ("em_coef", C.c_float), ("div_coef", C.c_float),
                 ("beta1", C.c_float), ("beta2", C.c_float), ("adam_eps", C.c_float), ("weight_decay", C.c_float),
                 ("reweight", C.c_int32), ("non_blank", C.c_int32), ("train_feature", C.c_int32),
-                ("bias_only", C.c_int32), ("episodic", C.c_int32)]
+                ("bias_only", C.c_int32), ("episodic", C.c_int32), ("pl_coef", C.c_float)]
 
 
 @dataclass
@@ -55,11 +55,12 @@ class SutaHParams:
     betas: tuple = (0.9, 0.999)
     eps: float = 1e-8
     weight_decay: float = 0.0
+    pl_coef: float = 0.0  # SDPL mix (main_SDPL.py:143-209); 0 = SUTA
 
     def to_c(self) -> HParamsC:
         return HParamsC(self.lr, self.temp, self.em_coef, self.div_coef, self.betas[0], self.betas[1], self.eps,
                         self.weight_decay, int(self.reweight), int(self.non_blank), int(self.train_feature),
-                        int(self.bias_only), int(self.episodic))
+                        int(self.bias_only), int(self.episodic), float(self.pl_coef))
 
 
 _lib = None

@@ -28,18 +28,19 @@ SAMPLE_RATE = 16000
 CHECKPOINTS = (1, 3, 5, 10, 20, 40)
 
 
-def build_parser():
+def build_parser(sdpl: bool = False):
+    """main.py:221-241 flags; sdpl: main_SDPL.py's (steps 10, opt Adam, em_coef 1, --pl_coef)."""
     p = argparse.ArgumentParser(description="TTA ASR")
     p.add_argument("--asr", type=str, default="facebook/wav2vec2-base-960h")
-    p.add_argument("--steps", type=int, default=40)
+    p.add_argument("--steps", type=int, default=10 if sdpl else 40)
     p.add_argument("--episodic", action="store_true")
     p.add_argument("--div_coef", type=float, default=0.0)
-    p.add_argument("--opt", type=str, default="AdamW")
+    p.add_argument("--opt", type=str, default="Adam" if sdpl else "AdamW")
     p.add_argument("--dataset_name", type=str, default="librispeech")
     p.add_argument("--dataset_dir", type=str, default="/home/daniel094144/data/LibriSpeech")
     p.add_argument("--split", default=["test-other"])
     p.add_argument("--lr", type=float, default=1e-4)
-    p.add_argument("--em_coef", type=float, default=1.0)
+    p.add_argument("--em_coef", type=float, default=1.0)  # (both scripts)
     p.add_argument("--reweight", action="store_true")
     p.add_argument("--bias_only", action="store_true")
     p.add_argument("--train_feature", action="store_true")
@@ -50,6 +51,8 @@ def build_parser():
     p.add_argument("--log_dir", type=str, default="./exps")
     p.add_argument("--extra_noise", type=float, default=0.0)
     p.add_argument("--scheduler", default=None)
+    if sdpl:
+        p.add_argument("--pl_coef", type=float, default=1)
     # engine-only options
     p.add_argument("--synthetic_weights", action="store_true", help="seeded random weights (no checkpoint)")
     p.add_argument("--device", type=int, default=None)
@@ -58,12 +61,15 @@ def build_parser():
     return p
 
 
-def exp_name_of(a) -> str:
-    """main.py:267."""
-    return (a.dataset_name + "_" + str(a.em_coef) + "_" + str(a.steps) + "_" + str(a.temp) + "_" +
+def exp_name_of(a, sdpl: bool = False) -> str:
+    """main.py:267 (main_SDPL.py:266 when sdpl)."""
+    base = (a.dataset_name + "_" + str(a.em_coef) + "_" + str(a.steps) + "_" + str(a.temp) + "_" +
             a.asr.split("/")[-1] + "_" + "non_blank" + str(a.non_blank) + "_noise_" + str(a.extra_noise) + "_rew_" +
             str(a.reweight) + "_div_" + str(a.div_coef) + "_bias_" + str(a.bias_only) + "_feat_" +
-            str(a.train_feature) + "_all_" + str(a.train_all) + "_LN_" + str(True))
+            str(a.train_feature))
+    if sdpl:
+        return base + "_se_" + "_pl_" + str(a.pl_coef)
+    return base + "_all_" + str(a.train_all) + "_LN_" + str(True)
 
 
 def load_model(asr: str, synthetic: bool):
@@ -83,8 +89,13 @@ def load_model(asr: str, synthetic: bool):
     return cfg, synth_weights(cfg)
 
 
-def main(argv=None):
-    a = build_parser().parse_args(argv)
+def main(argv=None, sdpl: bool = False):
+    """sdpl: the main_SDPL.py driver (pseudo-label CTC objective, main_SDPL.py:143-209).  As there, the
+    adaptation loss uses pl_coef = 1 whatever --pl_coef says (main_SDPL.py:345-346 passes `pl_coef=1.`);
+    --pl_coef only enters the experiment name and log."""
+    a = build_parser(sdpl).parse_args(argv)
+    if sdpl:
+        a.train_all = False
     if a.opt not in ("AdamW", "Adam"):
         raise SystemExit(f"--opt {a.opt}: only AdamW/Adam are implemented by the engine")
     if a.scheduler is not None:
@@ -111,23 +122,27 @@ def main(argv=None):
     from .engine import SutaEngine, SutaHParams
     from .synth import normalize
 
-    exp_name = exp_name_of(a)
+    exp_name = exp_name_of(a, sdpl)
+    if sdpl:
+        from .decode import VOCAB
+        say({t: i for i, t in enumerate(VOCAB)})  # main_SDPL.py:269-271 prints vocab.json
     dataset = load_dataset(a.split, a.dataset_name, a.dataset_dir, a.batch_size, a.extra_noise)
     say("------------------------------------")
     say(f"exp: {exp_name}")
+    tail = ((f"pl_coef = {a.pl_coef}",) if sdpl else (f"train_all = {a.train_all}", f"train_LN = {True}"))
     for line in (f"eposidic? {a.episodic}", f"lr = {a.lr}", f"optim = {a.opt}", f"step = {a.steps}",
                  f"em_coef = {a.em_coef}", f"reweight = {a.reweight}", f"batch size = {a.batch_size}",
                  f"temperature = {a.temp}", f"non_blank = {str(a.non_blank)}", f"extra_noise = {a.extra_noise}",
                  f"scheduler = {str(a.scheduler)}", f"div_coef = {str(a.div_coef)}", f"bias_only = {a.bias_only}",
-                 f"train_feature = {a.train_feature}", f"train_all = {a.train_all}", f"train_LN = {True}"):
+                 f"train_feature = {a.train_feature}") + tail:
         say(line)
 
     cfg, weights = load_model(a.asr, a.synthetic_weights)
     gb = max(1, a.gpu_batch) if a.episodic else 1  # non-episodic adaptation is sequential
     engine = SutaEngine(cfg, weights, device=device, max_batch=gb)
-    hp = SutaHParams(lr=a.lr, temp=a.temp, em_coef=a.em_coef, div_coef=a.div_coef, reweight=a.reweight,
-                     non_blank=a.non_blank, train_feature=a.train_feature, bias_only=a.bias_only,
-                     episodic=a.episodic)
+    hp = SutaHParams(lr=a.lr, temp=a.temp, em_coef=a.em_coef, div_coef=0.0 if sdpl else a.div_coef,
+                     reweight=a.reweight, non_blank=a.non_blank, train_feature=a.train_feature,
+                     bias_only=a.bias_only, episodic=a.episodic, pl_coef=1.0 if sdpl else 0.0)
     record = [0] + ([c for c in CHECKPOINTS if c <= a.steps] if a.episodic else [])
     if not a.episodic:
         record = sorted(set([0, a.steps]))
@@ -209,13 +224,15 @@ def main(argv=None):
         if a.steps >= 40:
             lines.append(f"TTA-40 WER: {cw(40)}")
         print("asr:", a.asr)
-        print("non-adapted count = 0")
-        print(f"dataset num = {len(batches)}")
+        if not sdpl:  # main_SDPL.py:395-407 prints neither line and writes no CSV
+            print("non-adapted count = 0")
+            print(f"dataset num = {len(batches)}")
         for ln in lines:
             print(ln)
         print("------------------------------------")
         print(f"[suta_amd] adapted {len(allres)} utterances in {elapsed:.1f} s on rank 0's shard, {world} rank(s)")
         os.makedirs(a.log_dir, exist_ok=True)
+        tail = ((f"pl_coef = {a.pl_coef}",) if sdpl else (f"train_all = {str(a.train_all)}", f"train_LN = {str(True)}"))
         with open(os.path.join(a.log_dir, exp_name), "w") as f:
             for ln in lines:
                 f.write(ln + "\n")
@@ -223,13 +240,13 @@ def main(argv=None):
                        f"em_coef = {a.em_coef}", f"reweight = {a.reweight}", f"batch size = {a.batch_size}",
                        f"temperature = {a.temp}", f"non_blank = {str(a.non_blank)}", f"extra_noise = {a.extra_noise}",
                        f"scheduler = {str(a.scheduler)}", f"div_coef = {str(a.div_coef)}",
-                       f"bias_only = {str(a.bias_only)}", f"train_feature = {str(a.train_feature)}",
-                       f"train_all = {str(a.train_all)}", f"train_LN = {str(True)}"):
+                       f"bias_only = {str(a.bias_only)}", f"train_feature = {str(a.train_feature)}") + tail:
                 f.write(ln + "\n")
-        import pandas as pd
-        durations = [r["duration"] for r in allres]
-        werrs = [r.get("werr", np.nan) for r in allres]
-        pd.DataFrame({"duration": durations, "WERR": werrs}).to_csv(os.path.join(a.log_dir, exp_name + ".csv"))
+        if not sdpl:
+            import pandas as pd
+            durations = [r["duration"] for r in allres]
+            werrs = [r.get("werr", np.nan) for r in allres]
+            pd.DataFrame({"duration": durations, "WERR": werrs}).to_csv(os.path.join(a.log_dir, exp_name + ".csv"))
     engine.close()
     if world > 1:
         import torch.distributed as tdist

@@ -18,6 +18,15 @@ Fixtures written next to this file:
                      every step + final trainable tensors
   g4_base_<N>.npz    base-size (w2v2-base shapes) SUTA, canonical scripts/LS.sh flags:
                      logits at steps 0,1,3,5,10 + digests of the adapted tensors
+  g5_ctc_decode.json HF Wav2Vec2CTCTokenizer.batch_decode on the reference vocab.json
+  g6_sdpl_loss.npz   SDPL pseudo-label CTC loss + dL/dlogits through the reference
+                     main_SDPL.forward_and_adapt (main_SDPL.py:143-209) with a fake model
+  g6_sdpl_tiny_<variant>.npz  tiny-config episodic SDPL runs (main_SDPL.py:327-349)
+
+main_SDPL.py is imported the same way, after transformers (so transformers' own soundfile
+probe sees the real environment) with stub `jiwer` and `soundfile` modules (neither is
+installed; neither is called here); its processor is built locally from the reference
+vocab.json (no network).
 """
 import contextlib
 import hashlib
@@ -49,6 +58,27 @@ def import_reference():
     import main as ref  # noqa: E402
     sys.path.remove(REF)
     return ref
+
+
+def import_reference_sdpl():
+    import transformers  # noqa: F401  (before the soundfile stub)
+    from transformers import Wav2Vec2ForCTC, Wav2Vec2Processor  # noqa: F401
+    if "jiwer" not in sys.modules:
+        jiwer = types.ModuleType("jiwer")
+        jiwer.wer = lambda *a, **k: float("nan")
+        sys.modules["jiwer"] = jiwer
+    sys.modules.setdefault("soundfile", types.ModuleType("soundfile"))
+    sys.path.insert(0, REF)
+    import main_SDPL as sdpl  # noqa: E402
+    sys.path.remove(REF)
+    return sdpl
+
+
+def local_processor():
+    from transformers import Wav2Vec2CTCTokenizer, Wav2Vec2FeatureExtractor, Wav2Vec2Processor
+    fe = Wav2Vec2FeatureExtractor(feature_size=1, sampling_rate=16000, padding_value=0.0, do_normalize=True,
+                                  return_attention_mask=False)
+    return Wav2Vec2Processor(feature_extractor=fe, tokenizer=Wav2Vec2CTCTokenizer(os.path.join(REF, "vocab.json")))
 
 
 def weights_digest(sd):
@@ -221,9 +251,107 @@ def g5(ref):
         json.dump(cases, f)
 
 
+def _sdpl_logits(rng, T, kind):
+    """Random logits whose greedy path avoids the special tokens <s>, </s>, <unk> (ids 1-3): the
+    reference maps every decoded character through vocab.json and raises KeyError on '<'."""
+    L = (rng.standard_normal((1, T, 32)) * 3).astype(np.float32)
+    L[..., 1:4] -= 40.0
+    if kind == "blanky":
+        L[..., 0] += 3.0
+    elif kind == "allblank":
+        L[..., 0] += 60.0
+    elif kind == "delims":  # leading / trailing / doubled word delimiters (stripped / kept by decode)
+        L[0, :2, 4] += 40.0
+        L[0, -3:, 4] += 40.0
+        L[0, T // 2, 4] += 40.0
+        L[0, T // 2 + 2, 4] += 40.0
+    elif kind == "repeats":  # same letter in consecutive segments: CTC needs a blank between them
+        for t in range(0, T, 3):
+            L[0, t, 15] += 40.0
+        L[0, 1::6, 0] += 60.0
+    return L
+
+
+def g6(ref):
+    import json
+    sdpl = import_reference_sdpl()
+    proc = local_processor()
+    vocab = json.load(open(os.path.join(REF, "vocab.json")))
+    rng = np.random.default_rng(6)
+    # (name, T, kind, em, reweight, non_blank, pl_coef)
+    specs = [("pl_T7", 7, "plain", 1.0, False, True, 1.0), ("pl_T49", 49, "plain", 1.0, False, True, 1.0),
+             ("pl_T120_blanky", 120, "blanky", 1.0, False, True, 1.0), ("pl_T399", 399, "blanky", 1.0, False, True, 1.0),
+             ("pl_allblank_T49", 49, "allblank", 1.0, False, True, 1.0),
+             ("pl_delims_T60", 60, "delims", 1.0, False, True, 1.0),
+             ("pl_repeats_T48", 48, "repeats", 1.0, False, True, 1.0),
+             ("mix_T49", 49, "blanky", 0.3, True, True, 0.5), ("mix_T120", 120, "plain", 0.3, True, True, 0.25)]
+    out, cases = {}, []
+    for name, T, kind, em, rw, nb, pl in specs:
+        L = _sdpl_logits(rng, T, kind)
+        for dt in (torch.float32, torch.float64):
+            fake = _FakeLogits(torch.from_numpy(L).to(dt))
+            grads, losses = [], []
+            fake.L.register_post_accumulate_grad_hook(lambda p: grads.append(p.grad.detach().clone()))
+            orig = torch.Tensor.backward
+
+            def bw(self, *a, **k):
+                losses.append(self.detach().clone())
+                return orig(self, *a, **k)
+            torch.Tensor.backward = bw
+            try:
+                opt = torch.optim.SGD([fake.L], lr=1.0)
+                sdpl.forward_and_adapt(None, fake, opt, em, rw, 2.5, nb, None, 0, True, pl, vocab, proc)
+            finally:
+                torch.Tensor.backward = orig
+            tag = "f32" if dt == torch.float32 else "f64"
+            out[f"{name}/grad_{tag}"] = grads[0][0].numpy()
+            out[f"{name}/loss_{tag}"] = np.array(losses[0].item())
+        out[f"{name}/logits"] = L[0]
+        out[f"{name}/hp"] = np.array([2.5, em, float(rw), float(nb), pl])
+        ids = L[0].argmax(-1)
+        out[f"{name}/transcript"] = np.array(proc.batch_decode(torch.from_numpy(ids)[None])[0])
+        cases.append(name)
+    out["cases"] = np.array(cases)
+    np.savez_compressed(os.path.join(HERE, "g6_sdpl_loss.npz"), **out)
+    print("g6 loss done")
+
+    # tiny episodic SDPL runs: reference defaults opt 'Adam', lr 1e-4, em_coef 1; the driver
+    # hard-codes pl_coef=1. and div_coef=0 in its forward_and_adapt call (main_SDPL.py:345-346)
+    from transformers import Wav2Vec2Config, Wav2Vec2ForCTC
+    for vname, preset, lr in (("group", "tiny-group", 1e-4), ("layer", "tiny-layer", 5e-4)):
+        cfg = get_config(preset)
+        sd = synth_weights(cfg, blank_bias=0.0)
+        sd["lm_head.bias"][1:4] -= 30.0  # keep <s>, </s>, <unk> off the greedy path (reference KeyError)
+        res = {"weights_sha256": np.array(weights_digest(sd)), "lr": np.array(lr)}
+        for j, n in enumerate((8000, 12345)):
+            x = wave(n, 60 + j)
+            torch.manual_seed(0)
+            model = Wav2Vec2ForCTC(Wav2Vec2Config(**cfg)).eval()
+            model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+            model = sdpl.configure_model(model)
+            with contextlib.redirect_stdout(io.StringIO()):
+                params, names = sdpl.collect_params(model, False, True)
+                opt, sch = sdpl.setup_optimizer(params, "Adam", lr, scheduler=None)
+            xt = torch.from_numpy(x)[None]
+            logits = []
+            with torch.no_grad():
+                logits.append(model(xt).logits[0].numpy().copy())
+            for i in range(5):
+                o = sdpl.forward_and_adapt(xt, model, opt, 1.0, False, 2.5, True, sch, div_coef=0,
+                                           repeat_inference=True, pl_coef=1., vocab=vocab, processor=proc)
+                logits.append(o[0].detach().numpy().copy())
+            res[f"N{n}/x"] = x
+            res[f"N{n}/logits"] = np.stack(logits)
+            sdf = model.state_dict()
+            for k in dict.fromkeys(names):
+                res[f"N{n}/final/{k}"] = sdf[k].numpy().copy()
+        np.savez_compressed(os.path.join(HERE, f"g6_sdpl_tiny_{vname}.npz"), **res)
+        print("g6", vname, "done")
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
     ref = import_reference()
-    which = sys.argv[1:] or ["g1", "g2", "g3", "g4", "g5"]
+    which = sys.argv[1:] or ["g1", "g2", "g3", "g4", "g5", "g6"]
     for w in which:
         globals()[w](ref)

@@ -30,3 +30,27 @@ def logits_tol(lr):
     lr 5e-4 (adaptation moves logits by ~5 there), so fp32 reordering noise grows with lr.
     """
     return 2e-5 + 0.2 * lr
+
+
+def sdpl_logits_tol(lr, step):
+    """Absolute logits tolerance after `step` SDPL steps.
+
+    The pseudo-label CTC gradient through the time log-softmax is exactly zero in exact arithmetic
+    for every class outside the pseudo label (g = exp(lp)/U and sum_t softmax_t = 1), so those logit
+    gradients are pure fp32 rounding noise, which Adam turns into +-lr steps of implementation-
+    dependent sign.  Two fp32-equivalent implementations therefore drift apart by O(lr) per step:
+    the CPU oracle (fp32 or fp64) and the reference measured up to 6*lr per step on the tiny goldens,
+    libsuta and the reference up to 10*lr.  Valid while both runs adapt toward the same pseudo
+    label: a greedy flip on one frame changes the CTC target and the trajectories separate
+    (same_pseudo_labels below).
+    """
+    return 2e-5 + 12.0 * lr * step
+
+
+def same_pseudo_labels(logits_a, logits_b, upto):
+    """True when the greedy pseudo-label transcripts of two runs agree at every step < upto."""
+    from oracle.w2v2_cpu import pseudo_label_target
+    for i in range(upto):
+        if pseudo_label_target(logits_a[i].argmax(-1)) != pseudo_label_target(logits_b[i].argmax(-1)):
+            return False
+    return True

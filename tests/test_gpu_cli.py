@@ -66,3 +66,40 @@ def test_cli_end_to_end_matches_oracle(tmp_path, capsys, gpu_batch):
             hyps[k].append(batch_decode(lg[k].argmax(-1).numpy())[0])
     for k in hyps:
         assert tuple(counts[str(k)]) == wer_counts(list(ds.text), hyps[k]), k
+
+
+def test_sdpl_cli_end_to_end(tmp_path, capsys):
+    """main_SDPL.py drop-in: runs, prints the reference's lines, writes its log; the vanilla (step 0)
+    WER equals the oracle's.  Adapted WERs follow pseudo-label trajectories that a single greedy flip
+    can redirect (tests/parity.sdpl_logits_tol), so they are checked for presence, not equality."""
+    import json
+    from safetensors.numpy import save_file
+    from oracle import w2v2_cpu as W
+    _corpus(tmp_path)
+    # a local checkpoint whose greedy path avoids <s>, </s>, <unk> (the reference raises KeyError there)
+    cfg = get_config("tiny-group")
+    sdn = synth_weights(cfg)
+    sdn["lm_head.bias"][1:4] -= 30.0
+    ck = tmp_path / "ckpt"
+    ck.mkdir()
+    json.dump(cfg, open(ck / "config.json", "w"))
+    save_file(sdn, str(ck / "model.safetensors"))
+    args = (f"--asr {ck} --steps 10 --dataset_name chime --dataset_dir {tmp_path} "
+            f"--episodic --log_dir {tmp_path}/exps --train_feature --pl_coef 1").split()
+    counts = M.main(args, sdpl=True)
+    out = capsys.readouterr().out
+    assert "'<pad>': 0" in out and "pl_coef = 1.0" in out and "adapt-10 WER: " in out and "TTA-10 WER:" in out
+    a = M.build_parser(sdpl=True).parse_args(args)
+    log = open(os.path.join(a.log_dir, M.exp_name_of(a, sdpl=True))).read().splitlines()
+    assert log[0].startswith("original WER: ") and log[-1] == "pl_coef = 1.0"
+    sd = {k: torch.from_numpy(v) for k, v in sdn.items()}
+    from suta_amd.data import CHiMEDataset
+    ds = CHiMEDataset(None, 1, str(tmp_path))
+    reader = AudioReader(0.0)
+    hyp0 = []
+    for f in ds.file_list:
+        x = torch.from_numpy(normalize(reader(str(f))))[None]
+        hyp0.append(batch_decode(W.forward(sd, cfg, x).argmax(-1).numpy())[0])
+    assert tuple(counts["0"]) == wer_counts(list(ds.text), hyp0)
+    for k in (1, 3, 5, 10):
+        assert counts[str(k)][1] == counts["0"][1]

@@ -98,6 +98,24 @@ def test_cli_flags_and_exp_name():
                               "_bias_False_feat_True_all_False_LN_True")
 
 
+def test_sdpl_cli_defaults_and_exp_name():
+    """main_SDPL.py:218-241 defaults and its exp_name (main_SDPL.py:266)."""
+    a = build_parser(sdpl=True).parse_args("--asr facebook/wav2vec2-base-960h --dataset_name chime --episodic "
+                                           "--train_feature --pl_coef 0.5".split())
+    assert (a.steps, a.opt, a.em_coef, a.lr, a.pl_coef) == (10, "Adam", 1.0, 1e-4, 0.5)
+    assert exp_name_of(a, sdpl=True) == ("chime_1.0_10_2.5_wav2vec2-base-960h_non_blankFalse_noise_0.0_rew_False_"
+                                         "div_0.0_bias_False_feat_True_se__pl_0.5")
+
+
+def test_sdpl_pseudo_label_target_rules():
+    from oracle.w2v2_cpu import pseudo_label_target
+    # collapse repeats, drop blanks, strip leading/trailing delimiters, keep inner ones
+    assert pseudo_label_target([4, 0, 4, 5, 5, 0, 5, 4, 0, 4, 6, 4, 4]) == [5, 5, 4, 4, 6]
+    assert pseudo_label_target([0, 0, 0]) == []
+    with pytest.raises(KeyError):
+        pseudo_label_target([5, 3, 6])
+
+
 def test_lpt_shard_balances_and_covers():
     rng = np.random.default_rng(3)
     costs = list(rng.uniform(1, 30, size=101))

@@ -13,7 +13,7 @@ from oracle import w2v2_cpu as W
 from oracle.suta_loss_np import suta_loss_and_grad
 from suta_amd.config import get_config
 from suta_amd.weights import synth_weights
-from tests.parity import assert_params_close, logits_tol
+from tests.parity import assert_params_close, logits_tol, same_pseudo_labels, sdpl_logits_tol
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 G = os.path.join(HERE, "golden")
@@ -127,3 +127,49 @@ def test_g4_base_oracle_matches_reference(n):
     for k, v in final.items():
         idx = z[f"final/{k}/idx"]
         assert_params_close(v.numpy().reshape(-1)[idx], z[f"final/{k}/val"], 2e-5, 10, max_frac=0.05, name=k)
+
+
+# ---------------------------------------------------------------------------------------------
+# SDPL (reference main_SDPL.py:143-209): g6 fixtures
+# ---------------------------------------------------------------------------------------------
+def test_g6_sdpl_target_matches_reference_transcript():
+    from suta_amd.decode import VOCAB
+    z = _load("g6_sdpl_loss.npz")
+    for case in z["cases"]:
+        ids = z[f"{case}/logits"].argmax(-1)
+        tgt = W.pseudo_label_target(ids)
+        text = str(z[f"{case}/transcript"])
+        assert "".join(" " if VOCAB[i] == "|" else VOCAB[i] for i in tgt) == text, case
+
+
+def test_g6_sdpl_torch_restatement_matches_reference():
+    z = _load("g6_sdpl_loss.npz")
+    for case in z["cases"]:
+        temp, em, rw, nb, pl = z[f"{case}/hp"]
+        L = torch.tensor(z[f"{case}/logits"][None], dtype=torch.float64, requires_grad=True)
+        loss = W.sdpl_loss(L, em, bool(rw), temp, bool(nb), pl)
+        loss.backward()
+        ref = z[f"{case}/grad_f64"]
+        np.testing.assert_allclose(L.grad[0].numpy(), ref, rtol=1e-9, atol=1e-12, err_msg=case)
+        rl = float(z[f"{case}/loss_f64"])
+        assert (np.isnan(rl) and np.isnan(loss.item())) or abs(loss.item() - rl) <= 1e-9 * max(1, abs(rl)), case
+
+
+@pytest.mark.parametrize("variant", ["group", "layer"])
+def test_g6_sdpl_tiny_oracle_matches_reference(variant):
+    z = _load(f"g6_sdpl_tiny_{variant}.npz")
+    cfg = get_config(f"tiny-{variant}")
+    sd = synth_weights(cfg, blank_bias=0.0)
+    sd["lm_head.bias"][1:4] -= 30.0
+    params = {k: torch.from_numpy(v) for k, v in sd.items()}
+    lr = float(z["lr"])
+    x = torch.from_numpy(z["N8000/x"])[None]
+    out, final = W.run_suta(params, cfg, x, 5, lr=lr, em_coef=1.0, reweight=False, non_blank=True, pl_coef=1.0)
+    for i in range(6):
+        np.testing.assert_allclose(out[i][0].numpy(), z["N8000/logits"][i], rtol=0, atol=sdpl_logits_tol(lr, i),
+                                   err_msg=f"step {i}")
+        assert np.mean(out[i][0].numpy().argmax(-1) == z["N8000/logits"][i].argmax(-1)) >= 0.9
+    for key in z.files:
+        if key.startswith("N8000/final/"):
+            name = key[len("N8000/final/"):]
+            assert_params_close(final[name].numpy(), z[key], lr, 5, max_frac=1.0, name=name)
