@@ -185,6 +185,30 @@ struct suta_engine {
     std::vector<hipEvent_t> evpool;
     bool use_graphs = true;
     int gemm_mode = 0;  // SUTA_PRECISION_*
+    // Adam step tables on the device (tab[step0][step_size | bc2_sqrt][k-1][j-1]) and the step counter the
+    // kernel reads: a captured SUTA step replays with the right bias corrections
+    float* d_adam_tab = nullptr;
+    long adam_tab_cap = 0;
+    int* d_step = nullptr;
+    int h_step = 0;
+    std::vector<float> h_tab;
+    // one captured SUTA step (backward + Adam + forward) replayed per step of suta_adapt
+    struct GraphKey {
+        int B = 0;
+        long N = 0;
+        int ragged = 0, mode = 0;
+        suta_hparams hp{};
+    };
+    hipGraphExec_t step_graph = nullptr;
+    GraphKey gkey;
+    bool gkey_seen = false;  // the key ran eagerly once (lazy allocations done): capture on its next step
+    void prepare_adam(const suta_hparams& hp, int steps);
+    void suta_step_once(int B, const suta_hparams& hp);
+    void drop_graph() {
+        if (step_graph) (void)hipGraphExecDestroy(step_graph);
+        step_graph = nullptr;
+        gkey_seen = false;
+    }
     std::vector<float*> owned;
 
     ~suta_engine();
@@ -256,6 +280,8 @@ struct suta_engine {
 };
 
 suta_engine::~suta_engine() {
+    if (step_graph) (void)hipGraphExecDestroy(step_graph);
+    if (d_adam_tab) (void)hipFree(d_adam_tab);
     for (float* p : owned) (void)hipFree(p);
     for (auto& pe : pending) {
         (void)hipEventDestroy(pe.second.first);
@@ -270,6 +296,7 @@ suta_engine::~suta_engine() {
 // ----------------------------------------------------------------------------------------------
 void suta_engine::build_plan(int B, long N) {
     if (plan.B == B && plan.N == N) return;
+    drop_graph();
     const Cfg& k = c;
     Plan pl;
     pl.B = B;
@@ -1162,8 +1189,86 @@ void suta_engine::adam(int B, const suta_hparams& hp) {
             a.step_size[kk - 1][j - 1] = (float)(lr / bc1);
             a.bc2_sqrt[kk - 1][j - 1] = (float)std::sqrt(bc2);
         }
-    timed(F_ADAM, [&] { launch_adam(P, G, Mo, Vo, Pn, B, a, st); });
+    a.tab = d_adam_tab;
+    a.step = d_step;
+    timed(F_ADAM, [&] {
+        launch_adam(P, G, Mo, Vo, Pn, B, a, st);
+        launch_step_advance(d_step, st);
+    });
     opt_steps += 1;
+}
+
+// Device Adam tables for optimizer steps [0, opt_steps + steps) and the device step counter = opt_steps.
+void suta_engine::prepare_adam(const suta_hparams& hp, int steps) {
+    const long need = opt_steps + std::max(steps, 1);
+    if (need > adam_tab_cap) {
+        const long cap = std::max<long>(need, 2 * adam_tab_cap);
+        if (d_adam_tab) HIPCHK(hipFree(d_adam_tab));
+        HIPCHK(hipMalloc(&d_adam_tab, cap * 50 * sizeof(float)));
+        adam_tab_cap = cap;
+        drop_graph();  // captured steps point at the old table
+    }
+    const double lr = py_double(hp.lr), b1 = py_double(hp.beta1), b2 = py_double(hp.beta2);
+    h_tab.assign(need * 50, 0.f);
+    for (long s0 = 0; s0 < need; ++s0)
+        for (int kk = 1; kk <= 5; ++kk)
+            for (int j = 1; j <= kk; ++j) {
+                const double t = (double)(s0 * kk + j);
+                h_tab[s0 * 50 + (kk - 1) * 5 + (j - 1)] = (float)(lr / (1.0 - std::pow(b1, t)));
+                h_tab[s0 * 50 + 25 + (kk - 1) * 5 + (j - 1)] = (float)std::sqrt(1.0 - std::pow(b2, t));
+            }
+    h_step = (int)opt_steps;
+    HIPCHK(hipMemcpyAsync(d_adam_tab, h_tab.data(), h_tab.size() * sizeof(float), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_step, &h_step, sizeof(int), hipMemcpyHostToDevice, st));
+    HIPCHK(hipStreamSynchronize(st));  // pageable sources
+}
+
+// One SUTA step after a forward: backward, Adam, forward.  With graphs on (and per-kernel timing off)
+// the step is captured once per (batch, layout, ragged, precision, hparams) key and replayed.
+void suta_engine::suta_step_once(int B, const suta_hparams& hp) {
+    if (!use_graphs || timing) {
+        backward(B, hp);
+        adam(B, hp);
+        forward(B);
+        return;
+    }
+    GraphKey k;
+    k.B = B;
+    k.N = plan.N;
+    k.ragged = plan.ragged;
+    k.mode = gemm_mode;
+    k.hp = hp;
+    const bool same = gkey_seen && gkey.B == k.B && gkey.N == k.N && gkey.ragged == k.ragged &&
+                      gkey.mode == k.mode && std::memcmp(&gkey.hp, &k.hp, sizeof(suta_hparams)) == 0;
+    if (!same) {  // first step of a new key: eager (lazy allocations happen here), capture next time
+        drop_graph();
+        gkey = k;
+        gkey_seen = true;
+        backward(B, hp);
+        adam(B, hp);
+        forward(B);
+        return;
+    }
+    if (!step_graph) {
+        hipGraph_t g = nullptr;
+        HIPCHK(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
+        try {
+            backward(B, hp);
+            adam(B, hp);
+            forward(B);
+        } catch (...) {
+            (void)hipStreamEndCapture(st, &g);
+            if (g) (void)hipGraphDestroy(g);
+            throw;
+        }
+        HIPCHK(hipStreamEndCapture(st, &g));
+        opt_steps -= 1;  // the capture recorded the Adam step without running it
+        HIPCHK(hipGraphInstantiate(&step_graph, g, nullptr, nullptr, 0));
+        HIPCHK(hipGraphDestroy(g));
+    }
+    HIPCHK(hipGraphLaunch(step_graph, st));
+    opt_steps += 1;
+    if (hp.pl_coef > 0.f) sdpl_used = true;  // the replayed SDPL kernels may raise the error flag
 }
 
 void suta_engine::reset_slots(int B) {
@@ -1172,6 +1277,9 @@ void suta_engine::reset_slots(int B) {
     HIPCHK(hipMemsetAsync(Mo, 0, (size_t)B * Pn * sizeof(float), st));
     HIPCHK(hipMemsetAsync(Vo, 0, (size_t)B * Pn * sizeof(float), st));
     opt_steps = 0;
+    h_step = 0;
+    HIPCHK(hipMemcpyAsync(d_step, &h_step, sizeof(int), hipMemcpyHostToDevice, st));
+    HIPCHK(hipStreamSynchronize(st));
 }
 
 void suta_engine::stage_input(const float* wav, int on_dev, int norm, int B, long N, long stride) {
@@ -1263,6 +1371,8 @@ int32_t suta_create(const suta_model_config* cfg, const char* const* names, cons
         e->max_samples = max_samples;
         HIPCHK(hipSetDevice(device));
         HIPCHK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
+        e->d_step = reinterpret_cast<int*>(e->dalloc(1));
+        HIPCHK(hipMemset(e->d_step, 0, sizeof(int)));
         std::map<std::string, std::pair<const float*, long>> w;
         for (int i = 0; i < n; ++i) w[names[i]] = {data[i], numels[i]};
         auto get = [&](const std::string& nm, long numel) -> const float* {
@@ -1459,6 +1569,7 @@ int32_t suta_step(suta_engine* e, const float* wav, int32_t on_dev, int32_t norm
         e->build_plan(batch, n);
         e->set_lengths(batch, nullptr);
         e->stage_input(wav, on_dev, norm, batch, n);
+        e->prepare_adam(*hp, 1);
         e->forward(batch);
         e->backward(batch, *hp);
         e->adam(batch, *hp);
@@ -1494,8 +1605,10 @@ static void adapt_impl(suta_engine* e, const float* wav, int32_t on_dev, int32_t
     const size_t per = (size_t)batch * T * V;
     e->stage_input(wav, on_dev, norm, batch, n, stride);
     if (hp->episodic) e->reset_slots(batch);
+    e->prepare_adam(*hp, steps);
     for (int s = 0; s <= steps; ++s) {
-        e->forward(batch);
+        if (s == 0) e->forward(batch);
+        else e->suta_step_once(batch, *hp);
         for (int i = 0; i < nrec; ++i) {
             if (rec[i] != s) continue;
             if (logits_out)
@@ -1507,9 +1620,6 @@ static void adapt_impl(suta_engine* e, const float* wav, int32_t on_dev, int32_t
                                       hipMemcpyDeviceToHost, e->st));
             }
         }
-        if (s == steps) break;
-        e->backward(batch, *hp);
-        e->adam(batch, *hp);
     }
     HIPCHK(hipStreamSynchronize(e->st));
     if (e->timing) e->collect_timing();

@@ -1123,8 +1123,9 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
             else launch_x6<64, 64, 32, 1>(p, grid, st);
         }
     } else if (g_nbuf >= 3 && p.va && p.vb && (p.ta || p.K % 4 == 0) && (!p.tb || p.K % 4 == 0)) {
-        // LDS-DMA variants: 3 = BK32 x 2 stages, 4 = BK16 x 4, 5 = BK16 x 3, 6 = BK32 x 3
-        if (g_nbuf == 4) launch_glds_tile<16, 4>(tile, p, grid, st);
+        // LDS-DMA variants: 3 = BK32 x 2 stages, 4 = BK16 x 4, 5 = BK16 x 3, 6 = BK32 x 3, 7 = BK64 x 2
+        if (g_nbuf == 7) launch_glds_tile<64, 2>(tile, p, grid, st);
+        else if (g_nbuf == 4) launch_glds_tile<16, 4>(tile, p, grid, st);
         else if (g_nbuf == 5) launch_glds_tile<16, 3>(tile, p, grid, st);
         else if (g_nbuf == 6) launch_glds_tile<32, 3>(tile, p, grid, st);
         else launch_glds_tile<32, 2>(tile, p, grid, st);

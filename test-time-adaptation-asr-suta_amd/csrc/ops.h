@@ -85,6 +85,12 @@ struct AdamArgs {
     // per sub-step j (1-based t = step0*k + j): step_size and sqrt(bias_correction2), indexed [k-1][j-1]
     float step_size[5][5];
     float bc2_sqrt[5][5];
+    // device-resident alternative (graph-replayable): tab[step0][0|1][k-1][j-1] = step_size | bc2_sqrt,
+    // step0 read from *step (advanced by launch_step_advance); used when tab != null
+    const float* tab;
+    const int* step;
 };
+// *step += 1 (one thread): the Adam step counter of graph-replayed SUTA steps.
+void launch_step_advance(int* step, hipStream_t st);
 void launch_adam(float* P, const float* G, float* M, float* V, long pstride, int B, const AdamArgs& a,
                  hipStream_t st);

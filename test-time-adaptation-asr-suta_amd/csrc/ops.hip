@@ -695,6 +695,7 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ P, const 
                                                    AdamArgs a, long total) {
     const int b = blockIdx.y;
     const long base = (long)b * pstride;
+    const float* tab = a.tab ? a.tab + (long)(*a.step) * 50 : nullptr;
     for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
         // map i to (run, offset)
         long rem = i;
@@ -712,8 +713,10 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ P, const 
             if (a.lr_wd != 0.f) p *= 1.0f - a.lr_wd;
             m = m + a.omb1 * (g - m);                 // lerp_(g, 1-beta1), weight < 0.5 form
             v = v * a.beta2 + a.omb2 * (g * g);        // mul_(beta2).addcmul_(g, g, 1-beta2)
-            const float denom = sqrtf(v) / a.bc2_sqrt[k - 1][j] + a.eps;
-            p = p + (-a.step_size[k - 1][j]) * (m / denom);      // addcdiv_(m, denom, -step_size)
+            const float ss = tab ? tab[(k - 1) * 5 + j] : a.step_size[k - 1][j];
+            const float bs = tab ? tab[25 + (k - 1) * 5 + j] : a.bc2_sqrt[k - 1][j];
+            const float denom = sqrtf(v) / bs + a.eps;
+            p = p + (-ss) * (m / denom);                  // addcdiv_(m, denom, -step_size)
         }
         P[idx] = p;
         M[idx] = m;
@@ -804,6 +807,12 @@ void launch_suta_loss(const float* logits, int B, int T, int V, LossHP hp, const
 
 void launch_argmax(const float* logits, long rows, int V, int* ids, hipStream_t st) {
     hipLaunchKernelGGL(argmax_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, st, logits, rows, V, ids);
+}
+
+__global__ void step_advance_kernel(int* step) { *step += 1; }
+
+void launch_step_advance(int* step, hipStream_t st) {
+    hipLaunchKernelGGL(step_advance_kernel, dim3(1), dim3(1), 0, st, step);
 }
 
 void launch_adam(float* P, const float* G, float* M, float* V, long pstride, int B, const AdamArgs& a,

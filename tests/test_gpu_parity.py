@@ -167,6 +167,21 @@ def test_bitwise_deterministic(precision):
     assert np.array_equal(a[3], b[3])
 
 
+@pytest.mark.parametrize("preset,n", [("tiny-group", 11000), ("wav2vec2-base", 32000)])
+def test_graph_replay_equals_eager(preset, n):
+    """suta_adapt replays one captured SUTA step (backward + Adam + forward) per step: bitwise == eager."""
+    eng, cfg = engine(preset)
+    x = synth.batch(n, 2, start=90)
+    hp = SutaHParams(lr=5e-4)
+    eng.set_graphs(False)
+    a, _, _ = eng.adapt(x, 4, hp, record=[1, 2, 4])
+    eng.set_graphs(True)
+    b, _, _ = eng.adapt(x, 4, hp, record=[1, 2, 4])   # step 1 eager (new key), step 2 captured, 3-4 replayed
+    c, _, _ = eng.adapt(x, 4, hp, record=[1, 2, 4])   # every step replayed
+    for r in (1, 2, 4):
+        assert np.array_equal(a[r], b[r]) and np.array_equal(a[r], c[r]), r
+
+
 def test_episodic_reset_restores_pristine_tensors():
     eng, cfg = engine("tiny-layer")
     sd = synth_weights(cfg)

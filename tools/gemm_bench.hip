@@ -89,11 +89,11 @@ int main(int argc, char** argv) {
     hipLaunchKernelGGL(fill, dim3((maxB + 255) / 256), dim3(256), 0, 0, B, maxB, 2u);
     hipStream_t st; CK(hipStreamCreate(&st));
     hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-    const int variants[][2] = {{-1, 1}, {-1, 3}, {0, 3}, {0, 4}, {0, 5}, {0, 6}, {1, 3}, {1, 4},
-                               {3, 3}, {3, 4}, {3, 5}, {3, 6}, {0, 1}, {3, 1}, {-1, 2}};
-    const char* vname[] = {"auto/1buf", "auto/g32x2", "128/g32x2", "128/g16x4", "128/g16x3", "128/g32x3",
-                           "128x64/g32x2", "128x64/g16x4", "64/g32x2", "64/g16x4", "64/g16x3", "64/g32x3",
-                           "128/1buf", "64/1buf", "auto/2buf"};
+    const int variants[][2] = {{-1, 1}, {-1, 3}, {0, 3}, {0, 7}, {0, 5}, {0, 6}, {1, 3}, {1, 7},
+                               {3, 3}, {3, 7}, {2, 3}, {2, 7}, {0, 1}, {3, 1}, {-1, 7}};
+    const char* vname[] = {"auto/1buf", "auto/g32x2", "128/g32x2", "128/g64x2", "128/g16x3", "128/g32x3",
+                           "128x64/g32x2", "128x64/g64x2", "64/g32x2", "64/g64x2", "64x128/g32", "64x128/g64",
+                           "128/1buf", "64/1buf", "auto/g64x2"};
     const int NV = 15;
     bool check = argc < 2 || atoi(argv[1]) != 0;
     int only_v = argc >= 3 ? atoi(argv[2]) : -1;
