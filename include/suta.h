@@ -127,11 +127,12 @@ int32_t suta_adapt(suta_engine* e, const float* wav, int32_t wav_on_device, int3
                    int32_t logits_on_device, int32_t* ids_out, int64_t* frames_out);
 
 /* suta_adapt over a ragged batch: utterance b has n_samples[b] samples at wav + b*stride
- * (stride >= max n_samples), and is adapted exactly as if it were run alone (the reference
+ * (stride >= max n_samples; stride is also the layout length, so a caller can quantise it to
+ * let repeated layouts replay the captured SUTA step), and is adapted exactly as if it were run alone (the reference
  * processes one utterance per forward_and_adapt, main.py:327-398; no padding enters any
  * statistic, softmax or gradient).  frames_out receives `batch` frame counts T_b.  logits_out /
- * ids_out use the layout of the longest utterance: [n_record][batch][Tmax][vocab] / [..][Tmax],
- * Tmax = max T_b; rows t >= T_b of utterance b are padding. */
+ * ids_out use the layout: [n_record][batch][Tl][vocab] / [..][Tl], Tl = suta_num_frames(stride);
+ * rows t >= T_b of utterance b are padding. */
 int32_t suta_adapt_varlen(suta_engine* e, const float* wav, int32_t wav_on_device, int32_t normalize,
                           int32_t batch, const int64_t* n_samples, int64_t stride, int32_t steps,
                           const suta_hparams* hp, const int32_t* record_steps, int32_t n_record,
@@ -173,7 +174,9 @@ int32_t suta_get_timing(suta_engine* e, double* ms_out /*[6]*/, int64_t* launche
 #define SUTA_PRECISION_FP32_SPLIT_BF16 1
 int32_t suta_set_precision(suta_engine* e, int32_t mode);
 
-/* Use hipGraph capture/replay for suta_adapt (default on). */
+/* Use hipGraph capture/replay for suta_adapt (default on): when a call repeats the previous call's
+ * (batch, layout, precision, hparams), one SUTA step (backward + AdamW + forward) is captured once
+ * and replayed for every step; per-kernel timing (suta_set_timing) disables it. */
 int32_t suta_set_graphs(suta_engine* e, int32_t enable);
 
 const char* suta_last_error(void);

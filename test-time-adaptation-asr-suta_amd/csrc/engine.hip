@@ -201,9 +201,10 @@ struct suta_engine {
     };
     hipGraphExec_t step_graph = nullptr;
     GraphKey gkey;
-    bool gkey_seen = false;  // the key ran eagerly once (lazy allocations done): capture on its next step
+    bool gkey_seen = false;  // key of the previous suta_adapt call (its lazy allocations are done)
     void prepare_adam(const suta_hparams& hp, int steps);
-    void suta_step_once(int B, const suta_hparams& hp);
+    bool graph_key_repeats(int B, const suta_hparams& hp);
+    void suta_step_once(int B, const suta_hparams& hp, bool graph_ok);
     void drop_graph() {
         if (step_graph) (void)hipGraphExecDestroy(step_graph);
         step_graph = nullptr;
@@ -1223,27 +1224,11 @@ void suta_engine::prepare_adam(const suta_hparams& hp, int steps) {
     HIPCHK(hipStreamSynchronize(st));  // pageable sources
 }
 
-// One SUTA step after a forward: backward, Adam, forward.  With graphs on (and per-kernel timing off)
-// the step is captured once per (batch, layout, ragged, precision, hparams) key and replayed.
-void suta_engine::suta_step_once(int B, const suta_hparams& hp) {
-    if (!use_graphs || timing) {
-        backward(B, hp);
-        adam(B, hp);
-        forward(B);
-        return;
-    }
-    GraphKey k;
-    k.B = B;
-    k.N = plan.N;
-    k.ragged = plan.ragged;
-    k.mode = gemm_mode;
-    k.hp = hp;
-    const bool same = gkey_seen && gkey.B == k.B && gkey.N == k.N && gkey.ragged == k.ragged &&
-                      gkey.mode == k.mode && std::memcmp(&gkey.hp, &k.hp, sizeof(suta_hparams)) == 0;
-    if (!same) {  // first step of a new key: eager (lazy allocations happen here), capture next time
-        drop_graph();
-        gkey = k;
-        gkey_seen = true;
+// One SUTA step after a forward: backward, Adam, forward.  With graphs on, per-kernel timing off and
+// `graph_ok` (this call repeats the previous call's (batch, layout, ragged, precision, hparams) key),
+// the step is captured once and replayed; a one-off key runs eagerly (no capture cost).
+void suta_engine::suta_step_once(int B, const suta_hparams& hp, bool graph_ok) {
+    if (!use_graphs || timing || !graph_ok) {
         backward(B, hp);
         adam(B, hp);
         forward(B);
@@ -1269,6 +1254,24 @@ void suta_engine::suta_step_once(int B, const suta_hparams& hp) {
     HIPCHK(hipGraphLaunch(step_graph, st));
     opt_steps += 1;
     if (hp.pl_coef > 0.f) sdpl_used = true;  // the replayed SDPL kernels may raise the error flag
+}
+
+// Key of this call; true when it equals the previous call's (graph capture pays off from the 2nd call)
+bool suta_engine::graph_key_repeats(int B, const suta_hparams& hp) {
+    GraphKey k;
+    k.B = B;
+    k.N = plan.N;
+    k.ragged = plan.ragged;
+    k.mode = gemm_mode;
+    k.hp = hp;
+    const bool same = gkey_seen && gkey.B == k.B && gkey.N == k.N && gkey.ragged == k.ragged &&
+                      gkey.mode == k.mode && std::memcmp(&gkey.hp, &k.hp, sizeof(suta_hparams)) == 0;
+    if (!same) {
+        drop_graph();
+        gkey = k;
+        gkey_seen = true;
+    }
+    return same;
 }
 
 void suta_engine::reset_slots(int B) {
@@ -1606,9 +1609,10 @@ static void adapt_impl(suta_engine* e, const float* wav, int32_t on_dev, int32_t
     e->stage_input(wav, on_dev, norm, batch, n, stride);
     if (hp->episodic) e->reset_slots(batch);
     e->prepare_adam(*hp, steps);
+    const bool graph_ok = e->graph_key_repeats(batch, *hp);
     for (int s = 0; s <= steps; ++s) {
         if (s == 0) e->forward(batch);
-        else e->suta_step_once(batch, *hp);
+        else e->suta_step_once(batch, *hp, graph_ok);
         for (int i = 0; i < nrec; ++i) {
             if (rec[i] != s) continue;
             if (logits_out)
@@ -1646,7 +1650,8 @@ int32_t suta_adapt_varlen(suta_engine* e, const float* wav, int32_t on_dev, int3
         int64_t nmax = 0;
         for (int b = 0; b < batch; ++b) nmax = std::max<int64_t>(nmax, n_samples[b]);
         if (stride < nmax) throw SutaError(SUTA_ERR_ARG, "stride < max(n_samples)");
-        adapt_impl(e, wav, on_dev, norm, batch, nmax, n_samples, stride, steps, hp, rec, nrec, logits_out,
+        // the layout length is `stride`: callers quantise it so repeated layouts reuse the captured step
+        adapt_impl(e, wav, on_dev, norm, batch, stride, n_samples, stride, steps, hp, rec, nrec, logits_out,
                    logits_on_dev, ids_out, frames_out);
     });
 }

@@ -233,21 +233,24 @@ class SutaEngine:
         return lg, {r: ids[i] for i, r in enumerate(rec)}, frames.value
 
     def adapt_varlen(self, wavs, steps: int, hp: SutaHParams, record: Sequence[int] = (), normalize: bool = False,
-                     want_logits: bool = True, lengths: Optional[Sequence[int]] = None):
+                     want_logits: bool = True, lengths: Optional[Sequence[int]] = None, quantum: int = 1):
         """Ragged batch (suta_adapt_varlen): `wavs` is a list of 1-D waveforms, or a padded (B, stride)
-        array / tensor with `lengths`.  Each utterance is adapted as if alone.  Returns
+        array / tensor with `lengths`.  Each utterance is adapted as if alone.  The layout length is the
+        padded width (for a list: max length rounded up to `quantum` samples, so that batches of
+        similar lengths share a layout and replay one captured step).  Returns
         (logits {r: [ (T_b, V) ]} or None, ids {r: [ (T_b,) ]}, [T_b])."""
         if lengths is None:
             arrs = [np.ascontiguousarray(w.detach().cpu().numpy() if hasattr(w, "detach") else w,
                                          dtype=np.float32).reshape(-1) for w in wavs]
             lengths = [a.size for a in arrs]
-            pad = np.zeros((len(arrs), max(lengths)), np.float32)
+            width = -(-max(lengths) // max(1, quantum)) * max(1, quantum)
+            pad = np.zeros((len(arrs), width), np.float32)
             for b, a in enumerate(arrs):
                 pad[b, :a.size] = a
             wavs = pad
         p, dev, B, stride, keep = self._wav(wavs)
         ns = (C.c_int64 * B)(*[int(n) for n in lengths])
-        T = self.num_frames(max(lengths))
+        T = self.num_frames(stride)
         rec = list(record)
         crec = (C.c_int32 * max(1, len(rec)))(*rec)
         ids = np.empty((max(1, len(rec)), B, T), np.int32)

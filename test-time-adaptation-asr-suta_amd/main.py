@@ -26,6 +26,7 @@ import numpy as np
 
 SAMPLE_RATE = 16000
 CHECKPOINTS = (1, 3, 5, 10, 20, 40)
+LAYOUT_QUANTUM = 1600  # samples: ragged-batch layout lengths are multiples of 0.1 s (5 frames)
 
 
 def build_parser(sdpl: bool = False):
@@ -56,9 +57,26 @@ def build_parser(sdpl: bool = False):
     # engine-only options
     p.add_argument("--synthetic_weights", action="store_true", help="seeded random weights (no checkpoint)")
     p.add_argument("--device", type=int, default=None)
-    p.add_argument("--gpu_batch", type=int, default=16,
-                   help="utterances adapted together as one ragged batch (episodic runs; 1 = one per call)")
+    p.add_argument("--gpu_batch", type=int, default=64,
+                   help="max utterances adapted together as one ragged batch (episodic runs; 1 = one per call)")
+    p.add_argument("--gpu_budget_s", type=float, default=512.0,
+                   help="max padded audio seconds per ragged batch (utterances x longest)")
     return p
+
+
+def ragged_groups(sorted_lengths, max_batch: int, budget_samples: float):
+    """Consecutive groups of length-sorted utterances: at most max_batch utterances and at most
+    budget_samples of padded audio (count x longest, layout rounded up to LAYOUT_QUANTUM)."""
+    groups, cur = [], []
+    for j, n in enumerate(sorted_lengths):
+        width = -(-n // LAYOUT_QUANTUM) * LAYOUT_QUANTUM
+        if cur and (len(cur) >= max_batch or (len(cur) + 1) * width > budget_samples):
+            groups.append(cur)
+            cur = []
+        cur.append(j)
+    if cur:
+        groups.append(cur)
+    return groups
 
 
 def exp_name_of(a, sdpl: bool = False) -> str:
@@ -160,14 +178,14 @@ def main(argv=None, sdpl: bool = False):
         """ids {record step: (T,)} per item, adapting length-sorted groups of gb as ragged batches."""
         order = sorted(range(len(items)), key=lambda i: len(items[i][1])) if gb > 1 else list(range(len(items)))
         out = [None] * len(items)
-        for s0 in range(0, len(order), gb):
-            grp = order[s0:s0 + gb]
-            if len(grp) == 1:
+        for grp in ragged_groups([len(items[i][1]) for i in order], gb, a.gpu_budget_s * SAMPLE_RATE):
+            grp = [order[j] for j in grp]
+            if gb == 1:
                 _, ids, _ = engine.adapt(items[grp[0]][1], a.steps, hp, record=record, want_logits=False)
                 out[grp[0]] = {r: ids[r][0] for r in record}
-            else:
+            else:  # layout rounded up to LAYOUT_QUANTUM: equal layouts replay one captured step
                 _, ids, _ = engine.adapt_varlen([items[i][1] for i in grp], a.steps, hp, record=record,
-                                                want_logits=False)
+                                                want_logits=False, quantum=LAYOUT_QUANTUM)
                 for j, i in enumerate(grp):
                     out[i] = {r: ids[r][j] for r in record}
         return out

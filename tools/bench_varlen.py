@@ -2,9 +2,9 @@
 
 Synthetic utterances with lengths drawn from a seeded LibriSpeech-test-like distribution
 (log-normal around 6.5 s, clipped to [1.5 s, 35 s]); w2v2-base shapes, 10 SUTA steps, LS.sh flags.
-Compares one utterance per engine call against length-sorted ragged batches (suta_adapt_varlen)
-over the same utterances, inputs resident in HBM.  Prints one JSON line.
-usage: python tools/bench_varlen.py [--n 128] [--gpu-batch 16] [--steps 10]
+Compares one utterance per engine call against length-sorted ragged batches (suta_adapt_varlen,
+grouped as the driver does) over the same utterances, inputs resident in HBM.  Prints one JSON line.
+usage: python tools/bench_varlen.py [--n 256] [--gpu-batch 64] [--budget-s 512] [--steps 10]
 """
 import argparse
 import json
@@ -25,6 +25,7 @@ from suta_amd import synth  # noqa: E402
 from suta_amd.config import get_config  # noqa: E402
 from suta_amd.engine import SutaEngine, SutaHParams  # noqa: E402
 from suta_amd.flops import suta_flops  # noqa: E402
+from suta_amd.main import LAYOUT_QUANTUM, ragged_groups  # noqa: E402
 from suta_amd.weights import synth_weights  # noqa: E402
 
 
@@ -36,20 +37,24 @@ def lengths(n, seed=20260415):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--n", type=int, default=128)
-    ap.add_argument("--gpu-batch", type=int, default=16)
+    ap.add_argument("--n", type=int, default=256)
+    ap.add_argument("--gpu-batch", type=int, default=64)
+    ap.add_argument("--budget-s", type=float, default=512.0, help="padded audio seconds per ragged batch")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--single", type=int, default=16, help="utterances timed one per call (subset)")
     args = ap.parse_args()
     cfg = get_config("wav2vec2-base")
     ns = lengths(args.n)
     waves = [torch.from_numpy(synth.wave(int(n), 5000 + i)).cuda() for i, n in enumerate(ns)]
-    eng = SutaEngine(cfg, synth_weights(cfg), max_batch=args.gpu_batch, max_samples=int(ns.max()))
+    eng = SutaEngine(cfg, synth_weights(cfg), max_batch=args.gpu_batch, max_samples=int(ns.max()) + 1600)
     hp = SutaHParams()
     rec = [0, 1, 3, 5, 10] if args.steps >= 10 else [0, args.steps]
     order = np.argsort(ns)
-    groups = [order[i:i + args.gpu_batch] for i in range(0, len(order), args.gpu_batch)]
-    padded = [torch.zeros((len(g), int(ns[g].max())), device="cuda") for g in groups]
+    # the driver's grouping (suta_amd/main.py ragged_groups): length-sorted, <= gpu_batch utterances and
+    # <= budget seconds of padded audio per batch, layout rounded up to LAYOUT_QUANTUM
+    groups = [order[g] for g in ragged_groups([int(ns[i]) for i in order], args.gpu_batch, args.budget_s * 16000)]
+    q = LAYOUT_QUANTUM
+    padded = [torch.zeros((len(g), -(-int(ns[g].max()) // q) * q), device="cuda") for g in groups]
     for p, g in zip(padded, groups):
         for j, i in enumerate(g):
             p[j, :ns[i]] = waves[i]
@@ -72,10 +77,10 @@ def main():
     t_single = time.perf_counter() - t0
 
     flops = sum(suta_flops(cfg, int(n), args.steps) for n in ns)
-    pad = sum(len(g) * int(ns[g].max()) for g in groups) / float(ns.sum())
+    pad = sum(p.shape[0] * p.shape[1] for p in padded) / float(ns.sum())
     out = {"metric": "adapted utterances/sec, ragged length mix (1.5-35 s), w2v2-base, 10 SUTA steps",
            "n_utterances": int(args.n), "mean_seconds": round(float(ns.mean()) / 16000, 2),
-           "gpu_batch": args.gpu_batch, "ragged_utt_per_s": round(args.n / t_batch, 3),
+           "gpu_batch": args.gpu_batch, "n_batches": len(groups), "ragged_utt_per_s": round(args.n / t_batch, 3),
            "single_utt_per_s": round(len(sub) / t_single, 3),
            "ragged_speedup": round((args.n / t_batch) / (len(sub) / t_single), 2),
            "ragged_algorithmic_tflops": round(flops / t_batch / 1e12, 2),
