@@ -379,7 +379,7 @@ void suta_engine::build_plan(int B, long N) {
         pl.dzc = ar.take<float>((size_t)B * maxLC);
         pl.dzc2 = ar.take<float>((size_t)B * maxLC);
         const long lnrows = std::max<long>(pl.Lc[0], T);
-        pl.lnpart = ar.take<float>((size_t)B * ((lnrows + 31) / 32) * 2 * std::max<long>(H, maxLC / pl.Lc[0] + 1) + 64);
+        pl.lnpart = ar.take<float>((size_t)B * ((lnrows + 15) / 16) * 2 * std::max<long>(H, maxLC / pl.Lc[0] + 1) + 64);
         pl.dpart = ar.take<double>((size_t)B * ((pl.Lc[0] + 127) / 128 + 2) * 2 * k.C[0] + (size_t)B * k.C[0] * 2);
         pl.c0part = ar.take<float>((size_t)B * ((pl.Lc[0] + 127) / 128) * k.K[0] * k.C[0] + 64);
         pl.loss = ar.take<float>(B);

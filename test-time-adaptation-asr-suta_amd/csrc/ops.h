@@ -33,7 +33,7 @@ void launch_layernorm_fwd(const float* x, const float* g, const float* beta, lon
                           hipStream_t st);
 // LayerNorm backward.  gin = dy (times gelu'(xhat*g+beta) when gelu_in); dx = LN-bwd(gin)
 // (times gelu'(post_aux) when post_aux) (+ resid).  dgamma/dbeta (may be null) summed per
-// utterance into the grad buffer (gstride per utterance).  part: >= B*ceil(rows_per_utt/32)*2*D floats.
+// utterance into the grad buffer (gstride per utterance).  part: >= B*ceil(rows_per_utt/16)*2*D floats.
 void launch_layernorm_bwd(const float* dy, const float* xhat, const float* rstd, const float* g, const float* beta,
                           long pstride, int rows_per_utt, int B, int D, int gelu_in, const float* post_aux,
                           const float* resid, float* dx, float* dgamma, float* dbeta, long gstride, float* part,

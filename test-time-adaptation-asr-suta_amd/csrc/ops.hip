@@ -290,7 +290,7 @@ __global__ __launch_bounds__(256) void layernorm_fwd_kernel(const float* __restr
     if (lane == 0) rstd[row] = rs;
 }
 
-constexpr int LNB_ROWS = 32;
+constexpr int LNB_ROWS = 16;
 template <int NPL>
 __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ xhat,
                                                             const float* __restrict__ rstd, const float* __restrict__ g,
@@ -362,6 +362,149 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* __restr
         for (int c = threadIdx.x; c < D; c += 256) {
             pp[c] = red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c];
             pp[D + c] = red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
+        }
+    }
+}
+
+// Vectorised LayerNorm forward for D = 256 * NV: one wave per row, lane l owns the 16-B column
+// groups l + 64 i.  gamma / beta are read as scalars (their offsets in the flat parameter buffer need
+// not be 16-B aligned).
+template <int NV>
+__global__ __launch_bounds__(256) void layernorm_fwd_vec_kernel(const float* __restrict__ x,
+                                                                const float* __restrict__ g,
+                                                                const float* __restrict__ beta, long pstride,
+                                                                int rows_per_utt, float* __restrict__ y,
+                                                                float* __restrict__ xhat, float* __restrict__ rstd,
+                                                                int rows, float eps, int gelu_out) {
+    constexpr int D = 256 * NV;
+    const int lane = threadIdx.x & 63;
+    const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const int u = (int)(row / rows_per_utt);
+    f32x4 v[NV];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        v[i] = reinterpret_cast<const f32x4*>(x + row * D)[lane + 64 * i];
+        s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
+    }
+    s = wave_sum(s);
+    const float mean = s / D;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float d = v[i][e] - mean;
+            q += d * d;
+        }
+    q = wave_sum(q);
+    const float rs = 1.0f / sqrtf(q / D + eps);
+    const float* gu = g + (long)u * pstride;
+    const float* bu = beta + (long)u * pstride;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        const int c = 4 * (lane + 64 * i);
+        f32x4 xh, o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            xh[e] = (v[i][e] - mean) * rs;
+            const float t = xh[e] * gu[c + e] + bu[c + e];
+            o[e] = gelu_out ? gelu_f(t) : t;
+        }
+        reinterpret_cast<f32x4*>(xhat + row * D)[lane + 64 * i] = xh;
+        reinterpret_cast<f32x4*>(y + row * D)[lane + 64 * i] = o;
+    }
+    if (lane == 0) rstd[row] = rs;
+}
+
+// Vectorised LayerNorm backward for D = 256 * NV: lane l owns the 16-B column groups l + 64 i
+// (i < NV) of every row, so every row access is a fully coalesced 1-KiB wave load.  Same arithmetic,
+// order and partial layout as layernorm_bwd_kernel.
+template <int NV>
+__global__ __launch_bounds__(256) void layernorm_bwd_vec_kernel(
+    const float* __restrict__ dy, const float* __restrict__ xhat, const float* __restrict__ rstd,
+    const float* __restrict__ g, const float* __restrict__ beta, long pstride, int rows_per_utt, int gelu_in,
+    const float* __restrict__ post_aux, const float* __restrict__ resid, float* __restrict__ dx,
+    float* __restrict__ part, int nchunk) {
+    constexpr int D = 256 * NV;
+    __shared__ f32x4 red[4][2][NV * 64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int u = blockIdx.y, ch = blockIdx.x;
+    const float* gu = g + (long)u * pstride;
+    const float* bu = beta + (long)u * pstride;
+    f32x4 gam[NV], bet[NV], pg[NV], pb[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        const int c = 4 * (lane + 64 * i);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            gam[i][e] = gu[c + e];
+            bet[i][e] = bu[c + e];
+            pg[i][e] = pb[i][e] = 0.f;
+        }
+    }
+    const int r0 = ch * LNB_ROWS, r1 = min(rows_per_utt, r0 + LNB_ROWS);
+    for (int r = r0 + w; r < r1; r += 4) {
+        const long row = (long)u * rows_per_utt + r;
+        const f32x4* xr = reinterpret_cast<const f32x4*>(xhat + row * D);
+        const f32x4* dr = reinterpret_cast<const f32x4*>(dy + row * D);
+        f32x4 gi[NV], xh[NV];
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            xh[i] = xr[lane + 64 * i];
+            gi[i] = dr[lane + 64 * i];
+        }
+#pragma unroll
+        for (int i = 0; i < NV; ++i)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float d = gi[i][e];
+                if (gelu_in) d *= dgelu_f(xh[i][e] * gam[i][e] + bet[i][e]);
+                gi[i][e] = d;
+                pg[i][e] += d * xh[i][e];
+                pb[i][e] += d;
+                const float dg = d * gam[i][e];
+                s1 += dg;
+                s2 += dg * xh[i][e];
+            }
+        s1 = wave_sum(s1);
+        s2 = wave_sum(s2);
+        const float rs = rstd[row];
+        const float m1 = s1 / D, m2 = s2 / D;
+        f32x4 pa[NV], rr[NV];
+        if (post_aux) {
+#pragma unroll
+            for (int i = 0; i < NV; ++i) pa[i] = reinterpret_cast<const f32x4*>(post_aux + row * D)[lane + 64 * i];
+        }
+        if (resid) {
+#pragma unroll
+            for (int i = 0; i < NV; ++i) rr[i] = reinterpret_cast<const f32x4*>(resid + row * D)[lane + 64 * i];
+        }
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            f32x4 o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                o[e] = rs * (gi[i][e] * gam[i][e] - m1 - xh[i][e] * m2);
+                if (post_aux) o[e] *= dgelu_f(pa[i][e]);
+                if (resid) o[e] += rr[i][e];
+            }
+            reinterpret_cast<f32x4*>(dx + row * D)[lane + 64 * i] = o;
+        }
+    }
+    if (part) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            red[w][0][lane + i * 64] = pg[i];
+            red[w][1][lane + i * 64] = pb[i];
+        }
+        __syncthreads();
+        f32x4* pp = reinterpret_cast<f32x4*>(part + ((long)u * nchunk + ch) * 2 * D);
+        for (int c = threadIdx.x; c < D / 4; c += 256) {
+            pp[c] = red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c];
+            pp[D / 4 + c] = red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
         }
     }
 }
@@ -745,7 +888,18 @@ void launch_layernorm_fwd(const float* x, const float* g, const float* beta, lon
                           float* y, float* xhat, float* rstd, int rows, int D, float eps, int gelu_out,
                           hipStream_t st) {
     dim3 grid(cdiv(rows, 4));
-    if (D <= 256)
+    auto a16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+    const bool vec = a16(x) && a16(y) && a16(xhat);
+    if (vec && D == 768)
+        hipLaunchKernelGGL(layernorm_fwd_vec_kernel<3>, grid, dim3(256), 0, st, x, g, beta, pstride, rows_per_utt, y,
+                           xhat, rstd, rows, eps, gelu_out);
+    else if (vec && D == 1024)
+        hipLaunchKernelGGL(layernorm_fwd_vec_kernel<4>, grid, dim3(256), 0, st, x, g, beta, pstride, rows_per_utt, y,
+                           xhat, rstd, rows, eps, gelu_out);
+    else if (vec && D == 512)
+        hipLaunchKernelGGL(layernorm_fwd_vec_kernel<2>, grid, dim3(256), 0, st, x, g, beta, pstride, rows_per_utt, y,
+                           xhat, rstd, rows, eps, gelu_out);
+    else if (D <= 256)
         hipLaunchKernelGGL(layernorm_fwd_kernel<4>, grid, dim3(256), 0, st, x, g, beta, pstride, rows_per_utt, y, xhat,
                            rstd, rows, D, eps, gelu_out);
     else if (D <= 512)
@@ -763,7 +917,18 @@ void launch_layernorm_bwd(const float* dy, const float* xhat, const float* rstd,
     const int nchunk = cdiv(rows_per_utt, LNB_ROWS);
     float* pp = (dgamma || dbeta) ? part : nullptr;
     dim3 grid(nchunk, B);
-    if (D <= 256)
+    auto a16 = [](const void* q) { return q == nullptr || (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+    const bool vec = a16(dy) && a16(xhat) && a16(dx) && a16(post_aux) && a16(resid) && a16(part);
+    if (vec && D == 768)
+        hipLaunchKernelGGL(layernorm_bwd_vec_kernel<3>, grid, dim3(256), 0, st, dy, xhat, rstd, g, beta, pstride,
+                           rows_per_utt, gelu_in, post_aux, resid, dx, pp, nchunk);
+    else if (vec && D == 1024)
+        hipLaunchKernelGGL(layernorm_bwd_vec_kernel<4>, grid, dim3(256), 0, st, dy, xhat, rstd, g, beta, pstride,
+                           rows_per_utt, gelu_in, post_aux, resid, dx, pp, nchunk);
+    else if (vec && D == 512)
+        hipLaunchKernelGGL(layernorm_bwd_vec_kernel<2>, grid, dim3(256), 0, st, dy, xhat, rstd, g, beta, pstride,
+                           rows_per_utt, gelu_in, post_aux, resid, dx, pp, nchunk);
+    else if (D <= 256)
         hipLaunchKernelGGL(layernorm_bwd_kernel<4>, grid, dim3(256), 0, st, dy, xhat, rstd, g, beta, pstride,
                            rows_per_utt, D, gelu_in, post_aux, resid, dx, pp, nchunk);
     else if (D <= 512)
