@@ -32,7 +32,8 @@ from suta_amd.flops import suta_flops  # noqa: E402
 from suta_amd.weights import synth_weights  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
-BF16_SPLIT_PEAK_TFLOPS = 2500.0 / 6  # bf16 dense MFMA peak / 6 products per fp32-equivalent MAC
+BF16_PEAK_TFLOPS = 2500.0      # MI355X_MICROARCH.md: bf16 dense MFMA peak
+BF16_SPLIT_PEAK_TFLOPS = BF16_PEAK_TFLOPS / 6  # 6 bf16 products per fp32-equivalent MAC
 RECORD = [0, 1, 3, 5, 10]
 PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r1", "pmc_traffic.json")
 GEMM_KERNELS = ("gemm_glds_kernel", "gemm_f32_kernel")
@@ -70,6 +71,46 @@ def cpu_baseline(cfg, n_samples, suta_steps, budget_s=25.0):
                       f"run_suta (torch {torch.__version__} CPU, {cores} threads), {el:.1f} s"}
 
 
+def bench_c4(args, dev):
+    """BASELINE.json config C4: wav2vec2-large-960h-lv60 shapes, 20-step SUTA, bf16 GEMMs (operands
+    rounded to bf16, fp32 accumulation; norms, softmax, loss, AdamW and master tensors fp32), 1 GPU,
+    8 s utterances.  A secondary line beside the C2 headline."""
+    cfg = get_config("wav2vec2-large")
+    B, N, S = args.c4_batch, args.n_samples, 20
+    eng = SutaEngine(cfg, synth_weights(cfg), device=dev, max_batch=B, max_samples=N)
+    eng.set_precision("bf16")
+    hp = SutaHParams()
+    rec = [0, 1, 5, 10, 20]
+    steps = max(1, args.steps // 2)
+    waves = [torch.from_numpy(synth.batch(N, B, start=50000 + i * B)).to(f"cuda:{dev}") for i in range(steps + 1)]
+    eng.adapt(waves[0], S, hp, record=rec, want_logits=False)
+    if not args.no_timing:
+        eng.set_timing(True)
+    torch.cuda.synchronize()
+    eng.sync()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        eng.adapt(waves[1 + i], S, hp, record=rec, want_logits=False)
+    eng.sync()
+    el = time.perf_counter() - t0
+    flops_utt = suta_flops(cfg, N, S)
+    res = {"workload": f"wav2vec2-large SUTA {S} steps on {N}-sample (8 s) utterances, {B} utterances per step, "
+                       "scripts/LS.sh flags, bf16 GEMMs", "config": "C4", "precision": "bf16", "dtype": "bf16",
+           "value": round(B * steps / el, 4), "unit": "utt/s", "steps": steps,
+           "ms_per_step": round(1000 * el / steps, 3), "algorithmic_tflops": round(flops_utt * B * steps / el / 1e12, 3),
+           "rtf": round(el / (B * steps * N / 16000.0), 6)}
+    if not args.no_timing:
+        t = eng.get_timing()
+        gms, gn = t["gemm"]
+        ach = flops_utt * B * steps / (gms / 1000.0) / 1e12
+        res["roofline"] = {"bound": "mfma", "achieved": round(ach, 3), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                           "frac": round(ach / BF16_PEAK_TFLOPS, 4), "kernel": "bf16 GEMM family (gemm_gbf_kernel)",
+                           "launches": int(gn), "avg_launch_ms": round(gms / max(1, gn), 5)}
+        res["time_breakdown_ms"] = {k: round(v[0], 2) for k, v in t.items()}
+    eng.close()
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -81,8 +122,11 @@ def main():
     ap.add_argument("--model", default="wav2vec2-base")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP-event timing")
-    ap.add_argument("--precision", default="fp32", choices=["fp32", "fp32-split-bf16"],
-                    help="GEMM arithmetic: exact fp32 MFMA, or fp32-accurate 3-way bf16 split")
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "fp32-split-bf16", "bf16"],
+                    help="GEMM arithmetic: exact fp32 MFMA, fp32-accurate 3-way bf16 split, or bf16 (config C4)")
+    ap.add_argument("--no-c4", dest="c4", action="store_false",
+                    help="skip the config-C4 line (wav2vec2-large, 20 SUTA steps, bf16 GEMMs; 1 GPU only)")
+    ap.add_argument("--c4-batch", type=int, default=32)
     ap.add_argument("--no-split", dest="also_split", action="store_false",
                     help="do not also time the fp32-accurate split-bf16 GEMM mode")
     args = ap.parse_args()
@@ -195,9 +239,11 @@ def main():
         eng.set_precision("fp32")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cfg, N, S)
+    eng.close()
+    if world == 1 and args.c4 and args.precision == "fp32":
+        out["c4"] = bench_c4(args, dev)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    eng.close()
     if dist:
         tdist.destroy_process_group()
 

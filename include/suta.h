@@ -165,13 +165,21 @@ void* suta_stream(suta_engine* e);
 int32_t suta_set_timing(suta_engine* e, int32_t enable);
 int32_t suta_get_timing(suta_engine* e, double* ms_out /*[6]*/, int64_t* launches_out /*[6]*/);
 
-/* GEMM arithmetic.  Both are fp32-accurate; results agree to fp32 rounding (tests/test_gpu_parity.py):
+/* GEMM arithmetic.  The first two are fp32-accurate; results agree to fp32 rounding
+ * (tests/test_gpu_parity.py):
  *   SUTA_PRECISION_FP32_MFMA        v_mfma_f32_32x32x2_f32: exact fp32 products, fp32 accumulation
  *   SUTA_PRECISION_FP32_SPLIT_BF16  each fp32 operand split exactly into 3 bf16 terms; the 6 products
  *                                   of order <= 2 on v_mfma_f32_32x32x16_bf16, fp32 accumulation
- *                                   (dropped terms <= 2^-24 |ab|: the size of one fp32 rounding) */
+ *                                   (dropped terms <= 2^-24 |ab|: the size of one fp32 rounding)
+ *   SUTA_PRECISION_BF16             bf16 GEMMs (config C4, the reference has no bf16 path): every GEMM
+ *                                   operand rounded to bf16 (RNE) as it enters the MFMA, fp32
+ *                                   accumulation; activations, norms, softmax, loss, AdamW and the
+ *                                   trainable master tensors stay fp32 (torch.autocast(bf16)
+ *                                   semantics for the matmuls) -- tests/test_gpu_bf16.py states the
+ *                                   tolerance */
 #define SUTA_PRECISION_FP32_MFMA 0
 #define SUTA_PRECISION_FP32_SPLIT_BF16 1
+#define SUTA_PRECISION_BF16 2
 int32_t suta_set_precision(suta_engine* e, int32_t mode);
 
 /* Use hipGraph capture/replay for suta_adapt (default on): when a call repeats the previous call's

@@ -88,7 +88,7 @@ struct GemmParams {
     int splits, kchunk;
     float* ws;  // split-K workspace
     int va, vb; // vector (16 B) loads legal
-    int mode;   // 0 exact fp32 MFMA, 1 x6 (fp32-accurate bf16 split); gemm_init takes the default
+    int mode;   // 0 exact fp32 MFMA, 1 x6 (fp32-accurate bf16 split), 2 bf16 products; gemm_init takes the default
 };
 
 void gemm_init(GemmParams& p);
@@ -96,6 +96,7 @@ void gemm_init(GemmParams& p);
 void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats);
 // Benchmark/test override: tile (-1 auto, 0 128x128, 1 128x64, 2 64x128, 3 64x64), LDS buffers (1|2).
 void gemm_set_variant(int tile, int nbuf);
-// 0 = exact fp32 MFMA (v_mfma_f32_32x32x2_f32); 1 = fp32-accurate 3-way bf16 split (6 bf16 MFMA products).
+// 0 = exact fp32 MFMA (v_mfma_f32_32x32x2_f32); 1 = fp32-accurate 3-way bf16 split (6 bf16 MFMA products);
+// 2 = bf16 GEMM (operands rounded to bf16 once, one bf16 MFMA product, fp32 accumulate).
 void gemm_set_mode(int mode);
 int gemm_get_mode();

@@ -1753,7 +1753,7 @@ int32_t suta_get_timing(suta_engine* e, double* ms, int64_t* n) {
 
 int32_t suta_set_precision(suta_engine* e, int32_t mode) {
     return guard([&] {
-        if (mode != SUTA_PRECISION_FP32_MFMA && mode != SUTA_PRECISION_FP32_SPLIT_BF16)
+        if (mode != SUTA_PRECISION_FP32_MFMA && mode != SUTA_PRECISION_FP32_SPLIT_BF16 && mode != SUTA_PRECISION_BF16)
             throw SutaError(SUTA_ERR_ARG, "unknown precision mode");
         e->gemm_mode = mode;
     });

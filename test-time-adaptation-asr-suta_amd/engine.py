@@ -308,7 +308,7 @@ class SutaEngine:
         fams = ("gemm", "softmax", "norm", "elementwise", "loss", "adam")
         return {f: (ms[i], n[i]) for i, f in enumerate(fams)}
 
-    PRECISIONS = {"fp32": 0, "fp32-split-bf16": 1}
+    PRECISIONS = {"fp32": 0, "fp32-split-bf16": 1, "bf16": 2}
 
     def set_precision(self, mode: str):
         """'fp32' (exact fp32 MFMA) or 'fp32-split-bf16' (fp32-accurate 3-way bf16 split)."""

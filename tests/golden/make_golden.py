@@ -22,6 +22,9 @@ Fixtures written next to this file:
   g6_sdpl_loss.npz   SDPL pseudo-label CTC loss + dL/dlogits through the reference
                      main_SDPL.forward_and_adapt (main_SDPL.py:143-209) with a fake model
   g6_sdpl_tiny_<variant>.npz  tiny-config episodic SDPL runs (main_SDPL.py:327-349)
+  g7_large_16000.npz large-960h-lv60 shapes (layer-norm feature encoder, conv bias, stable
+                     pre-LN encoder), 20 SUTA steps (config C4's step count), scripts/LS.sh flags:
+                     logits at steps 0,1,5,10,20 + digests of the adapted tensors
 
 main_SDPL.py is imported the same way, after transformers (so transformers' own soundfile
 probe sees the real environment) with stub `jiwer` and `soundfile` modules (neither is
@@ -231,6 +234,26 @@ def g4(ref):
             out[f"final/{k}/delta_abs_sum"] = np.array(np.abs(flat.astype(np.float64) - sd[k].reshape(-1)).sum())
         np.savez_compressed(os.path.join(HERE, f"g4_base_{n}.npz"), **out)
         print("g4", n, "done")
+
+
+def g7(ref):
+    cfg = get_config("wav2vec2-large")
+    sd = synth_weights(cfg)
+    rec = (1, 5, 10, 20)
+    n = 16000
+    x = wave(n, 7)
+    logits, final, names = run_ref_suta(ref, cfg, sd, x, 20, lr=2e-5, record=rec)
+    out = {"weights_sha256": np.array(weights_digest(sd)), "x_sha256": np.array(hashlib.sha256(x.tobytes()).hexdigest())}
+    out["steps"] = np.array((0,) + rec)
+    out["logits"] = np.stack([logits[i] for i in (0,) + rec])
+    idx_rng = np.random.default_rng(7)
+    for k, v in final.items():
+        flat = v.reshape(-1)
+        idx = np.sort(idx_rng.choice(flat.size, size=min(32, flat.size), replace=False))
+        out[f"final/{k}/idx"] = idx
+        out[f"final/{k}/val"] = flat[idx]
+    np.savez_compressed(os.path.join(HERE, f"g7_large_{n}.npz"), **out)
+    print("g7", n, "done")
 
 
 def g5(ref):

@@ -1,0 +1,106 @@
+"""GPU tier: the large-960h-lv60 geometry and the bf16 GEMM mode (BASELINE.json config C4).
+
+* large (layer-norm feature encoder, conv bias, stable pre-LN encoder, H = 1024, 24 layers) in the
+  fp32 modes against the reference's own 20-step SUTA run (golden g7): logits within 5e-5 absolute
+  (measured 7.6e-6 at step 20), adapted tensors by tests/parity.assert_params_close.
+* bf16 mode (every GEMM operand rounded to bf16, fp32 accumulation; the reference has no bf16 path):
+  against the fp32 reference goldens and the exact-fp32 engine, tests/parity.assert_bf16_close
+  (logits within 6 % of max |ref|; greedy ids agreeing on >= 90 % of frames on the 24-frame tiny
+  configs, >= 97 % on base / large).
+"""
+import ast
+import os
+
+import numpy as np
+import pytest
+
+from suta_amd import synth
+from suta_amd.config import get_config
+from suta_amd.engine import SutaEngine, SutaHParams
+from suta_amd.weights import synth_weights
+from tests.parity import assert_bf16_close, assert_params_close, logits_tol
+
+pytestmark = pytest.mark.gpu
+
+G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+_ENGINES = {}
+
+
+def engine(preset, precision, max_samples=128000):
+    if preset not in _ENGINES:
+        cfg = get_config(preset)
+        _ENGINES[preset] = SutaEngine(cfg, synth_weights(cfg), max_batch=2, max_samples=max_samples)
+    _ENGINES[preset].set_precision(precision)
+    return _ENGINES[preset]
+
+
+def _load(name):
+    return np.load(os.path.join(G, name), allow_pickle=False)
+
+
+def _g7_wave():
+    from tests.golden.make_golden import wave
+    return wave(16000, 7)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "fp32-split-bf16"])
+def test_large_suta_matches_reference(precision):
+    z = _load("g7_large_16000.npz")
+    eng = engine("wav2vec2-large", precision)
+    steps = [int(s) for s in z["steps"]]
+    logits, ids, T = eng.adapt(_g7_wave(), 20, SutaHParams(), record=steps)
+    for j, s in enumerate(steps):
+        np.testing.assert_allclose(logits[s][0], z["logits"][j], rtol=0, atol=5e-5, err_msg=f"step {s}")
+    for key in z.files:
+        if key.startswith("final/") and key.endswith("/idx"):
+            name = key[len("final/"):-len("/idx")]
+            got = eng.get_param(0, name).reshape(-1)[z[key]]
+            assert_params_close(got, z[f"final/{name}/val"], 2e-5, 20, max_frac=0.05, name=name)
+
+
+@pytest.mark.parametrize("variant", ["group", "group_lr5e-4", "layer", "layer_lr5e-4"])
+def test_bf16_tiny_tracks_reference(variant):
+    z = _load(f"g3_tiny_{variant}.npz")
+    eng = engine("tiny-group" if variant.startswith("group") else "tiny-layer", "bf16")
+    h = ast.literal_eval(str(z["hp_json"]))
+    hp = SutaHParams(lr=h["lr"], temp=h["temp"], em_coef=h["em"], reweight=h["rw"], non_blank=h["nb"],
+                     div_coef=h["div"], train_feature=h["train_feature"], bias_only=h["bias_only"])
+    for n in (8000, 12345):
+        logits, ids, T = eng.adapt(z[f"N{n}/x"], 10, hp, record=list(range(11)))
+        for i in (0, 1, 5, 10):
+            assert_bf16_close(logits[i][0], z[f"N{n}/logits"][i], 0.9, f"{variant} N{n} step {i}")
+            np.testing.assert_array_equal(ids[i][0], logits[i][0].argmax(-1))
+
+
+def test_bf16_large_tracks_reference():
+    z = _load("g7_large_16000.npz")
+    eng = engine("wav2vec2-large", "bf16")
+    steps = [int(s) for s in z["steps"]]
+    logits, _, _ = eng.adapt(_g7_wave(), 20, SutaHParams(), record=steps)
+    for j, s in enumerate(steps):
+        assert_bf16_close(logits[s][0], z["logits"][j], 0.97, f"large step {s}")
+
+
+def test_bf16_base_tracks_reference_and_fp32_8s():
+    z = _load("g4_base_16000.npz")
+    eng = engine("wav2vec2-base", "bf16")
+    steps = [int(s) for s in z["steps"]]
+    logits, _, _ = eng.adapt(synth.wave(16000, 0), 10, SutaHParams(), record=steps)
+    for j, s in enumerate(steps):
+        assert_bf16_close(logits[s][0], z["logits"][j], 0.97, f"base N16000 step {s}")
+    x = synth.wave(128000, 4)
+    b, _, _ = eng.adapt(x, 10, SutaHParams(), record=[0, 10])
+    eng.set_precision("fp32")
+    a, _, _ = eng.adapt(x, 10, SutaHParams(), record=[0, 10])
+    for r in (0, 10):
+        assert_bf16_close(b[r][0], a[r][0], 0.97, f"base 8 s step {r} vs exact fp32")
+
+
+def test_bf16_batch_equals_single_and_deterministic():
+    eng = engine("wav2vec2-base", "bf16")
+    xs = synth.batch(32000, 2, start=40)
+    lb, _, _ = eng.adapt(xs, 3, SutaHParams(), record=[3])
+    l1, _, _ = eng.adapt(xs[1], 3, SutaHParams(), record=[3])
+    l2, _, _ = eng.adapt(xs[1], 3, SutaHParams(), record=[3])
+    assert np.array_equal(l1[3][0], l2[3][0])
+    np.testing.assert_allclose(lb[3][1], l1[3][0], rtol=0, atol=logits_tol(2e-5))

@@ -129,6 +129,24 @@ def test_g4_base_oracle_matches_reference(n):
         assert_params_close(v.numpy().reshape(-1)[idx], z[f"final/{k}/val"], 2e-5, 10, max_frac=0.05, name=k)
 
 
+@pytest.mark.slow
+def test_g7_large_oracle_matches_reference():
+    """large-960h-lv60 geometry (layer-norm conv stack, conv bias, stable LN), 20 SUTA steps."""
+    z = _load("g7_large_16000.npz")
+    cfg = get_config("wav2vec2-large")
+    sd = synth_weights(cfg)
+    params = {k: torch.from_numpy(v) for k, v in sd.items()}
+    from tests.golden.make_golden import wave
+    x = torch.from_numpy(wave(16000, 7))[None]
+    steps = [int(s) for s in z["steps"]]
+    out, final = W.run_suta(params, cfg, x, 20, record=steps)
+    for j, s in enumerate(steps):
+        np.testing.assert_allclose(out[s][0].numpy(), z["logits"][j], rtol=0, atol=5e-5, err_msg=f"step {s}")
+    for k, v in final.items():
+        idx = z[f"final/{k}/idx"]
+        assert_params_close(v.numpy().reshape(-1)[idx], z[f"final/{k}/val"], 2e-5, 20, max_frac=0.05, name=k)
+
+
 # ---------------------------------------------------------------------------------------------
 # SDPL (reference main_SDPL.py:143-209): g6 fixtures
 # ---------------------------------------------------------------------------------------------

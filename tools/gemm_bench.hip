@@ -1,6 +1,6 @@
 // Standalone fp32-MFMA GEMM microbenchmark + correctness check for the SUTA shapes.
-// Build: hipcc -O3 --offload-arch=gfx950 -I test-time-adaptation-asr-suta_amd/csrc tools/gemm_bench.hip
-//        test-time-adaptation-asr-suta_amd/csrc/gemm.hip -o tools/gemm_bench
+// Build (after make in csrc): hipcc -O3 --offload-arch=gfx950 -I test-time-adaptation-asr-suta_amd/csrc -c tools/gemm_bench.hip -o gb.o
+//        && hipcc --offload-arch=gfx950 gb.o test-time-adaptation-asr-suta_amd/csrc/gemm*.o -o tools/gemm_bench
 #include <hip/hip_runtime.h>
 #include <cmath>
 #include <cstdio>
@@ -90,17 +90,17 @@ int main(int argc, char** argv) {
     hipStream_t st; CK(hipStreamCreate(&st));
     hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     const int variants[][2] = {{-1, 1}, {-1, 3}, {0, 3}, {0, 7}, {0, 5}, {0, 6}, {1, 3}, {1, 7},
-                               {3, 3}, {3, 7}, {2, 3}, {2, 7}, {0, 1}, {3, 1}, {-1, 7}};
+                               {3, 3}, {3, 7}, {2, 3}, {2, 7}, {0, 1}, {3, 1}, {-1, 7}, {-1, 8}, {-1, 9}, {-1, 10}};
     const char* vname[] = {"auto/1buf", "auto/g32x2", "128/g32x2", "128/g64x2", "128/g16x3", "128/g32x3",
                            "128x64/g32x2", "128x64/g64x2", "64/g32x2", "64/g64x2", "64x128/g32", "64x128/g64",
-                           "128/1buf", "64/1buf", "auto/g64x2"};
-    const int NV = 15;
+                           "128/1buf", "64/1buf", "auto/g64x2", "auto/v8", "auto/v9", "auto/v10"};
+    const int NV = 18;
     bool check = argc < 2 || atoi(argv[1]) != 0;
     int only_v = argc >= 3 ? atoi(argv[2]) : -1;
     int only_s = argc >= 4 ? atoi(argv[3]) : -1;
     int mode = argc >= 5 ? atoi(argv[4]) : 0;
     gemm_set_mode(mode);
-    printf("GEMM mode %d (%s)\n", mode, mode ? "x6 bf16-split" : "exact fp32 MFMA");
+    printf("GEMM mode %d (%s)\n", mode, mode == 2 ? "bf16" : mode ? "x6 bf16-split" : "exact fp32 MFMA");
     {
         const int iters = 20000, blocks = 256 * 4;
         hipLaunchKernelGGL(mfma_peak, dim3(blocks), dim3(256), 0, st, C, 100, 0.001f);
