@@ -58,6 +58,32 @@ static int choose_tile(long M, long N, long Z, long K, int mode) {
     return best;
 }
 
+// bf16 mode (tools/gemm_bench, 64 utterances): the register-staged one-plane kernel beats the LDS-DMA
+// fp32-staged one on every operand layout except transposed A (weight gradients, TN), and its
+// 256x128 tile (wave tile 128x64: 1.3x fewer L2 bytes per flop) wins wherever the grid still fills
+// whole rounds of 512 resident blocks (2 per CU): 420-430 TF on FFN1 / QKV / conv1 vs 360-390.
+// Cost = rounds of 512 blocks x tile area / eff.
+static int choose_tile_bf16(long M, long N, long Z, bool big) {
+    struct Cand {
+        int id, bm, bn;
+        double eff;
+    };
+    static const Cand c[5] = {{0, 128, 128, 1.0}, {4, 256, 128, 1.12}, {1, 128, 64, 0.85}, {2, 64, 128, 0.85},
+                              {3, 64, 64, 0.6}};
+    int best = 0;
+    double bt = 1e300;
+    for (int i = 0; i < 5; ++i) {
+        if (c[i].id == 4 && !big) continue;
+        const long tiles = ((M + c[i].bm - 1) / c[i].bm) * ((N + c[i].bn - 1) / c[i].bn) * Z;
+        const double t = (double)((tiles + 511) / 512) * c[i].bm * c[i].bn / c[i].eff;
+        if (t < bt * 0.999) {
+            bt = t;
+            best = c[i].id;
+        }
+    }
+    return best;
+}
+
 void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
     if (p.M <= 0 || p.N <= 0 || p.Z <= 0) return;
     const int second = ((p.epi & EPI_RESID) != 0) + ((p.epi & EPI_ACCUM) != 0) + ((p.epi & EPI_SMBWD) != 0);
@@ -69,9 +95,14 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
     p.va = vec_ok(p.A, p.lda, p.sA0, p.sA1) && (p.segK == 0 || p.segK % 4 == 0);
     p.vb = vec_ok(p.B, p.ldb, p.sB0, p.sB1) && (!p.segB || (p.sBseg % 4 == 0 && p.segK % 4 == 0));
 
-    const int tile = g_force_tile >= 0 ? g_force_tile : choose_tile(p.M, p.N, p.Z, p.K, p.mode);
-    const int BM = (tile == 0 || tile == 1) ? 128 : 64;
-    const int BN = (tile == 0 || tile == 2) ? 128 : 64;
+    const bool glds_ok = p.va && p.vb && (p.ta || p.K % 4 == 0) && (!p.tb || p.K % 4 == 0);
+    const bool bf16_gbf = p.mode == 2 && glds_ok && p.ta;  // bf16 weight gradients: LDS-DMA fp32 stages
+    const int tile = g_force_tile >= 0 ? g_force_tile
+                     : p.mode == 2   ? choose_tile_bf16(p.M, p.N, p.Z, !bf16_gbf)
+                                     : choose_tile(p.M, p.N, p.Z, p.K, p.mode);
+    // tiles 0 = 128x128, 1 = 128x64, 2 = 64x128, 3 = 64x64; bf16 mode also 4 = 256x128, 5 = 128x256
+    const int BM = tile == 4 ? 256 : (tile == 0 || tile == 1 || tile == 5) ? 128 : 64;
+    const int BN = tile == 5 ? 256 : (tile == 0 || tile == 2 || tile == 4) ? 128 : 64;
     const int gx = (p.N + BN - 1) / BN, gy = (p.M + BM - 1) / BM;
     const long blocks = (long)gx * gy * p.Z;
 
@@ -87,11 +118,11 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
     p.splits = splits;
     p.ws = ws;
     dim3 grid(gx, gy, p.Z * splits);
-    const bool glds_ok = p.va && p.vb && (p.ta || p.K % 4 == 0) && (!p.tb || p.K % 4 == 0);
     if (p.mode == 2) {
-        // bf16: register-converted LDS-DMA stages (variant 8 = BK64 x 2), else the register-staged
-        // one-plane kernel
-        if (glds_ok) gemm_run_gbf(g_nbuf == 8, 1, tile, p, grid, st);
+        // bf16: register-staged one-plane kernel; weight gradients (and benchmark variants 3 / 8) on
+        // register-converted LDS-DMA stages (8 = BK64 x 2)
+        const bool gbf = glds_ok && tile < 4 && (g_force_tile >= 0 ? (g_nbuf == 3 || g_nbuf == 8) : bf16_gbf);
+        if (gbf) gemm_run_gbf(g_nbuf == 8, 1, tile, p, grid, st);
         else gemm_run_x6(tile, 0, 1, p, grid, st);
     } else if (p.mode == 1 && glds_ok && g_nbuf >= 9) {
         // x6 with register splits on LDS-DMA stages (benchmark variants 9 = BK32 x 2, 10 = BK64 x 2)

@@ -565,6 +565,10 @@ template <>
 struct bfvec<2> {
     typedef bf16x2 T;
 };
+template <>
+struct bfvec<8> {
+    typedef bf16x8 T;
+};
 
 template <int ROWS, int BKX, bool KC, int NPL>
 __device__ __forceinline__ void x6_store(__bf16* __restrict__ lds, const f32x4 (&r)[(X6<ROWS, BKX>::LOADS)]) {
@@ -606,7 +610,7 @@ __device__ __forceinline__ void x6_store(__bf16* __restrict__ lds, const f32x4 (
             }
         }
     } else {
-        constexpr int KPT = X6<ROWS, BKX>::KPT > 1 ? X6<ROWS, BKX>::KPT : 2;
+        constexpr int KPT = X6<ROWS, BKX>::KPT > 1 ? X6<ROWS, BKX>::KPT : 2;  // 2, 4 or 8
         typedef typename bfvec<KPT>::T V;
         const int i = f / X6<ROWS, BKX>::JN, j = f % X6<ROWS, BKX>::JN;
 #pragma unroll
@@ -631,7 +635,7 @@ __device__ __forceinline__ void x6_store(__bf16* __restrict__ lds, const f32x4 (
 }
 
 template <int BM, int BN, bool TA, bool TB, bool CONV, bool SEGB, int BKX, int NBUF, int NPL>
-__global__ __launch_bounds__(256, 3) void gemm_x6_kernel(GemmParams p) {
+__global__ __launch_bounds__(256, (BM * BN > 128 * 128) ? 2 : 3) void gemm_x6_kernel(GemmParams p) {
     constexpr int WTM = BM / 2, WTN = BN / 2;
     constexpr int RM = WTM / 32, RN = WTN / 32;
     constexpr bool AKC = !TA, BKC = TB;
