@@ -127,10 +127,15 @@ def main():
     ap.add_argument("--no-c4", dest="c4", action="store_false",
                     help="skip the config-C4 line (wav2vec2-large, 20 SUTA steps, bf16 GEMMs; 1 GPU only)")
     ap.add_argument("--c4-batch", type=int, default=32)
+    ap.add_argument("--only-c4", action="store_true", help="print only the config-C4 line (profiling)")
     ap.add_argument("--no-split", dest="also_split", action="store_false",
                     help="do not also time the fp32-accurate split-bf16 GEMM mode")
     args = ap.parse_args()
 
+    if args.only_c4:
+        torch.cuda.set_device(0)
+        print(json.dumps(bench_c4(args, 0)), flush=True)
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
