@@ -61,6 +61,8 @@ def build_parser(sdpl: bool = False):
                    help="max utterances adapted together as one ragged batch (episodic runs; 1 = one per call)")
     p.add_argument("--gpu_budget_s", type=float, default=512.0,
                    help="max padded audio seconds per ragged batch (utterances x longest)")
+    p.add_argument("--precision", default="fp32", choices=["fp32", "fp32-split-bf16", "bf16"],
+                   help="GEMM arithmetic (fp32 = the reference's; bf16 = BASELINE config C4)")
     return p
 
 
@@ -158,6 +160,7 @@ def main(argv=None, sdpl: bool = False):
     cfg, weights = load_model(a.asr, a.synthetic_weights)
     gb = max(1, a.gpu_batch) if a.episodic else 1  # non-episodic adaptation is sequential
     engine = SutaEngine(cfg, weights, device=device, max_batch=gb)
+    engine.set_precision(a.precision)
     hp = SutaHParams(lr=a.lr, temp=a.temp, em_coef=a.em_coef, div_coef=0.0 if sdpl else a.div_coef,
                      reweight=a.reweight, non_blank=a.non_blank, train_feature=a.train_feature,
                      bias_only=a.bias_only, episodic=a.episodic, pl_coef=1.0 if sdpl else 0.0)
