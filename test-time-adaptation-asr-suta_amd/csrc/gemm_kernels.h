@@ -896,6 +896,52 @@ __device__ __forceinline__ void glds_stage(float* dst, const float* __restrict__
     }
 }
 
+// Plain-operand (MODE 0) DMA sources, set up once per block and advanced by one K-step per stage: the
+// K-loop issues NI global_load_lds per operand with no address arithmetic beyond one add.  Lanes
+// outside the operand point at the zero page and never move.  Valid for full stages (k + BKS <= kend);
+// a partial last stage goes through glds_stage.
+template <int ROWS, int BKS, bool KC>
+struct GldsStream {
+    static constexpr int NI = ROWS * BKS / 1024;
+    const float* ptr[NI];
+    int inc[NI];  // floats per K-step (0 on zero-page lanes)
+    __device__ __forceinline__ void init(const float* __restrict__ src, long ld, int row0, int nrows, int k0, int w,
+                                         int lane) {
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int ci = i * 4 + w;
+            bool ok;
+            const float* g;
+            if (KC) {
+                constexpr int CPR = BKS / 4;
+                const int row = ci * (256 / BKS) + lane / CPR;
+                const int c = (lane % CPR) ^ glds_swz<BKS>(row);
+                ok = row0 + row < nrows;
+                g = src + (long)(row0 + row) * ld + k0 + c * 4;
+            } else {
+                const int f = ci * 256 + lane * 4;
+                const int k = f / ROWS, m = f % ROWS;
+                ok = row0 + m < nrows;
+                g = src + (long)(k0 + k) * ld + row0 + m;
+            }
+            ptr[i] = ok ? g : g_zero16;
+            inc[i] = ok ? (KC ? BKS : (int)(BKS * ld)) : 0;
+        }
+    }
+};
+
+// one full stage of a GldsStream operand (free function: a member-function form of this builtin call
+// made hipcc's host pass drop the kernels' launch stubs)
+template <int ROWS, int BKS, bool KC>
+__device__ __forceinline__ void glds_stream_issue(GldsStream<ROWS, BKS, KC>& sm, float* dst, int w) {
+#pragma unroll
+    for (int i = 0; i < GldsStream<ROWS, BKS, KC>::NI; ++i) {
+        const float* g = sm.ptr[i];
+        __builtin_amdgcn_global_load_lds(g, (lds_ptr_t)(dst + (i * 4 + w) * 256), 16, 0, 0);
+        sm.ptr[i] = g + sm.inc[i];
+    }
+}
+
 // fragment of 4 consecutive MFMA k-steps: tile k = h * BKS/2 + 4q + e  (q < BKS/8)
 template <int ROWS, int BKS, bool KC>
 __device__ __forceinline__ f32x4 glds_frag(const float* __restrict__ lds, int row, int h, int q) {
@@ -959,14 +1005,30 @@ __global__ __launch_bounds__(256, 2) void gemm_glds_kernel(GemmParams p) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
+    // plain operands stream from precomputed per-lane pointers (GldsStream); conv / segmented operands
+    // and the partial last stage recompute addresses (glds_stage)
+    constexpr bool STREAM = !CONV && !SEGB;
+    GldsStream<BM, BKS, AKC> sa;
+    GldsStream<BN, BKS, BKC> sb;
+    if (STREAM) {
+        sa.init(A, p.lda, m0, p.M, kbeg, wid, lane);
+        sb.init(B, p.ldb, n0, p.N, kbeg, wid, lane);
+    }
     auto issue = [&](int s) {
         float* st = smem + (s % NS) * STAGE;
         const int k = kbeg + s * BKS;
         const bool dummy = s >= nst;
-        glds_stage<BM, BKS, AKC, CONV ? 1 : 0>(st, A, p.lda, m0, p.M, k, kend, p.segK, p.pad, Mv, 0, wid,
-                                                lane, dummy);
-        glds_stage<BN, BKS, BKC, SEGB ? 2 : 0>(st + BM * BKS, B, p.ldb, n0, p.N, k, kend, p.segK, 0, 0, p.sBseg,
-                                                wid, lane, dummy);
+        if (NS == 2 && dummy) {
+            // vmcnt(0) waits: nothing to keep in step past the last stage
+        } else if (STREAM && k + BKS <= kend) {
+            glds_stream_issue(sa, st, wid);
+            glds_stream_issue(sb, st + BM * BKS, wid);
+        } else {
+            glds_stage<BM, BKS, AKC, CONV ? 1 : 0>(st, A, p.lda, m0, p.M, k, kend, p.segK, p.pad, Mv, 0, wid,
+                                                    lane, dummy);
+            glds_stage<BN, BKS, BKC, SEGB ? 2 : 0>(st + BM * BKS, B, p.ldb, n0, p.N, k, kend, p.segK, 0, 0,
+                                                    p.sBseg, wid, lane, dummy);
+        }
     };
     auto compute = [&](int s) {
         const float* As = smem + (s % NS) * STAGE;
