@@ -1152,14 +1152,28 @@ __global__ __launch_bounds__(256, 2) void gemm_gbf_kernel(GemmParams p) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
+    constexpr bool STREAM = !CONV && !SEGB;  // plain operands: per-block DMA source setup (GldsStream)
+    GldsStream<BM, BKS, AKC> sa;
+    GldsStream<BN, BKS, BKC> sb;
+    if (STREAM) {
+        sa.init(A, p.lda, m0, p.M, kbeg, wid, lane);
+        sb.init(B, p.ldb, n0, p.N, kbeg, wid, lane);
+    }
     auto issue = [&](int s) {
         float* st = smem + (s % NS) * STAGE;
         const int k = kbeg + s * BKS;
         const bool dummy = s >= nst;
-        glds_stage<BM, BKS, AKC, CONV ? 1 : 0>(st, A, p.lda, m0, p.M, k, kend, p.segK, p.pad, Mv, 0, wid,
-                                                lane, dummy);
-        glds_stage<BN, BKS, BKC, SEGB ? 2 : 0>(st + BM * BKS, B, p.ldb, n0, p.N, k, kend, p.segK, 0, 0, p.sBseg,
-                                                wid, lane, dummy);
+        if (NS == 2 && dummy) {
+            // vmcnt(0) waits: nothing to keep in step past the last stage
+        } else if (STREAM && k + BKS <= kend) {
+            glds_stream_issue(sa, st, wid);
+            glds_stream_issue(sb, st + BM * BKS, wid);
+        } else {
+            glds_stage<BM, BKS, AKC, CONV ? 1 : 0>(st, A, p.lda, m0, p.M, k, kend, p.segK, p.pad, Mv, 0, wid,
+                                                    lane, dummy);
+            glds_stage<BN, BKS, BKC, SEGB ? 2 : 0>(st + BM * BKS, B, p.ldb, n0, p.N, k, kend, p.segK, 0, 0,
+                                                    p.sBseg, wid, lane, dummy);
+        }
     };
     auto compute = [&](int s) {
         const float* As = smem + (s % NS) * STAGE;
