@@ -88,7 +88,9 @@ typedef struct suta_hparams {
 } suta_hparams;
 
 /* Weights: `n` tensors named by their HF state_dict key (e.g.
- * "wav2vec2.encoder.layers.0.attention.q_proj.weight"), float32, host memory, HF layout. */
+ * "wav2vec2.encoder.layers.0.attention.q_proj.weight"), float32, host memory, HF layout.
+ * max_samples: longest utterance any later call may pass (the reference truncates to 600000,
+ * data.py); longer inputs return SUTA_ERR_ARG; <= 0 means no limit beyond T <= 2048 frames. */
 int32_t suta_create(const suta_model_config* cfg, const char* const* names, const float* const* data,
                     const int64_t* numels, int32_t n, int32_t device, int32_t max_batch,
                     int64_t max_samples, suta_engine** out);

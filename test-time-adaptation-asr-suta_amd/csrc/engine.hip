@@ -1545,6 +1545,8 @@ int32_t suta_reset(suta_engine* e) {
 static void check_batch(suta_engine* e, int32_t batch, int64_t n) {
     if (batch < 1 || batch > e->max_batch) throw SutaError(SUTA_ERR_ARG, "batch outside [1, max_batch]");
     if (n < 1) throw SutaError(SUTA_ERR_ARG, "n_samples < 1");
+    if (e->max_samples > 0 && n > e->max_samples)
+        throw SutaError(SUTA_ERR_ARG, "n_samples > max_samples given to suta_create");
 }
 
 int32_t suta_forward(suta_engine* e, const float* wav, int32_t on_dev, int32_t norm, int32_t batch, int64_t n,
@@ -1650,6 +1652,8 @@ int32_t suta_adapt_varlen(suta_engine* e, const float* wav, int32_t on_dev, int3
         int64_t nmax = 0;
         for (int b = 0; b < batch; ++b) nmax = std::max<int64_t>(nmax, n_samples[b]);
         if (stride < nmax) throw SutaError(SUTA_ERR_ARG, "stride < max(n_samples)");
+        if (e->max_samples > 0 && nmax > e->max_samples)
+            throw SutaError(SUTA_ERR_ARG, "n_samples > max_samples given to suta_create");
         // the layout length is `stride`: callers quantise it so repeated layouts reuse the captured step
         adapt_impl(e, wav, on_dev, norm, batch, stride, n_samples, stride, steps, hp, rec, nrec, logits_out,
                    logits_on_dev, ids_out, frames_out);

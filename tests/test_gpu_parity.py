@@ -113,6 +113,40 @@ def test_base_forward_matches_oracle_8s(precision):
     np.testing.assert_allclose(got, ref, rtol=0, atol=5e-5)
 
 
+@pytest.mark.parametrize("n", [400, 719, 720, 1041])
+def test_shortest_inputs_match_oracle(n):
+    """Edge lengths of the conv stack: N = 400 is the shortest input with a frame (T = 1; the receptive
+    field), 719/720 straddle T = 1 -> 2, 1041 gives T = 3.  Two SUTA steps against the CPU oracle."""
+    from oracle import w2v2_cpu as W
+    eng, cfg = engine("wav2vec2-base")
+    sd = synth_weights(cfg)
+    x = synth.wave(n, 11)
+    logits, ids, T = eng.adapt(x, 2, SutaHParams(lr=5e-4), record=[0, 1, 2])
+    assert T == (n - 400) // 320 + 1
+    ref, _ = W.run_suta({k: torch.from_numpy(v) for k, v in sd.items()}, cfg, torch.from_numpy(x)[None], 2,
+                        lr=5e-4, record=[0, 1, 2])
+    for r in (0, 1, 2):
+        np.testing.assert_allclose(logits[r][0], ref[r][0].numpy(), rtol=0, atol=logits_tol(5e-4),
+                                   err_msg=f"N{n} step {r}")
+
+
+def test_longest_input_matches_oracle():
+    """The reference truncates every utterance to 600 000 samples (data.py, 37.5 s, T = 1874): the
+    engine's maximum size.  One SUTA step against the CPU oracle at that length."""
+    from oracle import w2v2_cpu as W
+    eng, cfg = engine("wav2vec2-base")
+    sd = synth_weights(cfg)
+    x = synth.wave(600000, 12)
+    logits, ids, T = eng.adapt(x, 1, SutaHParams(), record=[0, 1])
+    assert T == 1874
+    ref, _ = W.run_suta({k: torch.from_numpy(v) for k, v in sd.items()}, cfg, torch.from_numpy(x)[None], 1,
+                        record=[0, 1])
+    for r in (0, 1):
+        np.testing.assert_allclose(logits[r][0], ref[r][0].numpy(), rtol=0, atol=5e-5, err_msg=f"step {r}")
+    with pytest.raises(Exception):
+        eng.adapt(synth.wave(600001, 12), 1, SutaHParams(), record=[1])
+
+
 def test_raw_wave_normalisation_on_device():
     eng, cfg = engine("tiny-group")
     raw = synth.raw_wave(9000, 5)
