@@ -126,7 +126,7 @@ def main():
                     help="GEMM arithmetic: exact fp32 MFMA, fp32-accurate 3-way bf16 split, or bf16 (config C4)")
     ap.add_argument("--no-c4", dest="c4", action="store_false",
                     help="skip the config-C4 line (wav2vec2-large, 20 SUTA steps, bf16 GEMMs; 1 GPU only)")
-    ap.add_argument("--c4-batch", type=int, default=32)
+    ap.add_argument("--c4-batch", type=int, default=64)
     ap.add_argument("--only-c4", action="store_true", help="print only the config-C4 line (profiling)")
     ap.add_argument("--no-split", dest="also_split", action="store_false",
                     help="do not also time the fp32-accurate split-bf16 GEMM mode")

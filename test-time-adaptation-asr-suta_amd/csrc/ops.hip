@@ -4,6 +4,7 @@
 // duplicate-entry multiplicity.  All reductions are fixed-order (bitwise reproducible).
 #include "ops.h"
 #include <algorithm>
+#include <stdexcept>
 
 namespace {
 
@@ -510,6 +511,7 @@ __global__ __launch_bounds__(256) void layernorm_bwd_vec_kernel(
 }
 
 // sum partial slabs [B][nchunk][nvec][D] over chunks in order -> out_v[b*ostride + c]
+// (loads issued 8 chunks at a time, summed in chunk order: the result is that of the serial loop)
 __global__ __launch_bounds__(256) void chunk_reduce(const float* __restrict__ part, int nchunk, int nvec, int D,
                                                     float* __restrict__ out0, float* __restrict__ out1, long ostride) {
     const int b = blockIdx.y;
@@ -518,8 +520,18 @@ __global__ __launch_bounds__(256) void chunk_reduce(const float* __restrict__ pa
     for (int v = 0; v < nvec; ++v) {
         float* out = v == 0 ? out0 : out1;
         if (!out) continue;
+        const float* q = part + ((long)b * nchunk * nvec + v) * D + c;
+        const long cs = (long)nvec * D;  // chunk stride
         float s = 0.f;
-        for (int ch = 0; ch < nchunk; ++ch) s += part[(((long)b * nchunk + ch) * nvec + v) * D + c];
+        int ch = 0;
+        for (; ch + 8 <= nchunk; ch += 8) {
+            float t[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) t[u] = q[(ch + u) * cs];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s += t[u];
+        }
+        for (; ch < nchunk; ++ch) s += q[ch * cs];
         out[(long)b * ostride + c] = s;
     }
 }
@@ -531,7 +543,15 @@ __global__ __launch_bounds__(256) void colsum_partial(const float* __restrict__ 
     const float* xb = x + (long)b * rows * C;
     for (int c = threadIdx.x; c < C; c += 256) {
         float s = 0.f;
-        for (int r = r0; r < r1; ++r) s += xb[(long)r * C + c];
+        int r = r0;
+        for (; r + 8 <= r1; r += 8) {  // 8 loads in flight, summed in row order
+            float t[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) t[u] = xb[(long)(r + u) * C + c];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s += t[u];
+        }
+        for (; r < r1; ++r) s += xb[(long)r * C + c];
         part[((long)b * nchunk + ch) * C + c] = s;
     }
 }
@@ -835,35 +855,48 @@ __global__ __launch_bounds__(256) void argmax_kernel(const float* __restrict__ l
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ P, const float* __restrict__ G,
                                                    float* __restrict__ M, float* __restrict__ Vv, long pstride,
-                                                   AdamArgs a, long total) {
+                                                   AdamArgs a, long total4) {
+    // one thread per 16-B group of a run (run starts are 4-float aligned; elements past a run's end
+    // inside its last group are loaded and stored back unchanged)
     const int b = blockIdx.y;
     const long base = (long)b * pstride;
     const float* tab = a.tab ? a.tab + (long)(*a.step) * 50 : nullptr;
-    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-        // map i to (run, offset)
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total4; i += (long)gridDim.x * 256) {
         long rem = i;
         int run = 0;
-        while (run < a.nruns && rem >= a.runs[run].len) {
-            rem -= a.runs[run].len;
+        while (run < a.nruns && rem >= (a.runs[run].len + 3) / 4) {
+            rem -= (a.runs[run].len + 3) / 4;
             ++run;
         }
         if (run >= a.nruns) continue;
-        const long idx = base + a.runs[run].start + rem;
+        const long idx = base + a.runs[run].start + 4 * rem;
+        const int nv = (int)min(4L, a.runs[run].len - 4 * rem);
         const int k = a.runs[run].k;
-        const float g = G[idx];
-        float p = P[idx], m = M[idx], v = Vv[idx];
-        for (int j = 0; j < k; ++j) {
-            if (a.lr_wd != 0.f) p *= 1.0f - a.lr_wd;
-            m = m + a.omb1 * (g - m);                 // lerp_(g, 1-beta1), weight < 0.5 form
-            v = v * a.beta2 + a.omb2 * (g * g);        // mul_(beta2).addcmul_(g, g, 1-beta2)
-            const float ss = tab ? tab[(k - 1) * 5 + j] : a.step_size[k - 1][j];
-            const float bs = tab ? tab[25 + (k - 1) * 5 + j] : a.bc2_sqrt[k - 1][j];
-            const float denom = sqrtf(v) / bs + a.eps;
-            p = p + (-ss) * (m / denom);                  // addcdiv_(m, denom, -step_size)
+        const f32x4 g4 = *reinterpret_cast<const f32x4*>(G + idx);
+        f32x4 p4 = *reinterpret_cast<const f32x4*>(P + idx);
+        f32x4 m4 = *reinterpret_cast<const f32x4*>(M + idx);
+        f32x4 v4 = *reinterpret_cast<const f32x4*>(Vv + idx);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            if (e >= nv) break;
+            const float g = g4[e];
+            float p = p4[e], m = m4[e], v = v4[e];
+            for (int j = 0; j < k; ++j) {
+                if (a.lr_wd != 0.f) p *= 1.0f - a.lr_wd;
+                m = m + a.omb1 * (g - m);                 // lerp_(g, 1-beta1), weight < 0.5 form
+                v = v * a.beta2 + a.omb2 * (g * g);        // mul_(beta2).addcmul_(g, g, 1-beta2)
+                const float ss = tab ? tab[(k - 1) * 5 + j] : a.step_size[k - 1][j];
+                const float bs = tab ? tab[25 + (k - 1) * 5 + j] : a.bc2_sqrt[k - 1][j];
+                const float denom = sqrtf(v) / bs + a.eps;
+                p = p + (-ss) * (m / denom);                  // addcdiv_(m, denom, -step_size)
+            }
+            p4[e] = p;
+            m4[e] = m;
+            v4[e] = v;
         }
-        P[idx] = p;
-        M[idx] = m;
-        Vv[idx] = v;
+        *reinterpret_cast<f32x4*>(P + idx) = p4;
+        *reinterpret_cast<f32x4*>(M + idx) = m4;
+        *reinterpret_cast<f32x4*>(Vv + idx) = v4;
     }
 }
 
@@ -982,11 +1015,15 @@ void launch_step_advance(int* step, hipStream_t st) {
 
 void launch_adam(float* P, const float* G, float* M, float* V, long pstride, int B, const AdamArgs& a,
                  hipStream_t st) {
-    long total = 0;
-    for (int r = 0; r < a.nruns; ++r) total += a.runs[r].len;
-    if (total == 0) return;
-    const int gx = (int)std::min<long>(std::max<long>(1, 4096 / std::max(1, B)), (total + 255) / 256);
-    hipLaunchKernelGGL(adam_kernel, dim3(gx, B), dim3(256), 0, st, P, G, M, V, pstride, a, total);
+    long total4 = 0;
+    for (int r = 0; r < a.nruns; ++r) {
+        if (a.runs[r].start % 4) throw std::runtime_error("adam run start not 16-B aligned");
+        total4 += (a.runs[r].len + 3) / 4;
+    }
+    if (total4 == 0) return;
+    if (pstride % 4) throw std::runtime_error("adam slot stride not a multiple of 4");
+    const int gx = (int)std::min<long>(std::max<long>(1, 4096 / std::max(1, B)), (total4 + 255) / 256);
+    hipLaunchKernelGGL(adam_kernel, dim3(gx, B), dim3(256), 0, st, P, G, M, V, pstride, a, total4);
 }
 
 template <int MODE, typename... Args>
