@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -146,6 +147,7 @@ struct suta_engine {
     hipStream_t st = nullptr;
     int max_batch = 0;
     long max_samples = 0;
+    bool attn_fused = true;  // fused attention forward (launch_attn_fwd) where its shape holds; env SUTA_ATTN_FUSED=0 off
     // frozen weights
     std::vector<float*> wqkv, bqkv, wo, bo, w1, b1, w2, b2;
     float *wpos_f = nullptr, *wpos_b = nullptr, *bpos = nullptr, *wlm = nullptr, *blm = nullptr;
@@ -586,52 +588,61 @@ void suta_engine::forward(int B) {
             g.bias = bqkv[l];
             gemm(g);
         }
-        {  // S = Q K^T * scale
-            GemmParams g;
-            gemm_init(g);
-            g.A = lb.qkv;
-            g.lda = 3 * H;
-            g.B = lb.qkv + H;
-            g.tb = 1;
-            g.ldb = 3 * H;
-            g.C = lb.P;
-            g.ldc = pl.Tp;
-            g.M = T;
-            g.N = T;
-            g.K = d;
-            g.Z = B * NH;
-            g.zdiv = NH;
-            g.sA0 = d;
-            g.sA1 = (long)T * 3 * H;
-            g.sB0 = d;
-            g.sB1 = (long)T * 3 * H;
-            g.sC0 = (long)T * pl.Tp;
-            g.sC1 = (long)NH * T * pl.Tp;
-            g.alpha = scale;
-            gemm(g);
-        }
-        timed(F_SOFTMAX, [&] { launch_softmax_rows(lb.P, (long)B * NH * T, T, pl.Tp, rT(), (long)NH * T, st); });
-        {  // ctx = P V
-            GemmParams g;
-            gemm_init(g);
-            g.A = lb.P;
-            g.lda = pl.Tp;
-            g.B = lb.qkv + 2 * H;
-            g.ldb = 3 * H;
-            g.C = lb.ctx;
-            g.ldc = H;
-            g.M = T;
-            g.N = d;
-            g.K = T;
-            g.Z = B * NH;
-            g.zdiv = NH;
-            g.sA0 = (long)T * pl.Tp;
-            g.sA1 = (long)NH * T * pl.Tp;
-            g.sB0 = d;
-            g.sB1 = (long)T * 3 * H;
-            g.sC0 = d;
-            g.sC1 = (long)T * H;
-            gemm(g);
+        // S -> softmax -> P -> ctx in one kernel (timed with the MFMA contractions) where its shape holds
+        const bool fused = attn_fused && d == 64 && T <= 512;
+        if (fused)
+            timed(F_GEMM, [&] {
+                if (!launch_attn_fwd(lb.qkv, lb.P, lb.ctx, B, T, (int)pl.Tp, NH, H, d, scale, rT(), st))
+                    throw SutaError(SUTA_ERR_UNSUPPORTED, "fused attention shape");
+            });
+        if (!fused) {
+            {  // S = Q K^T * scale
+                GemmParams g;
+                gemm_init(g);
+                g.A = lb.qkv;
+                g.lda = 3 * H;
+                g.B = lb.qkv + H;
+                g.tb = 1;
+                g.ldb = 3 * H;
+                g.C = lb.P;
+                g.ldc = pl.Tp;
+                g.M = T;
+                g.N = T;
+                g.K = d;
+                g.Z = B * NH;
+                g.zdiv = NH;
+                g.sA0 = d;
+                g.sA1 = (long)T * 3 * H;
+                g.sB0 = d;
+                g.sB1 = (long)T * 3 * H;
+                g.sC0 = (long)T * pl.Tp;
+                g.sC1 = (long)NH * T * pl.Tp;
+                g.alpha = scale;
+                gemm(g);
+            }
+            timed(F_SOFTMAX, [&] { launch_softmax_rows(lb.P, (long)B * NH * T, T, pl.Tp, rT(), (long)NH * T, st); });
+            {  // ctx = P V
+                GemmParams g;
+                gemm_init(g);
+                g.A = lb.P;
+                g.lda = pl.Tp;
+                g.B = lb.qkv + 2 * H;
+                g.ldb = 3 * H;
+                g.C = lb.ctx;
+                g.ldc = H;
+                g.M = T;
+                g.N = d;
+                g.K = T;
+                g.Z = B * NH;
+                g.zdiv = NH;
+                g.sA0 = (long)T * pl.Tp;
+                g.sA1 = (long)NH * T * pl.Tp;
+                g.sB0 = d;
+                g.sB1 = (long)T * 3 * H;
+                g.sC0 = d;
+                g.sC1 = (long)T * H;
+                gemm(g);
+            }
         }
         {  // out projection + residual
             GemmParams g;
@@ -1372,6 +1383,7 @@ int32_t suta_create(const suta_model_config* cfg, const char* const* names, cons
         e->device = device;
         e->max_batch = max_batch;
         e->max_samples = max_samples;
+        if (const char* af = std::getenv("SUTA_ATTN_FUSED")) e->attn_fused = af[0] != '0';
         HIPCHK(hipSetDevice(device));
         HIPCHK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
         e->d_step = reinterpret_cast<int*>(e->dalloc(1));

@@ -44,6 +44,10 @@ void launch_colsum(const float* x, int B, int rows, int C, float* out, long ostr
 
 // In-place row softmax of `nrows` rows of length T (row stride ld).  tlen (device, may be null):
 // ragged batch, rows of utterance row / rows_per_utt use their first tlen[u] keys; the rest get 0.
+// fused S = QK^T*scale -> softmax -> P (stored) -> ctx = PV for head dim 64, T <= 512 (exact fp32 MFMA);
+// false (nothing launched) when the shape is outside that
+bool launch_attn_fwd(const float* qkv, float* P, float* ctx, int B, int T, int Tp, int NH, int H, int dh, float scale,
+                     const int* tlen, hipStream_t st);
 void launch_softmax_rows(float* s, long nrows, int T, long ld, const int* tlen, long rows_per_utt, hipStream_t st);
 
 // delta[b][h][t] = dot(dO[b][t][head h], O[b][t][head h]): the softmax-backward row term sum_j P_ij dP_ij.

@@ -557,6 +557,164 @@ __global__ __launch_bounds__(256) void colsum_partial(const float* __restrict__ 
 }
 
 // ------------------------------------------------------------------------------------------
+// Fused attention forward, one block (8 waves) per (utterance, head), head dim 64, T <= 16*NF:
+//   pass 1: K staged in LDS once; each wave takes 16-query groups: S^T = K Q^T on exact-fp32
+//           v_mfma_f32_16x16x4_f32, softmax over keys in registers, P row segments stored;
+//   pass 2: V staged in the same LDS; each wave reloads its own P rows (same lanes that stored
+//           them) and computes ctx = P V.
+// Replaces S-GEMM -> softmax (P read + written) -> PV-GEMM and loads K and V once per head.
+// LDS rows are [key][68] (16-B rows padded by 4 floats: conflict-free for both read patterns), rows
+// >= T zero.  Lane (r = lane & 15, g = lane >> 4) holds, for key fragment f,
+//   S^T[key 16f + 4g + i][query q0 + r], i = 0..3  (the MFMA C/D map),
+// which is a 16-B run of P's row q0 + r and, in pass 2, the A operand of P V
+// (A[row r][k g] = P[q0 + r][16f + 4g + i]).  The head-dim contraction takes d = 16g + m in MFMA m.
+// Keys >= the utterance's length get probability 0 (ragged batches); rows past T are not stored.
+// ------------------------------------------------------------------------------------------
+constexpr int AF_LD = 68;
+constexpr int AF_THREADS = 512;
+
+template <int NF>
+__device__ __forceinline__ void attn_stage_rows(float* __restrict__ lds, const float* __restrict__ src, long ld,
+                                                int T) {
+    constexpr int ITEMS = NF * 16 * 16, NPT = (ITEMS + AF_THREADS - 1) / AF_THREADS;
+    // all 16-B loads of a thread issued before its first LDS store (one memory round trip)
+    f32x4 v[NPT];
+#pragma unroll
+    for (int n = 0; n < NPT; ++n) {
+        const int it = threadIdx.x + n * AF_THREADS;
+        const int row = it >> 4, c4 = (it & 15) * 4;
+        v[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (it < ITEMS && row < T) v[n] = *reinterpret_cast<const f32x4*>(src + (long)row * ld + c4);
+    }
+#pragma unroll
+    for (int n = 0; n < NPT; ++n) {
+        const int it = threadIdx.x + n * AF_THREADS;
+        if (it < ITEMS) *reinterpret_cast<f32x4*>(lds + (it >> 4) * AF_LD + (it & 15) * 4) = v[n];
+    }
+}
+
+template <int NF>
+__global__ __launch_bounds__(AF_THREADS, 1) void attn_fwd_kernel(const float* __restrict__ qkv, float* __restrict__ P,
+                                                                 float* __restrict__ ctx, int T, int Tp, int NH,
+                                                                 int H, float scale, const int* __restrict__ tlen) {
+    __shared__ __attribute__((aligned(16))) float lds[NF * 16 * AF_LD];
+    const int bh = blockIdx.x;  // utterance * NH + head
+    const int hd = bh % NH, u = bh / NH;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int r = lane & 15, g = lane >> 4;
+    const int ngrp = (T + 15) >> 4;
+    const int tl = tlen ? tlen[u] : T;
+    const long ld = 3L * H;
+    const float* Qb = qkv + (long)u * T * ld + hd * 64;
+    float* Pb = P + (long)bh * T * Tp;
+
+    attn_stage_rows<NF>(lds, Qb + H, ld, T);  // K
+    __syncthreads();
+    for (int grp = w; grp < ngrp; grp += AF_THREADS / 64) {
+        const int q0 = grp * 16;
+        f32x4 qv[4];
+        {
+            const float* qp = Qb + (long)min(q0 + r, T - 1) * ld + 16 * g;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) qv[j] = *reinterpret_cast<const f32x4*>(qp + 4 * j);
+        }
+        f32x4 s[NF];
+        // two key fragments per pass: two independent MFMA chains
+#pragma unroll
+        for (int f = 0; f < NF; f += 2) {
+            const float* kp = lds + (16 * f + r) * AF_LD + 16 * g;
+            f32x4 k0[4], k1[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) k0[j] = *reinterpret_cast<const f32x4*>(kp + 4 * j);
+            if (f + 1 < NF) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) k1[j] = *reinterpret_cast<const f32x4*>(kp + 16 * AF_LD + 4 * j);
+            }
+            s[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (f + 1 < NF) s[f + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    s[f] = __builtin_amdgcn_mfma_f32_16x16x4f32(k0[j][e], qv[j][e], s[f], 0, 0, 0);
+                    if (f + 1 < NF) s[f + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(k1[j][e], qv[j][e], s[f + 1], 0, 0, 0);
+                }
+            __builtin_amdgcn_sched_barrier(0);  // bound the LDS reads hoisted ahead (register budget)
+        }
+        // softmax over the keys of query q0 + r: this lane's 4*NF values, then the 4 lanes r + 16g
+        float mx = -INFINITY;
+#pragma unroll
+        for (int f = 0; f < NF; ++f)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float v = scale * s[f][i];
+                s[f][i] = v;
+                if (16 * f + 4 * g + i < tl) mx = fmaxf(mx, v);
+            }
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        float sum = 0.f;
+#pragma unroll
+        for (int f = 0; f < NF; ++f)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float v = 16 * f + 4 * g + i < tl ? expf(s[f][i] - mx) : 0.f;
+                s[f][i] = v;
+                sum += v;
+            }
+        sum += __shfl_xor(sum, 16, 64);
+        sum += __shfl_xor(sum, 32, 64);
+        const float inv = 1.0f / sum;
+        if (q0 + r < T) {
+            float* prow = Pb + (long)(q0 + r) * Tp;
+#pragma unroll
+            for (int f = 0; f < NF; ++f)
+                if (16 * f + 4 * g < Tp) *reinterpret_cast<f32x4*>(prow + 16 * f + 4 * g) = s[f] * inv;
+        }
+    }
+    __syncthreads();  // every wave is done with K
+    attn_stage_rows<NF>(lds, Qb + 2 * H, ld, T);  // V
+    __syncthreads();
+    for (int grp = w; grp < ngrp; grp += AF_THREADS / 64) {
+        const int q0 = grp * 16;
+        // this lane's own P segments from pass 1 (zero for rows past T / keys past Tp)
+        f32x4 pf[NF];
+        const float* prow = Pb + (long)(q0 + r) * Tp;
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+            pf[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (q0 + r < T && 16 * f + 4 * g < Tp) pf[f] = *reinterpret_cast<const f32x4*>(prow + 16 * f + 4 * g);
+        }
+        // ctx[q0 + 4g + i][16 cf + r] = sum_key P[.][key] V[key][16 cf + r]
+        f32x4 o[4];
+#pragma unroll
+        for (int cf = 0; cf < 4; ++cf) o[cf] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int f = 0; f < NF; ++f)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float* vp = lds + (16 * f + 4 * g + i) * AF_LD + r;
+                float vv[4];
+#pragma unroll
+                for (int cf = 0; cf < 4; ++cf) vv[cf] = vp[16 * cf];
+#pragma unroll
+                for (int cf = 0; cf < 4; ++cf)
+                    o[cf] = __builtin_amdgcn_mfma_f32_16x16x4f32(pf[f][i], vv[cf], o[cf], 0, 0, 0);
+                if (i == 3) __builtin_amdgcn_sched_barrier(0);
+            }
+        float* cb = ctx + (long)u * T * H + hd * 64 + r;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int q = q0 + 4 * g + i;
+            if (q < T) {
+#pragma unroll
+                for (int cf = 0; cf < 4; ++cf) cb[(long)q * H + 16 * cf] = o[cf][i];
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // attention softmax over rows of length T (<= 64*NPL), one wave per row
 // ------------------------------------------------------------------------------------------
 template <int NPL>
@@ -992,6 +1150,21 @@ void launch_softmax_rows(float* s, long nrows, int T, long ld, const int* tlen, 
                                     rows_per_utt);
     else hipLaunchKernelGGL(softmax_rows_kernel<32>, grid, dim3(256), 0, st, s, nrows, T, ld, tlen,
                                     rows_per_utt);
+}
+
+bool launch_attn_fwd(const float* qkv, float* P, float* ctx, int B, int T, int Tp, int NH, int H, int dh, float scale,
+                     const int* tlen, hipStream_t st) {
+    if (dh != 64 || T < 1 || T > 512 || H % 4 || Tp % 4 || Tp < T) return false;
+    const dim3 grid((unsigned)((long)B * NH));
+#define AF(NF_) hipLaunchKernelGGL(attn_fwd_kernel<NF_>, grid, dim3(AF_THREADS), 0, st, qkv, P, ctx, T, Tp, NH, H, scale, tlen)
+    const int nf = (T + 15) / 16;
+    if (nf <= 4) AF(4);
+    else if (nf <= 8) AF(8);
+    else if (nf <= 16) AF(16);
+    else if (nf <= 25) AF(25);
+    else AF(32);
+#undef AF
+    return true;
 }
 
 void launch_dgelu_mul(const float* g, const float* z, float* out, long n, hipStream_t st) {

@@ -116,17 +116,18 @@ def test_base_forward_matches_oracle_8s(precision):
 @pytest.mark.parametrize("n", [400, 719, 720, 1041])
 def test_shortest_inputs_match_oracle(n):
     """Edge lengths of the conv stack: N = 400 is the shortest input with a frame (T = 1; the receptive
-    field), 719/720 straddle T = 1 -> 2, 1041 gives T = 3.  Two SUTA steps against the CPU oracle."""
+    field), 719/720 straddle T = 1 -> 2, 1041 gives T = 3.  Two SUTA steps (scripts' lr) against the CPU
+    oracle, with the base-size tolerance of test_base_suta_matches_reference."""
     from oracle import w2v2_cpu as W
     eng, cfg = engine("wav2vec2-base")
     sd = synth_weights(cfg)
     x = synth.wave(n, 11)
-    logits, ids, T = eng.adapt(x, 2, SutaHParams(lr=5e-4), record=[0, 1, 2])
+    logits, ids, T = eng.adapt(x, 2, SutaHParams(), record=[0, 1, 2])
     assert T == (n - 400) // 320 + 1
     ref, _ = W.run_suta({k: torch.from_numpy(v) for k, v in sd.items()}, cfg, torch.from_numpy(x)[None], 2,
-                        lr=5e-4, record=[0, 1, 2])
+                        record=[0, 1, 2])
     for r in (0, 1, 2):
-        np.testing.assert_allclose(logits[r][0], ref[r][0].numpy(), rtol=0, atol=logits_tol(5e-4),
+        np.testing.assert_allclose(logits[r][0], ref[r][0].numpy(), rtol=0, atol=1e-5 if r == 0 else 5e-5,
                                    err_msg=f"N{n} step {r}")
 
 
@@ -247,3 +248,27 @@ def test_all_blank_utterance_keeps_finite_params():
     assert np.isnan(loss).all()
     for name in eng.trainable_names():
         assert np.isfinite(eng.get_param(0, name)).all(), name
+
+
+@pytest.mark.parametrize("n", [32000, 128000])
+def test_fused_attention_equals_unfused(n, monkeypatch):
+    """The fused attention forward (S -> softmax -> P -> ctx in one kernel, exact fp32 MFMA) against the
+    S-GEMM / softmax / PV-GEMM path: 3 SUTA steps, ragged pair included (keys past an utterance's length
+    get probability 0 in both)."""
+    cfg = get_config("wav2vec2-base")
+    sd = synth_weights(cfg)
+    monkeypatch.setenv("SUTA_ATTN_FUSED", "0")
+    ref_eng = SutaEngine(cfg, sd, max_batch=2, max_samples=n)
+    monkeypatch.setenv("SUTA_ATTN_FUSED", "1")
+    eng, _ = engine("wav2vec2-base")
+    x = synth.wave(n, 21)
+    a, _, _ = ref_eng.adapt(x, 3, SutaHParams(), record=[0, 3])
+    b, _, _ = eng.adapt(x, 3, SutaHParams(), record=[0, 3])
+    for r in (0, 3):
+        np.testing.assert_allclose(b[r], a[r], rtol=0, atol=2e-5, err_msg=f"step {r}")
+    waves = [synth.wave(n, 22), synth.wave(n * 3 // 5, 23)]
+    a, _, _ = ref_eng.adapt_varlen(waves, 2, SutaHParams(), record=[2])
+    b, _, _ = eng.adapt_varlen(waves, 2, SutaHParams(), record=[2])
+    for u in range(2):
+        np.testing.assert_allclose(b[2][u], a[2][u], rtol=0, atol=2e-5, err_msg=f"ragged utterance {u}")
+    ref_eng.close()
