@@ -846,59 +846,70 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
         nn_gemm(dhres, H, wo[l], H, pl.ctx, H, (int)BT, H, H, 0, nullptr, 0, nullptr, 0);
         // softmax-backward row term delta = rowsum(dctx * ctx) per head, fused into the dP epilogue
         timed(F_SOFTMAX, [&] { launch_attn_delta(pl.ctx, lb.ctx, pl.delta, B, T, NH, d, st); });
-        {  // dS = scale * P * (dctx_h @ V_h^T - delta)
-            GemmParams g;
-            gemm_init(g);
-            g.A = pl.ctx;
-            g.lda = H;
-            g.B = lb.qkv + 2 * H;
-            g.tb = 1;
-            g.ldb = 3 * H;
-            g.C = pl.dP;
-            g.ldc = pl.Tp;
-            g.M = T;
-            g.N = T;
-            g.K = d;
-            g.Z = B * NH;
-            g.zdiv = NH;
-            g.sA0 = d;
-            g.sA1 = (long)T * H;
-            g.sB0 = d;
-            g.sB1 = (long)T * 3 * H;
-            g.sC0 = (long)T * pl.Tp;
-            g.sC1 = (long)NH * T * pl.Tp;
-            g.epi = EPI_SMBWD;
-            g.alpha = scale;
-            g.aux = lb.P;
-            g.ldaux = pl.Tp;
-            g.sAux0 = (long)T * pl.Tp;
-            g.sAux1 = (long)NH * T * pl.Tp;
-            g.rowv = pl.delta;
-            g.sRow0 = T;
-            g.sRow1 = (long)NH * T;
-            gemm(g);
-        }
-        {  // dQ = dS K_h
-            GemmParams g;
-            gemm_init(g);
-            g.A = pl.dP;
-            g.lda = pl.Tp;
-            g.B = lb.qkv + H;
-            g.ldb = 3 * H;
-            g.C = pl.dqkv;
-            g.ldc = 3 * H;
-            g.M = T;
-            g.N = d;
-            g.K = T;
-            g.Z = B * NH;
-            g.zdiv = NH;
-            g.sA0 = (long)T * pl.Tp;
-            g.sA1 = (long)NH * T * pl.Tp;
-            g.sB0 = d;
-            g.sB1 = (long)T * 3 * H;
-            g.sC0 = d;
-            g.sC1 = (long)T * 3 * H;
-            gemm(g);
+        // dS (stored) and dQ in one kernel where the fused attention shape holds (else dP GEMM with the
+        // softmax-backward epilogue, then the dQ GEMM)
+        const bool fused_bwd = attn_fused && d == 64 && T <= 512;
+        if (fused_bwd)
+            timed(F_GEMM, [&] {
+                if (!launch_attn_bwd(lb.qkv, lb.P, pl.ctx, pl.delta, pl.dP, pl.dqkv, B, T, (int)pl.Tp, NH, H, d, scale,
+                                     st))
+                    throw SutaError(SUTA_ERR_UNSUPPORTED, "fused attention shape");
+            });
+        if (!fused_bwd) {
+            {  // dS = scale * P * (dctx_h @ V_h^T - delta)
+                GemmParams g;
+                gemm_init(g);
+                g.A = pl.ctx;
+                g.lda = H;
+                g.B = lb.qkv + 2 * H;
+                g.tb = 1;
+                g.ldb = 3 * H;
+                g.C = pl.dP;
+                g.ldc = pl.Tp;
+                g.M = T;
+                g.N = T;
+                g.K = d;
+                g.Z = B * NH;
+                g.zdiv = NH;
+                g.sA0 = d;
+                g.sA1 = (long)T * H;
+                g.sB0 = d;
+                g.sB1 = (long)T * 3 * H;
+                g.sC0 = (long)T * pl.Tp;
+                g.sC1 = (long)NH * T * pl.Tp;
+                g.epi = EPI_SMBWD;
+                g.alpha = scale;
+                g.aux = lb.P;
+                g.ldaux = pl.Tp;
+                g.sAux0 = (long)T * pl.Tp;
+                g.sAux1 = (long)NH * T * pl.Tp;
+                g.rowv = pl.delta;
+                g.sRow0 = T;
+                g.sRow1 = (long)NH * T;
+                gemm(g);
+            }
+            {  // dQ = dS K_h
+                GemmParams g;
+                gemm_init(g);
+                g.A = pl.dP;
+                g.lda = pl.Tp;
+                g.B = lb.qkv + H;
+                g.ldb = 3 * H;
+                g.C = pl.dqkv;
+                g.ldc = 3 * H;
+                g.M = T;
+                g.N = d;
+                g.K = T;
+                g.Z = B * NH;
+                g.zdiv = NH;
+                g.sA0 = (long)T * pl.Tp;
+                g.sA1 = (long)NH * T * pl.Tp;
+                g.sB0 = d;
+                g.sB1 = (long)T * 3 * H;
+                g.sC0 = d;
+                g.sC1 = (long)T * 3 * H;
+                gemm(g);
+            }
         }
         {  // dK = dS^T Q_h
             GemmParams g;

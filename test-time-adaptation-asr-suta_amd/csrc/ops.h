@@ -48,6 +48,9 @@ void launch_colsum(const float* x, int B, int rows, int C, float* out, long ostr
 // false (nothing launched) when the shape is outside that
 bool launch_attn_fwd(const float* qkv, float* P, float* ctx, int B, int T, int Tp, int NH, int H, int dh, float scale,
                      const int* tlen, hipStream_t st);
+// fused dS = scale * P * (dctx V^T - delta) (stored) and dQ = dS K into dqkv's Q columns; same shape limits
+bool launch_attn_bwd(const float* qkv, const float* P, const float* dctx, const float* delta, float* dS, float* dqkv,
+                     int B, int T, int Tp, int NH, int H, int dh, float scale, hipStream_t st);
 void launch_softmax_rows(float* s, long nrows, int T, long ld, const int* tlen, long rows_per_utt, hipStream_t st);
 
 // delta[b][h][t] = dot(dO[b][t][head h], O[b][t][head h]): the softmax-backward row term sum_j P_ij dP_ij.

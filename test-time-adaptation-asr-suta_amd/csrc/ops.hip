@@ -715,6 +715,123 @@ __global__ __launch_bounds__(AF_THREADS, 1) void attn_fwd_kernel(const float* __
 }
 
 // ------------------------------------------------------------------------------------------
+// Fused attention backward, dS and dQ, one block (8 waves) per (utterance, head), same layout as
+// attn_fwd_kernel:
+//   pass 1: V staged; per 16-query group dP^T = V dctx^T (exact-fp32 16x16x4 MFMA), then
+//           dS = scale * P * (dP - delta) with the lane's P segments read from HBM, dS stored;
+//   pass 2: K staged; dQ = dS K from the lane's own dS segments (written into dqkv's Q columns).
+// Replaces the dP GEMM (softmax-backward epilogue) and the dQ GEMM; dK = dS^T Q and dV = P^T dctx
+// stay GEMMs.  delta[bh][q] = rowsum(dctx * ctx) (attn_delta_kernel).
+// ------------------------------------------------------------------------------------------
+template <int NF>
+__global__ __launch_bounds__(AF_THREADS, 1) void attn_bwd_kernel(const float* __restrict__ qkv,
+                                                                 const float* __restrict__ P,
+                                                                 const float* __restrict__ dctx,
+                                                                 const float* __restrict__ delta,
+                                                                 float* __restrict__ dS, float* __restrict__ dqkv,
+                                                                 int T, int Tp, int NH, int H, float scale) {
+    __shared__ __attribute__((aligned(16))) float lds[NF * 16 * AF_LD];
+    const int bh = blockIdx.x;  // utterance * NH + head
+    const int hd = bh % NH, u = bh / NH;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int r = lane & 15, g = lane >> 4;
+    const int ngrp = (T + 15) >> 4;
+    const long ld = 3L * H;
+    const float* Qb = qkv + (long)u * T * ld + hd * 64;
+    const float* Db = dctx + (long)u * T * H + hd * 64;
+    const float* Pb = P + (long)bh * T * Tp;
+    float* Sb = dS + (long)bh * T * Tp;
+    const float* dlt = delta + (long)bh * T;
+
+    attn_stage_rows<NF>(lds, Qb + 2 * H, ld, T);  // V
+    __syncthreads();
+    for (int grp = w; grp < ngrp; grp += AF_THREADS / 64) {
+        const int q0 = grp * 16;
+        const int qr = min(q0 + r, T - 1);
+        f32x4 dv[4];
+        {
+            const float* dp = Db + (long)qr * H + 16 * g;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) dv[j] = *reinterpret_cast<const f32x4*>(dp + 4 * j);
+        }
+        f32x4 s[NF];
+#pragma unroll
+        for (int f = 0; f < NF; f += 2) {
+            const float* vp = lds + (16 * f + r) * AF_LD + 16 * g;
+            f32x4 k0[4], k1[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) k0[j] = *reinterpret_cast<const f32x4*>(vp + 4 * j);
+            if (f + 1 < NF) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) k1[j] = *reinterpret_cast<const f32x4*>(vp + 16 * AF_LD + 4 * j);
+            }
+            s[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (f + 1 < NF) s[f + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    s[f] = __builtin_amdgcn_mfma_f32_16x16x4f32(k0[j][e], dv[j][e], s[f], 0, 0, 0);
+                    if (f + 1 < NF) s[f + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(k1[j][e], dv[j][e], s[f + 1], 0, 0, 0);
+                }
+            __builtin_amdgcn_sched_barrier(0);  // bound the LDS reads hoisted ahead (register budget)
+        }
+        if (q0 + r < T) {
+            const float dl = dlt[q0 + r];
+            const float* prow = Pb + (long)(q0 + r) * Tp;
+            float* srow = Sb + (long)(q0 + r) * Tp;
+#pragma unroll
+            for (int f = 0; f < NF; ++f)
+                if (16 * f + 4 * g < Tp) {
+                    const f32x4 pv = *reinterpret_cast<const f32x4*>(prow + 16 * f + 4 * g);
+                    f32x4 o;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) o[i] = scale * (pv[i] * (s[f][i] - dl));
+                    *reinterpret_cast<f32x4*>(srow + 16 * f + 4 * g) = o;
+                }
+        }
+    }
+    __syncthreads();  // every wave is done with V
+    attn_stage_rows<NF>(lds, Qb + H, ld, T);  // K
+    __syncthreads();
+    for (int grp = w; grp < ngrp; grp += AF_THREADS / 64) {
+        const int q0 = grp * 16;
+        f32x4 pf[NF];
+        const float* srow = Sb + (long)(q0 + r) * Tp;
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+            pf[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (q0 + r < T && 16 * f + 4 * g < Tp) pf[f] = *reinterpret_cast<const f32x4*>(srow + 16 * f + 4 * g);
+        }
+        f32x4 o[4];
+#pragma unroll
+        for (int cf = 0; cf < 4; ++cf) o[cf] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int f = 0; f < NF; ++f)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float* kp = lds + (16 * f + 4 * g + i) * AF_LD + r;
+                float kv[4];
+#pragma unroll
+                for (int cf = 0; cf < 4; ++cf) kv[cf] = kp[16 * cf];
+#pragma unroll
+                for (int cf = 0; cf < 4; ++cf)
+                    o[cf] = __builtin_amdgcn_mfma_f32_16x16x4f32(pf[f][i], kv[cf], o[cf], 0, 0, 0);
+                if (i == 3) __builtin_amdgcn_sched_barrier(0);
+            }
+        float* qb = dqkv + (long)u * T * ld + hd * 64 + r;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int q = q0 + 4 * g + i;
+            if (q < T) {
+#pragma unroll
+                for (int cf = 0; cf < 4; ++cf) qb[(long)q * ld + 16 * cf] = o[cf][i];
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // attention softmax over rows of length T (<= 64*NPL), one wave per row
 // ------------------------------------------------------------------------------------------
 template <int NPL>
@@ -1164,6 +1281,21 @@ bool launch_attn_fwd(const float* qkv, float* P, float* ctx, int B, int T, int T
     else if (nf <= 25) AF(25);
     else AF(32);
 #undef AF
+    return true;
+}
+
+bool launch_attn_bwd(const float* qkv, const float* P, const float* dctx, const float* delta, float* dS, float* dqkv,
+                     int B, int T, int Tp, int NH, int H, int dh, float scale, hipStream_t st) {
+    if (dh != 64 || T < 1 || T > 512 || H % 4 || Tp % 4 || Tp < T) return false;
+    const dim3 grid((unsigned)((long)B * NH));
+#define AB(NF_) hipLaunchKernelGGL(attn_bwd_kernel<NF_>, grid, dim3(AF_THREADS), 0, st, qkv, P, dctx, delta, dS, dqkv, T, Tp, NH, H, scale)
+    const int nf = (T + 15) / 16;
+    if (nf <= 4) AB(4);
+    else if (nf <= 8) AB(8);
+    else if (nf <= 16) AB(16);
+    else if (nf <= 25) AB(25);
+    else AB(32);
+#undef AB
     return true;
 }
 
