@@ -36,7 +36,7 @@ BF16_PEAK_TFLOPS = 2500.0      # MI355X_MICROARCH.md: bf16 dense MFMA peak
 BF16_SPLIT_PEAK_TFLOPS = BF16_PEAK_TFLOPS / 6  # 6 bf16 products per fp32-equivalent MAC
 RECORD = [0, 1, 3, 5, 10]
 PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r1", "pmc_traffic.json")
-GEMM_KERNELS = ("gemm_glds_kernel", "gemm_f32_kernel", "attn_fwd_kernel", "attn_bwd_kernel")
+GEMM_KERNELS = ("gemm_glds_kernel", "gemm_f32_kernel", "attn_fwd_kernel", "attn_bwd_kernel", "posconv_kernel")
 
 
 def gemm_traffic(args):
@@ -210,7 +210,7 @@ def main():
                            "traffic_unit": "HBM bytes per GEMM launch",
                            "traffic_source": "profiles/r1/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE "
                                              "passes of this workload)" if traffic else None,
-                           "kernel": "fp32 MFMA GEMM family: gemm_glds_kernel + gemm_f32_kernel + attn_fwd_kernel + attn_bwd_kernel (all launches)",
+                           "kernel": "fp32 MFMA GEMM family: gemm_glds_kernel + gemm_f32_kernel + attn_fwd_kernel + attn_bwd_kernel + posconv_kernel (all launches)",
                            "launches": int(gn), "avg_launch_ms": round(gms / max(1, gn), 5)}
         out["time_breakdown_ms"] = {k: round(v[0], 2) for k, v in timing.items()}
     if args.also_split and args.precision == "fp32":

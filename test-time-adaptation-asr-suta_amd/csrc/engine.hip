@@ -147,7 +147,8 @@ struct suta_engine {
     hipStream_t st = nullptr;
     int max_batch = 0;
     long max_samples = 0;
-    bool attn_fused = true;  // fused attention forward (launch_attn_fwd) where its shape holds; env SUTA_ATTN_FUSED=0 off
+    bool attn_fused = true;  // fused attention fwd/bwd kernels where their shape holds; env SUTA_ATTN_FUSED=0 off
+    bool posconv_kernel = true;  // dedicated positional-conv kernel (exact fp32 mode); env SUTA_POSCONV=0 off
     // frozen weights
     std::vector<float*> wqkv, bqkv, wo, bo, w1, b1, w2, b2;
     float *wpos_f = nullptr, *wpos_b = nullptr, *bpos = nullptr, *wlm = nullptr, *blm = nullptr;
@@ -517,7 +518,16 @@ void suta_engine::forward(int B) {
         g.sBias1 = Pn;
         gemm(g);
     }
-    {  // positional conv: e = h0 + gelu(posconv(h0)); pz = pre-activation
+    // dedicated kernel in exact fp32 mode for group widths 48 / 64 (timed with the MFMA contractions)
+    const bool pc_ok = posconv_kernel && gemm_get_mode() == 0 && (H / k.posG == 48 || H / k.posG == 64) &&
+                       k.posK % 2 == 0;
+    if (pc_ok)
+        timed(F_GEMM, [&] {
+            if (!launch_posconv(true, pl.h0, wpos_f, bpos, pl.h0, pl.e, pl.pz, B, T, H, k.posG, k.posK, k.posK / 2,
+                                rT(), st))
+                throw SutaError(SUTA_ERR_UNSUPPORTED, "positional conv shape");
+        });
+    if (!pc_ok) {  // positional conv: e = h0 + gelu(posconv(h0)); pz = pre-activation
         const int Cg = H / k.posG;
         GemmParams g;
         gemm_init(g);
@@ -983,7 +993,15 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
     float* dpz = (de == pl.d1) ? pl.d2 : (de == pl.d2 ? pl.d3 : pl.d1);
     float* dh0 = (dpz == pl.d1 || de == pl.d1) ? ((dpz == pl.d2 || de == pl.d2) ? pl.d3 : pl.d2) : pl.d1;
     timed(F_EW, [&] { launch_dgelu_mul(de, pl.pz, dpz, BT * H, st); });
-    {  // dh0 = posconv^T(dpz) + de
+    const bool pcb_ok = posconv_kernel && gemm_get_mode() == 0 && (H / k.posG == 48 || H / k.posG == 64) &&
+                        k.posK % 2 == 0;
+    if (pcb_ok)
+        timed(F_GEMM, [&] {
+            if (!launch_posconv(false, dpz, wpos_b, nullptr, de, dh0, nullptr, B, T, H, k.posG, k.posK,
+                                k.posK - 1 - k.posK / 2, rT(), st))
+                throw SutaError(SUTA_ERR_UNSUPPORTED, "positional conv shape");
+        });
+    if (!pcb_ok) {  // dh0 = posconv^T(dpz) + de
         const int Cg = H / k.posG;
         GemmParams g;
         gemm_init(g);
@@ -1395,6 +1413,7 @@ int32_t suta_create(const suta_model_config* cfg, const char* const* names, cons
         e->max_batch = max_batch;
         e->max_samples = max_samples;
         if (const char* af = std::getenv("SUTA_ATTN_FUSED")) e->attn_fused = af[0] != '0';
+        if (const char* pc = std::getenv("SUTA_POSCONV")) e->posconv_kernel = pc[0] != '0';
         HIPCHK(hipSetDevice(device));
         HIPCHK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
         e->d_step = reinterpret_cast<int*>(e->dalloc(1));

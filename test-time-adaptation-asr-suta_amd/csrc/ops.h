@@ -51,6 +51,10 @@ bool launch_attn_fwd(const float* qkv, float* P, float* ctx, int B, int T, int T
 // fused dS = scale * P * (dctx V^T - delta) (stored) and dQ = dS K into dqkv's Q columns; same shape limits
 bool launch_attn_bwd(const float* qkv, const float* P, const float* dctx, const float* delta, float* dS, float* dqkv,
                      int B, int T, int Tp, int NH, int H, int dh, float scale, hipStream_t st);
+// grouped positional conv (group width 48 or 64, exact fp32 MFMA); fwd: C = R + gelu(conv + bias), C2 = conv + bias;
+// bwd: C = conv + R (rows >= tlen -> 0).  false (nothing launched) outside the supported shapes
+bool launch_posconv(bool fwd, const float* x, const float* W, const float* bias, const float* R, float* C, float* C2,
+                    int B, int T, int H, int G, int K, int pad, const int* tlen, hipStream_t st);
 void launch_softmax_rows(float* s, long nrows, int T, long ld, const int* tlen, long rows_per_utt, hipStream_t st);
 
 // delta[b][h][t] = dot(dO[b][t][head h], O[b][t][head h]): the softmax-backward row term sum_j P_ij dP_ij.

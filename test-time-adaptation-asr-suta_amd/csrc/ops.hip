@@ -832,6 +832,132 @@ __global__ __launch_bounds__(AF_THREADS, 1) void attn_bwd_kernel(const float* __
 }
 
 // ------------------------------------------------------------------------------------------
+// Grouped positional conv (wav2vec2 pos_conv_embed: K taps, G groups of CG channels, "same" padding)
+// as one kernel: out[t][co] = sum_q sum_ci x[t + q - pad][ci] W[q][ci][co] over one group, x rows
+// outside [0, len) are zero.  Block = WB waves = 16*WB output frames x CG channels of one
+// (utterance, group): the input window (16*WB + K - 1 frames) is staged in LDS once, the group's
+// weights stream through two LDS buffers of CHT taps (register-staged, one barrier per chunk), and
+// each wave runs exact-fp32 v_mfma_f32_16x16x4_f32 on its 16 frames x CG channels (CG/16 fragments).
+//   FWD: C = R + gelu(acc + bias), C2 = acc + bias (pre-activation);  BWD: C = acc + R, rows >= len -> 0
+// Blocks of one group run on one XCD (its weights stay in that L2).
+// ------------------------------------------------------------------------------------------
+template <int CG>
+struct PcLayout {
+    static constexpr int XS = CG + 4;                        // window row stride (conflict-free A reads)
+    static constexpr int WS = (CG % 64 == 0) ? CG + 16 : CG;  // weight row stride (conflict-free B reads)
+};
+
+template <int CG, int WB, int CHT, bool FWD>
+__global__ __launch_bounds__(WB * 64, 1) void posconv_kernel(const float* __restrict__ x, const float* __restrict__ W,
+                                                             const float* __restrict__ bias,
+                                                             const float* __restrict__ R, float* __restrict__ C,
+                                                             float* __restrict__ C2, int T, int H, int G, int K,
+                                                             int pad, const int* __restrict__ tlen, int ntile,
+                                                             int nutt) {
+    constexpr int NT = WB * 64, NC = CG / 16, XS = PcLayout<CG>::XS, WS = PcLayout<CG>::WS;
+    constexpr int WROWS = 16 * WB;
+    constexpr int CHUNK4 = CHT * CG * CG / 4;             // float4 per weight chunk
+    constexpr int LPT = (CHUNK4 + NT - 1) / NT;           // float4 per thread per chunk
+    extern __shared__ __attribute__((aligned(16))) float pc_smem[];
+    float* win = pc_smem;                                  // [WROWS + K - 1][XS]
+    float* wbuf = pc_smem + (WROWS + K - 1) * XS;          // 2 x [CHT*CG][WS]
+
+    // block -> (group, utterance, tile) with each XCD owning whole groups: hardware block b runs on
+    // XCD b % 8; logical id = xcd-major
+    const int nb = gridDim.x;
+    int L = blockIdx.x;
+    if ((nb & 7) == 0) L = (L & 7) * (nb >> 3) + (L >> 3);
+    const int tile = L % ntile;
+    const int u = (L / ntile) % nutt;
+    const int gi = L / (ntile * nutt);
+    const int t0 = tile * WROWS;
+    const int tl = tlen ? tlen[u] : T;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int r = lane & 15, g = lane >> 4;
+    const float* xb = x + (long)u * T * H + gi * CG;
+    const float* wg = W + (long)gi * K * CG * CG;
+
+    // input window: frames t0 - pad .. t0 + WROWS - 1 + (K - 1 - pad)
+    const int nwin = (WROWS + K - 1) * (CG / 4);
+    for (int it = threadIdx.x; it < nwin; it += NT) {
+        const int row = it / (CG / 4), c4 = (it % (CG / 4)) * 4;
+        const int t = t0 - pad + row;
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        if (t >= 0 && t < tl) v = *reinterpret_cast<const f32x4*>(xb + (long)t * H + c4);
+        *reinterpret_cast<f32x4*>(win + row * XS + c4) = v;
+    }
+    f32x4 st[LPT];
+    auto load_chunk = [&](int c) {
+        const float* src = wg + (long)c * CHT * CG * CG;
+#pragma unroll
+        for (int n = 0; n < LPT; ++n) {
+            const int it = threadIdx.x + n * NT;
+            st[n] = it < CHUNK4 ? *reinterpret_cast<const f32x4*>(src + it * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    };
+    auto store_chunk = [&](int buf) {
+        float* dst = wbuf + buf * (CHT * CG * WS);
+#pragma unroll
+        for (int n = 0; n < LPT; ++n) {
+            const int it = threadIdx.x + n * NT;
+            if (it < CHUNK4) {
+                const int row = (it * 4) / CG, col = (it * 4) % CG;
+                *reinterpret_cast<f32x4*>(dst + row * WS + col) = st[n];
+            }
+        }
+    };
+    f32x4 acc[NC];
+#pragma unroll
+    for (int nf = 0; nf < NC; ++nf) acc[nf] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int nch = K / CHT;
+    load_chunk(0);
+    store_chunk(0);
+    __syncthreads();
+    const float* arow = win + (16 * w + r) * XS + g;
+    for (int c = 0; c < nch; ++c) {
+        if (c + 1 < nch) load_chunk(c + 1);
+        const float* wb = wbuf + (c & 1) * (CHT * CG * WS) + g * WS + r;
+#pragma unroll
+        for (int qq = 0; qq < CHT; ++qq) {
+            const float* ap = arow + (c * CHT + qq) * XS;
+            const float* bp = wb + qq * CG * WS;
+#pragma unroll
+            for (int j = 0; j < CG / 4; ++j) {
+                const float a = ap[4 * j];
+                float b[NC];
+#pragma unroll
+                for (int nf = 0; nf < NC; ++nf) b[nf] = bp[4 * j * WS + 16 * nf];
+#pragma unroll
+                for (int nf = 0; nf < NC; ++nf) acc[nf] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b[nf], acc[nf], 0, 0, 0);
+            }
+        }
+        if (c + 1 < nch) store_chunk((c + 1) & 1);
+        __syncthreads();
+    }
+    // epilogue: lane holds out[t0 + 16w + 4g + i][16nf + r]
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int t = t0 + 16 * w + 4 * g + i;
+        if (t >= T) continue;
+        const long o = ((long)u * T + t) * H + gi * CG;
+#pragma unroll
+        for (int nf = 0; nf < NC; ++nf) {
+            const int co = 16 * nf + r;
+            float v;
+            if (FWD) {
+                v = acc[nf][i] * 1.0f + bias[gi * CG + co];
+                C2[o + co] = v;
+                v = gelu_f(v) + R[o + co];
+            } else {
+                v = acc[nf][i] + R[o + co];
+                if (tlen && t >= tl) v = 0.f;
+            }
+            C[o + co] = v;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // attention softmax over rows of length T (<= 64*NPL), one wave per row
 // ------------------------------------------------------------------------------------------
 template <int NPL>
@@ -1296,6 +1422,68 @@ bool launch_attn_bwd(const float* qkv, const float* P, const float* dctx, const 
     else if (nf <= 25) AB(25);
     else AB(32);
 #undef AB
+    return true;
+}
+
+constexpr int PC_CHT = 2;  // taps per weight chunk: two chunks + the base window fit 2 blocks per CU
+#define HIPCHK_OPS(x)                                                                        \
+    do {                                                                                     \
+        if ((x) != hipSuccess) throw std::runtime_error("hipFuncSetAttribute(posconv) failed"); \
+    } while (0)
+
+template <int CG, bool FWD>
+static void posconv_go(int WB, dim3 grid, size_t lds, hipStream_t st, const float* x, const float* W,
+                       const float* bias, const float* R, float* C, float* C2, int T, int H, int G, int K, int pad,
+                       const int* tlen, int ntile, int B) {
+    // > 64 KiB of dynamic LDS must be allowed per kernel (once per instantiation)
+#define PC(WB_)                                                                                                   \
+    do {                                                                                                          \
+        static bool attr = false;                                                                                 \
+        if (!attr) {                                                                                              \
+            HIPCHK_OPS(hipFuncSetAttribute(reinterpret_cast<const void*>(&posconv_kernel<CG, WB_, PC_CHT, FWD>),   \
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));              \
+            attr = true;                                                                                          \
+        }                                                                                                         \
+        hipLaunchKernelGGL((posconv_kernel<CG, WB_, PC_CHT, FWD>), grid, dim3(WB_ * 64), lds, st, x, W, bias, R, C, \
+                           C2, T, H, G, K, pad, tlen, ntile, B);                                                  \
+    } while (0)
+    switch (WB) {
+        case 4: PC(4); break;
+        case 5: PC(5); break;
+        case 6: PC(6); break;
+        case 7: PC(7); break;
+        default: PC(8); break;
+    }
+#undef PC
+}
+
+bool launch_posconv(bool fwd, const float* x, const float* W, const float* bias, const float* R, float* C, float* C2,
+                    int B, int T, int H, int G, int K, int pad, const int* tlen, hipStream_t st) {
+    const int CG = H / G;
+    if ((CG != 48 && CG != 64) || K % PC_CHT || H % 4) return false;
+    // waves per block: fewest padded frames over ceil(T / (16 WB)) tiles (T = 399 -> 5 waves, 400 rows)
+    int WB = 8;
+    long best = 1L << 40;
+    for (int wb = 8; wb >= 4; --wb) {
+        const long tiles = (T + 16 * wb - 1) / (16 * wb);
+        const long waste = tiles * 16 * wb - T;
+        if (waste < best) {
+            best = waste;
+            WB = wb;
+        }
+    }
+    const int ntile = (T + 16 * WB - 1) / (16 * WB);
+    const int XS = CG + 4, WS = (CG % 64 == 0) ? CG + 16 : CG;
+    const size_t lds = ((size_t)(16 * WB + K - 1) * XS + 2 * PC_CHT * CG * WS) * sizeof(float);
+    if (lds > 160 * 1024) return false;
+    const dim3 grid((unsigned)((long)G * B * ntile));
+    if (CG == 48) {
+        if (fwd) posconv_go<48, true>(WB, grid, lds, st, x, W, bias, R, C, C2, T, H, G, K, pad, tlen, ntile, B);
+        else posconv_go<48, false>(WB, grid, lds, st, x, W, bias, R, C, C2, T, H, G, K, pad, tlen, ntile, B);
+    } else {
+        if (fwd) posconv_go<64, true>(WB, grid, lds, st, x, W, bias, R, C, C2, T, H, G, K, pad, tlen, ntile, B);
+        else posconv_go<64, false>(WB, grid, lds, st, x, W, bias, R, C, C2, T, H, G, K, pad, tlen, ntile, B);
+    }
     return true;
 }
 
