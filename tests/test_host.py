@@ -146,3 +146,25 @@ def test_gloo_world2_reduces_wer_counts():
     for rank, red, ranks in out:
         assert red == {"0": (3, 30), "10": (1, 10)}
         assert ranks == [0, 1]
+
+
+@pytest.mark.parametrize("min_fill", [0.0, 0.35])
+def test_ragged_groups_partition(min_fill):
+    """Driver grouping: an in-order partition of the length-sorted utterances, every group within
+    gpu_batch and the padded-audio budget (a single over-long utterance stands alone); the padding-
+    minimising partition pads no more than the greedy one on the bench's length mix."""
+    from suta_amd.main import LAYOUT_QUANTUM as Q, ragged_groups
+    rng = np.random.default_rng(20260415)
+    ns = np.sort((np.clip(rng.lognormal(np.log(6.5), 0.6, 256), 1.5, 35.0) * 16000).astype(np.int64))
+    budget = 512 * 16000
+    groups = ragged_groups(list(ns), 64, budget, min_fill)
+    assert [j for g in groups for j in g] == list(range(len(ns)))
+    width = lambda g: -(-int(ns[g[-1]]) // Q) * Q  # noqa: E731
+    for g in groups:
+        assert len(g) <= 64
+        assert len(g) == 1 or len(g) * width(g) <= budget
+    padded = sum(len(g) * width(g) for g in groups)
+    greedy = sum(len(g) * width(g) for g in ragged_groups(list(ns), 64, budget, 0.0))
+    assert padded <= greedy
+    assert ragged_groups([700000], 4, budget, min_fill) == [[0]]
+    assert ragged_groups([], 4, budget, min_fill) == []

@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--n", type=int, default=256)
     ap.add_argument("--gpu-batch", type=int, default=64)
     ap.add_argument("--budget-s", type=float, default=512.0, help="padded audio seconds per ragged batch")
+    ap.add_argument("--min-fill", type=float, default=0.35,
+                    help="0 = greedy grouping; > 0 = padding-minimising partition (suta_amd/main.py ragged_groups)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--single", type=int, default=16, help="utterances timed one per call (subset)")
     args = ap.parse_args()
@@ -52,7 +54,8 @@ def main():
     order = np.argsort(ns)
     # the driver's grouping (suta_amd/main.py ragged_groups): length-sorted, <= gpu_batch utterances and
     # <= budget seconds of padded audio per batch, layout rounded up to LAYOUT_QUANTUM
-    groups = [order[g] for g in ragged_groups([int(ns[i]) for i in order], args.gpu_batch, args.budget_s * 16000)]
+    groups = [order[g] for g in ragged_groups([int(ns[i]) for i in order], args.gpu_batch, args.budget_s * 16000,
+                                                  args.min_fill)]
     q = LAYOUT_QUANTUM
     padded = [torch.zeros((len(g), -(-int(ns[g].max()) // q) * q), device="cuda") for g in groups]
     for p, g in zip(padded, groups):
@@ -84,7 +87,7 @@ def main():
            "single_utt_per_s": round(len(sub) / t_single, 3),
            "ragged_speedup": round((args.n / t_batch) / (len(sub) / t_single), 2),
            "ragged_algorithmic_tflops": round(flops / t_batch / 1e12, 2),
-           "padding_overhead": round(pad - 1.0, 4),
+           "padding_overhead": round(pad - 1.0, 4), "grouping": "greedy" if args.min_fill <= 0 else f"min-padding DP (min_fill {args.min_fill})",
            "single_subset": f"{len(sub)} utterances spread over the length range"}
     print(json.dumps(out), flush=True)
     eng.close()
