@@ -190,7 +190,7 @@ __global__ __launch_bounds__(256) void conv0_gn_kernel(const float* __restrict__
         float dw[16];
 #pragma unroll
         for (int k = 0; k < 16; ++k) dw[k] = 0.f;
-#pragma unroll 2
+#pragma unroll 8  // 8 rows of io loads in flight per lane (the backward modes are latency-bound at 2)
         for (int r = 0; r < rows; ++r) {
             float z = 0.f;
 #pragma unroll
