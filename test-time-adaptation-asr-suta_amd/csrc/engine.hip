@@ -519,7 +519,7 @@ void suta_engine::forward(int B) {
         gemm(g);
     }
     // dedicated kernel in exact fp32 mode for group widths 48 / 64 (timed with the MFMA contractions)
-    const bool pc_ok = posconv_kernel && gemm_get_mode() == 0 && (H / k.posG == 48 || H / k.posG == 64) &&
+    const bool pc_ok = posconv_kernel && gemm_mode == SUTA_PRECISION_FP32_MFMA && (H / k.posG == 48 || H / k.posG == 64) &&
                        k.posK % 2 == 0;
     if (pc_ok)
         timed(F_GEMM, [&] {
@@ -602,7 +602,8 @@ void suta_engine::forward(int B) {
         const bool fused = attn_fused && d == 64 && T <= 512;
         if (fused)
             timed(F_GEMM, [&] {
-                if (!launch_attn_fwd(lb.qkv, lb.P, lb.ctx, B, T, (int)pl.Tp, NH, H, d, scale, rT(), st))
+                if (!launch_attn_fwd(lb.qkv, lb.P, lb.ctx, B, T, (int)pl.Tp, NH, H, d, scale, rT(),
+                                     gemm_mode == SUTA_PRECISION_BF16, st))
                     throw SutaError(SUTA_ERR_UNSUPPORTED, "fused attention shape");
             });
         if (!fused) {
@@ -862,7 +863,7 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
         if (fused_bwd)
             timed(F_GEMM, [&] {
                 if (!launch_attn_bwd(lb.qkv, lb.P, pl.ctx, pl.delta, pl.dP, pl.dqkv, B, T, (int)pl.Tp, NH, H, d, scale,
-                                     st))
+                                     gemm_mode == SUTA_PRECISION_BF16, st))
                     throw SutaError(SUTA_ERR_UNSUPPORTED, "fused attention shape");
             });
         if (!fused_bwd) {
@@ -993,7 +994,7 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
     float* dpz = (de == pl.d1) ? pl.d2 : (de == pl.d2 ? pl.d3 : pl.d1);
     float* dh0 = (dpz == pl.d1 || de == pl.d1) ? ((dpz == pl.d2 || de == pl.d2) ? pl.d3 : pl.d2) : pl.d1;
     timed(F_EW, [&] { launch_dgelu_mul(de, pl.pz, dpz, BT * H, st); });
-    const bool pcb_ok = posconv_kernel && gemm_get_mode() == 0 && (H / k.posG == 48 || H / k.posG == 64) &&
+    const bool pcb_ok = posconv_kernel && gemm_mode == SUTA_PRECISION_FP32_MFMA && (H / k.posG == 48 || H / k.posG == 64) &&
                         k.posK % 2 == 0;
     if (pcb_ok)
         timed(F_GEMM, [&] {

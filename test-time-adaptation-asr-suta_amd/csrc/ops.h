@@ -46,11 +46,12 @@ void launch_colsum(const float* x, int B, int rows, int C, float* out, long ostr
 // ragged batch, rows of utterance row / rows_per_utt use their first tlen[u] keys; the rest get 0.
 // fused S = QK^T*scale -> softmax -> P (stored) -> ctx = PV for head dim 64, T <= 512 (exact fp32 MFMA);
 // false (nothing launched) when the shape is outside that
+// bf16: S and PV operands rounded to bf16 on v_mfma_f32_16x16x32_bf16 (config C4), fp32 accumulate and softmax
 bool launch_attn_fwd(const float* qkv, float* P, float* ctx, int B, int T, int Tp, int NH, int H, int dh, float scale,
-                     const int* tlen, hipStream_t st);
+                     const int* tlen, bool bf16, hipStream_t st);
 // fused dS = scale * P * (dctx V^T - delta) (stored) and dQ = dS K into dqkv's Q columns; same shape limits
 bool launch_attn_bwd(const float* qkv, const float* P, const float* dctx, const float* delta, float* dS, float* dqkv,
-                     int B, int T, int Tp, int NH, int H, int dh, float scale, hipStream_t st);
+                     int B, int T, int Tp, int NH, int H, int dh, float scale, bool bf16, hipStream_t st);
 // grouped positional conv (group width 48 or 64, exact fp32 MFMA); fwd: C = R + gelu(conv + bias), C2 = conv + bias;
 // bwd: C = conv + R (rows >= tlen -> 0).  false (nothing launched) outside the supported shapes
 bool launch_posconv(bool fwd, const float* x, const float* W, const float* bias, const float* R, float* C, float* C2,

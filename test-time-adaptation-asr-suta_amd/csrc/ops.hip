@@ -593,32 +593,29 @@ __device__ __forceinline__ void attn_stage_rows(float* __restrict__ lds, const f
     }
 }
 
-template <int NF>
-__global__ __launch_bounds__(AF_THREADS, 1) void attn_fwd_kernel(const float* __restrict__ qkv, float* __restrict__ P,
-                                                                 float* __restrict__ ctx, int T, int Tp, int NH,
-                                                                 int H, float scale, const int* __restrict__ tlen) {
-    __shared__ __attribute__((aligned(16))) float lds[NF * 16 * AF_LD];
-    const int bh = blockIdx.x;  // utterance * NH + head
-    const int hd = bh % NH, u = bh / NH;
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int r = lane & 15, g = lane >> 4;
-    const int ngrp = (T + 15) >> 4;
-    const int tl = tlen ? tlen[u] : T;
-    const long ld = 3L * H;
-    const float* Qb = qkv + (long)u * T * ld + hd * 64;
-    float* Pb = P + (long)bh * T * Tp;
+typedef __bf16 abf16x8 __attribute__((ext_vector_type(8)));
 
-    attn_stage_rows<NF>(lds, Qb + H, ld, T);  // K
-    __syncthreads();
-    for (int grp = w; grp < ngrp; grp += AF_THREADS / 64) {
-        const int q0 = grp * 16;
-        f32x4 qv[4];
-        {
-            const float* qp = Qb + (long)min(q0 + r, T - 1) * ld + 16 * g;
+__device__ __forceinline__ abf16x8 af_cvt8(f32x4 lo, f32x4 hi) {
+    abf16x8 v;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) qv[j] = *reinterpret_cast<const f32x4*>(qp + 4 * j);
-        }
-        f32x4 s[NF];
+    for (int j = 0; j < 4; ++j) {
+        v[j] = (__bf16)lo[j];  // round to nearest even (v_cvt_pk_bf16_f32)
+        v[4 + j] = (__bf16)hi[j];
+    }
+    return v;
+}
+
+// Scores of one 16-query group against every staged key row: s[f] (lane (r, g), element i) =
+//   sum_d L[16f + 4g + i][d] * X[q0 + r][d]   with L = the LDS rows, xrow = &X[q0 + r][0] (64 floats).
+// fp32: v_mfma_f32_16x16x4_f32 with d = 16g + m in MFMA m; bf16 (config C4): operands rounded to bf16,
+// v_mfma_f32_16x16x32_bf16 with d = 32h + 8g + j (fp32 accumulation).
+template <int NF, bool BF16>
+__device__ __forceinline__ void af_scores(const float* __restrict__ lds, const float* __restrict__ xrow, int r, int g,
+                                          f32x4 (&s)[NF]) {
+    if constexpr (!BF16) {
+        f32x4 qv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) qv[j] = *reinterpret_cast<const f32x4*>(xrow + 16 * g + 4 * j);
         // two key fragments per pass: two independent MFMA chains
 #pragma unroll
         for (int f = 0; f < NF; f += 2) {
@@ -641,6 +638,100 @@ __global__ __launch_bounds__(AF_THREADS, 1) void attn_fwd_kernel(const float* __
                 }
             __builtin_amdgcn_sched_barrier(0);  // bound the LDS reads hoisted ahead (register budget)
         }
+    } else {
+        abf16x8 qb[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+            qb[h] = af_cvt8(*reinterpret_cast<const f32x4*>(xrow + 32 * h + 8 * g),
+                            *reinterpret_cast<const f32x4*>(xrow + 32 * h + 8 * g + 4));
+#pragma unroll
+        for (int f = 0; f < NF; f += 2) {
+            abf16x8 a0[2], a1[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const float* kp = lds + (16 * f + r) * AF_LD + 32 * h + 8 * g;
+                a0[h] = af_cvt8(*reinterpret_cast<const f32x4*>(kp), *reinterpret_cast<const f32x4*>(kp + 4));
+                if (f + 1 < NF)
+                    a1[h] = af_cvt8(*reinterpret_cast<const f32x4*>(kp + 16 * AF_LD),
+                                    *reinterpret_cast<const f32x4*>(kp + 16 * AF_LD + 4));
+            }
+            s[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (f + 1 < NF) s[f + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                s[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[h], qb[h], s[f], 0, 0, 0);
+                if (f + 1 < NF) s[f + 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[h], qb[h], s[f + 1], 0, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+}
+
+// o[cf] (lane (r, g), element i) = sum_key A[q0 + 4g + i][key] * L[key][16 cf + r], the A rows given as
+// the lanes' segments pf[f][i] = A[q0 + r][16f + 4g + i] (the C/D map of af_scores).
+// fp32: MFMA (f, i) takes keys 16f + 4g' + i; bf16: MFMA c takes the 32 keys of fragments 2c, 2c+1, slot
+// 8g + j <-> key 16(2c) + 4g + j (j < 4), 16(2c+1) + 4g + j - 4 (j >= 4).
+template <int NF, bool BF16>
+__device__ __forceinline__ void af_apply(const float* __restrict__ lds, const f32x4 (&pf)[NF], int r, int g,
+                                         f32x4 (&o)[4]) {
+#pragma unroll
+    for (int cf = 0; cf < 4; ++cf) o[cf] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (!BF16) {
+#pragma unroll
+        for (int f = 0; f < NF; ++f)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float* vp = lds + (16 * f + 4 * g + i) * AF_LD + r;
+                float vv[4];
+#pragma unroll
+                for (int cf = 0; cf < 4; ++cf) vv[cf] = vp[16 * cf];
+#pragma unroll
+                for (int cf = 0; cf < 4; ++cf)
+                    o[cf] = __builtin_amdgcn_mfma_f32_16x16x4f32(pf[f][i], vv[cf], o[cf], 0, 0, 0);
+                if (i == 3) __builtin_amdgcn_sched_barrier(0);
+            }
+    } else {
+#pragma unroll
+        for (int c = 0; c < (NF + 1) / 2; ++c) {
+            const int f0 = 2 * c, f1 = 2 * c + 1;
+            const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+            const abf16x8 a = af_cvt8(pf[f0], f1 < NF ? pf[f1] : z);
+#pragma unroll
+            for (int cf = 0; cf < 4; ++cf) {
+                f32x4 lo, hi = z;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    lo[j] = lds[(16 * f0 + 4 * g + j) * AF_LD + 16 * cf + r];
+                    if (f1 < NF) hi[j] = lds[(16 * f1 + 4 * g + j) * AF_LD + 16 * cf + r];
+                }
+                o[cf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, af_cvt8(lo, hi), o[cf], 0, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+}
+
+template <int NF, bool BF16>
+__global__ __launch_bounds__(AF_THREADS, 1) void attn_fwd_kernel(const float* __restrict__ qkv, float* __restrict__ P,
+                                                                 float* __restrict__ ctx, int T, int Tp, int NH,
+                                                                 int H, float scale, const int* __restrict__ tlen) {
+    __shared__ __attribute__((aligned(16))) float lds[NF * 16 * AF_LD];
+    const int bh = blockIdx.x;  // utterance * NH + head
+    const int hd = bh % NH, u = bh / NH;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int r = lane & 15, g = lane >> 4;
+    const int ngrp = (T + 15) >> 4;
+    const int tl = tlen ? tlen[u] : T;
+    const long ld = 3L * H;
+    const float* Qb = qkv + (long)u * T * ld + hd * 64;
+    float* Pb = P + (long)bh * T * Tp;
+
+    attn_stage_rows<NF>(lds, Qb + H, ld, T);  // K
+    __syncthreads();
+    for (int grp = w; grp < ngrp; grp += AF_THREADS / 64) {
+        const int q0 = grp * 16;
+        f32x4 s[NF];
+        af_scores<NF, BF16>(lds, Qb + (long)min(q0 + r, T - 1) * ld, r, g, s);
         // softmax over the keys of query q0 + r: this lane's 4*NF values, then the 4 lanes r + 16g
         float mx = -INFINITY;
 #pragma unroll
@@ -687,21 +778,7 @@ __global__ __launch_bounds__(AF_THREADS, 1) void attn_fwd_kernel(const float* __
         }
         // ctx[q0 + 4g + i][16 cf + r] = sum_key P[.][key] V[key][16 cf + r]
         f32x4 o[4];
-#pragma unroll
-        for (int cf = 0; cf < 4; ++cf) o[cf] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int f = 0; f < NF; ++f)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const float* vp = lds + (16 * f + 4 * g + i) * AF_LD + r;
-                float vv[4];
-#pragma unroll
-                for (int cf = 0; cf < 4; ++cf) vv[cf] = vp[16 * cf];
-#pragma unroll
-                for (int cf = 0; cf < 4; ++cf)
-                    o[cf] = __builtin_amdgcn_mfma_f32_16x16x4f32(pf[f][i], vv[cf], o[cf], 0, 0, 0);
-                if (i == 3) __builtin_amdgcn_sched_barrier(0);
-            }
+        af_apply<NF, BF16>(lds, pf, r, g, o);
         float* cb = ctx + (long)u * T * H + hd * 64 + r;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -723,7 +800,7 @@ __global__ __launch_bounds__(AF_THREADS, 1) void attn_fwd_kernel(const float* __
 // Replaces the dP GEMM (softmax-backward epilogue) and the dQ GEMM; dK = dS^T Q and dV = P^T dctx
 // stay GEMMs.  delta[bh][q] = rowsum(dctx * ctx) (attn_delta_kernel).
 // ------------------------------------------------------------------------------------------
-template <int NF>
+template <int NF, bool BF16>
 __global__ __launch_bounds__(AF_THREADS, 1) void attn_bwd_kernel(const float* __restrict__ qkv,
                                                                  const float* __restrict__ P,
                                                                  const float* __restrict__ dctx,
@@ -748,34 +825,8 @@ __global__ __launch_bounds__(AF_THREADS, 1) void attn_bwd_kernel(const float* __
     for (int grp = w; grp < ngrp; grp += AF_THREADS / 64) {
         const int q0 = grp * 16;
         const int qr = min(q0 + r, T - 1);
-        f32x4 dv[4];
-        {
-            const float* dp = Db + (long)qr * H + 16 * g;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) dv[j] = *reinterpret_cast<const f32x4*>(dp + 4 * j);
-        }
-        f32x4 s[NF];
-#pragma unroll
-        for (int f = 0; f < NF; f += 2) {
-            const float* vp = lds + (16 * f + r) * AF_LD + 16 * g;
-            f32x4 k0[4], k1[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) k0[j] = *reinterpret_cast<const f32x4*>(vp + 4 * j);
-            if (f + 1 < NF) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) k1[j] = *reinterpret_cast<const f32x4*>(vp + 16 * AF_LD + 4 * j);
-            }
-            s[f] = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (f + 1 < NF) s[f + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    s[f] = __builtin_amdgcn_mfma_f32_16x16x4f32(k0[j][e], dv[j][e], s[f], 0, 0, 0);
-                    if (f + 1 < NF) s[f + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(k1[j][e], dv[j][e], s[f + 1], 0, 0, 0);
-                }
-            __builtin_amdgcn_sched_barrier(0);  // bound the LDS reads hoisted ahead (register budget)
-        }
+        f32x4 s[NF];  // dP^T = V dctx^T
+        af_scores<NF, BF16>(lds, Db + (long)qr * H, r, g, s);
         if (q0 + r < T) {
             const float dl = dlt[q0 + r];
             const float* prow = Pb + (long)(q0 + r) * Tp;
@@ -803,22 +854,8 @@ __global__ __launch_bounds__(AF_THREADS, 1) void attn_bwd_kernel(const float* __
             pf[f] = f32x4{0.f, 0.f, 0.f, 0.f};
             if (q0 + r < T && 16 * f + 4 * g < Tp) pf[f] = *reinterpret_cast<const f32x4*>(srow + 16 * f + 4 * g);
         }
-        f32x4 o[4];
-#pragma unroll
-        for (int cf = 0; cf < 4; ++cf) o[cf] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int f = 0; f < NF; ++f)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const float* kp = lds + (16 * f + 4 * g + i) * AF_LD + r;
-                float kv[4];
-#pragma unroll
-                for (int cf = 0; cf < 4; ++cf) kv[cf] = kp[16 * cf];
-#pragma unroll
-                for (int cf = 0; cf < 4; ++cf)
-                    o[cf] = __builtin_amdgcn_mfma_f32_16x16x4f32(pf[f][i], kv[cf], o[cf], 0, 0, 0);
-                if (i == 3) __builtin_amdgcn_sched_barrier(0);
-            }
+        f32x4 o[4];  // dQ = dS K
+        af_apply<NF, BF16>(lds, pf, r, g, o);
         float* qb = dqkv + (long)u * T * ld + hd * 64 + r;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -1396,10 +1433,18 @@ void launch_softmax_rows(float* s, long nrows, int T, long ld, const int* tlen, 
 }
 
 bool launch_attn_fwd(const float* qkv, float* P, float* ctx, int B, int T, int Tp, int NH, int H, int dh, float scale,
-                     const int* tlen, hipStream_t st) {
+                     const int* tlen, bool bf16, hipStream_t st) {
     if (dh != 64 || T < 1 || T > 512 || H % 4 || Tp % 4 || Tp < T) return false;
     const dim3 grid((unsigned)((long)B * NH));
-#define AF(NF_) hipLaunchKernelGGL(attn_fwd_kernel<NF_>, grid, dim3(AF_THREADS), 0, st, qkv, P, ctx, T, Tp, NH, H, scale, tlen)
+#define AF(NF_)                                                                                                   \
+    do {                                                                                                          \
+        if (bf16)                                                                                                 \
+            hipLaunchKernelGGL((attn_fwd_kernel<NF_, true>), grid, dim3(AF_THREADS), 0, st, qkv, P, ctx, T, Tp, NH, H, \
+                               scale, tlen);                                                                      \
+        else                                                                                                      \
+            hipLaunchKernelGGL((attn_fwd_kernel<NF_, false>), grid, dim3(AF_THREADS), 0, st, qkv, P, ctx, T, Tp, NH,  \
+                               H, scale, tlen);                                                                   \
+    } while (0)
     const int nf = (T + 15) / 16;
     if (nf <= 4) AF(4);
     else if (nf <= 8) AF(8);
@@ -1411,10 +1456,18 @@ bool launch_attn_fwd(const float* qkv, float* P, float* ctx, int B, int T, int T
 }
 
 bool launch_attn_bwd(const float* qkv, const float* P, const float* dctx, const float* delta, float* dS, float* dqkv,
-                     int B, int T, int Tp, int NH, int H, int dh, float scale, hipStream_t st) {
+                     int B, int T, int Tp, int NH, int H, int dh, float scale, bool bf16, hipStream_t st) {
     if (dh != 64 || T < 1 || T > 512 || H % 4 || Tp % 4 || Tp < T) return false;
     const dim3 grid((unsigned)((long)B * NH));
-#define AB(NF_) hipLaunchKernelGGL(attn_bwd_kernel<NF_>, grid, dim3(AF_THREADS), 0, st, qkv, P, dctx, delta, dS, dqkv, T, Tp, NH, H, scale)
+#define AB(NF_)                                                                                                   \
+    do {                                                                                                          \
+        if (bf16)                                                                                                 \
+            hipLaunchKernelGGL((attn_bwd_kernel<NF_, true>), grid, dim3(AF_THREADS), 0, st, qkv, P, dctx, delta, dS,   \
+                               dqkv, T, Tp, NH, H, scale);                                                        \
+        else                                                                                                      \
+            hipLaunchKernelGGL((attn_bwd_kernel<NF_, false>), grid, dim3(AF_THREADS), 0, st, qkv, P, dctx, delta, dS,  \
+                               dqkv, T, Tp, NH, H, scale);                                                        \
+    } while (0)
     const int nf = (T + 15) / 16;
     if (nf <= 4) AB(4);
     else if (nf <= 8) AB(8);
