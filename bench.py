@@ -104,7 +104,7 @@ def bench_c4(args, dev):
         gms, gn = t["gemm"]
         ach = flops_utt * B * steps / (gms / 1000.0) / 1e12
         res["roofline"] = {"bound": "mfma", "achieved": round(ach, 3), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                           "frac": round(ach / BF16_PEAK_TFLOPS, 4), "kernel": "bf16 GEMM family (gemm_x6_kernel one-plane form + gemm_gbf_kernel for weight gradients)",
+                           "frac": round(ach / BF16_PEAK_TFLOPS, 4), "kernel": "bf16 GEMM family (gemm_x6_kernel one-plane form + gemm_gbf_kernel for weight gradients + attn_fwd_kernel / attn_bwd_kernel on bf16 MFMA)",
                            "launches": int(gn), "avg_launch_ms": round(gms / max(1, gn), 5)}
         res["time_breakdown_ms"] = {k: round(v[0], 2) for k, v in t.items()}
     eng.close()
