@@ -1155,12 +1155,31 @@ __global__ __launch_bounds__(256) void suta_loss_kernel(const float* __restrict_
     // ---- phase 2: C = P^T diag(w_hat) P ----
     double mcc = 0.0;
     if (use_mcc) {
-        for (int idx = threadIdx.x; idx < V * V; idx += 256) {
-            const int a = idx / V, c = idx % V;
-            double acc = 0.0;
-            for (int t = 0; t < T; ++t)
-                acc += (double)Ws[t] * (double)Ps[(long)t * 64 + a] * (double)Ps[(long)t * 64 + c];
-            Cm[a * 64 + c] = acc;
+        // P and w staged through LDS 64 frames at a time; each entry still sums over t in order
+        __shared__ float Pch[64 * 64], Wch[64];
+        double acc[16];  // V * V <= 4096 entries over 256 threads
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[e] = 0.0;
+        for (int t0 = 0; t0 < T; t0 += 64) {
+            const int n = min(64, T - t0);
+            __syncthreads();
+            for (int i = threadIdx.x; i < n * 64; i += 256) Pch[i] = Ps[(long)t0 * 64 + i];
+            if (threadIdx.x < n) Wch[threadIdx.x] = Ws[t0 + threadIdx.x];
+            __syncthreads();
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int idx = threadIdx.x + 256 * e;
+                if (idx < V * V) {
+                    const int a = idx / V, c = idx % V;
+                    for (int tt = 0; tt < n; ++tt)
+                        acc[e] += (double)Wch[tt] * (double)Pch[tt * 64 + a] * (double)Pch[tt * 64 + c];
+                }
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int idx = threadIdx.x + 256 * e;
+            if (idx < V * V) Cm[(idx / V) * 64 + idx % V] = acc[e];
         }
         __syncthreads();
         if (threadIdx.x < V) {  // r_j = sum_k C_jk (torch.sum(C, dim=1))
