@@ -168,53 +168,205 @@ def create_dataset(split, name, path, batch_size=1):
 # ---------------------------------------------------------------------------------------------
 # audio
 # ---------------------------------------------------------------------------------------------
+_AUDIO_LIB = None
+AUDIO_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsuta_audio.so")
+
+
+def _audio_lib():
+    """libsuta_audio.so (include/suta_audio.h): the from-spec FLAC decoder, host C++."""
+    global _AUDIO_LIB
+    if _AUDIO_LIB is None:
+        import ctypes as C
+        if not os.path.exists(AUDIO_LIB_PATH):
+            raise RuntimeError(f"libsuta_audio.so not found at {AUDIO_LIB_PATH}: build it with __graft_entry__.build()")
+        lib = C.CDLL(AUDIO_LIB_PATH)
+        u8p, i32p, i64p = C.POINTER(C.c_uint8), C.POINTER(C.c_int32), C.POINTER(C.c_int64)
+        lib.suta_flac_info.argtypes = [u8p, C.c_int64, i32p, i32p, i32p, i64p]
+        lib.suta_flac_info.restype = C.c_int32
+        lib.suta_flac_decode.argtypes = [u8p, C.c_int64, C.POINTER(C.c_float), C.c_int64, C.c_int32, i64p]
+        lib.suta_flac_decode.restype = C.c_int32
+        lib.suta_audio_last_error.restype = C.c_char_p
+        _AUDIO_LIB = lib
+    return _AUDIO_LIB
+
+
+def _as_bytes(src) -> bytes:
+    if isinstance(src, (bytes, bytearray, memoryview)):
+        return bytes(src)
+    with open(src, "rb") as f:
+        return f.read()
+
+
+def flac_info(src):
+    """(sample_rate, channels, bits_per_sample, total_samples) from STREAMINFO (path or bytes)."""
+    import ctypes as C
+    lib = _audio_lib()
+    buf = np.frombuffer(_as_bytes(src), dtype=np.uint8)
+    sr, ch, bps, n = C.c_int32(), C.c_int32(), C.c_int32(), C.c_int64()
+    st = lib.suta_flac_info(buf.ctypes.data_as(C.POINTER(C.c_uint8)), buf.size, C.byref(sr), C.byref(ch),
+                            C.byref(bps), C.byref(n))
+    if st:
+        raise RuntimeError(f"FLAC: {lib.suta_audio_last_error().decode()}")
+    return sr.value, ch.value, bps.value, n.value
+
+
+def flac_decode(src, verify_crc: bool = True) -> Tuple[np.ndarray, int]:
+    """torchaudio.load semantics for a FLAC file (reference data.py:15): ((C, N) float32 in [-1, 1),
+    sample_rate), samples scaled by 2^-(bps-1).  Decoded by libsuta_audio (GIL released)."""
+    import ctypes as C
+    lib = _audio_lib()
+    buf = np.frombuffer(_as_bytes(src), dtype=np.uint8)
+    bp = buf.ctypes.data_as(C.POINTER(C.c_uint8))
+    sr, ch, bps, total = C.c_int32(), C.c_int32(), C.c_int32(), C.c_int64()
+    st = lib.suta_flac_info(bp, buf.size, C.byref(sr), C.byref(ch), C.byref(bps), C.byref(total))
+    cap = total.value if (st == 0 and total.value > 0) else max(1, buf.size * 4)
+    for _ in range(2):
+        out = np.empty((max(1, ch.value), cap), np.float32)
+        n = C.c_int64()
+        st = lib.suta_flac_decode(bp, buf.size, out.ctypes.data_as(C.POINTER(C.c_float)), cap, int(verify_crc),
+                                  C.byref(n))
+        if st == 4 and n.value > cap:   # SUTA_AUDIO_ERR_SPACE: retry with the stated requirement
+            cap = n.value
+            continue
+        break
+    if st:
+        raise RuntimeError(f"FLAC: {lib.suta_audio_last_error().decode()}")
+    return out[:, :n.value], sr.value
+
+
+def audio_info(path: str) -> Tuple[int, int]:
+    """(samples per channel, sample rate) from the file header without decoding (WAV, FLAC), or by
+    decoding for other formats.  The driver's LPT cost model uses it."""
+    p = str(path)
+    low = p.lower()
+    if low.endswith(".flac"):
+        sr, ch, bps, n = flac_info(p)
+        if n > 0:
+            return n, sr
+    elif low.endswith(".wav"):
+        try:
+            with _wave.open(p, "rb") as f:
+                return f.getnframes(), f.getframerate()
+        except _wave.Error:
+            pass
+    x, sr = _decode_audio(p)
+    return x.size, sr
+
+
+def decoded_length(path: str, max_len: int = MAX_LEN) -> int:
+    """Samples the reader will hand to the engine: channels concatenated (reference data.py:18),
+    resampled to 16 kHz (torchaudio length rule ceil(n * 16000 / sr) per channel), truncated."""
+    p = str(path)
+    if p.lower().endswith(".flac"):
+        sr, ch, bps, n = flac_info(p)
+        per = n
+    elif p.lower().endswith(".wav"):
+        with _wave.open(p, "rb") as f:
+            sr, ch, per = f.getframerate(), f.getnchannels(), f.getnframes()
+    else:
+        x, sr = _decode_audio(p)
+        ch, per = 1, x.size
+    if sr != SAMPLE_RATE:
+        from math import gcd
+        g = gcd(sr, SAMPLE_RATE)
+        per = -(-(SAMPLE_RATE // g) * per // (sr // g))
+    return min(ch * per, max_len)
+
+
 def _decode_audio(path: str) -> Tuple[np.ndarray, int]:
-    try:
-        import soundfile as sf  # noqa: F401
-        x, sr = sf.read(path, dtype="float32", always_2d=True)
-        return x.mean(1).astype(np.float32) if x.shape[1] > 1 else x[:, 0], sr
-    except ImportError:
-        pass
-    try:
-        import torchaudio
-        w, sr = torchaudio.load(path)
-        return w.reshape(-1).numpy().astype(np.float32), sr
-    except ImportError:
-        pass
-    if not path.lower().endswith(".wav"):
-        raise RuntimeError(f"cannot decode {path}: neither soundfile nor torchaudio is installed (WAV only)")
+    """torchaudio.load(...) then .reshape(-1) (reference data.py:15-18): channels concatenated."""
+    x, sr = decode_channels(path)
+    return np.ascontiguousarray(x.reshape(-1)), sr
+
+
+def decode_channels(path: str) -> Tuple[np.ndarray, int]:
+    """torchaudio.load(path) (reference data.py:15): ((C, N) float32, sample rate).  FLAC: libsuta_audio;
+    WAV: the standard library; anything else (CommonVoice MP3) needs soundfile or torchaudio, neither of
+    which is in this image."""
+    path = str(path)
+    low = path.lower()
+    if low.endswith(".flac"):
+        return flac_decode(path)
+    if not low.endswith(".wav"):
+        try:
+            import soundfile as sf
+            x, sr = sf.read(path, dtype="float32", always_2d=True)      # (N, C)
+            return np.ascontiguousarray(x.T), sr
+        except ImportError:
+            pass
+        try:
+            import torchaudio
+            w, sr = torchaudio.load(path)
+            return w.numpy().astype(np.float32), sr
+        except ImportError:
+            pass
+        raise RuntimeError(f"cannot decode {path}: FLAC and WAV are built in; other formats need soundfile or "
+                           "torchaudio (not installed)")
     with _wave.open(path, "rb") as f:
         sr, ch, sw, n = f.getframerate(), f.getnchannels(), f.getsampwidth(), f.getnframes()
         raw = f.readframes(n)
     if sw == 2:
         x = np.frombuffer(raw, dtype="<i2").astype(np.float32) / 32768.0
+    elif sw == 3:
+        b = np.frombuffer(raw, dtype=np.uint8).reshape(-1, 3).astype(np.int32)
+        v = (b[:, 0] | (b[:, 1] << 8) | (b[:, 2] << 16))
+        v = np.where(v >= 1 << 23, v - (1 << 24), v)
+        x = v.astype(np.float32) / 8388608.0
     elif sw == 4:
         x = np.frombuffer(raw, dtype="<i4").astype(np.float32) / 2147483648.0
     elif sw == 1:
         x = (np.frombuffer(raw, dtype=np.uint8).astype(np.float32) - 128.0) / 128.0
     else:
         raise RuntimeError(f"unsupported sample width {sw} in {path}")
-    if ch > 1:
-        x = x.reshape(-1, ch).reshape(-1)  # the reference reshapes (C, N) to (-1): channels concatenated
-    return x, sr
+    # interleaved frames -> (C, N)
+    return np.ascontiguousarray(x.reshape(-1, ch).T, dtype=np.float32), sr
+
+
+def sinc_resample_kernel(orig: int, new: int, lowpass_filter_width: int = 6, rolloff: float = 0.99):
+    """torchaudio.functional._get_sinc_resample_kernel, method "sinc_interp_hann" (torchaudio 2.x, the
+    default of torchaudio.transforms.Resample used at reference data.py:16-17): the Hann-windowed sinc
+    filter bank, built in float64 and cast to float32.  Returns ((new, 1, 2*width + orig) kernel, width)
+    for orig/new already divided by their gcd."""
+    import math
+    base = min(orig, new) * rolloff
+    width = math.ceil(lowpass_filter_width * orig / base)
+    idx = np.arange(-width, width + orig, dtype=np.float64)[None, None] / orig
+    t = np.arange(0, -new, -1, dtype=np.float64)[:, None, None] / new + idx
+    t *= base
+    t = np.clip(t, -lowpass_filter_width, lowpass_filter_width)
+    window = np.cos(t * math.pi / lowpass_filter_width / 2) ** 2
+    t *= math.pi
+    scale = base / orig
+    with np.errstate(invalid="ignore", divide="ignore"):
+        k = np.where(t == 0, 1.0, np.sin(t) / t)
+    k = k * window * scale
+    return k.astype(np.float32), width
 
 
 def resample(x: np.ndarray, sr: int, target: int = SAMPLE_RATE) -> np.ndarray:
+    """torchaudio.transforms.Resample(sr, target)(x) restated (reference data.py:16-17): pad by the
+    filter width, strided conv1d with the sinc bank, interleave the phases, keep ceil(target*n/sr)
+    samples.  torchaudio is absent here, so agreement with it is "parity unpinned" beyond this
+    restatement of its published algorithm (tests/test_audio.py checks band-limited behaviour)."""
     if sr == target:
         return x
-    try:
-        import torchaudio
-        import torch
-        return torchaudio.transforms.Resample(sr, target)(torch.from_numpy(x)[None])[0].numpy()
-    except ImportError:
-        from math import gcd
-        from scipy.signal import resample_poly
-        g = gcd(sr, target)
-        return resample_poly(x, target // g, sr // g).astype(np.float32)
+    import torch
+    from math import gcd
+    g = gcd(int(sr), int(target))
+    orig, new = int(sr) // g, int(target) // g
+    kern, width = sinc_resample_kernel(orig, new)
+    w = torch.from_numpy(np.ascontiguousarray(x, dtype=np.float32)).reshape(1, 1, -1)
+    n = w.shape[-1]
+    w = torch.nn.functional.pad(w, (width, width + orig))
+    y = torch.nn.functional.conv1d(w, torch.from_numpy(kern), stride=orig)   # (1, new, frames)
+    y = y.transpose(1, 2).reshape(-1)
+    target_len = -(-new * n // orig)
+    return y[:target_len].numpy()
 
 
 class AudioReader:
-    """data.py:13-25 with a deterministic noise generator."""
+    """data.py:13-25.  decode() is thread-safe (the loader runs it on worker threads); the noise is
+    drawn in load order by noise(), from a torch.Generator seeded 0 (see module docstring)."""
 
     def __init__(self, extra_noise: float = 0.0, max_len: int = MAX_LEN, seed: int = 0):
         import torch
@@ -222,24 +374,35 @@ class AudioReader:
         self.max_len = max_len
         self.gen = torch.Generator().manual_seed(seed)
 
-    def __call__(self, path: str) -> np.ndarray:
-        import torch
-        x, sr = _decode_audio(str(path))
-        x = resample(x, sr).reshape(-1)
+    def decode(self, path: str) -> np.ndarray:
+        x, sr = decode_channels(str(path))
+        if sr != SAMPLE_RATE:  # the reference resamples the (C, N) tensor per channel, then flattens
+            x = np.stack([resample(c, sr) for c in x])
+        x = x.reshape(-1)
         if x.shape[-1] >= self.max_len:
             print(f"{path} has len {x.shape}, truncate to {self.max_len}")
             x = x[: self.max_len]
-        w = torch.from_numpy(np.ascontiguousarray(x, dtype=np.float32))
+        return np.ascontiguousarray(x, dtype=np.float32)
+
+    def noise(self, x: np.ndarray) -> np.ndarray:
+        import torch
+        w = torch.from_numpy(x)
         if self.extra_noise:
             w = w + self.extra_noise * torch.randn(w.shape, generator=self.gen)
         return w.numpy()
 
+    def __call__(self, path: str) -> np.ndarray:
+        return self.noise(self.decode(path))
 
-def collect_audio_batch(batch, reader: AudioReader):
-    """data.py:9-45: read a bucket, sort by audio length descending."""
+
+def collect_audio_batch(batch, reader: AudioReader, decoded=None):
+    """data.py:9-45: read a bucket, sort by audio length descending.  `decoded`: the bucket's
+    waveforms already decoded (by loader threads); noise is still drawn here, in load order."""
     if type(batch[0]) is not tuple:
         batch = batch[0]
-    feats = [(reader(str(b[0])), str(b[0]).split("/")[-1].split(".")[0], b[1]) for b in batch]
+    if decoded is None:
+        decoded = [reader.decode(str(b[0])) for b in batch]
+    feats = [(reader.noise(w), str(b[0]).split("/")[-1].split(".")[0], b[1]) for w, b in zip(decoded, batch)]
     feats = sorted(((len(f), n, f, t) for f, n, t in feats), reverse=True, key=lambda x: x[0])
     lens, files, wavs, texts = zip(*feats)
     return lens, wavs, texts, files
@@ -263,11 +426,36 @@ def load_dataset(split=None, name="librispeech", path=None, batch_size=1, extra_
                 out.append(list(it) if isinstance(it, list) else [it])
             return out
 
-        def collate(self, items):
-            return collect_audio_batch(items, reader)
+        def collate(self, items, decoded=None):
+            return collect_audio_batch(items, reader, decoded)
+
+        def iter_collated(self, indices: Sequence[int], workers: int = 0, window: int = 32):
+            """(index, collated batch) for the given loader batches, in order.  workers > 1 decodes
+            ahead on a thread pool (the FLAC decoder and file reads release the GIL), at most
+            `window` batches in flight; the noise draw stays sequential (deterministic)."""
+            batches = self.raw_batches()
+            if workers <= 1:
+                for i in indices:
+                    yield i, self.collate(batches[i])
+                return
+            from collections import deque
+            from concurrent.futures import ThreadPoolExecutor
+            with ThreadPoolExecutor(max_workers=workers) as ex:
+                pending = deque()
+                it = iter(indices)
+                for i in it:
+                    pending.append((i, [ex.submit(reader.decode, str(f)) for f, _ in batches[i]]))
+                    if len(pending) >= window:
+                        break
+                while pending:
+                    i, futs = pending.popleft()
+                    yield i, self.collate(batches[i], [f.result() for f in futs])
+                    nxt = next(it, None)
+                    if nxt is not None:
+                        pending.append((nxt, [ex.submit(reader.decode, str(f)) for f, _ in batches[nxt]]))
 
         def __iter__(self):
-            for items in self.raw_batches():
-                yield self.collate(items)
+            for _, b in self.iter_collated(range(len(self)), num_workers):
+                yield b
 
     return _Loader()

@@ -9,7 +9,11 @@ file `log_dir/exp_name` and CSV.  Differences, all deliberate:
     utterances are length-sorted inside windows of 8 batches to keep padding low, and the
     per-utterance lines are printed in dataset order).  The reference's own --batch_size > 1
     pads without a mask and breaks mcc_loss (main.py:32); it is only used for loading here;
-  * under torchrun, utterances are LPT-sharded over ranks and WER counts are all_reduce'd;
+  * under torchrun (episodic runs only), utterances are LPT-sharded over ranks by their decoded
+    length (file headers), WER counts are all_reduce'd, and rank 0 prints every per-utterance line
+    after the gather, in dataset order (one ordered stream, as the reference's single process);
+    non-episodic adaptation carries state from one utterance to the next in dataset order
+    (reference main.py:323-348), so it refuses to shard;
   * pretrained weights load from a local checkpoint directory or the local HF cache (no
     network); `--synthetic_weights` uses the seeded generator instead;
   * when --steps < 10 the CSV is written with empty WERR (the reference raises there).
@@ -64,6 +68,10 @@ def build_parser(sdpl: bool = False):
     p.add_argument("--gpu_min_fill", type=float, default=0.35,
                    help="ragged grouping: 0 = greedy; > 0 = padding-minimising partition charging a batch at least "
                         "this fraction of --gpu_budget_s (tools/bench_varlen.py: 0.35 -> 27.2 vs greedy 26.3 utt/s)")
+    p.add_argument("--dist_backend", default="auto", choices=["auto", "nccl", "gloo"],
+                   help="torch.distributed backend under torchrun (auto: nccl = RCCL when a GPU is visible)")
+    p.add_argument("--num_workers", type=int, default=4,
+                   help="audio decode threads (FLAC/WAV decode + resample ahead of the engine)")
     p.add_argument("--precision", default="fp32", choices=["fp32", "fp32-split-bf16", "bf16"],
                    help="GEMM arithmetic (fp32 = the reference's; bf16 = BASELINE config C4)")
     return p
@@ -148,15 +156,23 @@ def main(argv=None, sdpl: bool = False):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not a.episodic:
+        raise SystemExit("non-episodic SUTA adapts utterances sequentially (state carries over, reference "
+                         "main.py:323-348): it cannot be sharded over ranks; run it with one process")
     import torch
+    device = a.device if a.device is not None else local
+    backend = a.dist_backend
+    if backend == "auto":
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    count_device = None
     if world > 1:
         import torch.distributed as tdist
-        if torch.cuda.is_available():
-            torch.cuda.set_device(local)
-            tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            torch.cuda.set_device(device)
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", device))
+            count_device = torch.device("cuda", device)   # RCCL reduces device tensors only
         else:
             tdist.init_process_group("gloo")
-    device = a.device if a.device is not None else local
     say = print if rank == 0 else (lambda *x, **k: None)
 
     from .data import load_dataset
@@ -191,10 +207,11 @@ def main(argv=None, sdpl: bool = False):
     if not a.episodic:
         record = sorted(set([0, a.steps]))
 
-    # shard batches over ranks by estimated cost (file size ~ duration)
+    # shard batches over ranks by estimated cost (decoded length from the file headers)
     batches = dataset.raw_batches()
     if world > 1:
-        costs = [sum(utterance_cost(max(1, os.path.getsize(str(f)) // 2), cfg, a.steps) for f, _ in b)
+        from .data import decoded_length
+        costs = [sum(utterance_cost(max(1, decoded_length(str(f))), cfg, a.steps) for f, _ in b)
                  for b in batches]
         mine = lpt_shard(costs, world)[rank]
     else:
@@ -221,27 +238,32 @@ def main(argv=None, sdpl: bool = False):
     start = time.time()
     window: List = []
 
+    def emit(rec):
+        for ln in rec["lines"]:
+            print(*ln)
+
     def flush():
         for (bi, x, text), ids in zip(window, adapt_window(window)):
-            rec = {"idx": bi, "text": text, "duration": len(x) / SAMPLE_RATE, "hyp": {}}
+            rec = {"idx": bi, "text": text, "duration": len(x) / SAMPLE_RATE, "hyp": {}, "lines": []}
             ori = batch_decode(ids[0][None])
             rec["hyp"][0] = ori[0]
             ori_wer = wer([text], ori)
-            print("original WER: ", ori_wer)
+            rec["lines"].append(("original WER: ", ori_wer))
             if a.episodic:
                 for c in CHECKPOINTS:
                     if c <= a.steps:
                         h = batch_decode(ids[c][None])
                         rec["hyp"][c] = h[0]
                         ada = wer([text], h)
-                        print(f"adapt-{c} WER: " + (" " if c < 10 else ""), ada)
+                        rec["lines"].append((f"adapt-{c} WER: " + (" " if c < 10 else ""), ada))
                         if c == 10:
                             rec["werr"] = ori_wer - ada
+            if world == 1:
+                emit(rec)   # one process: stream the lines as the reference does
             results.append(rec)
         window.clear()
 
-    for bi in mine:
-        lens, wavs, texts, files = dataset.collate(batches[bi])
+    for bi, (lens, wavs, texts, files) in dataset.iter_collated(mine, a.num_workers):
         for wav, text in zip(wavs, texts):
             window.append((bi, normalize(wav), text))
         if len(window) >= 8 * gb:
@@ -250,13 +272,16 @@ def main(argv=None, sdpl: bool = False):
     elapsed = time.time() - start
 
     allres = [r for part in gather_objects(results) for r in part]
-    allres.sort(key=lambda r: r["idx"])
+    allres.sort(key=lambda r: r["idx"])   # stable: utterances of one loader batch keep their order
+    if world > 1 and rank == 0:
+        for rec in allres:   # one ordered stream of per-utterance lines, in dataset order
+            emit(rec)
     # corpus WER counts, reduced over ranks (the one data collective)
     local_counts = {}
     for key in [0] + list(CHECKPOINTS):
         sel = [r for r in results if key in r["hyp"]]
         local_counts[str(key)] = wer_counts([r["text"] for r in sel], [r["hyp"][key] for r in sel]) if sel else (0, 0)
-    counts = reduce_counts(local_counts)
+    counts = reduce_counts(local_counts, device=count_device)
     if rank == 0:
         def cw(k):
             e, w = counts[str(k)]

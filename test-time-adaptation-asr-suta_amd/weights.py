@@ -54,24 +54,30 @@ def synth_weights(cfg: dict, seed: int = DEFAULT_SEED, blank_bias: float = 1.0) 
     return out
 
 
+LEGACY_NAMES = (("weight_g", "parametrizations.weight.original0"),
+                ("weight_v", "parametrizations.weight.original1"))
+
+
+def remap_legacy(sd: Dict[str, np.ndarray]) -> Dict[str, np.ndarray]:
+    """Checkpoints saved before torch's parametrized weight_norm name the positional conv's
+    weight-norm tensors `weight_g` / `weight_v`; HF maps them to `parametrizations.weight.original0/1`
+    on load.  Applied to every checkpoint format."""
+    for old, new in LEGACY_NAMES:
+        key = "wav2vec2.encoder.pos_conv_embed.conv." + old
+        if key in sd:
+            sd["wav2vec2.encoder.pos_conv_embed.conv." + new] = sd.pop(key)
+    return sd
+
+
 def load_hf_checkpoint(path: str) -> Dict[str, np.ndarray]:
     """state_dict of a LOCAL HF checkpoint dir (safetensors preferred; torch files weights_only)."""
     st = os.path.join(path, "model.safetensors")
     if os.path.isfile(st):
         from safetensors.numpy import load_file
-        return {k: np.ascontiguousarray(v, dtype=np.float32) for k, v in load_file(st).items()}
+        return remap_legacy({k: np.ascontiguousarray(v, dtype=np.float32) for k, v in load_file(st).items()})
     pt = os.path.join(path, "pytorch_model.bin")
     if os.path.isfile(pt):
         import torch
         sd = torch.load(pt, map_location="cpu", weights_only=True)
-        out = {}
-        for k, v in sd.items():
-            out[k] = v.float().numpy()
-        # legacy weight_norm names (weight_g / weight_v) -> parametrizations names
-        for old, new in (("weight_g", "parametrizations.weight.original0"),
-                         ("weight_v", "parametrizations.weight.original1")):
-            key = "wav2vec2.encoder.pos_conv_embed.conv." + old
-            if key in out:
-                out["wav2vec2.encoder.pos_conv_embed.conv." + new] = out.pop(key)
-        return out
+        return remap_legacy({k: v.float().numpy() for k, v in sd.items()})
     raise FileNotFoundError(f"no model.safetensors / pytorch_model.bin under {path}")

@@ -1,0 +1,106 @@
+"""GPU tier: parity at the bench's own scale and on the replayed (hipGraph) ragged path.
+
+* The headline layout exactly as bench.py runs it: 64 x 128 000-sample utterances x 10 SUTA steps in
+  one suta_adapt call, scripts/LS.sh flags, record steps 0/1/3/5/10, the second call of a repeated
+  layout (so every step is a graph replay, as in the timed region).  Slots 0, 31 and 63 are compared
+  with the CPU oracle (oracle/w2v2_cpu.run_suta): logits within 5e-5 absolute (the base-size
+  tolerance of tests/test_gpu_parity.py), adapted tensors by tests/parity.assert_params_close.
+* Ragged batches that share a quantised layout but differ in per-utterance lengths: the second call
+  replays the captured step with new lengths (device-side length buffers); it must equal single runs
+  and the eager (graphs off) execution bitwise.
+* Ragged batches with T > 512 frames (long utterances: the attention path for long keys plus
+  ragged masks) against single runs.
+"""
+import numpy as np
+import pytest
+import torch
+
+from suta_amd import synth
+from suta_amd.config import get_config
+from suta_amd.engine import SutaEngine, SutaHParams
+from suta_amd.weights import synth_weights
+from tests.parity import assert_params_close, logits_tol
+
+pytestmark = pytest.mark.gpu
+
+BENCH_RECORD = [0, 1, 3, 5, 10]   # bench.py RECORD
+
+
+def test_bench_layout_matches_oracle():
+    from oracle import w2v2_cpu as W
+    import os
+    torch.set_num_threads(min(16, len(os.sched_getaffinity(0))))
+    cfg = get_config("wav2vec2-base")
+    sd = synth_weights(cfg)
+    B, N, S = 64, 128000, 10
+    eng = SutaEngine(cfg, sd, device=0, max_batch=B, max_samples=N)
+    hp = SutaHParams()
+    warm = torch.from_numpy(synth.batch(N, B, start=0)).cuda()
+    x = synth.batch(N, B, start=B)          # bench.py's first timed batch at --warmup 1
+    eng.adapt(warm, S, hp, record=BENCH_RECORD, want_logits=False)          # captures the step graph
+    logits, ids, T = eng.adapt(torch.from_numpy(x).cuda(), S, hp, record=BENCH_RECORD)   # replayed
+    assert T == 399
+    sdt = {k: torch.from_numpy(v) for k, v in sd.items()}
+    for slot in (0, 31, 63):
+        ref, final = W.run_suta(sdt, cfg, torch.from_numpy(x[slot])[None], S, record=[0, 1, 5, 10])
+        for r in (0, 1, 5, 10):
+            np.testing.assert_allclose(logits[r][slot], ref[r][0].numpy(), rtol=0, atol=5e-5,
+                                       err_msg=f"slot {slot} step {r}")
+            np.testing.assert_array_equal(ids[r][slot], logits[r][slot].argmax(-1))
+        for name, val in final.items():
+            assert_params_close(eng.get_param(slot, name), val.numpy(), hp.lr, S, name=f"slot {slot} {name}")
+    eng.close()
+
+
+def _singles(eng, waves, steps, hp, record):
+    out = []
+    for w in waves:
+        l1, _, t1 = eng.adapt(w, steps, hp, record=record)
+        out.append(({r: l1[r][0] for r in record}, {n: eng.get_param(0, n) for n in eng.trainable_names()}, t1))
+    return out
+
+
+def test_ragged_graph_replay_equals_singles_and_eager():
+    cfg = get_config("wav2vec2-base")
+    eng = SutaEngine(cfg, synth_weights(cfg), device=0, max_batch=3, max_samples=64000)
+    hp = SutaHParams()
+    rec = [0, 1, 3]
+    first = [synth.wave(n, 300 + i) for i, n in enumerate((32000, 17003, 24480))]
+    second = [synth.wave(n, 310 + i) for i, n in enumerate((30421, 31999, 16500))]   # same 32000 layout
+    eng.set_graphs(True)
+    eng.adapt_varlen(first, 3, hp, record=rec, quantum=1600)
+    lv, iv, tv = eng.adapt_varlen(second, 3, hp, record=rec, quantum=1600)   # every step replayed
+    finals = [{n: eng.get_param(b, n) for n in eng.trainable_names()} for b in range(3)]
+    eng.set_graphs(False)
+    le, _, te = eng.adapt_varlen(second, 3, hp, record=rec, quantum=1600)
+    assert tv == te
+    for r in rec:
+        for b in range(3):
+            assert np.array_equal(lv[r][b], le[r][b]), (r, b)
+    for b, (l1, p1, t1) in enumerate(_singles(eng, second, 3, hp, rec)):
+        assert tv[b] == t1
+        for r in rec:
+            np.testing.assert_allclose(lv[r][b], l1[r], rtol=0, atol=logits_tol(hp.lr), err_msg=f"utt {b} step {r}")
+        for n, v in p1.items():
+            assert_params_close(finals[b][n], v, hp.lr, 3, name=f"utt {b} {n}")
+    eng.set_graphs(True)
+    eng.close()
+
+
+def test_ragged_long_utterances_equal_singles():
+    """T up to 749 frames (> 512): long-key attention with ragged key masks, checked against runs alone."""
+    cfg = get_config("wav2vec2-base")
+    eng = SutaEngine(cfg, synth_weights(cfg), device=0, max_batch=3, max_samples=240000)
+    hp = SutaHParams()
+    rec = [0, 2]
+    waves = [synth.wave(n, 320 + i) for i, n in enumerate((240000, 170001, 120000))]
+    lv, iv, tv = eng.adapt_varlen(waves, 2, hp, record=rec)
+    assert max(tv) == 749
+    finals = [{n: eng.get_param(b, n) for n in eng.trainable_names()} for b in range(3)]
+    for b, (l1, p1, t1) in enumerate(_singles(eng, waves, 2, hp, rec)):
+        assert tv[b] == t1
+        for r in rec:
+            np.testing.assert_allclose(lv[r][b], l1[r], rtol=0, atol=logits_tol(hp.lr), err_msg=f"utt {b} step {r}")
+        for n, v in p1.items():
+            assert_params_close(finals[b][n], v, hp.lr, 2, name=f"utt {b} {n}")
+    eng.close()

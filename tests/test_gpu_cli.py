@@ -103,3 +103,59 @@ def test_sdpl_cli_end_to_end(tmp_path, capsys):
     assert tuple(counts["0"]) == wer_counts(list(ds.text), hyp0)
     for k in (1, 3, 5, 10):
         assert counts[str(k)][1] == counts["0"][1]
+
+
+def _oracle_counts(ds_files, ds_texts, cfg_name, steps, lr, extra_noise=0.0):
+    from oracle import w2v2_cpu as W
+    cfg = get_config(cfg_name)
+    sd = {k: torch.from_numpy(v) for k, v in synth_weights(cfg).items()}
+    reader = AudioReader(extra_noise)
+    rec = [0] + [c for c in (1, 3, 5, 10) if c <= steps]
+    hyps = {k: [] for k in rec}
+    for f in ds_files:
+        x = torch.from_numpy(normalize(reader(str(f))))[None]
+        lg, _ = W.run_suta(sd, cfg, x, steps, lr=lr, record=rec)
+        for k in rec:
+            hyps[k].append(batch_decode(lg[k].argmax(-1).numpy())[0])
+    return {k: wer_counts(list(ds_texts), hyps[k]) for k in rec}
+
+
+def test_cli_world2_gloo_on_one_gpu(tmp_path):
+    """Config C3's multi-rank plumbing on the one-GPU box: the real driver as 2 processes sharing
+    device 0 over gloo (LPT shards by decoded length, count all_reduce, transcript gather, rank-0
+    ordered print).  Counts equal the world-1 run and the CPU oracle; rank 1 prints no utterance line."""
+    from tests import corpus_fixtures as CF
+    from tests.multirank import run_ranks
+    from suta_amd.data import CHiMEDataset
+    CF.chime(tmp_path, n=5)
+    argv = (f"--asr tiny-group --synthetic_weights --steps 10 --dataset_name chime --dataset_dir {tmp_path} "
+            f"--temp 2.5 --episodic --em_coef 0.3 --reweight --log_dir {tmp_path}/exps --lr 5e-4 --non_blank "
+            f"--train_feature --extra_noise 0 --gpu_batch 2 --device 0 --dist_backend gloo").split()
+    (c1,), (o1,) = run_ranks(1, argv, tmp_path, fake=False)
+    c2, o2 = run_ranks(2, argv, tmp_path, fake=False)
+    assert c2[0] == c2[1] == c1
+    lines = lambda o: [ln for ln in o.splitlines() if ln.startswith(("original WER:", "adapt-"))]  # noqa: E731
+    assert lines(o2[0]) == lines(o1) and lines(o2[1]) == []
+    ds = CHiMEDataset(None, 1, str(tmp_path))
+    ref = _oracle_counts(ds.file_list, ds.text, "tiny-group", 10, 5e-4)
+    for k, v in ref.items():
+        assert c1[str(k)] == v, k
+
+
+def test_cli_librispeech_flac_ls_flags(tmp_path, capsys):
+    """scripts/LS.sh (LS + 0.01 noise) flags on a LibriSpeech-layout FLAC corpus (FLAC decoded by
+    libsuta_audio): the driver's corpus WER counts equal the CPU oracle's on the same decoded, noised,
+    normalised audio (w2v2-base shapes, seeded weights)."""
+    from tests import corpus_fixtures as CF
+    from suta_amd.data import LibriDataset
+    CF.librispeech(tmp_path)
+    args = (f"--asr facebook/wav2vec2-base-960h --synthetic_weights --steps 10 --dataset_name librispeech "
+            f"--dataset_dir {tmp_path} --temp 2.5 --episodic --em_coef 0.3 --reweight --log_dir {tmp_path}/exps "
+            f"--lr 2e-5 --non_blank --train_feature --extra_noise 0.01").split()
+    counts = M.main(args)
+    out = capsys.readouterr().out
+    assert out.count("original WER: ") >= 5 and "TTA-10 WER:" in out
+    ds = LibriDataset(None, 1, str(tmp_path))
+    ref = _oracle_counts(ds.file_list, ds.text, "wav2vec2-base", 10, 2e-5, extra_noise=0.01)
+    for k, v in ref.items():
+        assert tuple(counts[str(k)]) == v, k

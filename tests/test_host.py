@@ -168,3 +168,72 @@ def test_ragged_groups_partition(min_fill):
     assert padded <= greedy
     assert ragged_groups([700000], 4, budget, min_fill) == [[0]]
     assert ragged_groups([], 4, budget, min_fill) == []
+
+
+def _per_utt_lines(out):
+    return [ln for ln in out.splitlines() if ln.startswith(("original WER:", "adapt-"))]
+
+
+@pytest.mark.parametrize("corpus", ["chime", "librispeech"])
+def test_driver_world2_gloo_equals_world1(tmp_path, corpus):
+    """The real driver (suta_amd/main.py) as 2 gloo ranks with a deterministic stand-in engine: LPT
+    sharding by decoded length, the count all_reduce and the object gather give the world-1 counts, and
+    rank 0 alone prints every per-utterance line, in the world-1 (dataset) order."""
+    from tests import corpus_fixtures as CF
+    from tests.multirank import run_ranks
+    if corpus == "chime":
+        CF.chime(tmp_path, n=5)
+        flags = f"--dataset_name chime --dataset_dir {tmp_path}"
+    else:
+        CF.librispeech(tmp_path)
+        flags = f"--dataset_name librispeech --dataset_dir {tmp_path}"
+    argv = (f"--asr tiny-group --synthetic_weights --steps 10 {flags} --temp 2.5 --episodic --em_coef 0.3 "
+            f"--reweight --log_dir {tmp_path}/exps --lr 5e-4 --non_blank --train_feature --gpu_batch 2 "
+            f"--dist_backend gloo").split()
+    (c1,), (o1,) = run_ranks(1, argv, tmp_path, fake=True)
+    c2, o2 = run_ranks(2, argv, tmp_path, fake=True)
+    assert c2[0] == c2[1] == c1
+    assert _per_utt_lines(o2[0]) == _per_utt_lines(o1) and len(_per_utt_lines(o1)) > 0
+    assert _per_utt_lines(o2[1]) == []
+    assert "TTA-10 WER:" in o2[0] and "TTA-10 WER:" not in o2[1]
+
+
+def test_driver_refuses_to_shard_non_episodic(tmp_path):
+    from tests import corpus_fixtures as CF
+    from tests.multirank import run_ranks
+    CF.chime(tmp_path, n=2)
+    argv = (f"--asr tiny-group --synthetic_weights --steps 2 --dataset_name chime --dataset_dir {tmp_path} "
+            f"--log_dir {tmp_path}/exps --dist_backend gloo").split()
+    with pytest.raises(AssertionError, match="cannot be sharded"):
+        run_ranks(2, argv, tmp_path, fake=True)
+
+
+def test_lpt_cost_uses_decoded_length(tmp_path):
+    """FLAC files compress: the shard cost comes from STREAMINFO, not the file size."""
+    from suta_amd.data import decoded_length
+    from tests import corpus_fixtures as CF
+    CF.librispeech(tmp_path, lengths=(6000, 9100))
+    fl = sorted((tmp_path / "test-other").rglob("*.flac"))
+    assert [decoded_length(str(f)) for f in fl] == [6000, 9100]
+    CF.chime(tmp_path / "c", n=2)
+    wv = sorted((tmp_path / "c").rglob("*.wav"))
+    assert [decoded_length(str(f)) for f in wv] == [6000, 7500]
+
+
+def test_legacy_weight_norm_names_in_safetensors(tmp_path):
+    """Checkpoints converted from older torch name the pos-conv weight norm weight_g / weight_v; both
+    checkpoint formats map them to the parametrizations names the engine expects."""
+    import json
+    from safetensors.numpy import save_file
+    from suta_amd.weights import load_hf_checkpoint, synth_weights
+    cfg = get_config("tiny-group")
+    sd = synth_weights(cfg)
+    pre = "wav2vec2.encoder.pos_conv_embed.conv."
+    legacy = dict(sd)
+    legacy[pre + "weight_g"] = legacy.pop(pre + "parametrizations.weight.original0")
+    legacy[pre + "weight_v"] = legacy.pop(pre + "parametrizations.weight.original1")
+    json.dump(cfg, open(tmp_path / "config.json", "w"))
+    save_file(legacy, str(tmp_path / "model.safetensors"))
+    got = load_hf_checkpoint(str(tmp_path))
+    assert sorted(got) == sorted(sd)
+    assert np.array_equal(got[pre + "parametrizations.weight.original1"], sd[pre + "parametrizations.weight.original1"])
