@@ -33,22 +33,47 @@ from suta_amd.weights import synth_weights  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
 BF16_PEAK_TFLOPS = 2500.0      # MI355X_MICROARCH.md: bf16 dense MFMA peak
-BF16_SPLIT_PEAK_TFLOPS = BF16_PEAK_TFLOPS / 6  # 6 bf16 products per fp32-equivalent MAC
+BF16_SPLIT_PEAK_TFLOPS = BF16_PEAK_TFLOPS / 6
+HBM_PEAK_TBS = 8.0             # MI355X_MICROARCH.md: HBM3E peak  # 6 bf16 products per fp32-equivalent MAC
 RECORD = [0, 1, 3, 5, 10]
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r1", "pmc_traffic.json")
-GEMM_KERNELS = ("gemm_glds_kernel", "gemm_f32_kernel", "attn_fwd_kernel", "attn_bwd_kernel", "posconv_kernel")
+# newest committed rocprofv3 PMC reduction of this workload (tools/pmc_traffic.py; profiles/<round>/README.md)
+PMC_TRAFFIC = next((p for p in (os.path.join(ROOT, "profiles", r, "pmc_traffic.json") for r in ("r2", "r1"))
+                    if os.path.exists(p)), None)
+GEMM_KERNELS = ("gemm_glds_kernel", "gemm_f32_kernel", "attn_fwd_kernel", "attn_bwd_kernel", "posconv_kernel",
+                "flash_fwd_kernel", "flash_bwd_kernel", "flash_dq_kernel")
+FRONT_KERNELS = ("conv0_gn_kernel", "col_stats_final", "gn_bwd_final", "conv0_dw_reduce")
 
 
-def gemm_traffic(args):
-    """HBM bytes per GEMM launch from the committed rocprofv3 PMC passes of this same workload
-    (profiles/r1/README.md); None for other workloads."""
+def pmc(args):
+    """The committed PMC reduction when this run is its workload (w2v2-base, 64 x 8 s, 10 steps)."""
     if not (args.model == "wav2vec2-base" and args.batch == 64 and args.n_samples == 128000 and args.suta_steps == 10
-            and os.path.exists(PMC_TRAFFIC)):
+            and PMC_TRAFFIC):
         return None
-    d = json.load(open(PMC_TRAFFIC))
+    return json.load(open(PMC_TRAFFIC))
+
+
+def gemm_traffic(d):
+    """HBM bytes per GEMM-family launch from the PMC passes."""
     n = sum(d[k]["launches"] for k in GEMM_KERNELS if k in d)
     b = sum(d[k]["launches"] * d[k]["hbm_bytes_per_launch"] for k in GEMM_KERNELS if k in d)
     return round(b / n) if n else None
+
+
+def frontend_traffic(d):
+    """HBM bytes per conv front-end call (a forward call = 2 conv0_gn passes + the statistics finaliser; a
+    backward call = 2 passes + the GroupNorm-backward finaliser + the conv0 dW reduction)."""
+    if "conv0_gn_kernel" not in d:
+        return None
+    b = sum(d[k]["launches"] * d[k]["hbm_bytes_per_launch"] for k in FRONT_KERNELS if k in d)
+    return b / (d["conv0_gn_kernel"]["launches"] / 2)
+
+
+def attention_flops(cfg, T, B):
+    """Algorithmic FLOPs of the attention products per (forward, backward) layer call: S and PV forward,
+    dP, dQ, dK, dV backward, for B utterances of T frames."""
+    d = cfg["hidden_size"] // cfg["num_attention_heads"]
+    unit = 2.0 * T * T * d * cfg["num_attention_heads"] * B
+    return 2 * unit, 4 * unit
 
 
 def cpu_baseline(cfg, n_samples, suta_steps, budget_s=25.0):
@@ -200,6 +225,7 @@ def main():
         eng.sync()
         timing_el = time.perf_counter() - t1
         timing = eng.get_timing()
+        timing_ex = eng.get_timing_ex()
         eng.set_timing(False)
 
     utts = B * args.steps * world
@@ -221,21 +247,50 @@ def main():
         # dominant kernel family: the fp32 MFMA GEMM (every conv/linear/attention product)
         gemm_flops = flops_utt * B * tsteps  # per-rank algorithmic GEMM-shaped FLOPs of the timing pass
         achieved = gemm_flops / (gms / 1000.0) / 1e12 if gms > 0 else None
-        traffic = gemm_traffic(args)
+        d = pmc(args)
+        traffic = gemm_traffic(d) if d else None
+        gx, ax, fx = timing_ex["gemm"], timing_ex["attention"], timing_ex["frontend"]
+        traffic_alg = round((gx[2] + ax[2]) / max(1, gx[1] + ax[1]))
         out["roofline"] = {"bound": "mfma", "achieved": round(achieved, 3) if achieved else None,
                            "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                            "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4) if achieved else None,
                            "traffic": traffic,
                            "traffic_unit": "HBM bytes per GEMM launch",
-                           "traffic_source": "profiles/r1/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE "
-                                             "passes of this workload)" if traffic else None,
+                           "traffic_source": f"{os.path.relpath(PMC_TRAFFIC, ROOT)} (rocprofv3 --pmc FETCH_SIZE x2 + "
+                                             "WRITE_SIZE passes of this workload)" if traffic else None,
+                           "traffic_alg": traffic_alg,
+                           "traffic_alg_def": "algorithmic bytes per GEMM-family launch, measured in this run: every "
+                                              "operand touched once (A unique rows, B per distinct slice, C written, "
+                                              "epilogue operands), no tile re-reads or split-K partials",
+                           "traffic_ratio": round(traffic / traffic_alg, 3) if traffic and traffic_alg else None,
                            "kernel": "fp32 MFMA GEMM family: gemm_glds_kernel + gemm_f32_kernel + attn_fwd_kernel + attn_bwd_kernel + posconv_kernel (all launches)",
                            "launches": int(gn), "avg_launch_ms": round(gms / max(1, gn), 5),
                            "measured": f"HIP events around every GEMM-family launch on the engine stream, separate "
                                        f"pass of {tsteps} batch(es) after the timed region (eager path: "
                                        f"{round(1000 * timing_el / tsteps, 1)} ms per batch vs "
                                        f"{round(1000 * el / args.steps, 1)} ms replayed)"}
-        out["time_breakdown_ms"] = {k: round(v[0], 2) for k, v in timing.items()}
+        out["time_breakdown_ms"] = {k: round(v[0], 2) for k, v in timing_ex.items()}
+        # conv feature-encoder front-end (north_star: achieved HBM GB/s on the conv front-end)
+        if fx[1]:
+            fms = fx[0] / fx[1]
+            fb = frontend_traffic(d) if d else None
+            out["frontend"] = {"kernel": "conv0_gn_kernel passes (conv0 + GroupNorm + GELU, fwd and bwd) + finalisers",
+                               "calls": int(fx[1]), "avg_call_ms": round(fms, 4),
+                               "alg_bytes_per_call": round(fx[2] / fx[1]),
+                               "alg_tbs": round(fx[2] / fx[1] / (fms / 1000) / 1e12, 3),
+                               "hbm_bytes_per_call": round(fb) if fb else None,
+                               "peak_tbs": HBM_PEAK_TBS}
+            if fb:
+                out["frontend"]["hbm_tbs"] = round(fb / (fms / 1000) / 1e12, 3)
+                out["roofline"]["frontend_hbm_tbs"] = out["frontend"]["hbm_tbs"]
+        # attention products alone (fused kernels): algorithmic FLOPs / their time
+        if ax[1]:
+            T = num_frames(cfg, N)
+            af, ab = attention_flops(cfg, T, B)
+            layers = cfg["num_hidden_layers"]
+            nf, nb = (S + 1) * layers * tsteps, S * layers * tsteps
+            out["attention"] = {"launches": int(ax[1]), "ms": round(ax[0], 2),
+                                "tflops": round((nf * af + nb * ab) / (ax[0] / 1000) / 1e12, 3)}
     if args.also_split and args.precision == "fp32":
         # same workload with the fp32-accurate split-bf16 GEMMs (reported beside the headline)
         eng.set_precision("fp32-split-bf16")

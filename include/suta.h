@@ -167,6 +167,16 @@ void* suta_stream(suta_engine* e);
 int32_t suta_set_timing(suta_engine* e, int32_t enable);
 int32_t suta_get_timing(suta_engine* e, double* ms_out /*[6]*/, int64_t* launches_out /*[6]*/);
 
+/* The same counters over SUTA_TIMING_FAMILIES finer families (the first nfam are written): 0 = MFMA
+ * GEMMs and the positional-conv kernel, 1 = softmax-backward row term, 2 = norm, 3 = elementwise,
+ * 4 = loss, 5 = adam, 6 = conv feature-encoder front-end (conv0 + GroupNorm / conv0), 7 = fused
+ * attention kernels; alg_bytes_out (may be null) = algorithmic HBM bytes of the timed launches (each
+ * operand touched once; GEMM families only, 0 elsewhere).  (bench.py roofline; no reference
+ * counterpart: the reference has no kernel timing.) */
+#define SUTA_TIMING_FAMILIES 8
+int32_t suta_get_timing_ex(suta_engine* e, int32_t nfam, double* ms_out, int64_t* launches_out,
+                           double* alg_bytes_out);
+
 /* GEMM arithmetic.  The first two are fp32-accurate; results agree to fp32 rounding
  * (tests/test_gpu_parity.py):
  *   SUTA_PRECISION_FP32_MFMA        v_mfma_f32_32x32x2_f32: exact fp32 products, fp32 accumulation
@@ -185,8 +195,10 @@ int32_t suta_get_timing(suta_engine* e, double* ms_out /*[6]*/, int64_t* launche
 int32_t suta_set_precision(suta_engine* e, int32_t mode);
 
 /* Use hipGraph capture/replay for suta_adapt (default on): when a call repeats the previous call's
- * (batch, layout, precision, hparams), one SUTA step (backward + AdamW + forward) is captured once
- * and replayed for every step; per-kernel timing (suta_set_timing) disables it. */
+ * key (batch, layout, ragged, precision, hparams, steps, record set, requested outputs), the call's
+ * whole loop -- episodic slot reset, vanilla forward, steps x (backward + AdamW + forward), recorded
+ * logits and greedy ids into device staging -- is captured once as one graph and replayed per call;
+ * a call with a new key runs eagerly.  Per-kernel timing (suta_set_timing) disables it. */
 int32_t suta_set_graphs(suta_engine* e, int32_t enable);
 
 const char* suta_last_error(void);

@@ -76,7 +76,9 @@ struct TP {
     int feat_depth = 0;       // feature-branch module count containing it (train_feature)
 };
 
-enum Fam { F_GEMM = 0, F_SOFTMAX = 1, F_NORM = 2, F_EW = 3, F_LOSS = 4, F_ADAM = 5, NFAM = 6 };
+// kernel families of the per-launch timing (suta_get_timing_ex); the legacy 6-family view folds
+// F_ATTN into F_GEMM and F_FRONT into F_NORM
+enum Fam { F_GEMM = 0, F_SOFTMAX = 1, F_NORM = 2, F_EW = 3, F_LOSS = 4, F_ADAM = 5, F_FRONT = 6, F_ATTN = 7, NFAM = 8 };
 
 struct DevBuf {
     float* p = nullptr;
@@ -108,6 +110,35 @@ struct Arena {
         return r;
     }
 };
+
+// Algorithmic (compulsory) HBM bytes of one GEMM launch: every operand element touched once — A's unique
+// rows (overlapping strided conv rows and conv-A windows counted once), B once per distinct batch slice
+// (shared weights once), C written (read too when accumulating), and the epilogue's stored
+// pre-activation, residual and auxiliary operands.  Split-K partials and tile re-reads are not counted.
+double gemm_alg_bytes(const GemmParams& p) {
+    auto zeff = [&](long s0, long s1) -> double {
+        if (s0 == 0 && s1 == 0) return 1.0;
+        if (s0 == 0) return (double)((p.Z + p.zdiv - 1) / std::max(1, p.zdiv));
+        return (double)p.Z;
+    };
+    double a;
+    if (p.segK > 0) {
+        const long rows = std::min<long>((long)p.M + p.K / p.segK - 1, p.Mvalid > 0 ? p.Mvalid : p.M);
+        a = (double)rows * p.segK;
+    } else if (!p.ta) {
+        a = p.lda < p.K ? (double)(p.M - 1) * p.lda + p.K : (double)p.M * p.K;
+    } else {
+        a = p.lda < p.M ? (double)(p.K - 1) * p.lda + p.M : (double)p.M * p.K;
+    }
+    const double mn = (double)p.M * p.N;
+    double bytes = a * zeff(p.sA0, p.sA1) + (double)p.K * p.N * zeff(p.sB0, p.sB1);
+    double c = mn * ((p.epi & EPI_ACCUM) ? 2 : 1);
+    if (p.epi & EPI_STORE_PRE) c += mn;
+    if (p.epi & EPI_RESID) c += mn;
+    if (p.epi & (EPI_DGELU | EPI_SMBWD)) c += mn;
+    bytes += c * p.Z;
+    return 4.0 * bytes;
+}
 
 struct LayerBufs {
     float *x_in, *xhat1, *rstd1, *y1, *qkv, *P, *ctx, *hmid, *xhat2, *rstd2, *y2, *u, *x_out;
@@ -195,22 +226,28 @@ struct suta_engine {
     int* d_step = nullptr;
     int h_step = 0;
     std::vector<float> h_tab;
-    // one captured SUTA step (backward + Adam + forward) replayed per step of suta_adapt
+    // the whole S-step loop of one suta_adapt call (slot reset, forward, S x (backward + Adam + forward),
+    // recorded argmax ids and logits into device staging) captured as one graph per key
     struct GraphKey {
         int B = 0;
         long N = 0;
-        int ragged = 0, mode = 0;
+        int ragged = 0, mode = 0, steps = 0, want_logits = 0, want_ids = 0;
         suta_hparams hp{};
+        std::vector<int> rec;
     };
-    hipGraphExec_t step_graph = nullptr;
+    hipGraphExec_t loop_graph = nullptr;
     GraphKey gkey;
     bool gkey_seen = false;  // key of the previous suta_adapt call (its lazy allocations are done)
+    DevBuf recbuf;           // recorded logits [nrec][B*T*V] then ids [nrec][B*T]
     void prepare_adam(const suta_hparams& hp, int steps);
-    bool graph_key_repeats(int B, const suta_hparams& hp);
-    void suta_step_once(int B, const suta_hparams& hp, bool graph_ok);
+    bool graph_key_repeats(const GraphKey& k);
+    void adapt_loop(int B, const suta_hparams& hp, int steps, const int* rec, int nrec, float* rec_logits,
+                    int* rec_ids);
+    void run_adapt_loop(int B, const suta_hparams& hp, int steps, const int* rec, int nrec, float* rec_logits,
+                        int* rec_ids, bool graph_ok);
     void drop_graph() {
-        if (step_graph) (void)hipGraphExecDestroy(step_graph);
-        step_graph = nullptr;
+        if (loop_graph) (void)hipGraphExecDestroy(loop_graph);
+        loop_graph = nullptr;
         gkey_seen = false;
     }
     std::vector<float*> owned;
@@ -234,12 +271,14 @@ struct suta_engine {
         HIPCHK(hipEventCreate(&e));
         return e;
     }
+    double fam_bytes[NFAM] = {0};  // algorithmic HBM bytes of the timed launches (each operand touched once)
     template <typename Fn>
-    void timed(int fam, Fn&& fn) {
+    void timed(int fam, Fn&& fn, double alg_bytes = 0.0) {
         if (!timing) {
             fn();
             return;
         }
+        fam_bytes[fam] += alg_bytes;
         hipEvent_t a = ev(), b = ev();
         HIPCHK(hipEventRecord(a, st));
         fn();
@@ -261,7 +300,7 @@ struct suta_engine {
     void gemm(const GemmParams& p0) {
         GemmParams p = p0;
         p.mode = gemm_mode;
-        timed(F_GEMM, [&] { gemm_launch(p, st, plan.splitws, plan.splitws_floats); });
+        timed(F_GEMM, [&] { gemm_launch(p, st, plan.splitws, plan.splitws_floats); }, timing ? gemm_alg_bytes(p) : 0.0);
     }
 
     int multiplicity(const TP& t, int train_feature, int bias_only) const {
@@ -279,12 +318,12 @@ struct suta_engine {
     void forward(int B);
     void backward(int B, const suta_hparams& hp);
     void adam(int B, const suta_hparams& hp);
-    void reset_slots(int B);
+    void reset_slots(int B, bool zero_moments);
     void stage_input(const float* wav, int on_dev, int norm, int B, long N, long stride = 0);
 };
 
 suta_engine::~suta_engine() {
-    if (step_graph) (void)hipGraphExecDestroy(step_graph);
+    if (loop_graph) (void)hipGraphExecDestroy(loop_graph);
     if (d_adam_tab) (void)hipFree(d_adam_tab);
     for (float* p : owned) (void)hipFree(p);
     for (auto& pe : pending) {
@@ -438,16 +477,16 @@ void suta_engine::forward(int B) {
     const long BT = (long)B * T;
     if (!k.layer_mode) {
         // conv0 + GroupNorm + GELU, conv0 recomputed in each pass (never stored)
-        timed(F_NORM, [&] {
+        timed(F_FRONT, [&] {
             launch_front_gn_fwd(pl.x, pl.N, P + o_cw[0], k.conv_bias ? P + o_cb[0] : nullptr, Pn, B, pl.Lc[0], k.C[0],
                                 k.K[0], k.S[0], P + o_cg[0], P + o_cbeta[0], pl.gn_mean, pl.gn_rstd, pl.a[0],
                                 pl.dpart, rL0(), st);
-        });
+        }, 4.0 * B * ((double)pl.N + (double)pl.Lc[0] * k.C[0]));  // waveform read, activation written
     } else {
-        timed(F_EW, [&] {
+        timed(F_FRONT, [&] {
             launch_conv0(pl.x, pl.N, P + o_cw[0], k.conv_bias ? P + o_cb[0] : nullptr, Pn, pl.z[0], B, pl.Lc[0],
                          k.C[0], k.K[0], k.S[0], st);
-        });
+        }, 4.0 * B * ((double)pl.N + (double)pl.Lc[0] * k.C[0]));
         timed(F_NORM, [&] {
             launch_layernorm_fwd(pl.z[0], P + o_cg[0], P + o_cbeta[0], Pn, pl.Lc[0], pl.a[0], pl.cxhat[0],
                                  pl.crstd[0], B * pl.Lc[0], k.C[0], 1e-5f, 1, st);
@@ -601,7 +640,7 @@ void suta_engine::forward(int B) {
         // S -> softmax -> P -> ctx in one kernel (timed with the MFMA contractions) where its shape holds
         const bool fused = attn_fused && d == 64 && T <= 512;
         if (fused)
-            timed(F_GEMM, [&] {
+            timed(F_ATTN, [&] {
                 if (!launch_attn_fwd(lb.qkv, lb.P, lb.ctx, B, T, (int)pl.Tp, NH, H, d, scale, rT(),
                                      gemm_mode == SUTA_PRECISION_BF16, st))
                     throw SutaError(SUTA_ERR_UNSUPPORTED, "fused attention shape");
@@ -861,7 +900,7 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
         // softmax-backward epilogue, then the dQ GEMM)
         const bool fused_bwd = attn_fused && d == 64 && T <= 512;
         if (fused_bwd)
-            timed(F_GEMM, [&] {
+            timed(F_ATTN, [&] {
                 if (!launch_attn_bwd(lb.qkv, lb.P, pl.ctx, pl.delta, pl.dP, pl.dqkv, B, T, (int)pl.Tp, NH, H, d, scale,
                                      gemm_mode == SUTA_PRECISION_BF16, st))
                     throw SutaError(SUTA_ERR_UNSUPPORTED, "fused attention shape");
@@ -1163,11 +1202,11 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
     }
     // conv0: cur = da0
     if (!k.layer_mode) {
-        timed(F_NORM, [&] {
+        timed(F_FRONT, [&] {
             launch_front_gn_bwd(pl.x, pl.N, P + o_cw[0], k.conv_bias ? P + o_cb[0] : nullptr, Pn, B, pl.Lc[0], k.C[0],
                                 k.K[0], k.S[0], P + o_cg[0], P + o_cbeta[0], pl.gn_mean, pl.gn_rstd, cur, G + o_cg[0],
                                 G + o_cbeta[0], G + o_cw[0], Pn, pl.dpart, pl.c0part, rL0(), st);
-        });
+        }, 4.0 * B * ((double)pl.N + (double)pl.Lc[0] * k.C[0]));  // waveform and activation gradient read
         return;
     }
     timed(F_NORM, [&] {
@@ -1265,48 +1304,67 @@ void suta_engine::prepare_adam(const suta_hparams& hp, int steps) {
     HIPCHK(hipStreamSynchronize(st));  // pageable sources
 }
 
-// One SUTA step after a forward: backward, Adam, forward.  With graphs on, per-kernel timing off and
-// `graph_ok` (this call repeats the previous call's (batch, layout, ragged, precision, hparams) key),
-// the step is captured once and replayed; a one-off key runs eagerly (no capture cost).
-void suta_engine::suta_step_once(int B, const suta_hparams& hp, bool graph_ok) {
-    if (!use_graphs || timing || !graph_ok) {
-        backward(B, hp);
-        adam(B, hp);
+// The device work of one suta_adapt call after its input is staged: episodic slot reset (pristine
+// tensors broadcast into the slots; the moments are implicit zeros at Adam step 0), the vanilla forward,
+// then S x (backward, Adam, forward); at each recorded step the logits are copied and the greedy ids
+// computed into device staging.  Ordered on the engine stream only, so it captures as one graph.
+void suta_engine::adapt_loop(int B, const suta_hparams& hp, int steps, const int* rec, int nrec, float* rec_logits,
+                             int* rec_ids) {
+    const long rows = (long)B * plan.T;
+    if (hp.episodic) launch_broadcast(P, P0, Pn, B, st);
+    for (int s = 0; s <= steps; ++s) {
+        if (s > 0) {
+            backward(B, hp);
+            adam(B, hp);
+        }
         forward(B);
+        for (int i = 0; i < nrec; ++i) {
+            if (rec[i] != s) continue;
+            if (rec_logits)
+                HIPCHK(hipMemcpyAsync(rec_logits + i * rows * c.V, plan.logits, rows * c.V * sizeof(float),
+                                      hipMemcpyDeviceToDevice, st));
+            if (rec_ids) launch_argmax(plan.logits, rows, c.V, rec_ids + i * rows, st);
+        }
+    }
+}
+
+// With graphs on, per-kernel timing off and `graph_ok` (this call repeats the previous call's key: batch,
+// layout, ragged, precision, hparams, steps, record set, outputs), the whole loop is captured once and
+// replayed per call; a one-off key runs eagerly (no capture cost).  Replay == eager bitwise (GPU test).
+void suta_engine::run_adapt_loop(int B, const suta_hparams& hp, int steps, const int* rec, int nrec,
+                                 float* rec_logits, int* rec_ids, bool graph_ok) {
+    if (!use_graphs || timing || !graph_ok) {
+        adapt_loop(B, hp, steps, rec, nrec, rec_logits, rec_ids);
         return;
     }
-    if (!step_graph) {
+    if (!loop_graph) {
+        const long steps0 = opt_steps;
         hipGraph_t g = nullptr;
         HIPCHK(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
         try {
-            backward(B, hp);
-            adam(B, hp);
-            forward(B);
+            adapt_loop(B, hp, steps, rec, nrec, rec_logits, rec_ids);
         } catch (...) {
             (void)hipStreamEndCapture(st, &g);
             if (g) (void)hipGraphDestroy(g);
+            opt_steps = steps0;
             throw;
         }
         HIPCHK(hipStreamEndCapture(st, &g));
-        opt_steps -= 1;  // the capture recorded the Adam step without running it
-        HIPCHK(hipGraphInstantiate(&step_graph, g, nullptr, nullptr, 0));
+        opt_steps = steps0;  // the capture recorded the Adam steps without running them
+        HIPCHK(hipGraphInstantiate(&loop_graph, g, nullptr, nullptr, 0));
         HIPCHK(hipGraphDestroy(g));
     }
-    HIPCHK(hipGraphLaunch(step_graph, st));
-    opt_steps += 1;
-    if (hp.pl_coef > 0.f) sdpl_used = true;  // the replayed SDPL kernels may raise the error flag
+    HIPCHK(hipGraphLaunch(loop_graph, st));
+    opt_steps += steps;
+    if (hp.pl_coef > 0.f && steps > 0) sdpl_used = true;  // the replayed SDPL kernels may raise the error flag
 }
 
 // Key of this call; true when it equals the previous call's (graph capture pays off from the 2nd call)
-bool suta_engine::graph_key_repeats(int B, const suta_hparams& hp) {
-    GraphKey k;
-    k.B = B;
-    k.N = plan.N;
-    k.ragged = plan.ragged;
-    k.mode = gemm_mode;
-    k.hp = hp;
+bool suta_engine::graph_key_repeats(const GraphKey& k) {
     const bool same = gkey_seen && gkey.B == k.B && gkey.N == k.N && gkey.ragged == k.ragged &&
-                      gkey.mode == k.mode && std::memcmp(&gkey.hp, &k.hp, sizeof(suta_hparams)) == 0;
+                      gkey.mode == k.mode && gkey.steps == k.steps && gkey.want_logits == k.want_logits &&
+                      gkey.want_ids == k.want_ids && gkey.rec == k.rec &&
+                      std::memcmp(&gkey.hp, &k.hp, sizeof(suta_hparams)) == 0;
     if (!same) {
         drop_graph();
         gkey = k;
@@ -1315,11 +1373,14 @@ bool suta_engine::graph_key_repeats(int B, const suta_hparams& hp) {
     return same;
 }
 
-void suta_engine::reset_slots(int B) {
-    for (int b = 0; b < B; ++b)
-        HIPCHK(hipMemcpyAsync(P + (long)b * Pn, P0, Pn * sizeof(float), hipMemcpyDeviceToDevice, st));
-    HIPCHK(hipMemsetAsync(Mo, 0, (size_t)B * Pn * sizeof(float), st));
-    HIPCHK(hipMemsetAsync(Vo, 0, (size_t)B * Pn * sizeof(float), st));
+// Pristine tensors into slots [0, B) and the Adam step counter to 0.  The moments need no clearing: the
+// Adam kernel takes them as zero at step 0 (zero_moments only keeps unused slots deterministic).
+void suta_engine::reset_slots(int B, bool zero_moments) {
+    launch_broadcast(P, P0, Pn, B, st);
+    if (zero_moments) {
+        HIPCHK(hipMemsetAsync(Mo, 0, (size_t)B * Pn * sizeof(float), st));
+        HIPCHK(hipMemsetAsync(Vo, 0, (size_t)B * Pn * sizeof(float), st));
+    }
     opt_steps = 0;
     h_step = 0;
     HIPCHK(hipMemcpyAsync(d_step, &h_step, sizeof(int), hipMemcpyHostToDevice, st));
@@ -1564,7 +1625,7 @@ int32_t suta_create(const suta_model_config* cfg, const char* const* names, cons
             HIPCHK(hipMemcpy(e->wpos_b, wb.data(), wb.size() * 4, hipMemcpyHostToDevice));
             e->bpos = up(b + "bias", H);
         }
-        e->reset_slots(max_batch);
+        e->reset_slots(max_batch, true);
         HIPCHK(hipStreamSynchronize(e->st));
         *out = e.release();
     });
@@ -1580,7 +1641,7 @@ int32_t suta_destroy(suta_engine* e) {
 
 int32_t suta_reset(suta_engine* e) {
     return guard([&] {
-        e->reset_slots(e->max_batch);
+        e->reset_slots(e->max_batch, true);
         HIPCHK(hipStreamSynchronize(e->st));
     });
 }
@@ -1652,24 +1713,29 @@ static void adapt_impl(suta_engine* e, const float* wav, int32_t on_dev, int32_t
     }
     const size_t per = (size_t)batch * T * V;
     e->stage_input(wav, on_dev, norm, batch, n, stride);
-    if (hp->episodic) e->reset_slots(batch);
+    if (hp->episodic) e->opt_steps = 0;  // slots are reset inside the loop (adapt_loop)
     e->prepare_adam(*hp, steps);
-    const bool graph_ok = e->graph_key_repeats(batch, *hp);
-    for (int s = 0; s <= steps; ++s) {
-        if (s == 0) e->forward(batch);
-        else e->suta_step_once(batch, *hp, graph_ok);
-        for (int i = 0; i < nrec; ++i) {
-            if (rec[i] != s) continue;
-            if (logits_out)
-                HIPCHK(hipMemcpyAsync(logits_out + i * per, e->plan.logits, per * 4,
-                                      logits_on_dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, e->st));
-            if (ids_out) {
-                launch_argmax(e->plan.logits, (long)batch * T, V, e->plan.ids, e->st);
-                HIPCHK(hipMemcpyAsync(ids_out + (size_t)i * batch * T, e->plan.ids, (size_t)batch * T * 4,
-                                      hipMemcpyDeviceToHost, e->st));
-            }
-        }
-    }
+    // device staging of the recorded outputs (the loop is graph-captured; it never touches host memory)
+    const size_t rl = logits_out ? (size_t)nrec * per : 0, ri = ids_out ? (size_t)nrec * batch * T : 0;
+    if (e->recbuf.alloc((rl + ri) * sizeof(float) + 256)) e->drop_graph();
+    float* rec_logits = logits_out ? e->recbuf.p : nullptr;
+    int* rec_ids = ids_out ? reinterpret_cast<int*>(e->recbuf.p + rl) : nullptr;
+    suta_engine::GraphKey key;
+    key.B = batch;
+    key.N = e->plan.N;
+    key.ragged = e->plan.ragged;
+    key.mode = e->gemm_mode;
+    key.steps = steps;
+    key.want_logits = logits_out != nullptr;
+    key.want_ids = ids_out != nullptr;
+    key.hp = *hp;
+    key.rec.assign(rec, rec + nrec);
+    const bool graph_ok = e->graph_key_repeats(key);
+    e->run_adapt_loop(batch, *hp, steps, rec, nrec, rec_logits, rec_ids, graph_ok);
+    if (logits_out && nrec)
+        HIPCHK(hipMemcpyAsync(logits_out, rec_logits, rl * 4, logits_on_dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost,
+                              e->st));
+    if (ids_out && nrec) HIPCHK(hipMemcpyAsync(ids_out, rec_ids, ri * 4, hipMemcpyDeviceToHost, e->st));
     HIPCHK(hipStreamSynchronize(e->st));
     if (e->timing) e->collect_timing();
     e->check_sdpl();
@@ -1784,6 +1850,7 @@ int32_t suta_set_timing(suta_engine* e, int32_t enable) {
         for (int i = 0; i < NFAM; ++i) {
             e->fam_ms[i] = 0;
             e->fam_n[i] = 0;
+            e->fam_bytes[i] = 0;
         }
     });
 }
@@ -1791,9 +1858,25 @@ int32_t suta_set_timing(suta_engine* e, int32_t enable) {
 int32_t suta_get_timing(suta_engine* e, double* ms, int64_t* n) {
     return guard([&] {
         e->collect_timing();
-        for (int i = 0; i < NFAM; ++i) {
+        for (int i = 0; i < 6; ++i) {
             ms[i] = e->fam_ms[i];
             n[i] = e->fam_n[i];
+        }
+        ms[F_GEMM] += e->fam_ms[F_ATTN];
+        n[F_GEMM] += e->fam_n[F_ATTN];
+        ms[F_NORM] += e->fam_ms[F_FRONT];
+        n[F_NORM] += e->fam_n[F_FRONT];
+    });
+}
+
+int32_t suta_get_timing_ex(suta_engine* e, int32_t nfam, double* ms, int64_t* n, double* alg_bytes) {
+    return guard([&] {
+        if (nfam < 1 || nfam > NFAM) throw SutaError(SUTA_ERR_ARG, "nfam outside [1, SUTA_TIMING_FAMILIES]");
+        e->collect_timing();
+        for (int i = 0; i < nfam; ++i) {
+            ms[i] = e->fam_ms[i];
+            n[i] = e->fam_n[i];
+            if (alg_bytes) alg_bytes[i] = e->fam_bytes[i];
         }
     });
 }

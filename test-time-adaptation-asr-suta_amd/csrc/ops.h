@@ -93,15 +93,19 @@ struct AdamRun {
 struct AdamArgs {
     int nruns;
     AdamRun runs[SUTA_MAX_RUNS];
+    int blk0[SUTA_MAX_RUNS];  // first block of each run (filled by launch_adam)
     float beta1, beta2, omb1, omb2, eps, lr_wd;  // omb = (1 - beta) rounded from double; lr_wd = lr * wd
     // per sub-step j (1-based t = step0*k + j): step_size and sqrt(bias_correction2), indexed [k-1][j-1]
     float step_size[5][5];
     float bc2_sqrt[5][5];
     // device-resident alternative (graph-replayable): tab[step0][0|1][k-1][j-1] = step_size | bc2_sqrt,
-    // step0 read from *step (advanced by launch_step_advance); used when tab != null
+    // step0 read from *step (advanced by launch_step_advance); used when tab != null.  At *step == 0 the
+    // moments are taken as zero (not read): every reset of the slots sets the step counter to 0
     const float* tab;
     const int* step;
 };
+// dst[b][0:n] = src[0:n] for b in [0, B) (n a multiple of 4, 16-B aligned): the episodic slot reset.
+void launch_broadcast(float* dst, const float* src, long n, int B, hipStream_t st);
 // *step += 1 (one thread): the Adam step counter of graph-replayed SUTA steps.
 void launch_step_advance(int* step, hipStream_t st);
 void launch_adam(float* P, const float* G, float* M, float* V, long pstride, int B, const AdamArgs& a,

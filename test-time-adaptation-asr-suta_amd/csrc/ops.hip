@@ -1310,50 +1310,97 @@ __global__ __launch_bounds__(256) void argmax_kernel(const float* __restrict__ l
 // ------------------------------------------------------------------------------------------
 // AdamW (torch single-tensor path, decoupled wd) with k sub-steps per element
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ P, const float* __restrict__ G,
-                                                   float* __restrict__ M, float* __restrict__ Vv, long pstride,
-                                                   AdamArgs a, long total4) {
-    // one thread per 16-B group of a run (run starts are 4-float aligned; elements past a run's end
-    // inside its last group are loaded and stored back unchanged)
-    const int b = blockIdx.y;
-    const long base = (long)b * pstride;
-    const float* tab = a.tab ? a.tab + (long)(*a.step) * 50 : nullptr;
-    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total4; i += (long)gridDim.x * 256) {
-        long rem = i;
-        int run = 0;
-        while (run < a.nruns && rem >= (a.runs[run].len + 3) / 4) {
-            rem -= (a.runs[run].len + 3) / 4;
-            ++run;
+// One block = ADAM_GPT x 256 consecutive 16-B groups of ONE run (block -> run from the host's
+// cumulative block table, a uniform scalar search), so the multiplicity K is a template constant and
+// the K sub-steps unroll with their step sizes in scalar registers.  Every load of a thread is issued
+// before its first update.  Run starts are 4-float aligned; elements past a run's end inside its last
+// group are loaded and stored back unchanged.  At device step 0 the moments are zero by definition
+// (every reset sets the step counter to 0), so they are not read: the episodic reset needs no memset.
+constexpr int ADAM_GPT = 2;
+
+template <int K>
+__device__ __forceinline__ void adam_body(float* __restrict__ P, const float* __restrict__ G, float* __restrict__ M,
+                                          float* __restrict__ Vv, long base, long g0, long ngroups, long len,
+                                          const AdamArgs& a, const float* __restrict__ tab, bool first) {
+    float ss[K], bs[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        ss[j] = tab ? tab[(K - 1) * 5 + j] : a.step_size[K - 1][j];
+        bs[j] = tab ? tab[25 + (K - 1) * 5 + j] : a.bc2_sqrt[K - 1][j];
+    }
+    f32x4 g4[ADAM_GPT], p4[ADAM_GPT], m4[ADAM_GPT], v4[ADAM_GPT];
+    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < ADAM_GPT; ++u) {
+        const long gi = g0 + u * 256;
+        m4[u] = v4[u] = g4[u] = p4[u] = z;
+        if (gi < ngroups) {
+            const long idx = base + 4 * gi;
+            g4[u] = *reinterpret_cast<const f32x4*>(G + idx);
+            p4[u] = *reinterpret_cast<const f32x4*>(P + idx);
+            if (!first) {
+                m4[u] = *reinterpret_cast<const f32x4*>(M + idx);
+                v4[u] = *reinterpret_cast<const f32x4*>(Vv + idx);
+            }
         }
-        if (run >= a.nruns) continue;
-        const long idx = base + a.runs[run].start + 4 * rem;
-        const int nv = (int)min(4L, a.runs[run].len - 4 * rem);
-        const int k = a.runs[run].k;
-        const f32x4 g4 = *reinterpret_cast<const f32x4*>(G + idx);
-        f32x4 p4 = *reinterpret_cast<const f32x4*>(P + idx);
-        f32x4 m4 = *reinterpret_cast<const f32x4*>(M + idx);
-        f32x4 v4 = *reinterpret_cast<const f32x4*>(Vv + idx);
+    }
+#pragma unroll
+    for (int u = 0; u < ADAM_GPT; ++u) {
+        const long gi = g0 + u * 256;
+        if (gi >= ngroups) continue;
+        const int nv = (int)min(4L, len - 4 * gi);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             if (e >= nv) break;
-            const float g = g4[e];
-            float p = p4[e], m = m4[e], v = v4[e];
-            for (int j = 0; j < k; ++j) {
+            const float g = g4[u][e];
+            float p = p4[u][e], m = m4[u][e], v = v4[u][e];
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
                 if (a.lr_wd != 0.f) p *= 1.0f - a.lr_wd;
                 m = m + a.omb1 * (g - m);                 // lerp_(g, 1-beta1), weight < 0.5 form
                 v = v * a.beta2 + a.omb2 * (g * g);        // mul_(beta2).addcmul_(g, g, 1-beta2)
-                const float ss = tab ? tab[(k - 1) * 5 + j] : a.step_size[k - 1][j];
-                const float bs = tab ? tab[25 + (k - 1) * 5 + j] : a.bc2_sqrt[k - 1][j];
-                const float denom = sqrtf(v) / bs + a.eps;
-                p = p + (-ss) * (m / denom);                  // addcdiv_(m, denom, -step_size)
+                const float denom = sqrtf(v) / bs[j] + a.eps;
+                p = p + (-ss[j]) * (m / denom);           // addcdiv_(m, denom, -step_size)
             }
-            p4[e] = p;
-            m4[e] = m;
-            v4[e] = v;
+            p4[u][e] = p;
+            m4[u][e] = m;
+            v4[u][e] = v;
         }
-        *reinterpret_cast<f32x4*>(P + idx) = p4;
-        *reinterpret_cast<f32x4*>(M + idx) = m4;
-        *reinterpret_cast<f32x4*>(Vv + idx) = v4;
+        const long idx = base + 4 * gi;
+        *reinterpret_cast<f32x4*>(P + idx) = p4[u];
+        *reinterpret_cast<f32x4*>(M + idx) = m4[u];
+        *reinterpret_cast<f32x4*>(Vv + idx) = v4[u];
+    }
+}
+
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ P, const float* __restrict__ G,
+                                                   float* __restrict__ M, float* __restrict__ Vv, long pstride,
+                                                   AdamArgs a) {
+    const int bx = blockIdx.x;
+    // this block's run: an unrolled uniform select (constant indices keep the kernel arguments in scalar
+    // registers; a dynamic index would copy the argument block to scratch per thread)
+    long start = 0, len = 0;
+    int k = 1, blk = 0;
+#pragma unroll
+    for (int r = 0; r < SUTA_MAX_RUNS; ++r)
+        if (r < a.nruns && bx >= a.blk0[r]) {
+            start = a.runs[r].start;
+            len = a.runs[r].len;
+            k = a.runs[r].k;
+            blk = a.blk0[r];
+        }
+    const long ngroups = (len + 3) / 4;
+    const long g0 = (long)(bx - blk) * (256 * ADAM_GPT) + threadIdx.x;
+    const long base = (long)blockIdx.y * pstride + start;
+    const int step = a.step ? *a.step : 1;
+    const float* tab = a.tab ? a.tab + (long)step * 50 : nullptr;
+    const bool first = a.step && step == 0;
+    switch (k) {
+        case 1: adam_body<1>(P, G, M, Vv, base, g0, ngroups, len, a, tab, first); break;
+        case 2: adam_body<2>(P, G, M, Vv, base, g0, ngroups, len, a, tab, first); break;
+        case 3: adam_body<3>(P, G, M, Vv, base, g0, ngroups, len, a, tab, first); break;
+        case 4: adam_body<4>(P, G, M, Vv, base, g0, ngroups, len, a, tab, first); break;
+        default: adam_body<5>(P, G, M, Vv, base, g0, ngroups, len, a, tab, first); break;
     }
 }
 
@@ -1572,6 +1619,19 @@ void launch_argmax(const float* logits, long rows, int V, int* ids, hipStream_t 
     hipLaunchKernelGGL(argmax_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, st, logits, rows, V, ids);
 }
 
+__global__ __launch_bounds__(256) void broadcast_kernel(f32x4* __restrict__ dst, const f32x4* __restrict__ src,
+                                                        long n4) {
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    if (i < n4) dst[(long)blockIdx.y * n4 + i] = src[i];
+}
+
+void launch_broadcast(float* dst, const float* src, long n, int B, hipStream_t st) {
+    if (n % 4) throw std::runtime_error("broadcast length not a multiple of 4");
+    const long n4 = n / 4;
+    hipLaunchKernelGGL(broadcast_kernel, dim3((unsigned)((n4 + 255) / 256), B), dim3(256), 0, st,
+                       reinterpret_cast<f32x4*>(dst), reinterpret_cast<const f32x4*>(src), n4);
+}
+
 __global__ void step_advance_kernel(int* step) { *step += 1; }
 
 void launch_step_advance(int* step, hipStream_t st) {
@@ -1580,15 +1640,17 @@ void launch_step_advance(int* step, hipStream_t st) {
 
 void launch_adam(float* P, const float* G, float* M, float* V, long pstride, int B, const AdamArgs& a,
                  hipStream_t st) {
-    long total4 = 0;
+    AdamArgs aa = a;
+    long nblk = 0;
     for (int r = 0; r < a.nruns; ++r) {
         if (a.runs[r].start % 4) throw std::runtime_error("adam run start not 16-B aligned");
-        total4 += (a.runs[r].len + 3) / 4;
+        if (a.runs[r].k < 1 || a.runs[r].k > 5) throw std::runtime_error("adam multiplicity outside [1, 5]");
+        aa.blk0[r] = (int)nblk;
+        nblk += ((a.runs[r].len + 3) / 4 + 256 * ADAM_GPT - 1) / (256 * ADAM_GPT);
     }
-    if (total4 == 0) return;
+    if (nblk == 0) return;
     if (pstride % 4) throw std::runtime_error("adam slot stride not a multiple of 4");
-    const int gx = (int)std::min<long>(std::max<long>(1, 4096 / std::max(1, B)), (total4 + 255) / 256);
-    hipLaunchKernelGGL(adam_kernel, dim3(gx, B), dim3(256), 0, st, P, G, M, V, pstride, a, total4);
+    hipLaunchKernelGGL(adam_kernel, dim3((unsigned)nblk, B), dim3(256), 0, st, P, G, M, V, pstride, aa);
 }
 
 template <int MODE, typename... Args>

@@ -20,7 +20,7 @@ MAX_CONV = 8
 # exported symbols (kept in sync with include/suta.h; tests/test_abi.py checks both)
 EXPORTS = ("suta_create", "suta_destroy", "suta_reset", "suta_num_frames", "suta_forward", "suta_step",
            "suta_adapt", "suta_adapt_varlen", "suta_loss_grad", "suta_get_param", "suta_param_info", "suta_sync", "suta_stream", "suta_set_timing",
-           "suta_get_timing", "suta_set_precision", "suta_set_graphs", "suta_last_error")
+           "suta_get_timing", "suta_get_timing_ex", "suta_set_precision", "suta_set_graphs", "suta_last_error")
 
 
 class ModelConfigC(C.Structure):
@@ -99,6 +99,8 @@ def load_library(path: str = LIB_PATH):
                                           C.c_void_p, i64p]
     lib.suta_set_timing.argtypes = [C.c_void_p, C.c_int32]
     lib.suta_get_timing.argtypes = [C.c_void_p, P(C.c_double), i64p]
+    if hasattr(lib, "suta_get_timing_ex"):
+        lib.suta_get_timing_ex.argtypes = [C.c_void_p, C.c_int32, P(C.c_double), i64p, P(C.c_double)]
     lib.suta_set_graphs.argtypes = [C.c_void_p, C.c_int32]
     lib.suta_set_precision.argtypes = [C.c_void_p, C.c_int32]
     lib.suta_last_error.restype = C.c_char_p
@@ -307,6 +309,16 @@ class SutaEngine:
         _check(self.lib.suta_get_timing(self.handle, ms, n))
         fams = ("gemm", "softmax", "norm", "elementwise", "loss", "adam")
         return {f: (ms[i], n[i]) for i, f in enumerate(fams)}
+
+    TIMING_FAMILIES = ("gemm", "softmax", "norm", "elementwise", "loss", "adam", "frontend", "attention")
+
+    def get_timing_ex(self):
+        """Finer families (suta_get_timing_ex): {family: (ms, launches, algorithmic HBM bytes)};
+        'gemm' here excludes the fused attention kernels ('attention') and 'norm' the conv front-end."""
+        k = len(self.TIMING_FAMILIES)
+        ms, n, by = (C.c_double * k)(), (C.c_int64 * k)(), (C.c_double * k)()
+        _check(self.lib.suta_get_timing_ex(self.handle, k, ms, n, by))
+        return {f: (ms[i], n[i], by[i]) for i, f in enumerate(self.TIMING_FAMILIES)}
 
     PRECISIONS = {"fp32": 0, "fp32-split-bf16": 1, "bf16": 2}
 

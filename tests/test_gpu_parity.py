@@ -204,17 +204,30 @@ def test_bitwise_deterministic(precision):
 
 @pytest.mark.parametrize("preset,n", [("tiny-group", 11000), ("wav2vec2-base", 32000)])
 def test_graph_replay_equals_eager(preset, n):
-    """suta_adapt replays one captured SUTA step (backward + Adam + forward) per step: bitwise == eager."""
+    """suta_adapt captures its whole loop (slot reset, vanilla forward, S x (backward + Adam + forward),
+    recorded logits and greedy ids) as one graph and replays it: bitwise == eager, incl. final tensors."""
     eng, cfg = engine(preset)
     x = synth.batch(n, 2, start=90)
     hp = SutaHParams(lr=5e-4)
+    names = eng.trainable_names()
     eng.set_graphs(False)
-    a, _, _ = eng.adapt(x, 4, hp, record=[1, 2, 4])
+    a, ia, _ = eng.adapt(x, 4, hp, record=[1, 2, 4])
+    pa = [{k: eng.get_param(b, k) for k in names} for b in range(2)]
     eng.set_graphs(True)
-    b, _, _ = eng.adapt(x, 4, hp, record=[1, 2, 4])   # step 1 eager (new key), step 2 captured, 3-4 replayed
-    c, _, _ = eng.adapt(x, 4, hp, record=[1, 2, 4])   # every step replayed
+    b, ib, _ = eng.adapt(x, 4, hp, record=[1, 2, 4])   # same key as the eager call: captured, then launched
+    c, ic, _ = eng.adapt(x, 4, hp, record=[1, 2, 4])   # replayed
+    pc = [{k: eng.get_param(u, k) for k in names} for u in range(2)]
     for r in (1, 2, 4):
         assert np.array_equal(a[r], b[r]) and np.array_equal(a[r], c[r]), r
+        assert np.array_equal(ia[r], ib[r]) and np.array_equal(ia[r], ic[r]), r
+    for u in range(2):
+        for k in names:
+            assert np.array_equal(pa[u][k], pc[u][k]), (u, k)
+    # a different record set is a different key: eager first, then its own graph
+    d, _, _ = eng.adapt(x, 4, hp, record=[0, 3])
+    e2, _, _ = eng.adapt(x, 4, hp, record=[0, 3])
+    for r in (0, 3):
+        assert np.array_equal(d[r], e2[r]), r
 
 
 def test_episodic_reset_restores_pristine_tensors():
