@@ -131,7 +131,7 @@ def bench_c4(args, dev):
         gms, gn = t["gemm"]
         ach = flops_utt * B / (gms / 1000.0) / 1e12
         res["roofline"] = {"bound": "mfma", "achieved": round(ach, 3), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                           "frac": round(ach / BF16_PEAK_TFLOPS, 4), "kernel": "bf16 GEMM family (gemm_x6_kernel one-plane form + gemm_gbf_kernel for weight gradients + attn_fwd_kernel / attn_bwd_kernel on bf16 MFMA)",
+                           "frac": round(ach / BF16_PEAK_TFLOPS, 4), "kernel": "bf16 GEMM family (gemm_x6_kernel one-plane form + gemm_gbf_kernel for weight gradients + flash attention kernels on bf16 MFMA)",
                            "launches": int(gn), "avg_launch_ms": round(gms / max(1, gn), 5)}
         res["time_breakdown_ms"] = {k: round(v[0], 2) for k, v in t.items()}
     eng.close()
@@ -263,7 +263,7 @@ def main():
                                               "operand touched once (A unique rows, B per distinct slice, C written, "
                                               "epilogue operands), no tile re-reads or split-K partials",
                            "traffic_ratio": round(traffic / traffic_alg, 3) if traffic and traffic_alg else None,
-                           "kernel": "fp32 MFMA GEMM family: gemm_glds_kernel + gemm_f32_kernel + attn_fwd_kernel + attn_bwd_kernel + posconv_kernel (all launches)",
+                           "kernel": "fp32 MFMA GEMM family: gemm_glds_kernel + gemm_f32_kernel + posconv_kernel + flash attention (flash_fwd_kernel, flash_bwd_kernel + flash_dq_reduce) (all launches)",
                            "launches": int(gn), "avg_launch_ms": round(gms / max(1, gn), 5),
                            "measured": f"HIP events around every GEMM-family launch on the engine stream, separate "
                                        f"pass of {tsteps} batch(es) after the timed region (eager path: "

@@ -1,0 +1,541 @@
+// Flash-style fused attention for head dim 64 and any T (reference: the HF Wav2Vec2Attention the
+// SUTA loop runs, modeling_wav2vec2.py Wav2Vec2Attention.forward: softmax(q k^T * d^-1/2) v, and its
+// autograd backward).  No T x T matrix is stored: the forward keeps the per-row log-sum-exp, the
+// backward recomputes the probabilities from it.
+//
+//   flash_fwd_kernel  block = NW waves of one (utterance, head); wave = 32 queries.  Key tiles of 32
+//                     stream through LDS (double-buffered, one barrier per tile): K row-major, V
+//                     transposed.  S^T = K Q^T (key in the accumulator rows, query on the lane), online
+//                     softmax in registers, O^T += V^T P^T with the lane's own probabilities as the B
+//                     operand (no LDS round trip for P); the rescale is lane-local because the query
+//                     is the lane.  Writes ctx and LSE[q] = max + log(sum).
+//   flash_bwd_kernel  block = NW waves = a block of key groups of one (utterance, head); wave = 32
+//                     keys whose K and V rows stay in registers.  Query tiles of 32 stream through
+//                     LDS (Q, dO, LSE, delta; double-buffered).  S = Q K^T and dP = dO V^T (key on the
+//                     lane), P = exp(scale S - LSE), dS = scale P (dP - delta); dV^T += dO^T P and
+//                     dK^T += Q^T dS accumulate in registers over all query tiles (written once, no
+//                     cross-block sum).  dS crosses LDS once: the block's dQ partial over its keys,
+//                     dQ_kb = dS K, is written to scratch per key block.
+//   flash_dq_reduce   dQ = sum over key blocks in fixed order -> dqkv's Q columns (bitwise
+//                     deterministic: no float atomics).
+//
+// Contractions: exact fp32 v_mfma_f32_32x32x2_f32 (and 16x16x4 for dQ), or in bf16 mode (config C4)
+// the operands rounded to bf16 (RNE) on v_mfma_f32_32x32x16_bf16 / 16x16x32 with fp32 accumulation;
+// softmax, LSE, delta and every stored value are fp32.
+// Ragged batches: keys >= the utterance's length get probability 0; query tiles past it are skipped in
+// the backward (their dO rows are exactly 0, so they contribute nothing).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <stdexcept>
+
+#include "common.h"
+#include "ops.h"
+
+namespace {
+
+typedef __bf16 fbf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int FA_LD = 68;   // [row][64] tiles: 16-B rows padded by 4 floats (conflict-free row reads)
+constexpr int FA_LDT = 36;  // [64][32] transposed tiles
+
+__device__ __forceinline__ fbf16x8 cvt8(f32x4 lo, f32x4 hi) {
+    fbf16x8 v;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        v[j] = (__bf16)lo[j];
+        v[4 + j] = (__bf16)hi[j];
+    }
+    return v;
+}
+
+// accumulator register v of a 32x32 MFMA tile holds row r8(v, h) of column (lane & 31)
+__device__ __forceinline__ int r8(int v, int h) { return 8 * (v >> 2) + 4 * h + (v & 3); }
+
+// 1-D XCD-aware renumbering (cdna_hip_programming.md T1, bijective): consecutive logical blocks (the
+// query or key blocks of one head) run on one XCD and share its L2.
+__device__ __forceinline__ int xcd_block() {
+    const int nwg = gridDim.x, orig = blockIdx.x;
+    const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
+// The lane's 64-wide register row (the B operand of prod_rows): fp32 X[row][32h + 4m + e], m < 8;
+// bf16 X[row][16s + 8h + j], s < 4.
+template <bool BF16>
+struct RowReg;
+template <>
+struct RowReg<false> {
+    f32x4 v[8];
+    __device__ __forceinline__ void load(const float* __restrict__ row, int h) {
+#pragma unroll
+        for (int m = 0; m < 8; ++m) v[m] = *reinterpret_cast<const f32x4*>(row + 32 * h + 4 * m);
+    }
+};
+template <>
+struct RowReg<true> {
+    fbf16x8 v[4];
+    __device__ __forceinline__ void load(const float* __restrict__ row, int h) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+            v[s] = cvt8(*reinterpret_cast<const f32x4*>(row + 16 * s + 8 * h),
+                        *reinterpret_cast<const f32x4*>(row + 16 * s + 8 * h + 4));
+    }
+};
+
+// acc[r8(v,h)][l32] += sum_d L[r8-row i = l32 of the A operand][d] * X[l32][d]:
+//   C[i][j] = sum_d L[i][d] X[j][d], L = 32 LDS rows of stride FA_LD (row i read by lane i), X the
+//   lane's register row.  Output: row i in the accumulator registers, column j on the lane.
+template <bool BF16>
+__device__ __forceinline__ void prod_rows(f32x16& acc, const float* __restrict__ L, const RowReg<BF16>& x, int l32,
+                                          int h) {
+    const float* lr = L + l32 * FA_LD;
+    if constexpr (!BF16) {
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            const f32x4 a = *reinterpret_cast<const f32x4*>(lr + 32 * h + 4 * m);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[e], x.v[m][e], acc, 0, 0, 0);
+        }
+    } else {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const fbf16x8 a = cvt8(*reinterpret_cast<const f32x4*>(lr + 16 * s + 8 * h),
+                                   *reinterpret_cast<const f32x4*>(lr + 16 * s + 8 * h + 4));
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, x.v[s], acc, 0, 0, 0);
+        }
+    }
+}
+
+// o[t][n = 32t + r8(v,h)][l32] += sum_r L[r][32t + n'] pv_r, the contraction index r being the
+// accumulator row of pv (pv[v] holds row r8(v,h) of column l32): A operand = L rows read by column
+// (L row-major [r][FA_LD], one float per lane), B operand = the lane's own pv registers.
+template <bool BF16>
+__device__ __forceinline__ void apply_rows(f32x16 (&o)[2], const float* __restrict__ L, const f32x16& pv, int l32,
+                                           int h) {
+    if constexpr (!BF16) {
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+            const float* lr = L + r8(v, h) * FA_LD + l32;
+            const float a0 = lr[0], a1 = lr[32];
+            o[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, pv[v], o[0], 0, 0, 0);
+            o[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, pv[v], o[1], 0, 0, 0);
+        }
+    } else {
+        // MFMA c takes k-slot 8h + j <-> accumulator register v = 8c + j (row r8(8c + j, h))
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            fbf16x8 b;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) b[j] = (__bf16)pv[8 * c + j];
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                fbf16x8 a;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) a[j] = (__bf16)L[r8(8 * c + j, h) * FA_LD + 32 * t + l32];
+                o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, o[t], 0, 0, 0);
+            }
+        }
+    }
+}
+
+// Same contraction with L stored transposed (Lt[n][LDT], n the output row; contraction rows from
+// column c0): 16-B reads of four consecutive contraction rows r8(4a + 0..3, h) = 8a + 4h + 0..3.
+template <bool BF16, int LDT>
+__device__ __forceinline__ void apply_cols(f32x16 (&o)[2], const float* __restrict__ Lt, const f32x16& pv, int l32,
+                                           int h) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const float* lr = Lt + (32 * t + l32) * LDT + 4 * h;
+        if constexpr (!BF16) {
+#pragma unroll
+            for (int a = 0; a < 4; ++a) {
+                const f32x4 x = *reinterpret_cast<const f32x4*>(lr + 8 * a);
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    o[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(x[b], pv[4 * a + b], o[t], 0, 0, 0);
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                fbf16x8 b;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) b[j] = (__bf16)pv[8 * c + j];
+                const fbf16x8 a = cvt8(*reinterpret_cast<const f32x4*>(lr + 16 * c),
+                                       *reinterpret_cast<const f32x4*>(lr + 16 * c + 8));
+                o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, o[t], 0, 0, 0);
+            }
+        }
+    }
+}
+
+constexpr float LOG2E = 1.4426950408889634f;
+
+// ------------------------------------------------------------------------------------------------
+// forward: key tiles of FK = 64 (two 32-key sub-tiles: two independent S^T chains, one softmax
+// update, one O rescale and one barrier per 64 keys).  Probabilities via v_exp_f32 on log2-domain
+// scores (scale * log2 e folded into one multiply).
+// ------------------------------------------------------------------------------------------------
+constexpr int FK = 64;
+constexpr int FK_LDT = FK + 4;  // transposed V tile row stride
+
+template <int NW, bool BF16>
+__global__ __launch_bounds__(NW * 64) void flash_fwd_kernel(const float* __restrict__ qkv, float* __restrict__ ctx,
+                                                            float* __restrict__ lse, int T, int NH, int H, float scale,
+                                                            const int* __restrict__ tlen, int nqb) {
+    constexpr int NT = NW * 64;
+    constexpr int ITEMS = FK * 16, NPT = (ITEMS + NT - 1) / NT;  // float4 of a FK x 64 tile per thread
+    __shared__ __attribute__((aligned(16))) float Ks[2][FK * FA_LD];
+    __shared__ __attribute__((aligned(16))) float Vt[2][64 * FK_LDT];
+    const int id = xcd_block();
+    const int qb = id % nqb, bh = id / nqb, hd = bh % NH, u = bh / NH;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, l32 = lane & 31, h = lane >> 5;
+    const int tl = tlen ? tlen[u] : T;
+    const long ld = 3L * H;
+    const float* Qb = qkv + (long)u * T * ld + hd * 64;
+    const float* Kb = Qb + H;
+    const float* Vb = Qb + 2 * H;
+    const int q0 = (qb * NW + w) * 32;
+    const bool active = q0 < T;
+    const float sl2 = scale * LOG2E;
+    RowReg<BF16> qv;
+    qv.load(Qb + (long)min(q0 + l32, T - 1) * ld, h);
+
+    f32x4 kr[NPT], vr[NPT];
+    auto fetch = [&](int kt) {
+#pragma unroll
+        for (int n = 0; n < NPT; ++n) {
+            const int it = threadIdx.x + n * NT, row = it >> 4, c4 = (it & 15) * 4, key = kt * FK + row;
+            kr[n] = vr[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (it < ITEMS && key < T) {
+                kr[n] = *reinterpret_cast<const f32x4*>(Kb + (long)key * ld + c4);
+                vr[n] = *reinterpret_cast<const f32x4*>(Vb + (long)key * ld + c4);
+            }
+        }
+    };
+    auto put = [&](int buf) {
+#pragma unroll
+        for (int n = 0; n < NPT; ++n) {
+            const int it = threadIdx.x + n * NT, row = it >> 4, c4 = (it & 15) * 4;
+            if (it < ITEMS) {
+                *reinterpret_cast<f32x4*>(&Ks[buf][row * FA_LD + c4]) = kr[n];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) Vt[buf][(c4 + e) * FK_LDT + row] = vr[n][e];
+            }
+        }
+    };
+
+    const int nkt = (tl + FK - 1) / FK;  // key tiles holding a valid key (later ones have probability 0)
+    f32x16 o[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) o[t][v] = 0.f;
+    float m_run = -INFINITY, l_run = 0.f;  // log2-domain running maximum; this lane's half of the sum
+    fetch(0);
+    put(0);
+    __syncthreads();
+    for (int kt = 0; kt < nkt; ++kt) {
+        const int buf = kt & 1;
+        if (kt + 1 < nkt) fetch(kt + 1);
+        if (active) {
+            f32x16 s[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+#pragma unroll
+                for (int v = 0; v < 16; ++v) s[j][v] = 0.f;
+                prod_rows<BF16>(s[j], Ks[buf] + 32 * j * FA_LD, qv, l32, h);  // S^T: key r8(v,h), query l32
+            }
+            float mx = -INFINITY;
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int v = 0; v < 16; ++v) {
+                    const bool ok = kt * FK + 32 * j + r8(v, h) < tl;
+                    s[j][v] = ok ? sl2 * s[j][v] : -INFINITY;
+                    mx = fmaxf(mx, s[j][v]);
+                }
+            mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+            const float m_new = fmaxf(m_run, mx);
+            float ls = 0.f;
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int v = 0; v < 16; ++v) {
+                    s[j][v] = __builtin_amdgcn_exp2f(s[j][v] - m_new);
+                    ls += s[j][v];
+                }
+            if (m_new != m_run) {  // rescale only when the maximum moved (exact: alpha = 1 otherwise)
+                const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);  // 0 on the first tile
+                l_run *= alpha;
+#pragma unroll
+                for (int t = 0; t < 2; ++t)
+#pragma unroll
+                    for (int v = 0; v < 16; ++v) o[t][v] *= alpha;
+                m_run = m_new;
+            }
+            l_run += ls;
+#pragma unroll
+            for (int j = 0; j < 2; ++j)  // O^T[n][q] += sum_key V[key][n] P[q][key]
+                apply_cols<BF16, FK_LDT>(o, Vt[buf] + 32 * j, s[j], l32, h);
+        }
+        if (kt + 1 < nkt) put(buf ^ 1);
+        __syncthreads();
+    }
+    if (!active) return;
+    const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+    const int q = q0 + l32;
+    if (q >= T) return;
+    const float inv = 1.0f / l_tot;
+    float* cr = ctx + ((long)u * T + q) * H + hd * 64 + 4 * h;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+            f32x4 r;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) r[b] = o[t][4 * a + b] * inv;
+            *reinterpret_cast<f32x4*>(cr + 32 * t + 8 * a) = r;
+        }
+    if (h == 0) lse[(long)bh * T + q] = (m_run + log2f(l_tot)) * (1.0f / LOG2E);  // natural-log LSE
+}
+
+// ------------------------------------------------------------------------------------------------
+// backward
+// ------------------------------------------------------------------------------------------------
+constexpr int FB_NW = 8;                 // waves per block = key groups of 32 per block
+constexpr int FB_KBP = FB_NW * 32 + 4;   // row stride of the block's transposed K and of the dS tile
+
+template <bool BF16>
+__global__ __launch_bounds__(FB_NW * 64, 1) void flash_bwd_kernel(
+    const float* __restrict__ qkv, const float* __restrict__ dctx, const float* __restrict__ lse,
+    const float* __restrict__ delta, float* __restrict__ dqkv, float* __restrict__ dqp, int T, int NH, int H,
+    float scale, const int* __restrict__ tlen, int nkb, int gpb, int B) {
+    constexpr int NT = FB_NW * 64;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* Kt = smem;                              // [64][FB_KBP]: K of the block's keys, transposed
+    float* Ss = Kt + 64 * FB_KBP;                  // [32][FB_KBP]: dS of the current query tile
+    float* Qs = Ss + 32 * FB_KBP;                  // [2][32][FA_LD]
+    float* Ds = Qs + 2 * 32 * FA_LD;               // [2][32][FA_LD]  (dO = dctx rows)
+    float* Ls = Ds + 2 * 32 * FA_LD;               // [2][32] LSE
+    float* Dl = Ls + 64;                           // [2][32] delta
+    const int id = xcd_block();
+    const int kb = id % nkb, bh = id / nkb, hd = bh % NH, u = bh / NH;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, l32 = lane & 31, h = lane >> 5;
+    const int tl = tlen ? tlen[u] : T;
+    const int ng = (T + 31) >> 5;
+    const int g0 = kb * gpb, ngb = min(gpb, ng - g0);  // key groups of this block
+    const int kbase = g0 * 32;
+    const long ld = 3L * H;
+    const float* Qb = qkv + (long)u * T * ld + hd * 64;
+    const float* Kb = Qb + H;
+    const float* Vb = Qb + 2 * H;
+    const float* Ob = dctx + (long)u * T * H + hd * 64;
+    const float* lb = lse + (long)bh * T;
+    const float* db = delta + (long)bh * T;
+    const bool active = w < ngb && kbase + 32 * w < tl;
+    const int key = kbase + 32 * w + l32;
+    const float sl2 = scale * LOG2E;
+    RowReg<BF16> kv, vv;
+    kv.load(Kb + (long)min(key, T - 1) * ld, h);
+    vv.load(Vb + (long)min(key, T - 1) * ld, h);
+
+    // the block's keys transposed into LDS (zero past T) for the dQ product
+    for (int it = threadIdx.x; it < ngb * 32 * 16; it += NT) {
+        const int row = it >> 4, c4 = (it & 15) * 4, k = kbase + row;
+        f32x4 x = {0.f, 0.f, 0.f, 0.f};
+        if (k < T) x = *reinterpret_cast<const f32x4*>(Kb + (long)k * ld + c4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) Kt[(c4 + e) * FB_KBP + row] = x[e];
+    }
+    // query tiles: Q and dO rows (one float4 each per thread), LSE and delta
+    f32x4 qr, orr;
+    float lr = 0.f;
+    auto fetch = [&](int qt) {
+        const int row = threadIdx.x >> 4, c4 = (threadIdx.x & 15) * 4, q = qt * 32 + row;
+        qr = orr = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (q < T) {
+            qr = *reinterpret_cast<const f32x4*>(Qb + (long)q * ld + c4);
+            orr = *reinterpret_cast<const f32x4*>(Ob + (long)q * H + c4);
+        }
+        lr = 0.f;
+        const int qq = qt * 32 + (threadIdx.x & 31);
+        if (threadIdx.x < 64 && qq < T) lr = threadIdx.x < 32 ? lb[qq] : db[qq];
+    };
+    auto put = [&](int buf) {
+        const int row = threadIdx.x >> 4, c4 = (threadIdx.x & 15) * 4;
+        *reinterpret_cast<f32x4*>(Qs + (buf * 32 + row) * FA_LD + c4) = qr;
+        *reinterpret_cast<f32x4*>(Ds + (buf * 32 + row) * FA_LD + c4) = orr;
+        if (threadIdx.x < 32) Ls[buf * 32 + threadIdx.x] = lr;
+        else if (threadIdx.x < 64) Dl[buf * 32 + threadIdx.x - 32] = lr;
+    };
+
+    f32x16 dv[2], dk[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) dv[t][v] = dk[t][v] = 0.f;
+    // dQ subtiles of 16 x 16: wave w -> query half (w & 1), head-dim quarter (w >> 1)
+    const int qi = w & 1, di = w >> 1, g = lane >> 4, l16 = lane & 15;
+    const int kq = ngb * 32;  // contraction length of the dQ product
+    const long dq_stride = (long)B * NH * T * 64;
+    float* dqb = dqp + kb * dq_stride + (long)bh * T * 64;
+
+    const int nqt = (tl + 31) >> 5;  // query tiles past the length: dO rows are 0, nothing to add
+    if (!active && w < ngb)         // keys past the length: their dS columns stay 0 for the dQ product
+        for (int r = 0; r < 32; ++r) if (h == 0) Ss[r * FB_KBP + 32 * w + l32] = 0.f;
+    fetch(0);
+    put(0);
+    __syncthreads();
+    for (int qt = 0; qt < nqt; ++qt) {
+        const int buf = qt & 1, q0 = qt * 32;
+        if (qt + 1 < nqt) fetch(qt + 1);
+        const float* Qt = Qs + buf * 32 * FA_LD;
+        const float* Dt = Ds + buf * 32 * FA_LD;
+        if (active) {
+            f32x16 s, dp;
+#pragma unroll
+            for (int v = 0; v < 16; ++v) s[v] = dp[v] = 0.f;
+            prod_rows<BF16>(s, Qt, kv, l32, h);   // S[q][key]: query r8(v,h), key on the lane
+            prod_rows<BF16>(dp, Dt, vv, l32, h);  // dP[q][key]
+            const bool kok = key < tl;
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                const int r = r8(v, h);
+                const bool ok = kok && q0 + r < T;
+                const float p = ok ? __builtin_amdgcn_exp2f(sl2 * s[v] - LOG2E * Ls[buf * 32 + r]) : 0.f;
+                s[v] = p;
+                dp[v] = scale * (p * (dp[v] - Dl[buf * 32 + r]));
+            }
+            apply_rows<BF16>(dv, Dt, s, l32, h);   // dV^T[n][key] += sum_q dO[q][n] P[q][key]
+            apply_rows<BF16>(dk, Qt, dp, l32, h);  // dK^T[d][key] += sum_q Q[q][d] dS[q][key]
+#pragma unroll
+            for (int v = 0; v < 16; ++v) Ss[r8(v, h) * FB_KBP + 32 * w + l32] = dp[v];
+        }
+        __syncthreads();  // dS tile complete
+        {  // dQ partial of this key block: dQ[q][d] = sum_key dS[q][key] K[key][d]
+            const float* ar = Ss + (16 * qi + l16) * FB_KBP;
+            const float* br = Kt + (16 * di + l16) * FB_KBP;
+            f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
+            if constexpr (!BF16) {
+                for (int kc = 0; kc < kq; kc += 32) {
+                    const f32x4 a0 = *reinterpret_cast<const f32x4*>(ar + kc + 4 * g);
+                    const f32x4 b0 = *reinterpret_cast<const f32x4*>(br + kc + 4 * g);
+                    const f32x4 a1 = *reinterpret_cast<const f32x4*>(ar + kc + 16 + 4 * g);
+                    const f32x4 b1 = *reinterpret_cast<const f32x4*>(br + kc + 16 + 4 * g);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[e], b0[e], c0, 0, 0, 0);
+                        c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[e], b1[e], c1, 0, 0, 0);
+                    }
+                }
+            } else {
+                for (int kc = 0; kc < kq; kc += 32) {
+                    const fbf16x8 a = cvt8(*reinterpret_cast<const f32x4*>(ar + kc + 8 * g),
+                                           *reinterpret_cast<const f32x4*>(ar + kc + 8 * g + 4));
+                    const fbf16x8 b = cvt8(*reinterpret_cast<const f32x4*>(br + kc + 8 * g),
+                                           *reinterpret_cast<const f32x4*>(br + kc + 8 * g + 4));
+                    c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c0, 0, 0, 0);
+                }
+            }
+            float* dr = dqb + (long)(q0 + 16 * qi + 4 * g) * 64 + 16 * di + l16;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (q0 + 16 * qi + 4 * g + r < T) dr[r * 64] = c0[r] + c1[r];
+        }
+        if (qt + 1 < nqt) put(buf ^ 1);
+        __syncthreads();  // next tile visible; dS tile free
+    }
+    // dK, dV rows of this wave's keys (0 past the length): lane = key, registers = 4 consecutive columns
+    if (w >= ngb || key >= T) return;
+    float* dkr = dqkv + ((long)u * T + key) * ld + H + hd * 64 + 4 * h;
+    float* dvr = dkr + H;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+            f32x4 x, y;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                x[b] = dk[t][4 * a + b];
+                y[b] = dv[t][4 * a + b];
+            }
+            *reinterpret_cast<f32x4*>(dkr + 32 * t + 8 * a) = x;
+            *reinterpret_cast<f32x4*>(dvr + 32 * t + 8 * a) = y;
+        }
+}
+
+// dQ = sum over key blocks in order (query rows < tl; rows past it get 0, as their dS is 0)
+__global__ __launch_bounds__(256) void flash_dq_reduce(const float* __restrict__ dqp, float* __restrict__ dqkv, int B,
+                                                       int T, int NH, int H, int nkb, const int* __restrict__ tlen) {
+    const long n4 = (long)B * NH * T * 16;
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n4) return;
+    const int c4 = (int)(i & 15) * 4;
+    const long row = i >> 4;  // (u * NH + hd) * T + q
+    const int q = (int)(row % T);
+    const long bh = row / T;
+    const int hd = (int)(bh % NH), u = (int)(bh / NH);
+    const int tl = tlen ? tlen[u] : T;
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+    if (q < tl) {
+        const long stride = (long)B * NH * T * 64;
+        const f32x4* p = reinterpret_cast<const f32x4*>(dqp + row * 64 + c4);
+        for (int k = 0; k < nkb; ++k) s += p[k * (stride / 4)];
+    }
+    *reinterpret_cast<f32x4*>(dqkv + ((long)u * T + q) * 3 * H + hd * 64 + c4) = s;
+}
+
+}  // namespace
+
+constexpr int FF_NW = 4;
+
+long flash_dq_scratch_floats(int B, int T, int NH) {
+    const int ng = (T + 31) / 32, nkb = (ng + FB_NW - 1) / FB_NW;
+    return (long)nkb * B * NH * T * 64;
+}
+
+bool launch_flash_fwd(const float* qkv, float* ctx, float* lse, int B, int T, int NH, int H, int dh, float scale,
+                      const int* tlen, bool bf16, hipStream_t st) {
+    if (dh != 64 || T < 1 || H % 4) return false;
+    const int ng = (T + 31) / 32, nqb = (ng + FF_NW - 1) / FF_NW;
+    const dim3 grid((unsigned)((long)B * NH * nqb));
+    if (bf16)
+        hipLaunchKernelGGL((flash_fwd_kernel<FF_NW, true>), grid, dim3(FF_NW * 64), 0, st, qkv, ctx, lse, T, NH, H,
+                           scale, tlen, nqb);
+    else
+        hipLaunchKernelGGL((flash_fwd_kernel<FF_NW, false>), grid, dim3(FF_NW * 64), 0, st, qkv, ctx, lse, T, NH, H,
+                           scale, tlen, nqb);
+    return true;
+}
+
+bool launch_flash_bwd(const float* qkv, const float* dctx, const float* lse, const float* delta, float* dqkv,
+                      float* dqp, int B, int T, int NH, int H, int dh, float scale, const int* tlen, bool bf16,
+                      hipStream_t st) {
+    if (dh != 64 || T < 1 || H % 4) return false;
+    const int ng = (T + 31) / 32;
+    const int nkb = (ng + FB_NW - 1) / FB_NW;   // key blocks per head
+    const int gpb = (ng + nkb - 1) / nkb;       // key groups per block (balanced)
+    const size_t lds = sizeof(float) * ((size_t)(64 + 32) * FB_KBP + 4 * 32 * FA_LD + 128);
+    const dim3 grid((unsigned)((long)B * NH * nkb));
+    static bool attr_set[2] = {false, false};
+    if (!attr_set[bf16]) {
+        if (bf16)
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_bwd_kernel<true>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        else
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_bwd_kernel<false>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr_set[bf16] = true;
+    }
+    if (bf16)
+        hipLaunchKernelGGL(flash_bwd_kernel<true>, grid, dim3(FB_NW * 64), lds, st, qkv, dctx, lse, delta, dqkv, dqp, T,
+                           NH, H, scale, tlen, nkb, gpb, B);
+    else
+        hipLaunchKernelGGL(flash_bwd_kernel<false>, grid, dim3(FB_NW * 64), lds, st, qkv, dctx, lse, delta, dqkv, dqp,
+                           T, NH, H, scale, tlen, nkb, gpb, B);
+    const long n4 = (long)B * NH * T * 16;
+    hipLaunchKernelGGL(flash_dq_reduce, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, dqp, dqkv, B, T, NH, H,
+                       nkb, tlen);
+    return true;
+}

@@ -141,7 +141,7 @@ double gemm_alg_bytes(const GemmParams& p) {
 }
 
 struct LayerBufs {
-    float *x_in, *xhat1, *rstd1, *y1, *qkv, *P, *ctx, *hmid, *xhat2, *rstd2, *y2, *u, *x_out;
+    float *x_in, *xhat1, *rstd1, *y1, *qkv, *P, *lse, *ctx, *hmid, *xhat2, *rstd2, *y2, *u, *x_out;
 };
 
 struct Plan {
@@ -162,7 +162,8 @@ struct Plan {
     std::vector<LayerBufs> lay;
     float *ctx, *gu, *rtmp, *logits;
     // backward
-    float *dlogits, *d1, *d2, *d3, *dqkv, *dP, *du, *dzc, *dzc2, *lnpart, *loss, *loss_scratch, *c0part, *delta;
+    float *dlogits, *d1, *d2, *d3, *dqkv, *dP, *dqp, *du, *dzc, *dzc2, *lnpart, *loss, *loss_scratch, *c0part, *delta;
+    bool flash = false;  // flash attention kernels (head dim 64): no T x T matrices, per-row LSE
     double* dpart;
     int* ids;
     float* splitws;
@@ -386,14 +387,16 @@ void suta_engine::build_plan(int B, long N) {
         pl.enc_rstd = ar.take<float>(BT);
         pl.enc_y = ar.take<float>(BT * H);
         pl.lay.assign(k.L, LayerBufs{});
-        const long Psz = (long)B * k.NH * T * pl.Tp;
+        pl.flash = attn_fused && k.H / k.NH == 64;
+        const long Psz = pl.flash ? 0 : (long)B * k.NH * T * pl.Tp;
         for (int l = 0; l < k.L; ++l) {
             LayerBufs& lb = pl.lay[l];
             lb.xhat1 = ar.take<float>(BT * H);
             lb.rstd1 = ar.take<float>(BT);
             lb.y1 = ar.take<float>(BT * H);
             lb.qkv = ar.take<float>(BT * 3 * H);
-            lb.P = ar.take<float>(Psz);
+            lb.P = pl.flash ? nullptr : ar.take<float>(Psz);
+            lb.lse = pl.flash ? ar.take<float>((size_t)B * k.NH * T) : nullptr;
             lb.ctx = ar.take<float>(BT * H);
             lb.hmid = k.stable ? ar.take<float>(BT * H) : nullptr;
             lb.xhat2 = ar.take<float>(BT * H);
@@ -415,7 +418,8 @@ void suta_engine::build_plan(int B, long N) {
         pl.d2 = ar.take<float>(BT * H);
         pl.d3 = ar.take<float>(BT * H);
         pl.dqkv = ar.take<float>(BT * 3 * H);
-        pl.dP = ar.take<float>(Psz);
+        pl.dP = pl.flash ? nullptr : ar.take<float>(Psz);
+        pl.dqp = pl.flash ? ar.take<float>(flash_dq_scratch_floats(B, pl.T, k.NH)) : nullptr;
         pl.delta = ar.take<float>((size_t)B * k.NH * T);
         pl.du = ar.take<float>(BT * k.F);
         pl.dzc = ar.take<float>((size_t)B * maxLC);
@@ -637,14 +641,14 @@ void suta_engine::forward(int B) {
             g.bias = bqkv[l];
             gemm(g);
         }
-        // S -> softmax -> P -> ctx in one kernel (timed with the MFMA contractions) where its shape holds
-        const bool fused = attn_fused && d == 64 && T <= 512;
+        // flash attention (head dim 64, any T): ctx and the per-row LSE, no T x T matrix
+        const bool fused = pl.flash;
         if (fused)
             timed(F_ATTN, [&] {
-                if (!launch_attn_fwd(lb.qkv, lb.P, lb.ctx, B, T, (int)pl.Tp, NH, H, d, scale, rT(),
-                                     gemm_mode == SUTA_PRECISION_BF16, st))
-                    throw SutaError(SUTA_ERR_UNSUPPORTED, "fused attention shape");
-            });
+                if (!launch_flash_fwd(lb.qkv, lb.ctx, lb.lse, B, T, NH, H, d, scale, rT(),
+                                      gemm_mode == SUTA_PRECISION_BF16, st))
+                    throw SutaError(SUTA_ERR_UNSUPPORTED, "flash attention shape");
+            }, 4.0 * BT * (4.0 * H + NH));  // Q, K, V read; ctx and LSE written
         if (!fused) {
             {  // S = Q K^T * scale
                 GemmParams g;
@@ -896,15 +900,14 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
         nn_gemm(dhres, H, wo[l], H, pl.ctx, H, (int)BT, H, H, 0, nullptr, 0, nullptr, 0);
         // softmax-backward row term delta = rowsum(dctx * ctx) per head, fused into the dP epilogue
         timed(F_SOFTMAX, [&] { launch_attn_delta(pl.ctx, lb.ctx, pl.delta, B, T, NH, d, st); });
-        // dS (stored) and dQ in one kernel where the fused attention shape holds (else dP GEMM with the
-        // softmax-backward epilogue, then the dQ GEMM)
-        const bool fused_bwd = attn_fused && d == 64 && T <= 512;
+        // flash backward: P recomputed from the LSE, dQ, dK, dV into dqkv (else the GEMM path below)
+        const bool fused_bwd = pl.flash;
         if (fused_bwd)
             timed(F_ATTN, [&] {
-                if (!launch_attn_bwd(lb.qkv, lb.P, pl.ctx, pl.delta, pl.dP, pl.dqkv, B, T, (int)pl.Tp, NH, H, d, scale,
-                                     gemm_mode == SUTA_PRECISION_BF16, st))
-                    throw SutaError(SUTA_ERR_UNSUPPORTED, "fused attention shape");
-            });
+                if (!launch_flash_bwd(lb.qkv, pl.ctx, lb.lse, pl.delta, pl.dqkv, pl.dqp, B, T, NH, H, d, scale, rT(),
+                                      gemm_mode == SUTA_PRECISION_BF16, st))
+                    throw SutaError(SUTA_ERR_UNSUPPORTED, "flash attention shape");
+            }, 4.0 * BT * (7.0 * H + 2.0 * NH));  // Q, K, V, dctx, LSE, delta read; dQ, dK, dV written
         if (!fused_bwd) {
             {  // dS = scale * P * (dctx_h @ V_h^T - delta)
                 GemmParams g;
@@ -961,7 +964,7 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
                 gemm(g);
             }
         }
-        {  // dK = dS^T Q_h
+        if (!fused_bwd) {  // dK = dS^T Q_h
             GemmParams g;
             gemm_init(g);
             g.A = pl.dP;
@@ -984,7 +987,7 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
             g.sC1 = (long)T * 3 * H;
             gemm(g);
         }
-        {  // dV = P^T dctx_h
+        if (!fused_bwd) {  // dV = P^T dctx_h
             GemmParams g;
             gemm_init(g);
             g.A = lb.P;

@@ -42,20 +42,24 @@ void launch_layernorm_bwd(const float* dy, const float* xhat, const float* rstd,
 // Column sums per utterance: out[b][c] = sum_{t < rows} x[b][t][c]   (bias gradients).
 void launch_colsum(const float* x, int B, int rows, int C, float* out, long ostride, float* part, hipStream_t st);
 
-// In-place row softmax of `nrows` rows of length T (row stride ld).  tlen (device, may be null):
-// ragged batch, rows of utterance row / rows_per_utt use their first tlen[u] keys; the rest get 0.
-// fused S = QK^T*scale -> softmax -> P (stored) -> ctx = PV for head dim 64, T <= 512 (exact fp32 MFMA);
-// false (nothing launched) when the shape is outside that
-// bf16: S and PV operands rounded to bf16 on v_mfma_f32_16x16x32_bf16 (config C4), fp32 accumulate and softmax
-bool launch_attn_fwd(const float* qkv, float* P, float* ctx, int B, int T, int Tp, int NH, int H, int dh, float scale,
-                     const int* tlen, bool bf16, hipStream_t st);
-// fused dS = scale * P * (dctx V^T - delta) (stored) and dQ = dS K into dqkv's Q columns; same shape limits
-bool launch_attn_bwd(const float* qkv, const float* P, const float* dctx, const float* delta, float* dS, float* dqkv,
-                     int B, int T, int Tp, int NH, int H, int dh, float scale, bool bf16, hipStream_t st);
+// Flash-style fused attention (attn.hip), head dim 64, any T: forward writes ctx and the per-row
+// log-sum-exp lse[b][head][t] (no T x T matrix); backward recomputes P from lse and writes dQ, dK, dV
+// into dqkv's Q/K/V columns (dqp: flash_dq_scratch_floats floats of per-key-block dQ partials).
+// delta[b][head][t] = rowsum(dctx * ctx) (launch_attn_delta).  bf16: operands rounded to bf16 on the bf16
+// MFMAs (config C4).  false (nothing launched) when dh != 64.
+long flash_dq_scratch_floats(int B, int T, int NH);
+bool launch_flash_fwd(const float* qkv, float* ctx, float* lse, int B, int T, int NH, int H, int dh, float scale,
+                      const int* tlen, bool bf16, hipStream_t st);
+bool launch_flash_bwd(const float* qkv, const float* dctx, const float* lse, const float* delta, float* dqkv,
+                      float* dqp, int B, int T, int NH, int H, int dh, float scale, const int* tlen, bool bf16,
+                      hipStream_t st);
 // grouped positional conv (group width 48 or 64, exact fp32 MFMA); fwd: C = R + gelu(conv + bias), C2 = conv + bias;
 // bwd: C = conv + R (rows >= tlen -> 0).  false (nothing launched) outside the supported shapes
 bool launch_posconv(bool fwd, const float* x, const float* W, const float* bias, const float* R, float* C, float* C2,
                     int B, int T, int H, int G, int K, int pad, const int* tlen, hipStream_t st);
+// In-place row softmax of `nrows` rows of length T (row stride ld).  tlen (device, may be null):
+// ragged batch, rows of utterance row / rows_per_utt use their first tlen[u] keys; the rest get 0.
+// (GEMM attention path: head dims other than 64)
 void launch_softmax_rows(float* s, long nrows, int T, long ld, const int* tlen, long rows_per_utt, hipStream_t st);
 
 // delta[b][h][t] = dot(dO[b][t][head h], O[b][t][head h]): the softmax-backward row term sum_j P_ij dP_ij.

@@ -557,318 +557,6 @@ __global__ __launch_bounds__(256) void colsum_partial(const float* __restrict__ 
 }
 
 // ------------------------------------------------------------------------------------------
-// Fused attention forward, one block (8 waves) per (utterance, head), head dim 64, T <= 16*NF:
-//   pass 1: K staged in LDS once; each wave takes 16-query groups: S^T = K Q^T on exact-fp32
-//           v_mfma_f32_16x16x4_f32, softmax over keys in registers, P row segments stored;
-//   pass 2: V staged in the same LDS; each wave reloads its own P rows (same lanes that stored
-//           them) and computes ctx = P V.
-// Replaces S-GEMM -> softmax (P read + written) -> PV-GEMM and loads K and V once per head.
-// LDS rows are [key][68] (16-B rows padded by 4 floats: conflict-free for both read patterns), rows
-// >= T zero.  Lane (r = lane & 15, g = lane >> 4) holds, for key fragment f,
-//   S^T[key 16f + 4g + i][query q0 + r], i = 0..3  (the MFMA C/D map),
-// which is a 16-B run of P's row q0 + r and, in pass 2, the A operand of P V
-// (A[row r][k g] = P[q0 + r][16f + 4g + i]).  The head-dim contraction takes d = 16g + m in MFMA m.
-// Keys >= the utterance's length get probability 0 (ragged batches); rows past T are not stored.
-// ------------------------------------------------------------------------------------------
-constexpr int AF_LD = 68;
-constexpr int AF_THREADS = 512;
-
-template <int NF>
-__device__ __forceinline__ void attn_stage_rows(float* __restrict__ lds, const float* __restrict__ src, long ld,
-                                                int T) {
-    constexpr int ITEMS = NF * 16 * 16, NPT = (ITEMS + AF_THREADS - 1) / AF_THREADS;
-    // all 16-B loads of a thread issued before its first LDS store (one memory round trip)
-    f32x4 v[NPT];
-#pragma unroll
-    for (int n = 0; n < NPT; ++n) {
-        const int it = threadIdx.x + n * AF_THREADS;
-        const int row = it >> 4, c4 = (it & 15) * 4;
-        v[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (it < ITEMS && row < T) v[n] = *reinterpret_cast<const f32x4*>(src + (long)row * ld + c4);
-    }
-#pragma unroll
-    for (int n = 0; n < NPT; ++n) {
-        const int it = threadIdx.x + n * AF_THREADS;
-        if (it < ITEMS) *reinterpret_cast<f32x4*>(lds + (it >> 4) * AF_LD + (it & 15) * 4) = v[n];
-    }
-}
-
-typedef __bf16 abf16x8 __attribute__((ext_vector_type(8)));
-
-__device__ __forceinline__ abf16x8 af_cvt8(f32x4 lo, f32x4 hi) {
-    abf16x8 v;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        v[j] = (__bf16)lo[j];  // round to nearest even (v_cvt_pk_bf16_f32)
-        v[4 + j] = (__bf16)hi[j];
-    }
-    return v;
-}
-
-// Scores of one 16-query group against every staged key row: s[f] (lane (r, g), element i) =
-//   sum_d L[16f + 4g + i][d] * X[q0 + r][d]   with L = the LDS rows, xrow = &X[q0 + r][0] (64 floats).
-// fp32: v_mfma_f32_16x16x4_f32 with d = 16g + m in MFMA m; bf16 (config C4): operands rounded to bf16,
-// v_mfma_f32_16x16x32_bf16 with d = 32h + 8g + j (fp32 accumulation).
-template <int NF, bool BF16>
-__device__ __forceinline__ void af_scores(const float* __restrict__ lds, const float* __restrict__ xrow, int r, int g,
-                                          f32x4 (&s)[NF]) {
-    if constexpr (!BF16) {
-        f32x4 qv[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) qv[j] = *reinterpret_cast<const f32x4*>(xrow + 16 * g + 4 * j);
-        // two key fragments per pass: two independent MFMA chains
-#pragma unroll
-        for (int f = 0; f < NF; f += 2) {
-            const float* kp = lds + (16 * f + r) * AF_LD + 16 * g;
-            f32x4 k0[4], k1[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) k0[j] = *reinterpret_cast<const f32x4*>(kp + 4 * j);
-            if (f + 1 < NF) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) k1[j] = *reinterpret_cast<const f32x4*>(kp + 16 * AF_LD + 4 * j);
-            }
-            s[f] = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (f + 1 < NF) s[f + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    s[f] = __builtin_amdgcn_mfma_f32_16x16x4f32(k0[j][e], qv[j][e], s[f], 0, 0, 0);
-                    if (f + 1 < NF) s[f + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(k1[j][e], qv[j][e], s[f + 1], 0, 0, 0);
-                }
-            __builtin_amdgcn_sched_barrier(0);  // bound the LDS reads hoisted ahead (register budget)
-        }
-    } else {
-        abf16x8 qb[2];
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-            qb[h] = af_cvt8(*reinterpret_cast<const f32x4*>(xrow + 32 * h + 8 * g),
-                            *reinterpret_cast<const f32x4*>(xrow + 32 * h + 8 * g + 4));
-#pragma unroll
-        for (int f = 0; f < NF; f += 2) {
-            abf16x8 a0[2], a1[2];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const float* kp = lds + (16 * f + r) * AF_LD + 32 * h + 8 * g;
-                a0[h] = af_cvt8(*reinterpret_cast<const f32x4*>(kp), *reinterpret_cast<const f32x4*>(kp + 4));
-                if (f + 1 < NF)
-                    a1[h] = af_cvt8(*reinterpret_cast<const f32x4*>(kp + 16 * AF_LD),
-                                    *reinterpret_cast<const f32x4*>(kp + 16 * AF_LD + 4));
-            }
-            s[f] = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (f + 1 < NF) s[f + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                s[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[h], qb[h], s[f], 0, 0, 0);
-                if (f + 1 < NF) s[f + 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[h], qb[h], s[f + 1], 0, 0, 0);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    }
-}
-
-// o[cf] (lane (r, g), element i) = sum_key A[q0 + 4g + i][key] * L[key][16 cf + r], the A rows given as
-// the lanes' segments pf[f][i] = A[q0 + r][16f + 4g + i] (the C/D map of af_scores).
-// fp32: MFMA (f, i) takes keys 16f + 4g' + i; bf16: MFMA c takes the 32 keys of fragments 2c, 2c+1, slot
-// 8g + j <-> key 16(2c) + 4g + j (j < 4), 16(2c+1) + 4g + j - 4 (j >= 4).
-template <int NF, bool BF16>
-__device__ __forceinline__ void af_apply(const float* __restrict__ lds, const f32x4 (&pf)[NF], int r, int g,
-                                         f32x4 (&o)[4]) {
-#pragma unroll
-    for (int cf = 0; cf < 4; ++cf) o[cf] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if constexpr (!BF16) {
-#pragma unroll
-        for (int f = 0; f < NF; ++f)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const float* vp = lds + (16 * f + 4 * g + i) * AF_LD + r;
-                float vv[4];
-#pragma unroll
-                for (int cf = 0; cf < 4; ++cf) vv[cf] = vp[16 * cf];
-#pragma unroll
-                for (int cf = 0; cf < 4; ++cf)
-                    o[cf] = __builtin_amdgcn_mfma_f32_16x16x4f32(pf[f][i], vv[cf], o[cf], 0, 0, 0);
-                if (i == 3) __builtin_amdgcn_sched_barrier(0);
-            }
-    } else {
-#pragma unroll
-        for (int c = 0; c < (NF + 1) / 2; ++c) {
-            const int f0 = 2 * c, f1 = 2 * c + 1;
-            const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-            const abf16x8 a = af_cvt8(pf[f0], f1 < NF ? pf[f1] : z);
-#pragma unroll
-            for (int cf = 0; cf < 4; ++cf) {
-                f32x4 lo, hi = z;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    lo[j] = lds[(16 * f0 + 4 * g + j) * AF_LD + 16 * cf + r];
-                    if (f1 < NF) hi[j] = lds[(16 * f1 + 4 * g + j) * AF_LD + 16 * cf + r];
-                }
-                o[cf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, af_cvt8(lo, hi), o[cf], 0, 0, 0);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    }
-}
-
-template <int NF, bool BF16>
-__global__ __launch_bounds__(AF_THREADS, 1) void attn_fwd_kernel(const float* __restrict__ qkv, float* __restrict__ P,
-                                                                 float* __restrict__ ctx, int T, int Tp, int NH,
-                                                                 int H, float scale, const int* __restrict__ tlen) {
-    __shared__ __attribute__((aligned(16))) float lds[NF * 16 * AF_LD];
-    const int bh = blockIdx.x;  // utterance * NH + head
-    const int hd = bh % NH, u = bh / NH;
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int r = lane & 15, g = lane >> 4;
-    const int ngrp = (T + 15) >> 4;
-    const int tl = tlen ? tlen[u] : T;
-    const long ld = 3L * H;
-    const float* Qb = qkv + (long)u * T * ld + hd * 64;
-    float* Pb = P + (long)bh * T * Tp;
-
-    attn_stage_rows<NF>(lds, Qb + H, ld, T);  // K
-    __syncthreads();
-    for (int grp = w; grp < ngrp; grp += AF_THREADS / 64) {
-        const int q0 = grp * 16;
-        f32x4 s[NF];
-        af_scores<NF, BF16>(lds, Qb + (long)min(q0 + r, T - 1) * ld, r, g, s);
-        // softmax over the keys of query q0 + r: this lane's 4*NF values, then the 4 lanes r + 16g
-        float mx = -INFINITY;
-#pragma unroll
-        for (int f = 0; f < NF; ++f)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const float v = scale * s[f][i];
-                s[f][i] = v;
-                if (16 * f + 4 * g + i < tl) mx = fmaxf(mx, v);
-            }
-        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-        float sum = 0.f;
-#pragma unroll
-        for (int f = 0; f < NF; ++f)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const float v = 16 * f + 4 * g + i < tl ? expf(s[f][i] - mx) : 0.f;
-                s[f][i] = v;
-                sum += v;
-            }
-        sum += __shfl_xor(sum, 16, 64);
-        sum += __shfl_xor(sum, 32, 64);
-        const float inv = 1.0f / sum;
-        if (q0 + r < T) {
-            float* prow = Pb + (long)(q0 + r) * Tp;
-#pragma unroll
-            for (int f = 0; f < NF; ++f)
-                if (16 * f + 4 * g < Tp) *reinterpret_cast<f32x4*>(prow + 16 * f + 4 * g) = s[f] * inv;
-        }
-    }
-    __syncthreads();  // every wave is done with K
-    attn_stage_rows<NF>(lds, Qb + 2 * H, ld, T);  // V
-    __syncthreads();
-    for (int grp = w; grp < ngrp; grp += AF_THREADS / 64) {
-        const int q0 = grp * 16;
-        // this lane's own P segments from pass 1 (zero for rows past T / keys past Tp)
-        f32x4 pf[NF];
-        const float* prow = Pb + (long)(q0 + r) * Tp;
-#pragma unroll
-        for (int f = 0; f < NF; ++f) {
-            pf[f] = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (q0 + r < T && 16 * f + 4 * g < Tp) pf[f] = *reinterpret_cast<const f32x4*>(prow + 16 * f + 4 * g);
-        }
-        // ctx[q0 + 4g + i][16 cf + r] = sum_key P[.][key] V[key][16 cf + r]
-        f32x4 o[4];
-        af_apply<NF, BF16>(lds, pf, r, g, o);
-        float* cb = ctx + (long)u * T * H + hd * 64 + r;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int q = q0 + 4 * g + i;
-            if (q < T) {
-#pragma unroll
-                for (int cf = 0; cf < 4; ++cf) cb[(long)q * H + 16 * cf] = o[cf][i];
-            }
-        }
-    }
-}
-
-// ------------------------------------------------------------------------------------------
-// Fused attention backward, dS and dQ, one block (8 waves) per (utterance, head), same layout as
-// attn_fwd_kernel:
-//   pass 1: V staged; per 16-query group dP^T = V dctx^T (exact-fp32 16x16x4 MFMA), then
-//           dS = scale * P * (dP - delta) with the lane's P segments read from HBM, dS stored;
-//   pass 2: K staged; dQ = dS K from the lane's own dS segments (written into dqkv's Q columns).
-// Replaces the dP GEMM (softmax-backward epilogue) and the dQ GEMM; dK = dS^T Q and dV = P^T dctx
-// stay GEMMs.  delta[bh][q] = rowsum(dctx * ctx) (attn_delta_kernel).
-// ------------------------------------------------------------------------------------------
-template <int NF, bool BF16>
-__global__ __launch_bounds__(AF_THREADS, 1) void attn_bwd_kernel(const float* __restrict__ qkv,
-                                                                 const float* __restrict__ P,
-                                                                 const float* __restrict__ dctx,
-                                                                 const float* __restrict__ delta,
-                                                                 float* __restrict__ dS, float* __restrict__ dqkv,
-                                                                 int T, int Tp, int NH, int H, float scale) {
-    __shared__ __attribute__((aligned(16))) float lds[NF * 16 * AF_LD];
-    const int bh = blockIdx.x;  // utterance * NH + head
-    const int hd = bh % NH, u = bh / NH;
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int r = lane & 15, g = lane >> 4;
-    const int ngrp = (T + 15) >> 4;
-    const long ld = 3L * H;
-    const float* Qb = qkv + (long)u * T * ld + hd * 64;
-    const float* Db = dctx + (long)u * T * H + hd * 64;
-    const float* Pb = P + (long)bh * T * Tp;
-    float* Sb = dS + (long)bh * T * Tp;
-    const float* dlt = delta + (long)bh * T;
-
-    attn_stage_rows<NF>(lds, Qb + 2 * H, ld, T);  // V
-    __syncthreads();
-    for (int grp = w; grp < ngrp; grp += AF_THREADS / 64) {
-        const int q0 = grp * 16;
-        const int qr = min(q0 + r, T - 1);
-        f32x4 s[NF];  // dP^T = V dctx^T
-        af_scores<NF, BF16>(lds, Db + (long)qr * H, r, g, s);
-        if (q0 + r < T) {
-            const float dl = dlt[q0 + r];
-            const float* prow = Pb + (long)(q0 + r) * Tp;
-            float* srow = Sb + (long)(q0 + r) * Tp;
-#pragma unroll
-            for (int f = 0; f < NF; ++f)
-                if (16 * f + 4 * g < Tp) {
-                    const f32x4 pv = *reinterpret_cast<const f32x4*>(prow + 16 * f + 4 * g);
-                    f32x4 o;
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) o[i] = scale * (pv[i] * (s[f][i] - dl));
-                    *reinterpret_cast<f32x4*>(srow + 16 * f + 4 * g) = o;
-                }
-        }
-    }
-    __syncthreads();  // every wave is done with V
-    attn_stage_rows<NF>(lds, Qb + H, ld, T);  // K
-    __syncthreads();
-    for (int grp = w; grp < ngrp; grp += AF_THREADS / 64) {
-        const int q0 = grp * 16;
-        f32x4 pf[NF];
-        const float* srow = Sb + (long)(q0 + r) * Tp;
-#pragma unroll
-        for (int f = 0; f < NF; ++f) {
-            pf[f] = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (q0 + r < T && 16 * f + 4 * g < Tp) pf[f] = *reinterpret_cast<const f32x4*>(srow + 16 * f + 4 * g);
-        }
-        f32x4 o[4];  // dQ = dS K
-        af_apply<NF, BF16>(lds, pf, r, g, o);
-        float* qb = dqkv + (long)u * T * ld + hd * 64 + r;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int q = q0 + 4 * g + i;
-            if (q < T) {
-#pragma unroll
-                for (int cf = 0; cf < 4; ++cf) qb[(long)q * ld + 16 * cf] = o[cf][i];
-            }
-        }
-    }
-}
-
-// ------------------------------------------------------------------------------------------
 // Grouped positional conv (wav2vec2 pos_conv_embed: K taps, G groups of CG channels, "same" padding)
 // as one kernel: out[t][co] = sum_q sum_ci x[t + q - pad][ci] W[q][ci][co] over one group, x rows
 // outside [0, len) are zero.  Block = WB waves = 16*WB output frames x CG channels of one
@@ -1496,52 +1184,6 @@ void launch_softmax_rows(float* s, long nrows, int T, long ld, const int* tlen, 
                                     rows_per_utt);
     else hipLaunchKernelGGL(softmax_rows_kernel<32>, grid, dim3(256), 0, st, s, nrows, T, ld, tlen,
                                     rows_per_utt);
-}
-
-bool launch_attn_fwd(const float* qkv, float* P, float* ctx, int B, int T, int Tp, int NH, int H, int dh, float scale,
-                     const int* tlen, bool bf16, hipStream_t st) {
-    if (dh != 64 || T < 1 || T > 512 || H % 4 || Tp % 4 || Tp < T) return false;
-    const dim3 grid((unsigned)((long)B * NH));
-#define AF(NF_)                                                                                                   \
-    do {                                                                                                          \
-        if (bf16)                                                                                                 \
-            hipLaunchKernelGGL((attn_fwd_kernel<NF_, true>), grid, dim3(AF_THREADS), 0, st, qkv, P, ctx, T, Tp, NH, H, \
-                               scale, tlen);                                                                      \
-        else                                                                                                      \
-            hipLaunchKernelGGL((attn_fwd_kernel<NF_, false>), grid, dim3(AF_THREADS), 0, st, qkv, P, ctx, T, Tp, NH,  \
-                               H, scale, tlen);                                                                   \
-    } while (0)
-    const int nf = (T + 15) / 16;
-    if (nf <= 4) AF(4);
-    else if (nf <= 8) AF(8);
-    else if (nf <= 16) AF(16);
-    else if (nf <= 25) AF(25);
-    else AF(32);
-#undef AF
-    return true;
-}
-
-bool launch_attn_bwd(const float* qkv, const float* P, const float* dctx, const float* delta, float* dS, float* dqkv,
-                     int B, int T, int Tp, int NH, int H, int dh, float scale, bool bf16, hipStream_t st) {
-    if (dh != 64 || T < 1 || T > 512 || H % 4 || Tp % 4 || Tp < T) return false;
-    const dim3 grid((unsigned)((long)B * NH));
-#define AB(NF_)                                                                                                   \
-    do {                                                                                                          \
-        if (bf16)                                                                                                 \
-            hipLaunchKernelGGL((attn_bwd_kernel<NF_, true>), grid, dim3(AF_THREADS), 0, st, qkv, P, dctx, delta, dS,   \
-                               dqkv, T, Tp, NH, H, scale);                                                        \
-        else                                                                                                      \
-            hipLaunchKernelGGL((attn_bwd_kernel<NF_, false>), grid, dim3(AF_THREADS), 0, st, qkv, P, dctx, delta, dS,  \
-                               dqkv, T, Tp, NH, H, scale);                                                        \
-    } while (0)
-    const int nf = (T + 15) / 16;
-    if (nf <= 4) AB(4);
-    else if (nf <= 8) AB(8);
-    else if (nf <= 16) AB(16);
-    else if (nf <= 25) AB(25);
-    else AB(32);
-#undef AB
-    return true;
 }
 
 constexpr int PC_CHT = 2;  // taps per weight chunk: two chunks + the base window fit 2 blocks per CU

@@ -263,11 +263,11 @@ def test_all_blank_utterance_keeps_finite_params():
         assert np.isfinite(eng.get_param(0, name)).all(), name
 
 
-@pytest.mark.parametrize("n", [32000, 128000])
+@pytest.mark.parametrize("n", [32000, 128000, 240000])
 def test_fused_attention_equals_unfused(n, monkeypatch):
-    """The fused attention forward (S -> softmax -> P -> ctx in one kernel, exact fp32 MFMA) against the
-    S-GEMM / softmax / PV-GEMM path: 3 SUTA steps, ragged pair included (keys past an utterance's length
-    get probability 0 in both)."""
+    """The flash attention kernels (forward: online softmax, ctx + LSE; backward: P recomputed, dQ/dK/dV,
+    exact fp32 MFMA) against the S-GEMM / softmax / PV-GEMM path that stores P: 3 SUTA steps, ragged
+    pair included (keys past an utterance's length get probability 0 in both); T = 99, 399, 749."""
     cfg = get_config("wav2vec2-base")
     sd = synth_weights(cfg)
     monkeypatch.setenv("SUTA_ATTN_FUSED", "0")
