@@ -35,6 +35,7 @@
 namespace {
 
 typedef __bf16 fbf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 fbf16x4 __attribute__((ext_vector_type(4)));
 
 constexpr int FA_LD = 68;   // [row][64] tiles: 16-B rows padded by 4 floats (conflict-free row reads)
 constexpr int FA_LDT = 36;  // [64][32] transposed tiles
@@ -182,7 +183,8 @@ constexpr int FK_LDT = FK + 4;  // transposed V tile row stride
 template <int NW, bool BF16>
 __global__ __launch_bounds__(NW * 64) void flash_fwd_kernel(const float* __restrict__ qkv, float* __restrict__ ctx,
                                                             float* __restrict__ lse, int T, int NH, int H, float scale,
-                                                            const int* __restrict__ tlen, int nqb) {
+                                                            const int* __restrict__ tlen, int nqb,
+                                                            __bf16* __restrict__ ctxb) {
     constexpr int NT = NW * 64;
     constexpr int ITEMS = FK * 16, NPT = (ITEMS + NT - 1) / NT;  // float4 of a FK x 64 tile per thread
     __shared__ __attribute__((aligned(16))) float Ks[2][FK * FA_LD];
@@ -296,6 +298,12 @@ __global__ __launch_bounds__(NW * 64) void flash_fwd_kernel(const float* __restr
 #pragma unroll
             for (int b = 0; b < 4; ++b) r[b] = o[t][4 * a + b] * inv;
             *reinterpret_cast<f32x4*>(cr + 32 * t + 8 * a) = r;
+            if (ctxb) {  // bf16 plane of the out-projection's A operand
+                fbf16x4 b;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) b[e] = (__bf16)r[e];
+                *reinterpret_cast<fbf16x4*>(ctxb + ((long)u * T + q) * H + hd * 64 + 4 * h + 32 * t + 8 * a) = b;
+            }
         }
     if (h == 0) lse[(long)bh * T + q] = (m_run + log2f(l_tot)) * (1.0f / LOG2E);  // natural-log LSE
 }
@@ -310,7 +318,7 @@ template <bool BF16>
 __global__ __launch_bounds__(FB_NW * 64, 1) void flash_bwd_kernel(
     const float* __restrict__ qkv, const float* __restrict__ dctx, const float* __restrict__ lse,
     const float* __restrict__ delta, float* __restrict__ dqkv, float* __restrict__ dqp, int T, int NH, int H,
-    float scale, const int* __restrict__ tlen, int nkb, int gpb, int B) {
+    float scale, const int* __restrict__ tlen, int nkb, int gpb, int B, __bf16* __restrict__ dqkvb) {
     constexpr int NT = FB_NW * 64;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float* Kt = smem;                              // [64][FB_KBP]: K of the block's keys, transposed
@@ -462,12 +470,24 @@ __global__ __launch_bounds__(FB_NW * 64, 1) void flash_bwd_kernel(
             }
             *reinterpret_cast<f32x4*>(dkr + 32 * t + 8 * a) = x;
             *reinterpret_cast<f32x4*>(dvr + 32 * t + 8 * a) = y;
+            if (dqkvb) {
+                fbf16x4 bx, by;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    bx[e] = (__bf16)x[e];
+                    by[e] = (__bf16)y[e];
+                }
+                __bf16* kb = dqkvb + ((long)u * T + key) * ld + H + hd * 64 + 4 * h + 32 * t + 8 * a;
+                *reinterpret_cast<fbf16x4*>(kb) = bx;
+                *reinterpret_cast<fbf16x4*>(kb + H) = by;
+            }
         }
 }
 
 // dQ = sum over key blocks in order (query rows < tl; rows past it get 0, as their dS is 0)
 __global__ __launch_bounds__(256) void flash_dq_reduce(const float* __restrict__ dqp, float* __restrict__ dqkv, int B,
-                                                       int T, int NH, int H, int nkb, const int* __restrict__ tlen) {
+                                                       int T, int NH, int H, int nkb, const int* __restrict__ tlen,
+                                                       __bf16* __restrict__ dqkvb) {
     const long n4 = (long)B * NH * T * 16;
     const long i = (long)blockIdx.x * 256 + threadIdx.x;
     if (i >= n4) return;
@@ -484,6 +504,12 @@ __global__ __launch_bounds__(256) void flash_dq_reduce(const float* __restrict__
         for (int k = 0; k < nkb; ++k) s += p[k * (stride / 4)];
     }
     *reinterpret_cast<f32x4*>(dqkv + ((long)u * T + q) * 3 * H + hd * 64 + c4) = s;
+    if (dqkvb) {
+        fbf16x4 b;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) b[e] = (__bf16)s[e];
+        *reinterpret_cast<fbf16x4*>(dqkvb + ((long)u * T + q) * 3 * H + hd * 64 + c4) = b;
+    }
 }
 
 }  // namespace
@@ -496,22 +522,24 @@ long flash_dq_scratch_floats(int B, int T, int NH) {
 }
 
 bool launch_flash_fwd(const float* qkv, float* ctx, float* lse, int B, int T, int NH, int H, int dh, float scale,
-                      const int* tlen, bool bf16, hipStream_t st) {
+                      const int* tlen, bool bf16, hipStream_t st, void* ctxb_) {
+    __bf16* ctxb = reinterpret_cast<__bf16*>(ctxb_);
     if (dh != 64 || T < 1 || H % 4) return false;
     const int ng = (T + 31) / 32, nqb = (ng + FF_NW - 1) / FF_NW;
     const dim3 grid((unsigned)((long)B * NH * nqb));
     if (bf16)
         hipLaunchKernelGGL((flash_fwd_kernel<FF_NW, true>), grid, dim3(FF_NW * 64), 0, st, qkv, ctx, lse, T, NH, H,
-                           scale, tlen, nqb);
+                           scale, tlen, nqb, ctxb);
     else
         hipLaunchKernelGGL((flash_fwd_kernel<FF_NW, false>), grid, dim3(FF_NW * 64), 0, st, qkv, ctx, lse, T, NH, H,
-                           scale, tlen, nqb);
+                           scale, tlen, nqb, ctxb);
     return true;
 }
 
 bool launch_flash_bwd(const float* qkv, const float* dctx, const float* lse, const float* delta, float* dqkv,
                       float* dqp, int B, int T, int NH, int H, int dh, float scale, const int* tlen, bool bf16,
-                      hipStream_t st) {
+                      hipStream_t st, void* dqkvb_) {
+    __bf16* dqkvb = reinterpret_cast<__bf16*>(dqkvb_);
     if (dh != 64 || T < 1 || H % 4) return false;
     const int ng = (T + 31) / 32;
     const int nkb = (ng + FB_NW - 1) / FB_NW;   // key blocks per head
@@ -530,12 +558,12 @@ bool launch_flash_bwd(const float* qkv, const float* dctx, const float* lse, con
     }
     if (bf16)
         hipLaunchKernelGGL(flash_bwd_kernel<true>, grid, dim3(FB_NW * 64), lds, st, qkv, dctx, lse, delta, dqkv, dqp, T,
-                           NH, H, scale, tlen, nkb, gpb, B);
+                           NH, H, scale, tlen, nkb, gpb, B, dqkvb);
     else
         hipLaunchKernelGGL(flash_bwd_kernel<false>, grid, dim3(FB_NW * 64), lds, st, qkv, dctx, lse, delta, dqkv, dqp,
-                           T, NH, H, scale, tlen, nkb, gpb, B);
+                           T, NH, H, scale, tlen, nkb, gpb, B, dqkvb);
     const long n4 = (long)B * NH * T * 16;
     hipLaunchKernelGGL(flash_dq_reduce, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, dqp, dqkv, B, T, NH, H,
-                       nkb, tlen);
+                       nkb, tlen, dqkvb);
     return true;
 }

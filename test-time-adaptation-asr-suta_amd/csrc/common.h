@@ -89,6 +89,13 @@ struct GemmParams {
     float* ws;  // split-K workspace
     int va, vb; // vector (16 B) loads legal
     int mode;   // 0 exact fp32 MFMA, 1 x6 (fp32-accurate bf16 split), 2 bf16 products; gemm_init takes the default
+    // bf16 mode with bf16 operand planes (Z == 1, both k-contiguous): A(m,k) = Ab[m*ldab + k],
+    // B(k,n) = Bb[n*ldbb + k] (16-B aligned, ldab % 8 == ldbb % 8 == K % 8 == 0) -> gemm_hb_kernel
+    const void* Ab;
+    const void* Bb;
+    long ldab, ldbb;
+    void* Cb;   // optional bf16 copy of the stored C (Z == 1): the A plane of the next bf16-plane GEMM
+    long ldcb;
 };
 
 void gemm_init(GemmParams& p);
@@ -99,4 +106,7 @@ void gemm_set_variant(int tile, int nbuf);
 // 0 = exact fp32 MFMA (v_mfma_f32_32x32x2_f32); 1 = fp32-accurate 3-way bf16 split (6 bf16 MFMA products);
 // 2 = bf16 GEMM (operands rounded to bf16 once, one bf16 MFMA product, fp32 accumulate).
 void gemm_set_mode(int mode);
+// dst[r][0:K] = bf16(src[r * lds + 0:K]) (RNE) for r < rows; K % 8 == 0, src/lds 16-B aligned, dst 16-B aligned
+// with row stride K: the A plane of a bf16-plane GEMM.
+void launch_to_bf16(const float* src, long lds, long rows, int K, void* dst, hipStream_t st);
 int gemm_get_mode();

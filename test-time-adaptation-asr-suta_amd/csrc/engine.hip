@@ -181,6 +181,7 @@ struct suta_engine {
     long max_samples = 0;
     bool attn_fused = true;  // fused attention fwd/bwd kernels where their shape holds; env SUTA_ATTN_FUSED=0 off
     bool posconv_kernel = true;  // dedicated positional-conv kernel (exact fp32 mode); env SUTA_POSCONV=0 off
+    bool bf16_planes = true;     // bf16 mode: linears on bf16 operand planes; env SUTA_BF16_PLANES=0 off
     // frozen weights
     std::vector<float*> wqkv, bqkv, wo, bo, w1, b1, w2, b2;
     float *wpos_f = nullptr, *wpos_b = nullptr, *bpos = nullptr, *wlm = nullptr, *blm = nullptr;
@@ -298,10 +299,49 @@ struct suta_engine {
         }
         pending.clear();
     }
+    // bf16 mode: bf16 planes of the frozen linear weights, {[N][K] for x W^T, [in][out] for dY W}, keyed by
+    // the fp32 weight pointer (built once when the mode is selected), and the A plane of the current GEMM
+    std::map<const float*, std::pair<void*, void*>> wplanes;
+    DevBuf abuf;
+    // two bf16 activation planes [B*T][<= max(3H, F)] (ping-pong): written by the producer of a linear's A
+    // operand (LayerNorm, flash attention, GEMM epilogue), read by the linear right after
+    DevBuf planebuf;
+    bool use_planes() const { return gemm_mode == SUTA_PRECISION_BF16 && !wplanes.empty(); }
+    void* plane(int i) {
+        if (!use_planes()) return nullptr;
+        const size_t half = rup((long)plan.B * plan.T * std::max(3 * c.H, c.F) * 2, 256);
+        if (planebuf.alloc(2 * half)) drop_graph();
+        return reinterpret_cast<char*>(planebuf.p) + i * half;
+    }
+    void build_weight_planes();
     void gemm(const GemmParams& p0) {
         GemmParams p = p0;
         p.mode = gemm_mode;
-        timed(F_GEMM, [&] { gemm_launch(p, st, plan.splitws, plan.splitws_floats); }, timing ? gemm_alg_bytes(p) : 0.0);
+        const double ab = timing ? gemm_alg_bytes(p) : 0.0;
+        if (gemm_mode == SUTA_PRECISION_BF16 && p.segK == 0 && !p.ta && p.Z == 1 && p.K % 8 == 0 && p.lda % 4 == 0 &&
+            (reinterpret_cast<uintptr_t>(p.A) & 15) == 0) {
+            auto it = wplanes.find(p.B);
+            const bool fits = it != wplanes.end() && (p.tb ? p.ldb == p.K : p.ldb == p.N);
+            if (fits) {  // linear with a frozen weight: the bf16-plane GEMM
+                p.Bb = p.tb ? it->second.first : it->second.second;
+                p.ldbb = p.K;
+                if (p.Ab) {  // the producer of A wrote its bf16 plane
+                    timed(F_GEMM, [&] { gemm_launch(p, st, plan.splitws, plan.splitws_floats); }, ab);
+                    return;
+                }
+                if (abuf.alloc((size_t)p.M * p.K * 2 + 256)) drop_graph();
+                p.Ab = abuf.p;
+                p.ldab = p.K;
+                timed(F_GEMM, [&] {
+                    launch_to_bf16(p.A, p.lda, p.M, p.K, abuf.p, st);
+                    gemm_launch(p, st, plan.splitws, plan.splitws_floats);
+                }, ab);
+                return;
+            }
+        }
+        p.Ab = nullptr;  // (plane-less GEMM: a plane given for a non-frozen B is ignored)
+        p.Cb = nullptr;
+        timed(F_GEMM, [&] { gemm_launch(p, st, plan.splitws, plan.splitws_floats); }, ab);
     }
 
     int multiplicity(const TP& t, int train_feature, int bias_only) const {
@@ -610,17 +650,20 @@ void suta_engine::forward(int B) {
     if (!k.stable) {
         timed(F_NORM, [&] {
             launch_layernorm_fwd(pl.e, P + o_eg, P + o_eb, Pn, T, pl.enc_y, pl.enc_xhat, pl.enc_rstd, (int)BT, H,
-                                 k.eps, 0, st);
+                                 k.eps, 0, st, plane(0));
         });
     }
     const float scale = 1.0f / std::sqrt((float)d);
+    // bf16 mode: producers of the linears' A operands also write bf16 planes (P0 / P1, ping-pong)
+    void* P0 = plane(0);
+    void* P1 = plane(1);
     for (int l = 0; l < k.L; ++l) {
         LayerBufs& lb = pl.lay[l];
         const float* attn_in = lb.x_in;
         if (k.stable) {
             timed(F_NORM, [&] {
                 launch_layernorm_fwd(lb.x_in, P + o_l1g[l], P + o_l1b[l], Pn, T, lb.y1, lb.xhat1, lb.rstd1, (int)BT, H,
-                                     k.eps, 0, st);
+                                     k.eps, 0, st, P0);
             });
             attn_in = lb.y1;
         }
@@ -629,6 +672,8 @@ void suta_engine::forward(int B) {
             gemm_init(g);
             g.A = attn_in;
             g.lda = H;
+            g.Ab = P0;  // LN output plane (stable: LN1; post-LN: the previous LayerNorm)
+            g.ldab = H;
             g.B = wqkv[l];
             g.tb = 1;
             g.ldb = H;
@@ -646,7 +691,7 @@ void suta_engine::forward(int B) {
         if (fused)
             timed(F_ATTN, [&] {
                 if (!launch_flash_fwd(lb.qkv, lb.ctx, lb.lse, B, T, NH, H, d, scale, rT(),
-                                      gemm_mode == SUTA_PRECISION_BF16, st))
+                                      gemm_mode == SUTA_PRECISION_BF16, st, P0))
                     throw SutaError(SUTA_ERR_UNSUPPORTED, "flash attention shape");
             }, 4.0 * BT * (4.0 * H + NH));  // Q, K, V read; ctx and LSE written
         if (!fused) {
@@ -703,6 +748,10 @@ void suta_engine::forward(int B) {
             gemm_init(g);
             g.A = lb.ctx;
             g.lda = H;
+            if (fused) {
+                g.Ab = P0;
+                g.ldab = H;
+            }
             g.B = wo[l];
             g.tb = 1;
             g.ldb = H;
@@ -723,7 +772,7 @@ void suta_engine::forward(int B) {
         if (k.stable) {
             timed(F_NORM, [&] {
                 launch_layernorm_fwd(lb.hmid, P + o_l2g[l], P + o_l2b[l], Pn, T, lb.y2, lb.xhat2, lb.rstd2, (int)BT, H,
-                                     k.eps, 0, st);
+                                     k.eps, 0, st, P0);
             });
             ffn_in = lb.y2;
             ffn_res = lb.hmid;
@@ -731,7 +780,7 @@ void suta_engine::forward(int B) {
         } else {
             timed(F_NORM, [&] {
                 launch_layernorm_fwd(pl.rtmp, P + o_l1g[l], P + o_l1b[l], Pn, T, lb.y1, lb.xhat1, lb.rstd1, (int)BT, H,
-                                     k.eps, 0, st);
+                                     k.eps, 0, st, P0);
             });
             ffn_in = lb.y1;
             ffn_res = lb.y1;
@@ -742,6 +791,10 @@ void suta_engine::forward(int B) {
             gemm_init(g);
             g.A = ffn_in;
             g.lda = H;
+            g.Ab = P0;
+            g.ldab = H;
+            g.Cb = P1;  // gelu(u) plane for FFN2
+            g.ldcb = k.F;
             g.B = w1[l];
             g.tb = 1;
             g.ldb = H;
@@ -761,6 +814,8 @@ void suta_engine::forward(int B) {
             gemm_init(g);
             g.A = pl.gu;
             g.lda = k.F;
+            g.Ab = P1;
+            g.ldab = k.F;
             g.B = w2[l];
             g.tb = 1;
             g.ldb = k.F;
@@ -778,7 +833,7 @@ void suta_engine::forward(int B) {
         if (!k.stable) {
             timed(F_NORM, [&] {
                 launch_layernorm_fwd(pl.rtmp, P + o_l2g[l], P + o_l2b[l], Pn, T, lb.x_out, lb.xhat2, lb.rstd2, (int)BT,
-                                     H, k.eps, 0, st);
+                                     H, k.eps, 0, st, P0);
             });
         }
     }
@@ -786,7 +841,7 @@ void suta_engine::forward(int B) {
     if (k.stable) {
         timed(F_NORM, [&] {
             launch_layernorm_fwd(hfin, P + o_eg, P + o_eb, Pn, T, pl.enc_y, pl.enc_xhat, pl.enc_rstd, (int)BT, H, k.eps,
-                                 0, st);
+                                 0, st, P0);
         });
         hfin = pl.enc_y;
     }
@@ -795,6 +850,8 @@ void suta_engine::forward(int B) {
         gemm_init(g);
         g.A = hfin;
         g.lda = H;
+        g.Ab = P0;  // final LayerNorm output plane (stable: enc LN; post-LN: the last layer's LN2)
+        g.ldab = H;
         g.B = wlm;
         g.tb = 1;
         g.ldb = H;
@@ -835,12 +892,18 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
         sdpl_err = err;
     }
 
+    // Ab: bf16 plane of A written by its producer; Cb: bf16 plane of C for the next linear (bf16 mode)
     auto nn_gemm = [&](const float* A, int lda, const float* Bm, int ldb, float* C, int ldc, int M, int N, int K,
-                       int epi, const float* R, int ldr, const float* aux, int ldaux) {
+                       int epi, const float* R, int ldr, const float* aux, int ldaux, const void* Ab = nullptr,
+                       void* Cb = nullptr) {
         GemmParams g;
         gemm_init(g);
         g.A = A;
         g.lda = lda;
+        g.Ab = Ab;
+        g.ldab = K;
+        g.Cb = Cb;
+        g.ldcb = N;
         g.B = Bm;
         g.ldb = ldb;
         g.C = C;
@@ -855,6 +918,8 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
         g.ldaux = ldaux;
         gemm(g);
     };
+    void* P0 = plane(0);  // bf16 planes of the linears' A operands (ping-pong), null outside bf16 mode
+    void* P1 = plane(1);
     // d hfin = dlogits @ Wlm
     nn_gemm(pl.dlogits, k.V, wlm, H, pl.d1, H, (int)BT, H, k.V, 0, nullptr, 0, nullptr, 0);
     float* dx = pl.d1;  // grad wrt current residual stream
@@ -863,7 +928,7 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
     if (k.stable) {
         timed(F_NORM, [&] {
             launch_layernorm_bwd(dx, pl.enc_xhat, pl.enc_rstd, P + o_eg, P + o_eb, Pn, T, B, H, 0, nullptr, nullptr, t1,
-                                 G + o_eg, G + o_eb, Pn, pl.lnpart, st);
+                                 G + o_eg, G + o_eb, Pn, pl.lnpart, st, P0);
         });
         std::swap(dx, t1);
     }
@@ -874,30 +939,30 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
             // dr2 = LN2 bwd(dx)
             timed(F_NORM, [&] {
                 launch_layernorm_bwd(dx, lb.xhat2, lb.rstd2, P + o_l2g[l], P + o_l2b[l], Pn, T, B, H, 0, nullptr,
-                                     nullptr, t1, G + o_l2g[l], G + o_l2b[l], Pn, pl.lnpart, st);
+                                     nullptr, t1, G + o_l2g[l], G + o_l2b[l], Pn, pl.lnpart, st, P0);
             });
             // du = (dr2 @ W2) * gelu'(u)
-            nn_gemm(t1, H, w2[l], k.F, pl.du, k.F, (int)BT, k.F, H, EPI_DGELU, nullptr, 0, lb.u, k.F);
+            nn_gemm(t1, H, w2[l], k.F, pl.du, k.F, (int)BT, k.F, H, EPI_DGELU, nullptr, 0, lb.u, k.F, P0, P1);
             // dh1 = du @ W1 + dr2
-            nn_gemm(pl.du, k.F, w1[l], H, t2, H, (int)BT, H, k.F, EPI_RESID, t1, H, nullptr, 0);
+            nn_gemm(pl.du, k.F, w1[l], H, t2, H, (int)BT, H, k.F, EPI_RESID, t1, H, nullptr, 0, P1);
             // dr1 = LN1 bwd(dh1)
             timed(F_NORM, [&] {
                 launch_layernorm_bwd(t2, lb.xhat1, lb.rstd1, P + o_l1g[l], P + o_l1b[l], Pn, T, B, H, 0, nullptr,
-                                     nullptr, t1, G + o_l1g[l], G + o_l1b[l], Pn, pl.lnpart, st);
+                                     nullptr, t1, G + o_l1g[l], G + o_l1b[l], Pn, pl.lnpart, st, P0);
             });
             dhres = t1;  // dr1
         } else {
             // du = (dx @ W2) * gelu'(u); dy2 = du @ W1; dhmid = LN2 bwd(dy2) + dx
-            nn_gemm(dx, H, w2[l], k.F, pl.du, k.F, (int)BT, k.F, H, EPI_DGELU, nullptr, 0, lb.u, k.F);
-            nn_gemm(pl.du, k.F, w1[l], H, t2, H, (int)BT, H, k.F, 0, nullptr, 0, nullptr, 0);
+            nn_gemm(dx, H, w2[l], k.F, pl.du, k.F, (int)BT, k.F, H, EPI_DGELU, nullptr, 0, lb.u, k.F, P0, P1);
+            nn_gemm(pl.du, k.F, w1[l], H, t2, H, (int)BT, H, k.F, 0, nullptr, 0, nullptr, 0, P1);
             timed(F_NORM, [&] {
                 launch_layernorm_bwd(t2, lb.xhat2, lb.rstd2, P + o_l2g[l], P + o_l2b[l], Pn, T, B, H, 0, nullptr, dx,
-                                     t1, G + o_l2g[l], G + o_l2b[l], Pn, pl.lnpart, st);
+                                     t1, G + o_l2g[l], G + o_l2b[l], Pn, pl.lnpart, st, P0);
             });
             dhres = t1;  // dhmid
         }
         // dctx = dhres @ Wo
-        nn_gemm(dhres, H, wo[l], H, pl.ctx, H, (int)BT, H, H, 0, nullptr, 0, nullptr, 0);
+        nn_gemm(dhres, H, wo[l], H, pl.ctx, H, (int)BT, H, H, 0, nullptr, 0, nullptr, 0, P0);
         // softmax-backward row term delta = rowsum(dctx * ctx) per head, fused into the dP epilogue
         timed(F_SOFTMAX, [&] { launch_attn_delta(pl.ctx, lb.ctx, pl.delta, B, T, NH, d, st); });
         // flash backward: P recomputed from the LSE, dQ, dK, dV into dqkv (else the GEMM path below)
@@ -905,7 +970,7 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
         if (fused_bwd)
             timed(F_ATTN, [&] {
                 if (!launch_flash_bwd(lb.qkv, pl.ctx, lb.lse, pl.delta, pl.dqkv, pl.dqp, B, T, NH, H, d, scale, rT(),
-                                      gemm_mode == SUTA_PRECISION_BF16, st))
+                                      gemm_mode == SUTA_PRECISION_BF16, st, P1))
                     throw SutaError(SUTA_ERR_UNSUPPORTED, "flash attention shape");
             }, 4.0 * BT * (7.0 * H + 2.0 * NH));  // Q, K, V, dctx, LSE, delta read; dQ, dK, dV written
         if (!fused_bwd) {
@@ -1012,14 +1077,16 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
         }
         if (!k.stable) {
             // dx_in = dqkv @ Wqkv + dr1
-            nn_gemm(pl.dqkv, 3 * H, wqkv[l], H, t2, H, (int)BT, H, 3 * H, EPI_RESID, dhres, H, nullptr, 0);
+            nn_gemm(pl.dqkv, 3 * H, wqkv[l], H, t2, H, (int)BT, H, 3 * H, EPI_RESID, dhres, H, nullptr, 0,
+                    fused_bwd ? P1 : nullptr);
             std::swap(dx, t2);
         } else {
             // dy1 = dqkv @ Wqkv ; dx_in = LN1 bwd(dy1) + dhmid
-            nn_gemm(pl.dqkv, 3 * H, wqkv[l], H, t2, H, (int)BT, H, 3 * H, 0, nullptr, 0, nullptr, 0);
+            nn_gemm(pl.dqkv, 3 * H, wqkv[l], H, t2, H, (int)BT, H, 3 * H, 0, nullptr, 0, nullptr, 0,
+                    fused_bwd ? P1 : nullptr);
             timed(F_NORM, [&] {
                 launch_layernorm_bwd(t2, lb.xhat1, lb.rstd1, P + o_l1g[l], P + o_l1b[l], Pn, T, B, H, 0, nullptr, dhres,
-                                     dx, G + o_l1g[l], G + o_l1b[l], Pn, pl.lnpart, st);
+                                     dx, G + o_l1g[l], G + o_l1b[l], Pn, pl.lnpart, st, P0);
             });
             // dx now holds grad wrt x_in; t1/t2 free
         }
@@ -1376,6 +1443,36 @@ bool suta_engine::graph_key_repeats(const GraphKey& k) {
     return same;
 }
 
+// bf16 planes of the frozen linear weights (RNE, as the bf16 GEMMs round every operand): W [N][K] for the
+// forward x W^T and W^T [in][out] for the input gradient dY W, so both GEMMs read k-contiguous planes.
+void suta_engine::build_weight_planes() {
+    if (!wplanes.empty()) return;
+    auto add = [&](const float* w, long rows, long cols) {  // w: [rows = out][cols = in]
+        std::vector<float> hw((size_t)rows * cols);
+        HIPCHK(hipMemcpy(hw.data(), w, hw.size() * 4, hipMemcpyDeviceToHost));
+        std::vector<__bf16> a(hw.size()), t(hw.size());
+        for (long r = 0; r < rows; ++r)
+            for (long c2 = 0; c2 < cols; ++c2) {
+                const __bf16 v = (__bf16)hw[(size_t)r * cols + c2];
+                a[(size_t)r * cols + c2] = v;
+                t[(size_t)c2 * rows + r] = v;
+            }
+        float* pa = dalloc((long)(a.size() + 1) / 2 + 4);
+        float* pt = dalloc((long)(t.size() + 1) / 2 + 4);
+        HIPCHK(hipMemcpy(pa, a.data(), a.size() * 2, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(pt, t.data(), t.size() * 2, hipMemcpyHostToDevice));
+        wplanes[w] = {pa, pt};
+    };
+    const long H = c.H, F = c.F;
+    for (int l = 0; l < c.L; ++l) {
+        add(wqkv[l], 3 * H, H);
+        add(wo[l], H, H);
+        add(w1[l], F, H);
+        add(w2[l], H, F);
+    }
+    add(wlm, c.V, H);
+}
+
 // Pristine tensors into slots [0, B) and the Adam step counter to 0.  The moments need no clearing: the
 // Adam kernel takes them as zero at step 0 (zero_moments only keeps unused slots deterministic).
 void suta_engine::reset_slots(int B, bool zero_moments) {
@@ -1479,6 +1576,7 @@ int32_t suta_create(const suta_model_config* cfg, const char* const* names, cons
         e->max_samples = max_samples;
         if (const char* af = std::getenv("SUTA_ATTN_FUSED")) e->attn_fused = af[0] != '0';
         if (const char* pc = std::getenv("SUTA_POSCONV")) e->posconv_kernel = pc[0] != '0';
+        if (const char* bp = std::getenv("SUTA_BF16_PLANES")) e->bf16_planes = bp[0] != '0';
         HIPCHK(hipSetDevice(device));
         HIPCHK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
         e->d_step = reinterpret_cast<int*>(e->dalloc(1));
@@ -1888,6 +1986,8 @@ int32_t suta_set_precision(suta_engine* e, int32_t mode) {
     return guard([&] {
         if (mode != SUTA_PRECISION_FP32_MFMA && mode != SUTA_PRECISION_FP32_SPLIT_BF16 && mode != SUTA_PRECISION_BF16)
             throw SutaError(SUTA_ERR_ARG, "unknown precision mode");
+        HIPCHK(hipSetDevice(e->device));
+        if (mode == SUTA_PRECISION_BF16 && e->bf16_planes) e->build_weight_planes();
         e->gemm_mode = mode;
     });
 }

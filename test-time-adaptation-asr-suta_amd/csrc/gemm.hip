@@ -84,6 +84,27 @@ static int choose_tile_bf16(long M, long N, long Z, bool big) {
     return best;
 }
 
+// bf16-plane GEMMs (tools/hb_bench, C4 linears at M = 25536): 128x128 with two LDS stages wins every
+// shape (460-660 TF vs 370-570 for 256x128 at one block per CU); smaller tiles only for small grids.
+static int choose_tile_hb(long M, long N) {
+    struct Cand {
+        int id, bm, bn;
+        double eff;
+    };
+    static const Cand c[4] = {{0, 128, 128, 1.0}, {1, 128, 64, 0.85}, {2, 64, 128, 0.85}, {3, 64, 64, 0.6}};
+    int best = 0;
+    double bt = 1e300;
+    for (int i = 0; i < 4; ++i) {
+        const long tiles = ((M + c[i].bm - 1) / c[i].bm) * ((N + c[i].bn - 1) / c[i].bn);
+        const double t = (double)((tiles + 511) / 512) * c[i].bm * c[i].bn / c[i].eff;
+        if (t < bt * 0.999) {
+            bt = t;
+            best = c[i].id;
+        }
+    }
+    return best;
+}
+
 void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
     if (p.M <= 0 || p.N <= 0 || p.Z <= 0) return;
     const int second = ((p.epi & EPI_RESID) != 0) + ((p.epi & EPI_ACCUM) != 0) + ((p.epi & EPI_SMBWD) != 0);
@@ -96,8 +117,14 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
     p.vb = vec_ok(p.B, p.ldb, p.sB0, p.sB1) && (!p.segB || (p.sBseg % 4 == 0 && p.segK % 4 == 0));
 
     const bool glds_ok = p.va && p.vb && (p.ta || p.K % 4 == 0) && (!p.tb || p.K % 4 == 0);
+    const bool hb = p.mode == 2 && p.Ab && p.Bb;  // bf16 operand planes (gemm_hb_kernel)
+    if (p.Cb && (!hb || p.Z != 1 || (reinterpret_cast<uintptr_t>(p.Cb) & 7)))
+        throw std::invalid_argument("gemm: a bf16 output plane needs the bf16-plane kernel, Z == 1, 8-B alignment");
+    if (hb && (p.Z != 1 || p.K % 8 || p.ldab % 8 || p.ldbb % 8 || !aligned16(p.Ab) || !aligned16(p.Bb)))
+        throw std::invalid_argument("gemm: bf16 planes need Z == 1, K, ld % 8 == 0 and 16-B alignment");
     const bool bf16_gbf = p.mode == 2 && glds_ok && p.ta;  // bf16 weight gradients: LDS-DMA fp32 stages
     const int tile = g_force_tile >= 0 ? g_force_tile
+                     : hb            ? choose_tile_hb(p.M, p.N)
                      : p.mode == 2   ? choose_tile_bf16(p.M, p.N, p.Z, !bf16_gbf)
                                      : choose_tile(p.M, p.N, p.Z, p.K, p.mode);
     // tiles 0 = 128x128, 1 = 128x64, 2 = 64x128, 3 = 64x64; bf16 mode also 4 = 256x128, 5 = 128x256
@@ -118,7 +145,9 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
     p.splits = splits;
     p.ws = ws;
     dim3 grid(gx, gy, p.Z * splits);
-    if (p.mode == 2) {
+    if (hb) {
+        gemm_run_hb(tile, g_force_tile >= 0 && g_nbuf == 3 ? 3 : 2, p, grid, st);
+    } else if (p.mode == 2) {
         // bf16: register-staged one-plane kernel; weight gradients (and benchmark variants 3 / 8) on
         // register-converted LDS-DMA stages (8 = BK64 x 2)
         const bool gbf = glds_ok && tile < 4 && (g_force_tile >= 0 ? (g_nbuf == 3 || g_nbuf == 8) : bf16_gbf);

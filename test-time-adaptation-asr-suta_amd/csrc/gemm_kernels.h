@@ -193,7 +193,7 @@ __device__ __forceinline__ TileId xcd_tile() {
 // indices so they are unpredicated, and every operand of a fragment is in registers before its first
 // store (C may alias aux / R in place).  Only the stores are predicated, and only on edge tiles.
 // gemm_launch guarantees RESID, ACCUM and SMBWD are mutually exclusive (they share xq).
-template <int RM, int RN>
+template <int RM, int RN, bool CB = false>
 __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, const f32x16 (&acc)[RM][RN], int z1, int z0,
                                               int rbase, int cbase, int h, int l32, bool interior, int tz) {
     if (p.splits > 1) {
@@ -300,7 +300,11 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, const f32x16 
                 for (int r = 0; r < CH; ++r) {
                     const int rr = r0 + r;
                     const int row = rbase + i * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * h;
-                    if (interior || (row < p.M && col < p.N)) C[(long)row * p.ldc + col] = row < rlim ? v[r] : 0.f;
+                    if (interior || (row < p.M && col < p.N)) {
+                        const float o = row < rlim ? v[r] : 0.f;
+                        C[(long)row * p.ldc + col] = o;
+                        if (CB) reinterpret_cast<__bf16*>(p.Cb)[(long)row * p.ldcb + col] = (__bf16)o;
+                    }
                 }
             }
 }
@@ -823,7 +827,9 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmParams p) {
         for (int sp = 0; sp < p.splits; ++sp) s += W[sp * MN + idx];
         const long row = idx / p.N, col = idx % p.N;
         const float v = epi_value(p, s, row, col, bias, R, aux, C2, C, rowv);
-        C[row * p.ldc + col] = ((p.epi & EPI_ROWMASK) && row >= p.zrows[z1]) ? 0.f : v;
+        const float o = ((p.epi & EPI_ROWMASK) && row >= p.zrows[z1]) ? 0.f : v;
+        C[row * p.ldc + col] = o;
+        if (p.Cb) reinterpret_cast<__bf16*>(p.Cb)[row * p.ldcb + col] = (__bf16)o;
     }
 }
 
@@ -1277,6 +1283,114 @@ void launch_tile(const GemmParams& p, dim3 grid, hipStream_t st) {
         hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, true, true, false, false, NBUF>), grid, dim3(256), 0, st, p);
 }
 
+
+// ============================================================================================
+// bf16 GEMM on bf16 operand planes ("hb", SUTA_PRECISION_BF16 with planes): both operands bf16 and
+// k-contiguous in HBM (A [M][K] activations converted once, B [N][K] frozen weights or their
+// transposes converted at engine setup), staged by the glds LDS-DMA machinery in 4-byte units (a
+// 64-deep bf16 K-step is a 32-float-wide stage image: 128-B rows, 16-B chunks XOR-swizzled by
+// (row / 2) % 8, conflict-free fragment reads), fp32 accumulation on v_mfma_f32_32x32x16_bf16 (lane l:
+// row l % 32, k = 16 kc + 8 (l / 32) + [0, 8) = one 16-B chunk), the fp32 epilogue of every kernel.
+// Half the operand bytes of the fp32-staged bf16 kernels, no conversion in the K-loop.
+// ============================================================================================
+template <int BM, int BN, int NS>
+__global__ __launch_bounds__(256, BM * BN > 128 * 128 ? 1 : 2) void gemm_hb_kernel(GemmParams p) {
+    constexpr int BKS = 32;                      // stage depth in 4-byte units (= 64 bf16)
+    constexpr int WTM = BM / 2, WTN = BN / 2;
+    constexpr int RM = WTM / 32, RN = WTN / 32;
+    constexpr int STAGE = (BM + BN) * BKS;       // 4-byte units per LDS stage
+    constexpr int NPW = (BM + BN) * BKS / 1024;  // DMA instructions per wave per stage
+    __shared__ __attribute__((aligned(16))) float smem[NS * STAGE];
+
+    const TileId tid = xcd_tile();
+    const int split = p.splits > 1 ? tid.z : 0;
+    const float* A = reinterpret_cast<const float*>(p.Ab);
+    const float* B = reinterpret_cast<const float*>(p.Bb);
+    const long lda = p.ldab / 2, ldb = p.ldbb / 2;  // in 4-byte units
+    const int m0 = tid.y * BM;
+    const int n0 = tid.x * BN;
+    const int kbeg = split * p.kchunk / 2;
+    const int kend = min(p.K, split * p.kchunk + p.kchunk) / 2;
+    const int nst = (kend - kbeg + BKS - 1) / BKS;
+
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wid >> 1, wn = wid & 1;
+    const int h = lane >> 5, l32 = lane & 31;
+
+    f32x16 acc[RM][RN];
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    GldsStream<BM, BKS, true> sa;
+    GldsStream<BN, BKS, true> sb;
+    sa.init(A, lda, m0, p.M, kbeg, wid, lane);
+    sb.init(B, ldb, n0, p.N, kbeg, wid, lane);
+    auto issue = [&](int s) {
+        float* st = smem + (s % NS) * STAGE;
+        const int k = kbeg + s * BKS;
+        if (s >= nst) {
+            if (NS > 2) {  // keep the per-wave DMA count uniform past the last stage
+                glds_stage<BM, BKS, true, 0>(st, A, lda, m0, p.M, k, kend, 0, 0, 0, 0, wid, lane, true);
+                glds_stage<BN, BKS, true, 0>(st + BM * BKS, B, ldb, n0, p.N, k, kend, 0, 0, 0, 0, wid, lane, true);
+            }
+        } else if (k + BKS <= kend) {
+            glds_stream_issue(sa, st, wid);
+            glds_stream_issue(sb, st + BM * BKS, wid);
+        } else {
+            glds_stage<BM, BKS, true, 0>(st, A, lda, m0, p.M, k, kend, 0, 0, 0, 0, wid, lane, false);
+            glds_stage<BN, BKS, true, 0>(st + BM * BKS, B, ldb, n0, p.N, k, kend, 0, 0, 0, 0, wid, lane, false);
+        }
+    };
+    auto frag = [&](const float* lds, int row, int kc) {
+        const int c = 2 * kc + h;
+        return *reinterpret_cast<const bf16x8*>(lds + row * BKS + ((c ^ glds_swz<BKS>(row)) * 4));
+    };
+    auto compute = [&](int s) {
+        const float* As = smem + (s % NS) * STAGE;
+        const float* Bs = As + BM * BKS;
+#pragma unroll
+        for (int kc = 0; kc < BKS / 8; ++kc) {
+            bf16x8 af[RM], bf[RN];
+#pragma unroll
+            for (int i = 0; i < RM; ++i) af[i] = frag(As, wm * WTM + i * 32 + l32, kc);
+#pragma unroll
+            for (int j = 0; j < RN; ++j) bf[j] = frag(Bs, wn * WTN + j * 32 + l32, kc);
+#pragma unroll
+            for (int i = 0; i < RM; ++i)
+#pragma unroll
+                for (int j = 0; j < RN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+        }
+    };
+
+#pragma unroll
+    for (int s = 0; s < NS - 1; ++s) issue(s);
+    for (int s = 0; s < nst; ++s) {
+        wait_vm<(NS - 2) * NPW>();  // stage s landed (this wave's share); later stages may be in flight
+        __builtin_amdgcn_s_barrier();
+        issue(s + NS - 1);
+        compute(s);
+    }
+    wait_vm<0>();
+    // only the bf16-plane GEMMs write a bf16 copy of C (the template keeps the other kernels' epilogue as it was)
+    if (p.Cb)
+        gemm_epilogue<RM, RN, true>(p, acc, 0, 0, m0 + wm * WTM, n0 + wn * WTN, h, l32,
+                                    m0 + BM <= p.M && n0 + BN <= p.N, tid.z);
+    else
+        gemm_epilogue<RM, RN, false>(p, acc, 0, 0, m0 + wm * WTM, n0 + wn * WTN, h, l32,
+                                     m0 + BM <= p.M && n0 + BN <= p.N, tid.z);
+}
+
+template <int BM, int BN, int NS>
+void launch_hb(const GemmParams& p, dim3 grid, hipStream_t st) {
+    hipLaunchKernelGGL((gemm_hb_kernel<BM, BN, NS>), grid, dim3(256), 0, st, p);
+}
+
 }  // namespace
 
 // Per-family launch wrappers (each defined in its own TU).
@@ -1284,3 +1398,4 @@ void gemm_run_f32(int tile, int nbuf, const GemmParams& p, dim3 grid, hipStream_
 void gemm_run_x6(int tile, int bk16, int npl, const GemmParams& p, dim3 grid, hipStream_t st);  // gemm_x6.hip
 void gemm_run_glds(int variant, int tile, const GemmParams& p, dim3 grid, hipStream_t st);  // gemm_glds.hip
 void gemm_run_gbf(int bk64, int nprod, int tile, const GemmParams& p, dim3 grid, hipStream_t st);  // gemm_gbf.hip
+void gemm_run_hb(int tile, int ns, const GemmParams& p, dim3 grid, hipStream_t st);                         // gemm_hb.hip

@@ -30,14 +30,14 @@ void launch_front_gn_bwd(const float* x, long N, const float* W, const float* bi
 // at pstride.  Stores y, xhat, rstd.  gelu_out: y = gelu(LN(x)) (feature-encoder "layer" mode).
 void launch_layernorm_fwd(const float* x, const float* g, const float* beta, long pstride, int rows_per_utt,
                           float* y, float* xhat, float* rstd, int rows, int D, float eps, int gelu_out,
-                          hipStream_t st);
+                          hipStream_t st, void* yb = nullptr);  // yb: optional bf16 copy of y (bf16-plane GEMMs)
 // LayerNorm backward.  gin = dy (times gelu'(xhat*g+beta) when gelu_in); dx = LN-bwd(gin)
 // (times gelu'(post_aux) when post_aux) (+ resid).  dgamma/dbeta (may be null) summed per
 // utterance into the grad buffer (gstride per utterance).  part: >= B*ceil(rows_per_utt/16)*2*D floats.
 void launch_layernorm_bwd(const float* dy, const float* xhat, const float* rstd, const float* g, const float* beta,
                           long pstride, int rows_per_utt, int B, int D, int gelu_in, const float* post_aux,
                           const float* resid, float* dx, float* dgamma, float* dbeta, long gstride, float* part,
-                          hipStream_t st);
+                          hipStream_t st, void* dxb = nullptr);  // dxb: optional bf16 copy of dx
 
 // Column sums per utterance: out[b][c] = sum_{t < rows} x[b][t][c]   (bias gradients).
 void launch_colsum(const float* x, int B, int rows, int C, float* out, long ostride, float* part, hipStream_t st);
@@ -48,11 +48,12 @@ void launch_colsum(const float* x, int B, int rows, int C, float* out, long ostr
 // delta[b][head][t] = rowsum(dctx * ctx) (launch_attn_delta).  bf16: operands rounded to bf16 on the bf16
 // MFMAs (config C4).  false (nothing launched) when dh != 64.
 long flash_dq_scratch_floats(int B, int T, int NH);
+// ctxb / dqkvb (may be null): bf16 copies of ctx / dqkv for the bf16-plane GEMMs that consume them.
 bool launch_flash_fwd(const float* qkv, float* ctx, float* lse, int B, int T, int NH, int H, int dh, float scale,
-                      const int* tlen, bool bf16, hipStream_t st);
+                      const int* tlen, bool bf16, hipStream_t st, void* ctxb = nullptr);
 bool launch_flash_bwd(const float* qkv, const float* dctx, const float* lse, const float* delta, float* dqkv,
                       float* dqp, int B, int T, int NH, int H, int dh, float scale, const int* tlen, bool bf16,
-                      hipStream_t st);
+                      hipStream_t st, void* dqkvb = nullptr);
 // grouped positional conv (group width 48 or 64, exact fp32 MFMA); fwd: C = R + gelu(conv + bias), C2 = conv + bias;
 // bwd: C = conv + R (rows >= tlen -> 0).  false (nothing launched) outside the supported shapes
 bool launch_posconv(bool fwd, const float* x, const float* W, const float* bias, const float* R, float* C, float* C2,

@@ -243,6 +243,14 @@ __global__ __launch_bounds__(256) void conv0_dw_reduce(const float* __restrict__
     dW[(long)b * gstride + i] = (float)s;
 }
 
+typedef __bf16 lnbf16x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void store_bf16x4(__bf16* dst, f32x4 v) {  // RNE, one 8-B store
+    lnbf16x4 b;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) b[e] = (__bf16)v[e];
+    *reinterpret_cast<lnbf16x4*>(dst) = b;
+}
+
 // ------------------------------------------------------------------------------------------
 // LayerNorm over D (<= 1024): one wave per row
 // ------------------------------------------------------------------------------------------
@@ -376,7 +384,8 @@ __global__ __launch_bounds__(256) void layernorm_fwd_vec_kernel(const float* __r
                                                                 const float* __restrict__ beta, long pstride,
                                                                 int rows_per_utt, float* __restrict__ y,
                                                                 float* __restrict__ xhat, float* __restrict__ rstd,
-                                                                int rows, float eps, int gelu_out) {
+                                                                int rows, float eps, int gelu_out,
+                                                                __bf16* __restrict__ yb) {
     constexpr int D = 256 * NV;
     const int lane = threadIdx.x & 63;
     const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -415,6 +424,7 @@ __global__ __launch_bounds__(256) void layernorm_fwd_vec_kernel(const float* __r
         }
         reinterpret_cast<f32x4*>(xhat + row * D)[lane + 64 * i] = xh;
         reinterpret_cast<f32x4*>(y + row * D)[lane + 64 * i] = o;
+        if (yb) store_bf16x4(yb + row * D + c, o);  // the bf16 plane of the next GEMM's A operand
     }
     if (lane == 0) rstd[row] = rs;
 }
@@ -427,7 +437,7 @@ __global__ __launch_bounds__(256) void layernorm_bwd_vec_kernel(
     const float* __restrict__ dy, const float* __restrict__ xhat, const float* __restrict__ rstd,
     const float* __restrict__ g, const float* __restrict__ beta, long pstride, int rows_per_utt, int gelu_in,
     const float* __restrict__ post_aux, const float* __restrict__ resid, float* __restrict__ dx,
-    float* __restrict__ part, int nchunk) {
+    float* __restrict__ part, int nchunk, __bf16* __restrict__ dxb) {
     constexpr int D = 256 * NV;
     __shared__ f32x4 red[4][2][NV * 64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -493,6 +503,7 @@ __global__ __launch_bounds__(256) void layernorm_bwd_vec_kernel(
                 if (resid) o[e] += rr[i][e];
             }
             reinterpret_cast<f32x4*>(dx + row * D)[lane + 64 * i] = o;
+            if (dxb) store_bf16x4(dxb + row * D + 4 * (lane + 64 * i), o);
         }
     }
     if (part) {
@@ -1111,19 +1122,20 @@ static int ew_grid(long n) { return (int)std::min<long>(2048, std::max<long>(1, 
 
 void launch_layernorm_fwd(const float* x, const float* g, const float* beta, long pstride, int rows_per_utt,
                           float* y, float* xhat, float* rstd, int rows, int D, float eps, int gelu_out,
-                          hipStream_t st) {
+                          hipStream_t st, void* yb_) {
+    __bf16* yb = reinterpret_cast<__bf16*>(yb_);
     dim3 grid(cdiv(rows, 4));
     auto a16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
     const bool vec = a16(x) && a16(y) && a16(xhat);
     if (vec && D == 768)
         hipLaunchKernelGGL(layernorm_fwd_vec_kernel<3>, grid, dim3(256), 0, st, x, g, beta, pstride, rows_per_utt, y,
-                           xhat, rstd, rows, eps, gelu_out);
+                           xhat, rstd, rows, eps, gelu_out, yb);
     else if (vec && D == 1024)
         hipLaunchKernelGGL(layernorm_fwd_vec_kernel<4>, grid, dim3(256), 0, st, x, g, beta, pstride, rows_per_utt, y,
-                           xhat, rstd, rows, eps, gelu_out);
+                           xhat, rstd, rows, eps, gelu_out, yb);
     else if (vec && D == 512)
         hipLaunchKernelGGL(layernorm_fwd_vec_kernel<2>, grid, dim3(256), 0, st, x, g, beta, pstride, rows_per_utt, y,
-                           xhat, rstd, rows, eps, gelu_out);
+                           xhat, rstd, rows, eps, gelu_out, yb);
     else if (D <= 256)
         hipLaunchKernelGGL(layernorm_fwd_kernel<4>, grid, dim3(256), 0, st, x, g, beta, pstride, rows_per_utt, y, xhat,
                            rstd, rows, D, eps, gelu_out);
@@ -1133,12 +1145,14 @@ void launch_layernorm_fwd(const float* x, const float* g, const float* beta, lon
     else
         hipLaunchKernelGGL(layernorm_fwd_kernel<16>, grid, dim3(256), 0, st, x, g, beta, pstride, rows_per_utt, y,
                            xhat, rstd, rows, D, eps, gelu_out);
+    if (yb && !(vec && (D == 768 || D == 1024 || D == 512))) launch_to_bf16(y, D, rows, D, yb, st);
 }
 
 void launch_layernorm_bwd(const float* dy, const float* xhat, const float* rstd, const float* g, const float* beta,
                           long pstride, int rows_per_utt, int B, int D, int gelu_in, const float* post_aux,
                           const float* resid, float* dx, float* dgamma, float* dbeta, long gstride, float* part,
-                          hipStream_t st) {
+                          hipStream_t st, void* dxb_) {
+    __bf16* dxb = reinterpret_cast<__bf16*>(dxb_);
     const int nchunk = cdiv(rows_per_utt, LNB_ROWS);
     float* pp = (dgamma || dbeta) ? part : nullptr;
     dim3 grid(nchunk, B);
@@ -1146,13 +1160,13 @@ void launch_layernorm_bwd(const float* dy, const float* xhat, const float* rstd,
     const bool vec = a16(dy) && a16(xhat) && a16(dx) && a16(post_aux) && a16(resid) && a16(part);
     if (vec && D == 768)
         hipLaunchKernelGGL(layernorm_bwd_vec_kernel<3>, grid, dim3(256), 0, st, dy, xhat, rstd, g, beta, pstride,
-                           rows_per_utt, gelu_in, post_aux, resid, dx, pp, nchunk);
+                           rows_per_utt, gelu_in, post_aux, resid, dx, pp, nchunk, dxb);
     else if (vec && D == 1024)
         hipLaunchKernelGGL(layernorm_bwd_vec_kernel<4>, grid, dim3(256), 0, st, dy, xhat, rstd, g, beta, pstride,
-                           rows_per_utt, gelu_in, post_aux, resid, dx, pp, nchunk);
+                           rows_per_utt, gelu_in, post_aux, resid, dx, pp, nchunk, dxb);
     else if (vec && D == 512)
         hipLaunchKernelGGL(layernorm_bwd_vec_kernel<2>, grid, dim3(256), 0, st, dy, xhat, rstd, g, beta, pstride,
-                           rows_per_utt, gelu_in, post_aux, resid, dx, pp, nchunk);
+                           rows_per_utt, gelu_in, post_aux, resid, dx, pp, nchunk, dxb);
     else if (D <= 256)
         hipLaunchKernelGGL(layernorm_bwd_kernel<4>, grid, dim3(256), 0, st, dy, xhat, rstd, g, beta, pstride,
                            rows_per_utt, D, gelu_in, post_aux, resid, dx, pp, nchunk);
@@ -1162,6 +1176,7 @@ void launch_layernorm_bwd(const float* dy, const float* xhat, const float* rstd,
     else
         hipLaunchKernelGGL(layernorm_bwd_kernel<16>, grid, dim3(256), 0, st, dy, xhat, rstd, g, beta, pstride,
                            rows_per_utt, D, gelu_in, post_aux, resid, dx, pp, nchunk);
+    if (dxb && !(vec && (D == 768 || D == 1024 || D == 512))) launch_to_bf16(dx, D, (long)B * rows_per_utt, D, dxb, st);
     if (pp)
         hipLaunchKernelGGL(chunk_reduce, dim3(cdiv(D, 256), B), dim3(256), 0, st, pp, nchunk, 2, D, dgamma, dbeta,
                            gstride);
