@@ -142,6 +142,7 @@ double gemm_alg_bytes(const GemmParams& p) {
 
 struct LayerBufs {
     float *x_in, *xhat1, *rstd1, *y1, *qkv, *P, *lse, *ctx, *hmid, *xhat2, *rstd2, *y2, *u, *x_out;
+    float *mean1, *mean2;  // row means when x-hat is recomputed from the stored LayerNorm input (xhat null)
 };
 
 struct Plan {
@@ -156,9 +157,13 @@ struct Plan {
     std::vector<int> h_n, h_T;
     // forward
     float *xraw, *x;
-    float *z[SUTA_MAX_CONV], *a[SUTA_MAX_CONV], *cxhat[SUTA_MAX_CONV], *crstd[SUTA_MAX_CONV];
+    float *z[SUTA_MAX_CONV], *a[SUTA_MAX_CONV], *cxhat[SUTA_MAX_CONV], *crstd[SUTA_MAX_CONV], *cmean[SUTA_MAX_CONV];
     float *gn_mean, *gn_rstd;
     float *fp_xhat, *fp_rstd, *fp_y, *h0, *pz, *e, *enc_xhat, *enc_rstd, *enc_y;
+    float *fp_mean, *enc_mean;
+    // LayerNorms whose input stays stored keep only the row means (x-hat recomputed in the backward):
+    // the conv LNs of layer mode, the feature-projection LN, the encoder LN, and every LN of stable
+    // (pre-LN) layers; post-LN layers' LN inputs are transient and keep x-hat
     std::vector<LayerBufs> lay;
     float *ctx, *gu, *rtmp, *logits;
     // backward
@@ -407,23 +412,26 @@ void suta_engine::build_plan(int B, long N) {
             const long n = (long)B * pl.Lc[i] * k.C[i];
             pl.z[i] = (i == 0 && !k.layer_mode) ? nullptr : ar.take<float>(n);  // group-mode conv0 is recomputed
             pl.a[i] = ar.take<float>(n);
+            pl.cxhat[i] = nullptr;
             if (k.layer_mode) {
-                pl.cxhat[i] = ar.take<float>(n);
                 pl.crstd[i] = ar.take<float>((size_t)B * pl.Lc[i]);
+                pl.cmean[i] = ar.take<float>((size_t)B * pl.Lc[i]);
             } else {
-                pl.cxhat[i] = pl.crstd[i] = nullptr;
+                pl.crstd[i] = pl.cmean[i] = nullptr;
             }
         }
         pl.gn_mean = ar.take<float>((size_t)B * k.C[0]);
         pl.gn_rstd = ar.take<float>((size_t)B * k.C[0]);
         const long C6 = k.C[k.nconv - 1];
-        pl.fp_xhat = ar.take<float>(BT * C6);
+        pl.fp_xhat = nullptr;
+        pl.fp_mean = ar.take<float>(BT);
         pl.fp_rstd = ar.take<float>(BT);
         pl.fp_y = ar.take<float>(BT * C6);
         pl.h0 = ar.take<float>(BT * H);
         pl.pz = ar.take<float>(BT * H);
         pl.e = ar.take<float>(BT * H);
-        pl.enc_xhat = ar.take<float>(BT * H);
+        pl.enc_xhat = nullptr;
+        pl.enc_mean = ar.take<float>(BT);
         pl.enc_rstd = ar.take<float>(BT);
         pl.enc_y = ar.take<float>(BT * H);
         pl.lay.assign(k.L, LayerBufs{});
@@ -431,7 +439,8 @@ void suta_engine::build_plan(int B, long N) {
         const long Psz = pl.flash ? 0 : (long)B * k.NH * T * pl.Tp;
         for (int l = 0; l < k.L; ++l) {
             LayerBufs& lb = pl.lay[l];
-            lb.xhat1 = ar.take<float>(BT * H);
+            lb.xhat1 = k.stable ? nullptr : ar.take<float>(BT * H);
+            lb.mean1 = k.stable ? ar.take<float>(BT) : nullptr;
             lb.rstd1 = ar.take<float>(BT);
             lb.y1 = ar.take<float>(BT * H);
             lb.qkv = ar.take<float>(BT * 3 * H);
@@ -439,7 +448,8 @@ void suta_engine::build_plan(int B, long N) {
             lb.lse = pl.flash ? ar.take<float>((size_t)B * k.NH * T) : nullptr;
             lb.ctx = ar.take<float>(BT * H);
             lb.hmid = k.stable ? ar.take<float>(BT * H) : nullptr;
-            lb.xhat2 = ar.take<float>(BT * H);
+            lb.xhat2 = k.stable ? nullptr : ar.take<float>(BT * H);
+            lb.mean2 = k.stable ? ar.take<float>(BT) : nullptr;
             lb.rstd2 = ar.take<float>(BT);
             lb.y2 = k.stable ? ar.take<float>(BT * H) : nullptr;
             lb.u = ar.take<float>(BT * k.F);
@@ -533,7 +543,7 @@ void suta_engine::forward(int B) {
         }, 4.0 * B * ((double)pl.N + (double)pl.Lc[0] * k.C[0]));
         timed(F_NORM, [&] {
             launch_layernorm_fwd(pl.z[0], P + o_cg[0], P + o_cbeta[0], Pn, pl.Lc[0], pl.a[0], pl.cxhat[0],
-                                 pl.crstd[0], B * pl.Lc[0], k.C[0], 1e-5f, 1, st);
+                                 pl.crstd[0], B * pl.Lc[0], k.C[0], 1e-5f, 1, st, nullptr, pl.cmean[0]);
         });
     }
     for (int i = 1; i < k.nconv; ++i) {
@@ -569,7 +579,7 @@ void suta_engine::forward(int B) {
             gemm(g);
             timed(F_NORM, [&] {
                 launch_layernorm_fwd(pl.z[i], P + o_cg[i], P + o_cbeta[i], Pn, pl.Lc[i], pl.a[i], pl.cxhat[i],
-                                     pl.crstd[i], B * pl.Lc[i], k.C[i], 1e-5f, 1, st);
+                                     pl.crstd[i], B * pl.Lc[i], k.C[i], 1e-5f, 1, st, nullptr, pl.cmean[i]);
             });
         }
     }
@@ -577,7 +587,7 @@ void suta_engine::forward(int B) {
     const float* feat = pl.a[k.nconv - 1];
     timed(F_NORM, [&] {
         launch_layernorm_fwd(feat, P + o_fpg, P + o_fpb, Pn, T, pl.fp_y, pl.fp_xhat, pl.fp_rstd, (int)BT, C6, k.eps, 0,
-                             st);
+                             st, nullptr, pl.fp_mean);
     });
     {  // projection (per-utterance trainable W, b)
         GemmParams g;
@@ -650,7 +660,7 @@ void suta_engine::forward(int B) {
     if (!k.stable) {
         timed(F_NORM, [&] {
             launch_layernorm_fwd(pl.e, P + o_eg, P + o_eb, Pn, T, pl.enc_y, pl.enc_xhat, pl.enc_rstd, (int)BT, H,
-                                 k.eps, 0, st, plane(0));
+                                 k.eps, 0, st, plane(0), pl.enc_mean);
         });
     }
     const float scale = 1.0f / std::sqrt((float)d);
@@ -663,7 +673,7 @@ void suta_engine::forward(int B) {
         if (k.stable) {
             timed(F_NORM, [&] {
                 launch_layernorm_fwd(lb.x_in, P + o_l1g[l], P + o_l1b[l], Pn, T, lb.y1, lb.xhat1, lb.rstd1, (int)BT, H,
-                                     k.eps, 0, st, P0);
+                                     k.eps, 0, st, P0, lb.mean1);
             });
             attn_in = lb.y1;
         }
@@ -772,7 +782,7 @@ void suta_engine::forward(int B) {
         if (k.stable) {
             timed(F_NORM, [&] {
                 launch_layernorm_fwd(lb.hmid, P + o_l2g[l], P + o_l2b[l], Pn, T, lb.y2, lb.xhat2, lb.rstd2, (int)BT, H,
-                                     k.eps, 0, st, P0);
+                                     k.eps, 0, st, P0, lb.mean2);
             });
             ffn_in = lb.y2;
             ffn_res = lb.hmid;
@@ -841,7 +851,7 @@ void suta_engine::forward(int B) {
     if (k.stable) {
         timed(F_NORM, [&] {
             launch_layernorm_fwd(hfin, P + o_eg, P + o_eb, Pn, T, pl.enc_y, pl.enc_xhat, pl.enc_rstd, (int)BT, H, k.eps,
-                                 0, st, P0);
+                                 0, st, P0, pl.enc_mean);
         });
         hfin = pl.enc_y;
     }
@@ -928,7 +938,7 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
     if (k.stable) {
         timed(F_NORM, [&] {
             launch_layernorm_bwd(dx, pl.enc_xhat, pl.enc_rstd, P + o_eg, P + o_eb, Pn, T, B, H, 0, nullptr, nullptr, t1,
-                                 G + o_eg, G + o_eb, Pn, pl.lnpart, st, P0);
+                                 G + o_eg, G + o_eb, Pn, pl.lnpart, st, P0, pl.lay[k.L - 1].x_out, pl.enc_mean);
         });
         std::swap(dx, t1);
     }
@@ -957,7 +967,7 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
             nn_gemm(pl.du, k.F, w1[l], H, t2, H, (int)BT, H, k.F, 0, nullptr, 0, nullptr, 0, P1);
             timed(F_NORM, [&] {
                 launch_layernorm_bwd(t2, lb.xhat2, lb.rstd2, P + o_l2g[l], P + o_l2b[l], Pn, T, B, H, 0, nullptr, dx,
-                                     t1, G + o_l2g[l], G + o_l2b[l], Pn, pl.lnpart, st, P0);
+                                     t1, G + o_l2g[l], G + o_l2b[l], Pn, pl.lnpart, st, P0, lb.hmid, lb.mean2);
             });
             dhres = t1;  // dhmid
         }
@@ -1086,7 +1096,7 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
                     fused_bwd ? P1 : nullptr);
             timed(F_NORM, [&] {
                 launch_layernorm_bwd(t2, lb.xhat1, lb.rstd1, P + o_l1g[l], P + o_l1b[l], Pn, T, B, H, 0, nullptr, dhres,
-                                     dx, G + o_l1g[l], G + o_l1b[l], Pn, pl.lnpart, st, P0);
+                                     dx, G + o_l1g[l], G + o_l1b[l], Pn, pl.lnpart, st, P0, lb.x_in, lb.mean1);
             });
             // dx now holds grad wrt x_in; t1/t2 free
         }
@@ -1096,7 +1106,7 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
     if (!k.stable) {
         timed(F_NORM, [&] {
             launch_layernorm_bwd(dx, pl.enc_xhat, pl.enc_rstd, P + o_eg, P + o_eb, Pn, T, B, H, 0, nullptr, nullptr, t1,
-                                 G + o_eg, G + o_eb, Pn, pl.lnpart, st);
+                                 G + o_eg, G + o_eb, Pn, pl.lnpart, st, nullptr, pl.e, pl.enc_mean);
         });
         de = t1;
     }
@@ -1193,7 +1203,7 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
     timed(F_NORM, [&] {
         launch_layernorm_bwd(pl.dzc, pl.fp_xhat, pl.fp_rstd, P + o_fpg, P + o_fpb, Pn, T, B, C6, 0,
                              (!k.layer_mode && hp.train_feature) ? pl.z[last] : nullptr, nullptr, cur, G + o_fpg,
-                             G + o_fpb, Pn, pl.lnpart, st);
+                             G + o_fpb, Pn, pl.lnpart, st, nullptr, pl.a[last], pl.fp_mean);
     });
     if (!hp.train_feature) return;
     float* other = pl.dzc;
@@ -1203,7 +1213,7 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
             timed(F_NORM, [&] {
                 launch_layernorm_bwd(cur, pl.cxhat[i], pl.crstd[i], P + o_cg[i], P + o_cbeta[i], Pn, pl.Lc[i], B,
                                      k.C[i], 1, nullptr, nullptr, other, G + o_cg[i], G + o_cbeta[i], Pn, pl.lnpart,
-                                     st);
+                                     st, nullptr, pl.z[i], pl.cmean[i]);
             });
             std::swap(cur, other);
         }
@@ -1281,7 +1291,8 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
     }
     timed(F_NORM, [&] {
         launch_layernorm_bwd(cur, pl.cxhat[0], pl.crstd[0], P + o_cg[0], P + o_cbeta[0], Pn, pl.Lc[0], B, k.C[0], 1,
-                             nullptr, nullptr, other, G + o_cg[0], G + o_cbeta[0], Pn, pl.lnpart, st);
+                             nullptr, nullptr, other, G + o_cg[0], G + o_cbeta[0], Pn, pl.lnpart, st, nullptr, pl.z[0],
+                             pl.cmean[0]);
     });
     if (k.conv_bias)
         timed(F_NORM, [&] { launch_colsum(other, B, pl.Lc[0], k.C[0], G + o_cb[0], Pn, pl.lnpart, st); });

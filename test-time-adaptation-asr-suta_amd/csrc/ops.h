@@ -30,14 +30,17 @@ void launch_front_gn_bwd(const float* x, long N, const float* W, const float* bi
 // at pstride.  Stores y, xhat, rstd.  gelu_out: y = gelu(LN(x)) (feature-encoder "layer" mode).
 void launch_layernorm_fwd(const float* x, const float* g, const float* beta, long pstride, int rows_per_utt,
                           float* y, float* xhat, float* rstd, int rows, int D, float eps, int gelu_out,
-                          hipStream_t st, void* yb = nullptr);  // yb: optional bf16 copy of y (bf16-plane GEMMs)
+                          hipStream_t st, void* yb = nullptr, float* mean = nullptr);
+// yb: optional bf16 copy of y (bf16-plane GEMMs); xhat may be null when `mean` is given: the row means
+// are stored instead and the backward recomputes x-hat from the (stored) input
 // LayerNorm backward.  gin = dy (times gelu'(xhat*g+beta) when gelu_in); dx = LN-bwd(gin)
 // (times gelu'(post_aux) when post_aux) (+ resid).  dgamma/dbeta (may be null) summed per
 // utterance into the grad buffer (gstride per utterance).  part: >= B*ceil(rows_per_utt/16)*2*D floats.
 void launch_layernorm_bwd(const float* dy, const float* xhat, const float* rstd, const float* g, const float* beta,
                           long pstride, int rows_per_utt, int B, int D, int gelu_in, const float* post_aux,
                           const float* resid, float* dx, float* dgamma, float* dbeta, long gstride, float* part,
-                          hipStream_t st, void* dxb = nullptr);  // dxb: optional bf16 copy of dx
+                          hipStream_t st, void* dxb = nullptr, const float* x = nullptr, const float* mean = nullptr);
+// dxb: optional bf16 copy of dx; xhat null: x-hat = (x - mean) * rstd recomputed from the LayerNorm input
 
 // Column sums per utterance: out[b][c] = sum_{t < rows} x[b][t][c]   (bias gradients).
 void launch_colsum(const float* x, int B, int rows, int C, float* out, long ostride, float* part, hipStream_t st);

@@ -259,7 +259,8 @@ __global__ __launch_bounds__(256) void layernorm_fwd_kernel(const float* __restr
                                                             const float* __restrict__ beta, long pstride,
                                                             int rows_per_utt, float* __restrict__ y,
                                                             float* __restrict__ xhat, float* __restrict__ rstd,
-                                                            int rows, int D, float eps, int gelu_out) {
+                                                            int rows, int D, float eps, int gelu_out,
+                                                            float* __restrict__ meanp) {
     const int lane = threadIdx.x & 63;
     const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= rows) return;
@@ -291,12 +292,15 @@ __global__ __launch_bounds__(256) void layernorm_fwd_kernel(const float* __restr
         const int c = lane + i * 64;
         if (c < D) {
             const float xh = (v[i] - mean) * rs;
-            xhat[row * D + c] = xh;
+            if (xhat) xhat[row * D + c] = xh;
             const float o = xh * gu[c] + bu[c];
             y[row * D + c] = gelu_out ? gelu_f(o) : o;
         }
     }
-    if (lane == 0) rstd[row] = rs;
+    if (lane == 0) {
+        rstd[row] = rs;
+        if (meanp) meanp[row] = mean;
+    }
 }
 
 constexpr int LNB_ROWS = 16;
@@ -307,7 +311,9 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* __restr
                                                             int rows_per_utt, int D, int gelu_in,
                                                             const float* __restrict__ post_aux,
                                                             const float* __restrict__ resid, float* __restrict__ dx,
-                                                            float* __restrict__ part, int nchunk) {
+                                                            float* __restrict__ part, int nchunk,
+                                                            const float* __restrict__ xin,
+                                                            const float* __restrict__ meanp) {
     __shared__ float red[4][2][NPL * 64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int u = blockIdx.y, ch = blockIdx.x;
@@ -328,11 +334,13 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* __restr
         const long row = (long)u * rows_per_utt + r;
         float gi[NPL], xh[NPL];
         float s1 = 0.f, s2 = 0.f;
+        const float rs = rstd[row];
+        const float mu = xhat ? 0.f : meanp[row];
 #pragma unroll
         for (int i = 0; i < NPL; ++i) {
             const int c = lane + i * 64;
             if (c < D) {
-                xh[i] = xhat[row * D + c];
+                xh[i] = xhat ? xhat[row * D + c] : (xin[row * D + c] - mu) * rs;  // recomputed: bitwise the fwd x-hat
                 float d = dy[row * D + c];
                 if (gelu_in) d *= dgelu_f(xh[i] * gam[i] + bet[i]);
                 gi[i] = d;
@@ -347,7 +355,6 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* __restr
         }
         s1 = wave_sum(s1);
         s2 = wave_sum(s2);
-        const float rs = rstd[row];
         const float m1 = s1 / D, m2 = s2 / D;
 #pragma unroll
         for (int i = 0; i < NPL; ++i) {
@@ -385,7 +392,7 @@ __global__ __launch_bounds__(256) void layernorm_fwd_vec_kernel(const float* __r
                                                                 int rows_per_utt, float* __restrict__ y,
                                                                 float* __restrict__ xhat, float* __restrict__ rstd,
                                                                 int rows, float eps, int gelu_out,
-                                                                __bf16* __restrict__ yb) {
+                                                                __bf16* __restrict__ yb, float* __restrict__ meanp) {
     constexpr int D = 256 * NV;
     const int lane = threadIdx.x & 63;
     const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -422,11 +429,14 @@ __global__ __launch_bounds__(256) void layernorm_fwd_vec_kernel(const float* __r
             const float t = xh[e] * gu[c + e] + bu[c + e];
             o[e] = gelu_out ? gelu_f(t) : t;
         }
-        reinterpret_cast<f32x4*>(xhat + row * D)[lane + 64 * i] = xh;
+        if (xhat) reinterpret_cast<f32x4*>(xhat + row * D)[lane + 64 * i] = xh;
         reinterpret_cast<f32x4*>(y + row * D)[lane + 64 * i] = o;
         if (yb) store_bf16x4(yb + row * D + c, o);  // the bf16 plane of the next GEMM's A operand
     }
-    if (lane == 0) rstd[row] = rs;
+    if (lane == 0) {
+        rstd[row] = rs;
+        if (meanp) meanp[row] = mean;
+    }
 }
 
 // Vectorised LayerNorm backward for D = 256 * NV: lane l owns the 16-B column groups l + 64 i
@@ -437,7 +447,8 @@ __global__ __launch_bounds__(256) void layernorm_bwd_vec_kernel(
     const float* __restrict__ dy, const float* __restrict__ xhat, const float* __restrict__ rstd,
     const float* __restrict__ g, const float* __restrict__ beta, long pstride, int rows_per_utt, int gelu_in,
     const float* __restrict__ post_aux, const float* __restrict__ resid, float* __restrict__ dx,
-    float* __restrict__ part, int nchunk, __bf16* __restrict__ dxb) {
+    float* __restrict__ part, int nchunk, __bf16* __restrict__ dxb, const float* __restrict__ xin,
+    const float* __restrict__ meanp) {
     constexpr int D = 256 * NV;
     __shared__ f32x4 red[4][2][NV * 64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -458,14 +469,22 @@ __global__ __launch_bounds__(256) void layernorm_bwd_vec_kernel(
     const int r0 = ch * LNB_ROWS, r1 = min(rows_per_utt, r0 + LNB_ROWS);
     for (int r = r0 + w; r < r1; r += 4) {
         const long row = (long)u * rows_per_utt + r;
-        const f32x4* xr = reinterpret_cast<const f32x4*>(xhat + row * D);
+        const f32x4* xr = reinterpret_cast<const f32x4*>((xhat ? xhat : xin) + row * D);
         const f32x4* dr = reinterpret_cast<const f32x4*>(dy + row * D);
         f32x4 gi[NV], xh[NV];
         float s1 = 0.f, s2 = 0.f;
+        const float rs = rstd[row];
 #pragma unroll
         for (int i = 0; i < NV; ++i) {
             xh[i] = xr[lane + 64 * i];
             gi[i] = dr[lane + 64 * i];
+        }
+        if (!xhat) {  // x-hat recomputed from the LayerNorm input: bitwise the forward's value
+            const float mu = meanp[row];
+#pragma unroll
+            for (int i = 0; i < NV; ++i)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) xh[i][e] = (xh[i][e] - mu) * rs;
         }
 #pragma unroll
         for (int i = 0; i < NV; ++i)
@@ -482,7 +501,6 @@ __global__ __launch_bounds__(256) void layernorm_bwd_vec_kernel(
             }
         s1 = wave_sum(s1);
         s2 = wave_sum(s2);
-        const float rs = rstd[row];
         const float m1 = s1 / D, m2 = s2 / D;
         f32x4 pa[NV], rr[NV];
         if (post_aux) {
@@ -1122,60 +1140,62 @@ static int ew_grid(long n) { return (int)std::min<long>(2048, std::max<long>(1, 
 
 void launch_layernorm_fwd(const float* x, const float* g, const float* beta, long pstride, int rows_per_utt,
                           float* y, float* xhat, float* rstd, int rows, int D, float eps, int gelu_out,
-                          hipStream_t st, void* yb_) {
+                          hipStream_t st, void* yb_, float* mean) {
     __bf16* yb = reinterpret_cast<__bf16*>(yb_);
+    if (!xhat && !mean) throw std::runtime_error("layernorm_fwd: x-hat or the row means must be stored");
     dim3 grid(cdiv(rows, 4));
     auto a16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
     const bool vec = a16(x) && a16(y) && a16(xhat);
     if (vec && D == 768)
         hipLaunchKernelGGL(layernorm_fwd_vec_kernel<3>, grid, dim3(256), 0, st, x, g, beta, pstride, rows_per_utt, y,
-                           xhat, rstd, rows, eps, gelu_out, yb);
+                           xhat, rstd, rows, eps, gelu_out, yb, mean);
     else if (vec && D == 1024)
         hipLaunchKernelGGL(layernorm_fwd_vec_kernel<4>, grid, dim3(256), 0, st, x, g, beta, pstride, rows_per_utt, y,
-                           xhat, rstd, rows, eps, gelu_out, yb);
+                           xhat, rstd, rows, eps, gelu_out, yb, mean);
     else if (vec && D == 512)
         hipLaunchKernelGGL(layernorm_fwd_vec_kernel<2>, grid, dim3(256), 0, st, x, g, beta, pstride, rows_per_utt, y,
-                           xhat, rstd, rows, eps, gelu_out, yb);
+                           xhat, rstd, rows, eps, gelu_out, yb, mean);
     else if (D <= 256)
         hipLaunchKernelGGL(layernorm_fwd_kernel<4>, grid, dim3(256), 0, st, x, g, beta, pstride, rows_per_utt, y, xhat,
-                           rstd, rows, D, eps, gelu_out);
+                           rstd, rows, D, eps, gelu_out, mean);
     else if (D <= 512)
         hipLaunchKernelGGL(layernorm_fwd_kernel<8>, grid, dim3(256), 0, st, x, g, beta, pstride, rows_per_utt, y, xhat,
-                           rstd, rows, D, eps, gelu_out);
+                           rstd, rows, D, eps, gelu_out, mean);
     else
         hipLaunchKernelGGL(layernorm_fwd_kernel<16>, grid, dim3(256), 0, st, x, g, beta, pstride, rows_per_utt, y,
-                           xhat, rstd, rows, D, eps, gelu_out);
+                           xhat, rstd, rows, D, eps, gelu_out, mean);
     if (yb && !(vec && (D == 768 || D == 1024 || D == 512))) launch_to_bf16(y, D, rows, D, yb, st);
 }
 
 void launch_layernorm_bwd(const float* dy, const float* xhat, const float* rstd, const float* g, const float* beta,
                           long pstride, int rows_per_utt, int B, int D, int gelu_in, const float* post_aux,
                           const float* resid, float* dx, float* dgamma, float* dbeta, long gstride, float* part,
-                          hipStream_t st, void* dxb_) {
+                          hipStream_t st, void* dxb_, const float* x, const float* mean) {
     __bf16* dxb = reinterpret_cast<__bf16*>(dxb_);
+    if (!xhat && (!x || !mean)) throw std::runtime_error("layernorm_bwd: x-hat or (x, row means) needed");
     const int nchunk = cdiv(rows_per_utt, LNB_ROWS);
     float* pp = (dgamma || dbeta) ? part : nullptr;
     dim3 grid(nchunk, B);
     auto a16 = [](const void* q) { return q == nullptr || (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
-    const bool vec = a16(dy) && a16(xhat) && a16(dx) && a16(post_aux) && a16(resid) && a16(part);
+    const bool vec = a16(dy) && a16(xhat) && a16(x) && a16(dx) && a16(post_aux) && a16(resid) && a16(part);
     if (vec && D == 768)
         hipLaunchKernelGGL(layernorm_bwd_vec_kernel<3>, grid, dim3(256), 0, st, dy, xhat, rstd, g, beta, pstride,
-                           rows_per_utt, gelu_in, post_aux, resid, dx, pp, nchunk, dxb);
+                           rows_per_utt, gelu_in, post_aux, resid, dx, pp, nchunk, dxb, x, mean);
     else if (vec && D == 1024)
         hipLaunchKernelGGL(layernorm_bwd_vec_kernel<4>, grid, dim3(256), 0, st, dy, xhat, rstd, g, beta, pstride,
-                           rows_per_utt, gelu_in, post_aux, resid, dx, pp, nchunk, dxb);
+                           rows_per_utt, gelu_in, post_aux, resid, dx, pp, nchunk, dxb, x, mean);
     else if (vec && D == 512)
         hipLaunchKernelGGL(layernorm_bwd_vec_kernel<2>, grid, dim3(256), 0, st, dy, xhat, rstd, g, beta, pstride,
-                           rows_per_utt, gelu_in, post_aux, resid, dx, pp, nchunk, dxb);
+                           rows_per_utt, gelu_in, post_aux, resid, dx, pp, nchunk, dxb, x, mean);
     else if (D <= 256)
         hipLaunchKernelGGL(layernorm_bwd_kernel<4>, grid, dim3(256), 0, st, dy, xhat, rstd, g, beta, pstride,
-                           rows_per_utt, D, gelu_in, post_aux, resid, dx, pp, nchunk);
+                           rows_per_utt, D, gelu_in, post_aux, resid, dx, pp, nchunk, x, mean);
     else if (D <= 512)
         hipLaunchKernelGGL(layernorm_bwd_kernel<8>, grid, dim3(256), 0, st, dy, xhat, rstd, g, beta, pstride,
-                           rows_per_utt, D, gelu_in, post_aux, resid, dx, pp, nchunk);
+                           rows_per_utt, D, gelu_in, post_aux, resid, dx, pp, nchunk, x, mean);
     else
         hipLaunchKernelGGL(layernorm_bwd_kernel<16>, grid, dim3(256), 0, st, dy, xhat, rstd, g, beta, pstride,
-                           rows_per_utt, D, gelu_in, post_aux, resid, dx, pp, nchunk);
+                           rows_per_utt, D, gelu_in, post_aux, resid, dx, pp, nchunk, x, mean);
     if (dxb && !(vec && (D == 768 || D == 1024 || D == 512))) launch_to_bf16(dx, D, (long)B * rows_per_utt, D, dxb, st);
     if (pp)
         hipLaunchKernelGGL(chunk_reduce, dim3(cdiv(D, 256), B), dim3(256), 0, st, pp, nchunk, 2, D, dgamma, dbeta,

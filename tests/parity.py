@@ -57,17 +57,22 @@ def same_pseudo_labels(logits_a, logits_b, upto):
 
 
 # bf16 GEMM mode (SUTA_PRECISION_BF16, config C4) against fp32 references.  Rounding every GEMM
-# operand to bf16 (8 significand bits, relative error 2^-9) moves logits by ~1 % of their range:
-# measured max |d| / max |ref| = 0.4-1.3 % at step 0 and <= 3.7 % after 10 steps at lr 5e-4 on the
-# tiny goldens, <= 1.7 % on base and <= 0.9 % on large (tools/bf16_report.py, MI355X).
+# operand to bf16 (8 significand bits, relative error 2^-9) moves logits by ~1 % of their range.
+# Measured max |d| / max |ref| (tools/bf16_report.py, MI355X, bf16-plane linears; profiles/r2/):
+#   wav2vec2-large (config C4's model), 20 steps: 0.93 % at step 0, <= 0.60 % after  -> rtol 0.025
+#   wav2vec2-base, 10 steps:                      0.98 % at step 0, 2.8 % at step 10  -> rtol 0.06
+#   tiny configs, 10 steps at lr 5e-4:            1.25 % at step 0, 3.7 % at step 10  -> rtol 0.06
+# (about 2x the measured worst case; Adam turns bf16 gradient noise into +-lr parameter steps, so the
+# error grows with steps and lr, most on the small random-weight models).
 BF16_LOGITS_RTOL = 0.06
+BF16_LOGITS_RTOL_LARGE = 0.025
 
 
-def assert_bf16_close(actual, ref, ids_min, what=""):
-    """bf16 logits within BF16_LOGITS_RTOL * max|ref| of an fp32 reference and greedy ids agreeing on
-    at least ids_min of the frames (a near-tie frame may flip)."""
+def assert_bf16_close(actual, ref, ids_min, what="", rtol=BF16_LOGITS_RTOL):
+    """bf16 logits within rtol * max|ref| of an fp32 reference and greedy ids agreeing on at least
+    ids_min of the frames (a near-tie frame may flip)."""
     a, r = np.asarray(actual, np.float64), np.asarray(ref, np.float64)
     d = float(np.abs(a - r).max())
-    assert d <= BF16_LOGITS_RTOL * float(np.abs(r).max()), f"{what}: max|d| {d:.3g} vs max|ref| {np.abs(r).max():.3g}"
+    assert d <= rtol * float(np.abs(r).max()), f"{what}: max|d| {d:.3g} vs max|ref| {np.abs(r).max():.3g}"
     agree = float((a.argmax(-1) == r.argmax(-1)).mean())
     assert agree >= ids_min, f"{what}: greedy ids agree on {agree:.3f} of frames"
