@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <stdexcept>
 
 #include "common.h"
@@ -311,22 +312,32 @@ __global__ __launch_bounds__(NW * 64) void flash_fwd_kernel(const float* __restr
 // ------------------------------------------------------------------------------------------------
 // backward
 // ------------------------------------------------------------------------------------------------
-constexpr int FB_NW = 8;                 // waves per block = key groups of 32 per block
-constexpr int FB_KBP = FB_NW * 32 + 4;   // row stride of the block's transposed K and of the dS tile
+// NW waves per block = NW key groups of 32.  Query tiles are single-buffered: the next tile's Q / dO /
+// LSE / delta are loaded into registers while the current tile computes and written to LDS right after
+// the barrier that completes the dS tile (the dQ product reads only dS and K^T), so one LDS image and
+// two barriers per tile suffice.  LDS: K^T [64][32 NW + 4] + dS [32][32 NW + 4] + Q, dO [32][68]:
+// NW = 4 -> 68 KB (two blocks per CU), NW = 8 -> 117 KB.
+template <int NW>
+constexpr int fb_kbp() { return NW * 32 + 4; }
+template <int NW>
+constexpr size_t fb_lds_bytes() { return sizeof(float) * ((size_t)(64 + 32) * fb_kbp<NW>() + 2 * 32 * FA_LD + 64); }
 
-template <bool BF16>
-__global__ __launch_bounds__(FB_NW * 64, 1) void flash_bwd_kernel(
+template <int NW, bool BF16>
+__global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void flash_bwd_kernel(
     const float* __restrict__ qkv, const float* __restrict__ dctx, const float* __restrict__ lse,
     const float* __restrict__ delta, float* __restrict__ dqkv, float* __restrict__ dqp, int T, int NH, int H,
     float scale, const int* __restrict__ tlen, int nkb, int gpb, int B, __bf16* __restrict__ dqkvb) {
-    constexpr int NT = FB_NW * 64;
+    constexpr int NT = NW * 64;
+    constexpr int KBP = fb_kbp<NW>();
+    constexpr int QPT = 512 / NT;       // float4 of a 32 x 64 tile per thread
+    constexpr int SUB = 8 / NW;         // 16 x 16 dQ subtiles per wave
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    float* Kt = smem;                              // [64][FB_KBP]: K of the block's keys, transposed
-    float* Ss = Kt + 64 * FB_KBP;                  // [32][FB_KBP]: dS of the current query tile
-    float* Qs = Ss + 32 * FB_KBP;                  // [2][32][FA_LD]
-    float* Ds = Qs + 2 * 32 * FA_LD;               // [2][32][FA_LD]  (dO = dctx rows)
-    float* Ls = Ds + 2 * 32 * FA_LD;               // [2][32] LSE
-    float* Dl = Ls + 64;                           // [2][32] delta
+    float* Kt = smem;                   // [64][KBP]: K of the block's keys, transposed
+    float* Ss = Kt + 64 * KBP;          // [32][KBP]: dS of the current query tile
+    float* Qs = Ss + 32 * KBP;          // [32][FA_LD]
+    float* Ds = Qs + 32 * FA_LD;        // [32][FA_LD]  (dO = dctx rows)
+    float* Ls = Ds + 32 * FA_LD;        // [32] LSE
+    float* Dl = Ls + 32;                // [32] delta
     const int id = xcd_block();
     const int kb = id % nkb, bh = id / nkb, hd = bh % NH, u = bh / NH;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, l32 = lane & 31, h = lane >> 5;
@@ -354,28 +365,34 @@ __global__ __launch_bounds__(FB_NW * 64, 1) void flash_bwd_kernel(
         f32x4 x = {0.f, 0.f, 0.f, 0.f};
         if (k < T) x = *reinterpret_cast<const f32x4*>(Kb + (long)k * ld + c4);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) Kt[(c4 + e) * FB_KBP + row] = x[e];
+        for (int e = 0; e < 4; ++e) Kt[(c4 + e) * KBP + row] = x[e];
     }
-    // query tiles: Q and dO rows (one float4 each per thread), LSE and delta
-    f32x4 qr, orr;
+    // query tiles: Q and dO rows, LSE and delta
+    f32x4 qr[QPT], orr[QPT];
     float lr = 0.f;
     auto fetch = [&](int qt) {
-        const int row = threadIdx.x >> 4, c4 = (threadIdx.x & 15) * 4, q = qt * 32 + row;
-        qr = orr = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (q < T) {
-            qr = *reinterpret_cast<const f32x4*>(Qb + (long)q * ld + c4);
-            orr = *reinterpret_cast<const f32x4*>(Ob + (long)q * H + c4);
+#pragma unroll
+        for (int n = 0; n < QPT; ++n) {
+            const int it = threadIdx.x + n * NT, row = it >> 4, c4 = (it & 15) * 4, q = qt * 32 + row;
+            qr[n] = orr[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (q < T) {
+                qr[n] = *reinterpret_cast<const f32x4*>(Qb + (long)q * ld + c4);
+                orr[n] = *reinterpret_cast<const f32x4*>(Ob + (long)q * H + c4);
+            }
         }
         lr = 0.f;
         const int qq = qt * 32 + (threadIdx.x & 31);
         if (threadIdx.x < 64 && qq < T) lr = threadIdx.x < 32 ? lb[qq] : db[qq];
     };
-    auto put = [&](int buf) {
-        const int row = threadIdx.x >> 4, c4 = (threadIdx.x & 15) * 4;
-        *reinterpret_cast<f32x4*>(Qs + (buf * 32 + row) * FA_LD + c4) = qr;
-        *reinterpret_cast<f32x4*>(Ds + (buf * 32 + row) * FA_LD + c4) = orr;
-        if (threadIdx.x < 32) Ls[buf * 32 + threadIdx.x] = lr;
-        else if (threadIdx.x < 64) Dl[buf * 32 + threadIdx.x - 32] = lr;
+    auto put = [&]() {
+#pragma unroll
+        for (int n = 0; n < QPT; ++n) {
+            const int it = threadIdx.x + n * NT, row = it >> 4, c4 = (it & 15) * 4;
+            *reinterpret_cast<f32x4*>(Qs + row * FA_LD + c4) = qr[n];
+            *reinterpret_cast<f32x4*>(Ds + row * FA_LD + c4) = orr[n];
+        }
+        if (threadIdx.x < 32) Ls[threadIdx.x] = lr;
+        else if (threadIdx.x < 64) Dl[threadIdx.x - 32] = lr;
     };
 
     f32x16 dv[2], dk[2];
@@ -383,47 +400,48 @@ __global__ __launch_bounds__(FB_NW * 64, 1) void flash_bwd_kernel(
     for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int v = 0; v < 16; ++v) dv[t][v] = dk[t][v] = 0.f;
-    // dQ subtiles of 16 x 16: wave w -> query half (w & 1), head-dim quarter (w >> 1)
-    const int qi = w & 1, di = w >> 1, g = lane >> 4, l16 = lane & 15;
+    const int g = lane >> 4, l16 = lane & 15;
     const int kq = ngb * 32;  // contraction length of the dQ product
     const long dq_stride = (long)B * NH * T * 64;
     float* dqb = dqp + kb * dq_stride + (long)bh * T * 64;
 
     const int nqt = (tl + 31) >> 5;  // query tiles past the length: dO rows are 0, nothing to add
     if (!active && w < ngb)         // keys past the length: their dS columns stay 0 for the dQ product
-        for (int r = 0; r < 32; ++r) if (h == 0) Ss[r * FB_KBP + 32 * w + l32] = 0.f;
+        for (int r = 0; r < 32; ++r)
+            if (h == 0) Ss[r * KBP + 32 * w + l32] = 0.f;
     fetch(0);
-    put(0);
+    put();
     __syncthreads();
     for (int qt = 0; qt < nqt; ++qt) {
-        const int buf = qt & 1, q0 = qt * 32;
+        const int q0 = qt * 32;
         if (qt + 1 < nqt) fetch(qt + 1);
-        const float* Qt = Qs + buf * 32 * FA_LD;
-        const float* Dt = Ds + buf * 32 * FA_LD;
         if (active) {
             f32x16 s, dp;
 #pragma unroll
             for (int v = 0; v < 16; ++v) s[v] = dp[v] = 0.f;
-            prod_rows<BF16>(s, Qt, kv, l32, h);   // S[q][key]: query r8(v,h), key on the lane
-            prod_rows<BF16>(dp, Dt, vv, l32, h);  // dP[q][key]
+            prod_rows<BF16>(s, Qs, kv, l32, h);   // S[q][key]: query r8(v,h), key on the lane
+            prod_rows<BF16>(dp, Ds, vv, l32, h);  // dP[q][key]
             const bool kok = key < tl;
 #pragma unroll
             for (int v = 0; v < 16; ++v) {
                 const int r = r8(v, h);
                 const bool ok = kok && q0 + r < T;
-                const float p = ok ? __builtin_amdgcn_exp2f(sl2 * s[v] - LOG2E * Ls[buf * 32 + r]) : 0.f;
+                const float p = ok ? __builtin_amdgcn_exp2f(sl2 * s[v] - LOG2E * Ls[r]) : 0.f;
                 s[v] = p;
-                dp[v] = scale * (p * (dp[v] - Dl[buf * 32 + r]));
+                dp[v] = scale * (p * (dp[v] - Dl[r]));
             }
-            apply_rows<BF16>(dv, Dt, s, l32, h);   // dV^T[n][key] += sum_q dO[q][n] P[q][key]
-            apply_rows<BF16>(dk, Qt, dp, l32, h);  // dK^T[d][key] += sum_q Q[q][d] dS[q][key]
+            apply_rows<BF16>(dv, Ds, s, l32, h);   // dV^T[n][key] += sum_q dO[q][n] P[q][key]
+            apply_rows<BF16>(dk, Qs, dp, l32, h);  // dK^T[d][key] += sum_q Q[q][d] dS[q][key]
 #pragma unroll
-            for (int v = 0; v < 16; ++v) Ss[r8(v, h) * FB_KBP + 32 * w + l32] = dp[v];
+            for (int v = 0; v < 16; ++v) Ss[r8(v, h) * KBP + 32 * w + l32] = dp[v];
         }
-        __syncthreads();  // dS tile complete
-        {  // dQ partial of this key block: dQ[q][d] = sum_key dS[q][key] K[key][d]
-            const float* ar = Ss + (16 * qi + l16) * FB_KBP;
-            const float* br = Kt + (16 * di + l16) * FB_KBP;
+        __syncthreads();  // dS tile complete; every wave is done with this tile's Q / dO / LSE / delta
+        if (qt + 1 < nqt) put();
+#pragma unroll
+        for (int j = 0; j < SUB; ++j) {  // dQ partial of this key block: dQ[q][d] = sum_key dS[q][key] K[key][d]
+            const int st = w * SUB + j, qi = st & 1, di = st >> 1;
+            const float* ar = Ss + (16 * qi + l16) * KBP;
+            const float* br = Kt + (16 * di + l16) * KBP;
             f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
             if constexpr (!BF16) {
                 for (int kc = 0; kc < kq; kc += 32) {
@@ -451,7 +469,6 @@ __global__ __launch_bounds__(FB_NW * 64, 1) void flash_bwd_kernel(
             for (int r = 0; r < 4; ++r)
                 if (q0 + 16 * qi + 4 * g + r < T) dr[r * 64] = c0[r] + c1[r];
         }
-        if (qt + 1 < nqt) put(buf ^ 1);
         __syncthreads();  // next tile visible; dS tile free
     }
     // dK, dV rows of this wave's keys (0 past the length): lane = key, registers = 4 consecutive columns
@@ -516,8 +533,17 @@ __global__ __launch_bounds__(256) void flash_dq_reduce(const float* __restrict__
 
 constexpr int FF_NW = 4;
 
+static int g_fb_nw = 0;  // backward block width: 4 or 8 waves (0 = unset: env SUTA_FLASH_BWD_NW, default 8)
+static int fb_nw() {
+    if (!g_fb_nw) {
+        const char* e = std::getenv("SUTA_FLASH_BWD_NW");
+        g_fb_nw = (e && atoi(e) == 4) ? 4 : 8;
+    }
+    return g_fb_nw;
+}
+
 long flash_dq_scratch_floats(int B, int T, int NH) {
-    const int ng = (T + 31) / 32, nkb = (ng + FB_NW - 1) / FB_NW;
+    const int ng = (T + 31) / 32, nkb = (ng + fb_nw() - 1) / fb_nw();
     return (long)nkb * B * NH * T * 64;
 }
 
@@ -536,32 +562,39 @@ bool launch_flash_fwd(const float* qkv, float* ctx, float* lse, int B, int T, in
     return true;
 }
 
+template <int NW, bool BF16>
+static void flash_bwd_go(dim3 grid, hipStream_t st, const float* qkv, const float* dctx, const float* lse,
+                         const float* delta, float* dqkv, float* dqp, int T, int NH, int H, float scale,
+                         const int* tlen, int nkb, int gpb, int B, __bf16* dqkvb) {
+    constexpr size_t lds = fb_lds_bytes<NW>();
+    static bool attr = false;
+    if (!attr) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_bwd_kernel<NW, BF16>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+            throw std::runtime_error("hipFuncSetAttribute(flash_bwd_kernel) failed");
+        attr = true;
+    }
+    hipLaunchKernelGGL((flash_bwd_kernel<NW, BF16>), grid, dim3(NW * 64), lds, st, qkv, dctx, lse, delta, dqkv, dqp,
+                       T, NH, H, scale, tlen, nkb, gpb, B, dqkvb);
+}
+
 bool launch_flash_bwd(const float* qkv, const float* dctx, const float* lse, const float* delta, float* dqkv,
                       float* dqp, int B, int T, int NH, int H, int dh, float scale, const int* tlen, bool bf16,
                       hipStream_t st, void* dqkvb_) {
     __bf16* dqkvb = reinterpret_cast<__bf16*>(dqkvb_);
     if (dh != 64 || T < 1 || H % 4) return false;
+    const int nw = fb_nw();
     const int ng = (T + 31) / 32;
-    const int nkb = (ng + FB_NW - 1) / FB_NW;   // key blocks per head
-    const int gpb = (ng + nkb - 1) / nkb;       // key groups per block (balanced)
-    const size_t lds = sizeof(float) * ((size_t)(64 + 32) * FB_KBP + 4 * 32 * FA_LD + 128);
+    const int nkb = (ng + nw - 1) / nw;   // key blocks per head
+    const int gpb = (ng + nkb - 1) / nkb;  // key groups per block (balanced)
     const dim3 grid((unsigned)((long)B * NH * nkb));
-    static bool attr_set[2] = {false, false};
-    if (!attr_set[bf16]) {
-        if (bf16)
-            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_bwd_kernel<true>),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        else
-            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_bwd_kernel<false>),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        attr_set[bf16] = true;
+    if (nw == 4) {
+        if (bf16) flash_bwd_go<4, true>(grid, st, qkv, dctx, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb);
+        else flash_bwd_go<4, false>(grid, st, qkv, dctx, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb);
+    } else {
+        if (bf16) flash_bwd_go<8, true>(grid, st, qkv, dctx, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb);
+        else flash_bwd_go<8, false>(grid, st, qkv, dctx, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb);
     }
-    if (bf16)
-        hipLaunchKernelGGL(flash_bwd_kernel<true>, grid, dim3(FB_NW * 64), lds, st, qkv, dctx, lse, delta, dqkv, dqp, T,
-                           NH, H, scale, tlen, nkb, gpb, B, dqkvb);
-    else
-        hipLaunchKernelGGL(flash_bwd_kernel<false>, grid, dim3(FB_NW * 64), lds, st, qkv, dctx, lse, delta, dqkv, dqp,
-                           T, NH, H, scale, tlen, nkb, gpb, B, dqkvb);
     const long n4 = (long)B * NH * T * 16;
     hipLaunchKernelGGL(flash_dq_reduce, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, dqp, dqkv, B, T, NH, H,
                        nkb, tlen, dqkvb);
