@@ -106,3 +106,26 @@ def test_bf16_batch_equals_single_and_deterministic():
     # batch and single runs choose different split-K / tile schedules: fp32 summation-order noise
     # flips bf16 roundings downstream, so they agree to bf16 (not fp32) tolerance
     assert_bf16_close(lb[3][1], l1[3][0], 0.97, "batch slot 1 vs single")
+
+
+def test_bf16_planes_equal_fp32_staged_path(monkeypatch):
+    """The bf16-plane linears (default) and the fp32-staged bf16 kernels (SUTA_BF16_PLANES=0) round the same
+    operands the same way (RNE to bf16, fp32 accumulation): they agree to bf16 tolerance, and each rerun
+    is bitwise identical."""
+    cfg = get_config("wav2vec2-large")
+    sd = synth_weights(cfg)
+    x = synth.batch(32000, 2, start=60)
+    out = {}
+    for planes in ("1", "0"):
+        monkeypatch.setenv("SUTA_BF16_PLANES", planes)
+        eng = SutaEngine(cfg, sd, max_batch=2, max_samples=32000)
+        eng.set_precision("bf16")
+        a, _, _ = eng.adapt(x, 3, SutaHParams(), record=[0, 3])
+        b, _, _ = eng.adapt(x, 3, SutaHParams(), record=[0, 3])
+        assert np.array_equal(a[3], b[3]), planes
+        out[planes] = a
+        eng.close()
+    for r in (0, 3):
+        for u in range(2):
+            assert_bf16_close(out["1"][r][u], out["0"][r][u], 0.97, f"planes vs fp32-staged step {r} utt {u}",
+                              rtol=BF16_LOGITS_RTOL_LARGE)
