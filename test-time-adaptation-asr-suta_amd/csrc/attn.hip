@@ -38,7 +38,9 @@ namespace {
 typedef __bf16 fbf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 fbf16x4 __attribute__((ext_vector_type(4)));
 
-constexpr int FA_LD = 68;   // [row][64] tiles: 16-B rows padded by 4 floats (conflict-free row reads)
+// [row][64] tiles padded to 72 floats: 16-B row reads of 8 consecutive rows hit 8 distinct 4-bank groups,
+// and the column reads of rows r and r + 4 (lane halves of apply_rows) land 32 banks apart
+constexpr int FA_LD = 72;
 constexpr int FA_LDT = 36;  // [64][32] transposed tiles
 
 __device__ __forceinline__ fbf16x8 cvt8(f32x4 lo, f32x4 hi) {
@@ -204,26 +206,36 @@ __global__ __launch_bounds__(NW * 64) void flash_fwd_kernel(const float* __restr
     RowReg<BF16> qv;
     qv.load(Qb + (long)min(q0 + l32, T - 1) * ld, h);
 
+    // K: 16 lanes per row (coalesced, row-major image).  V: a wave-instruction covers 16 keys x 4 column
+    // chunks, so the transposed 4-byte writes (c4 + e) * FK_LDT + key hit 64 distinct banks
+    // (FK_LDT = 68 = 4 mod 64) -- the row-per-16-lanes map was a 4-way conflict on every V write
+    auto vmap = [](int it, int& key, int& c4) {
+        const int l = it & 63, wi = it >> 6;
+        key = (l & 15) + 16 * (wi & 3);
+        c4 = 4 * ((l >> 4) + 4 * (wi >> 2));
+    };
     f32x4 kr[NPT], vr[NPT];
     auto fetch = [&](int kt) {
 #pragma unroll
         for (int n = 0; n < NPT; ++n) {
             const int it = threadIdx.x + n * NT, row = it >> 4, c4 = (it & 15) * 4, key = kt * FK + row;
+            int vk, vc;
+            vmap(it, vk, vc);
             kr[n] = vr[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (it < ITEMS && key < T) {
-                kr[n] = *reinterpret_cast<const f32x4*>(Kb + (long)key * ld + c4);
-                vr[n] = *reinterpret_cast<const f32x4*>(Vb + (long)key * ld + c4);
-            }
+            if (it < ITEMS && key < T) kr[n] = *reinterpret_cast<const f32x4*>(Kb + (long)key * ld + c4);
+            if (it < ITEMS && kt * FK + vk < T) vr[n] = *reinterpret_cast<const f32x4*>(Vb + (long)(kt * FK + vk) * ld + vc);
         }
     };
     auto put = [&](int buf) {
 #pragma unroll
         for (int n = 0; n < NPT; ++n) {
             const int it = threadIdx.x + n * NT, row = it >> 4, c4 = (it & 15) * 4;
+            int vk, vc;
+            vmap(it, vk, vc);
             if (it < ITEMS) {
                 *reinterpret_cast<f32x4*>(&Ks[buf][row * FA_LD + c4]) = kr[n];
 #pragma unroll
-                for (int e = 0; e < 4; ++e) Vt[buf][(c4 + e) * FK_LDT + row] = vr[n][e];
+                for (int e = 0; e < 4; ++e) Vt[buf][(vc + e) * FK_LDT + vk] = vr[n][e];
             }
         }
     };
