@@ -45,3 +45,21 @@ def librispeech(root, lengths=(6000, 9100, 7300, 12000, 4000), seed=12):
         by_dir.setdefault((d, f"{spk}-{ch}"), []).append(f"{name} " + " ".join(rng.choice(WORDS, size=2 + i)))
     for (d, stem), lines in by_dir.items():
         (d / f"{stem}.trans.txt").write_text("\n".join(lines) + "\n")
+
+
+def ted(root, lengths=(170000, 260000, 600000, 640000), seed=13):
+    """TED-LIUM 3 layout (reference corpus/ted.py:22-52): wav_segment/<id>.wav (16-bit mono 16 kHz) and
+    transcription/<id>.txt; long utterances (T = 531 .. 1874 frames; the last one is cut to 600 000
+    samples by the reader, reference data.py:19-22)."""
+    rng = np.random.default_rng(seed)
+    apath, tpath = root / "wav_segment", root / "transcription"
+    apath.mkdir(parents=True)
+    tpath.mkdir(parents=True)
+    for i, n in enumerate(lengths):
+        x = rng.standard_normal(n) * 0.1
+        with wave.open(str(apath / f"talk{i}.wav"), "wb") as f:
+            f.setnchannels(1)
+            f.setsampwidth(2)
+            f.setframerate(16000)
+            f.writeframes((np.clip(x, -1, 1) * 32767).astype("<i2").tobytes())
+        (tpath / f"talk{i}.txt").write_text(" ".join(rng.choice(WORDS, size=4 + 3 * i)) + "\n")

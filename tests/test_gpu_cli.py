@@ -159,3 +159,23 @@ def test_cli_librispeech_flac_ls_flags(tmp_path, capsys):
     ref = _oracle_counts(ds.file_list, ds.text, "wav2vec2-base", 10, 2e-5, extra_noise=0.01)
     for k, v in ref.items():
         assert tuple(counts[str(k)]) == v, k
+
+
+def test_cli_ted_long_utterances_ragged(tmp_path, capsys):
+    """Config C5's path on one GPU: a TED-layout corpus of long utterances (T = 531 .. 1874 frames, one
+    cut at the 600 000-sample cap) adapted by the driver as one ragged batch (--gpu_batch 64) on the
+    flash attention kernels; corpus WER counts equal the CPU oracle's."""
+    from tests import corpus_fixtures as CF
+    from suta_amd.data import TedDataset
+    CF.ted(tmp_path)
+    args = (f"--asr facebook/wav2vec2-base-960h --synthetic_weights --steps 3 --dataset_name ted "
+            f"--dataset_dir {tmp_path} --temp 2.5 --episodic --em_coef 0.3 --reweight --log_dir {tmp_path}/exps "
+            f"--lr 2e-5 --non_blank --train_feature --extra_noise 0 --gpu_batch 64").split()
+    counts = M.main(args)
+    out = capsys.readouterr().out
+    assert out.count("original WER: ") >= 4 and out.count("adapt-3 WER:") == 4
+    ds = TedDataset(None, 1, str(tmp_path))
+    assert len(ds.file_list) == 4
+    ref = _oracle_counts(ds.file_list, ds.text, "wav2vec2-base", 3, 2e-5)
+    for k, v in ref.items():
+        assert tuple(counts[str(k)]) == v, k
