@@ -324,15 +324,15 @@ __global__ __launch_bounds__(NW * 64) void flash_fwd_kernel(const float* __restr
 // ------------------------------------------------------------------------------------------------
 // backward
 // ------------------------------------------------------------------------------------------------
-// NW waves per block = NW key groups of 32.  Query tiles are single-buffered: the next tile's Q / dO /
-// LSE / delta are loaded into registers while the current tile computes and written to LDS right after
-// the barrier that completes the dS tile (the dQ product reads only dS and K^T), so one LDS image and
-// two barriers per tile suffice.  LDS: K^T [64][32 NW + 4] + dS [32][32 NW + 4] + Q, dO [32][68]:
-// NW = 4 -> 68 KB (two blocks per CU), NW = 8 -> 117 KB.
+// NW waves per block = NW key groups of 32.  Query tiles are double-buffered: the next tile's Q / dO /
+// LSE / delta are loaded into registers while the current tile computes and written to the other LDS
+// image after the dQ product (two barriers per tile).  LDS: K^T [64][32 NW + 4] + dS [32][32 NW + 4]
+// + 2 x (Q, dO [32][72]): NW = 8 -> 136 KB, NW = 4 -> 86 KB.  (A single-buffered form staged right after
+// the dS barrier measured equal in fp32 but spilled 132 B in the bf16 instantiation: 1.6x slower.)
 template <int NW>
 constexpr int fb_kbp() { return NW * 32 + 4; }
 template <int NW>
-constexpr size_t fb_lds_bytes() { return sizeof(float) * ((size_t)(64 + 32) * fb_kbp<NW>() + 2 * 32 * FA_LD + 64); }
+constexpr size_t fb_lds_bytes() { return sizeof(float) * ((size_t)(64 + 32) * fb_kbp<NW>() + 4 * 32 * FA_LD + 128); }
 
 template <int NW, bool BF16>
 __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void flash_bwd_kernel(
@@ -346,10 +346,10 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void flash_bwd_kernel(
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float* Kt = smem;                   // [64][KBP]: K of the block's keys, transposed
     float* Ss = Kt + 64 * KBP;          // [32][KBP]: dS of the current query tile
-    float* Qs = Ss + 32 * KBP;          // [32][FA_LD]
-    float* Ds = Qs + 32 * FA_LD;        // [32][FA_LD]  (dO = dctx rows)
-    float* Ls = Ds + 32 * FA_LD;        // [32] LSE
-    float* Dl = Ls + 32;                // [32] delta
+    float* Qs = Ss + 32 * KBP;          // [2][32][FA_LD]
+    float* Ds = Qs + 2 * 32 * FA_LD;    // [2][32][FA_LD]  (dO = dctx rows)
+    float* Ls = Ds + 2 * 32 * FA_LD;    // [2][32] LSE
+    float* Dl = Ls + 64;                // [2][32] delta
     const int id = xcd_block();
     const int kb = id % nkb, bh = id / nkb, hd = bh % NH, u = bh / NH;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, l32 = lane & 31, h = lane >> 5;
@@ -396,15 +396,15 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void flash_bwd_kernel(
         const int qq = qt * 32 + (threadIdx.x & 31);
         if (threadIdx.x < 64 && qq < T) lr = threadIdx.x < 32 ? lb[qq] : db[qq];
     };
-    auto put = [&]() {
+    auto put = [&](int buf) {
 #pragma unroll
         for (int n = 0; n < QPT; ++n) {
             const int it = threadIdx.x + n * NT, row = it >> 4, c4 = (it & 15) * 4;
-            *reinterpret_cast<f32x4*>(Qs + row * FA_LD + c4) = qr[n];
-            *reinterpret_cast<f32x4*>(Ds + row * FA_LD + c4) = orr[n];
+            *reinterpret_cast<f32x4*>(Qs + (buf * 32 + row) * FA_LD + c4) = qr[n];
+            *reinterpret_cast<f32x4*>(Ds + (buf * 32 + row) * FA_LD + c4) = orr[n];
         }
-        if (threadIdx.x < 32) Ls[threadIdx.x] = lr;
-        else if (threadIdx.x < 64) Dl[threadIdx.x - 32] = lr;
+        if (threadIdx.x < 32) Ls[buf * 32 + threadIdx.x] = lr;
+        else if (threadIdx.x < 64) Dl[buf * 32 + threadIdx.x - 32] = lr;
     };
 
     f32x16 dv[2], dk[2];
@@ -422,33 +422,36 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void flash_bwd_kernel(
         for (int r = 0; r < 32; ++r)
             if (h == 0) Ss[r * KBP + 32 * w + l32] = 0.f;
     fetch(0);
-    put();
+    put(0);
     __syncthreads();
     for (int qt = 0; qt < nqt; ++qt) {
-        const int q0 = qt * 32;
+        const int q0 = qt * 32, buf = qt & 1;
         if (qt + 1 < nqt) fetch(qt + 1);
+        const float* Qt = Qs + buf * 32 * FA_LD;
+        const float* Dt = Ds + buf * 32 * FA_LD;
+        const float* Lt = Ls + buf * 32;
+        const float* Dlt = Dl + buf * 32;
         if (active) {
             f32x16 s, dp;
 #pragma unroll
             for (int v = 0; v < 16; ++v) s[v] = dp[v] = 0.f;
-            prod_rows<BF16>(s, Qs, kv, l32, h);   // S[q][key]: query r8(v,h), key on the lane
-            prod_rows<BF16>(dp, Ds, vv, l32, h);  // dP[q][key]
+            prod_rows<BF16>(s, Qt, kv, l32, h);   // S[q][key]: query r8(v,h), key on the lane
+            prod_rows<BF16>(dp, Dt, vv, l32, h);  // dP[q][key]
             const bool kok = key < tl;
 #pragma unroll
             for (int v = 0; v < 16; ++v) {
                 const int r = r8(v, h);
                 const bool ok = kok && q0 + r < T;
-                const float p = ok ? __builtin_amdgcn_exp2f(sl2 * s[v] - LOG2E * Ls[r]) : 0.f;
+                const float p = ok ? __builtin_amdgcn_exp2f(sl2 * s[v] - LOG2E * Lt[r]) : 0.f;
                 s[v] = p;
-                dp[v] = scale * (p * (dp[v] - Dl[r]));
+                dp[v] = scale * (p * (dp[v] - Dlt[r]));
             }
-            apply_rows<BF16>(dv, Ds, s, l32, h);   // dV^T[n][key] += sum_q dO[q][n] P[q][key]
-            apply_rows<BF16>(dk, Qs, dp, l32, h);  // dK^T[d][key] += sum_q Q[q][d] dS[q][key]
+            apply_rows<BF16>(dv, Dt, s, l32, h);   // dV^T[n][key] += sum_q dO[q][n] P[q][key]
+            apply_rows<BF16>(dk, Qt, dp, l32, h);  // dK^T[d][key] += sum_q Q[q][d] dS[q][key]
 #pragma unroll
             for (int v = 0; v < 16; ++v) Ss[r8(v, h) * KBP + 32 * w + l32] = dp[v];
         }
-        __syncthreads();  // dS tile complete; every wave is done with this tile's Q / dO / LSE / delta
-        if (qt + 1 < nqt) put();
+        __syncthreads();  // dS tile complete
 #pragma unroll
         for (int j = 0; j < SUB; ++j) {  // dQ partial of this key block: dQ[q][d] = sum_key dS[q][key] K[key][d]
             const int st = w * SUB + j, qi = st & 1, di = st >> 1;
@@ -481,6 +484,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void flash_bwd_kernel(
             for (int r = 0; r < 4; ++r)
                 if (q0 + 16 * qi + 4 * g + r < T) dr[r * 64] = c0[r] + c1[r];
         }
+        if (qt + 1 < nqt) put(buf ^ 1);
         __syncthreads();  // next tile visible; dS tile free
     }
     // dK, dV rows of this wave's keys (0 past the length): lane = key, registers = 4 consecutive columns

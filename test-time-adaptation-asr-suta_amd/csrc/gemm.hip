@@ -146,7 +146,7 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
     p.ws = ws;
     dim3 grid(gx, gy, p.Z * splits);
     if (hb) {
-        gemm_run_hb(tile, g_force_tile >= 0 && g_nbuf == 3 ? 3 : 2, p, grid, st);
+        gemm_run_hb(tile, g_force_tile >= 0 ? g_nbuf : 2, p, grid, st);
     } else if (p.mode == 2) {
         // bf16: register-staged one-plane kernel; weight gradients (and benchmark variants 3 / 8) on
         // register-converted LDS-DMA stages (8 = BK64 x 2)

@@ -1,15 +1,32 @@
 // bf16 GEMM on bf16 operand planes (LDS-DMA staging, 64-deep K-steps) + the fp32 -> bf16 plane conversion.
 #include "gemm_kernels.h"
 
+// ns: 2 (default) | 3 = three LDS stages | 4 = 128-deep bf16 K-steps, two stages (benchmark variants,
+// tools/hb_bench); tile 4 = 256x128, 5 = 128x256 (benchmark only)
 void gemm_run_hb(int tile, int ns, const GemmParams& p, dim3 grid, hipStream_t st) {
+    if (tile == 4) {
+        launch_hb<256, 128, 2>(p, grid, st);
+        return;
+    }
+    if (tile == 5) {
+        launch_hb<128, 256, 2>(p, grid, st);
+        return;
+    }
+    if (ns == 4) {
+        if (tile == 0) launch_hb<128, 128, 2, 64>(p, grid, st);
+        else if (tile == 1) launch_hb<128, 64, 2, 64>(p, grid, st);
+        else if (tile == 2) launch_hb<64, 128, 2, 64>(p, grid, st);
+        else launch_hb<64, 64, 2, 64>(p, grid, st);
+        return;
+    }
     if (ns == 3) {
-        if (tile == 0 || tile == 4) launch_hb<128, 128, 3>(p, grid, st);
+        if (tile == 0) launch_hb<128, 128, 3>(p, grid, st);
         else if (tile == 1) launch_hb<128, 64, 3>(p, grid, st);
         else if (tile == 2) launch_hb<64, 128, 3>(p, grid, st);
         else launch_hb<64, 64, 3>(p, grid, st);
         return;
     }
-    if (tile == 0 || tile == 4) launch_hb<128, 128, 2>(p, grid, st);  // (256x128 spills at one block per CU)
+    if (tile == 0) launch_hb<128, 128, 2>(p, grid, st);
     else if (tile == 1) launch_hb<128, 64, 2>(p, grid, st);
     else if (tile == 2) launch_hb<64, 128, 2>(p, grid, st);
     else launch_hb<64, 64, 2>(p, grid, st);

@@ -1293,9 +1293,8 @@ void launch_tile(const GemmParams& p, dim3 grid, hipStream_t st) {
 // row l % 32, k = 16 kc + 8 (l / 32) + [0, 8) = one 16-B chunk), the fp32 epilogue of every kernel.
 // Half the operand bytes of the fp32-staged bf16 kernels, no conversion in the K-loop.
 // ============================================================================================
-template <int BM, int BN, int NS>
-__global__ __launch_bounds__(256, BM * BN > 128 * 128 ? 1 : 2) void gemm_hb_kernel(GemmParams p) {
-    constexpr int BKS = 32;                      // stage depth in 4-byte units (= 64 bf16)
+template <int BM, int BN, int NS, int BKS = 32>  // BKS: stage depth in 4-byte units (32 = 64 bf16)
+__global__ __launch_bounds__(256, BM * BN > 128 * 128 || BKS > 32 ? 1 : 2) void gemm_hb_kernel(GemmParams p) {
     constexpr int WTM = BM / 2, WTN = BN / 2;
     constexpr int RM = WTM / 32, RN = WTN / 32;
     constexpr int STAGE = (BM + BN) * BKS;       // 4-byte units per LDS stage
@@ -1365,6 +1364,7 @@ __global__ __launch_bounds__(256, BM * BN > 128 * 128 ? 1 : 2) void gemm_hb_kern
 #pragma unroll
                 for (int j = 0; j < RN; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+            if (RM * RN > 4) __builtin_amdgcn_sched_barrier(0);  // big tiles: bound the fragment reads hoisted ahead
         }
     };
 
@@ -1386,9 +1386,9 @@ __global__ __launch_bounds__(256, BM * BN > 128 * 128 ? 1 : 2) void gemm_hb_kern
                                      m0 + BM <= p.M && n0 + BN <= p.N, tid.z);
 }
 
-template <int BM, int BN, int NS>
+template <int BM, int BN, int NS, int BKS = 32>
 void launch_hb(const GemmParams& p, dim3 grid, hipStream_t st) {
-    hipLaunchKernelGGL((gemm_hb_kernel<BM, BN, NS>), grid, dim3(256), 0, st, p);
+    hipLaunchKernelGGL((gemm_hb_kernel<BM, BN, NS, BKS>), grid, dim3(256), 0, st, p);
 }
 
 }  // namespace
