@@ -128,8 +128,8 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
                      : p.mode == 2   ? choose_tile_bf16(p.M, p.N, p.Z, !bf16_gbf)
                                      : choose_tile(p.M, p.N, p.Z, p.K, p.mode);
     // tiles 0 = 128x128, 1 = 128x64, 2 = 64x128, 3 = 64x64; bf16 mode also 4 = 256x128, 5 = 128x256
-    const int BM = tile == 4 ? 256 : (tile == 0 || tile == 1 || tile == 5) ? 128 : 64;
-    const int BN = tile == 5 ? 256 : (tile == 0 || tile == 2 || tile == 4) ? 128 : 64;
+    const int BM = (tile == 4 || tile == 6) ? 256 : (tile == 0 || tile == 1 || tile == 5) ? 128 : 64;
+    const int BN = (tile == 5 || tile == 6) ? 256 : (tile == 0 || tile == 2 || tile == 4) ? 128 : 64;
     const int gx = (p.N + BN - 1) / BN, gy = (p.M + BM - 1) / BM;
     const long blocks = (long)gx * gy * p.Z;
 

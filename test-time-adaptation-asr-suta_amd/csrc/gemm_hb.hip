@@ -12,6 +12,7 @@ void gemm_run_hb(int tile, int ns, const GemmParams& p, dim3 grid, hipStream_t s
         launch_hb<128, 256, 2>(p, grid, st);
         return;
     }
+
     if (ns == 4) {
         if (tile == 0) launch_hb<128, 128, 2, 64>(p, grid, st);
         else if (tile == 1) launch_hb<128, 64, 2, 64>(p, grid, st);

@@ -863,15 +863,15 @@ __device__ __forceinline__ int glds_swz(int row) {
 //   KC = true : element (row, k) at src[row*ld + k]     (MODE 1: conv-A row shift, MODE 2: segmented)
 //   KC = false: element (row, k) at src[k*ld + row]
 // dummy: load the zero page (keeps the per-wave DMA count uniform past the last K-step).
-template <int ROWS, int BKS, bool KC, int MODE>
+template <int ROWS, int BKS, bool KC, int MODE, int NWV = 4>
 __device__ __forceinline__ void glds_stage(float* dst, const float* __restrict__ src, long ld, int row0, int nrows,
                                            int k0, int kend, int segK, int pad, int Mvalid, long sseg, int w,
                                            int lane, bool dummy) {
-    constexpr int NI = ROWS * BKS / 1024;  // wave-instructions per wave (ROWS * BKS * 4 B / 1 KiB / 4 waves)
-    static_assert(NI >= 1, "stage too small for 4 waves");
+    constexpr int NI = ROWS * BKS / (256 * NWV);  // wave-instructions per wave (1 KiB each, NWV waves)
+    static_assert(NI >= 1, "stage too small for the block's waves");
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-        const int ci = i * 4 + w;  // 1-KiB piece of the stage image
+        const int ci = i * NWV + w;  // 1-KiB piece of the stage image
         const float* g = g_zero16;
         if (!dummy) {
             if (KC) {
@@ -906,16 +906,16 @@ __device__ __forceinline__ void glds_stage(float* dst, const float* __restrict__
 // K-loop issues NI global_load_lds per operand with no address arithmetic beyond one add.  Lanes
 // outside the operand point at the zero page and never move.  Valid for full stages (k + BKS <= kend);
 // a partial last stage goes through glds_stage.
-template <int ROWS, int BKS, bool KC>
+template <int ROWS, int BKS, bool KC, int NWV = 4>
 struct GldsStream {
-    static constexpr int NI = ROWS * BKS / 1024;
+    static constexpr int NI = ROWS * BKS / (256 * NWV);
     const float* ptr[NI];
     int inc[NI];  // floats per K-step (0 on zero-page lanes)
     __device__ __forceinline__ void init(const float* __restrict__ src, long ld, int row0, int nrows, int k0, int w,
                                          int lane) {
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
-            const int ci = i * 4 + w;
+            const int ci = i * NWV + w;
             bool ok;
             const float* g;
             if (KC) {
@@ -938,12 +938,12 @@ struct GldsStream {
 
 // one full stage of a GldsStream operand (free function: a member-function form of this builtin call
 // made hipcc's host pass drop the kernels' launch stubs)
-template <int ROWS, int BKS, bool KC>
-__device__ __forceinline__ void glds_stream_issue(GldsStream<ROWS, BKS, KC>& sm, float* dst, int w) {
+template <int ROWS, int BKS, bool KC, int NWV>
+__device__ __forceinline__ void glds_stream_issue(GldsStream<ROWS, BKS, KC, NWV>& sm, float* dst, int w) {
 #pragma unroll
-    for (int i = 0; i < GldsStream<ROWS, BKS, KC>::NI; ++i) {
+    for (int i = 0; i < GldsStream<ROWS, BKS, KC, NWV>::NI; ++i) {
         const float* g = sm.ptr[i];
-        __builtin_amdgcn_global_load_lds(g, (lds_ptr_t)(dst + (i * 4 + w) * 256), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(g, (lds_ptr_t)(dst + (i * NWV + w) * 256), 16, 0, 0);
         sm.ptr[i] = g + sm.inc[i];
     }
 }
@@ -1293,12 +1293,14 @@ void launch_tile(const GemmParams& p, dim3 grid, hipStream_t st) {
 // row l % 32, k = 16 kc + 8 (l / 32) + [0, 8) = one 16-B chunk), the fp32 epilogue of every kernel.
 // Half the operand bytes of the fp32-staged bf16 kernels, no conversion in the K-loop.
 // ============================================================================================
-template <int BM, int BN, int NS, int BKS = 32>  // BKS: stage depth in 4-byte units (32 = 64 bf16)
-__global__ __launch_bounds__(256, BM * BN > 128 * 128 || BKS > 32 ? 1 : 2) void gemm_hb_kernel(GemmParams p) {
-    constexpr int WTM = BM / 2, WTN = BN / 2;
+// NWV = 4 waves (2 x 2) or 8 waves (2 x 4, the 256 x 256 tile: 128 x 64 per wave, 128 KB of LDS)
+template <int BM, int BN, int NS, int BKS = 32, int NWV = 4>  // BKS: stage depth in 4-byte units (32 = 64 bf16)
+__global__ __launch_bounds__(64 * NWV, (BM * BN > 128 * 128 || BKS > 32) ? 1 : 2) void gemm_hb_kernel(GemmParams p) {
+    constexpr int WNW = NWV / 2;                 // waves along N
+    constexpr int WTM = BM / 2, WTN = BN / WNW;
     constexpr int RM = WTM / 32, RN = WTN / 32;
     constexpr int STAGE = (BM + BN) * BKS;       // 4-byte units per LDS stage
-    constexpr int NPW = (BM + BN) * BKS / 1024;  // DMA instructions per wave per stage
+    constexpr int NPW = (BM + BN) * BKS / (256 * NWV);  // DMA instructions per wave per stage
     __shared__ __attribute__((aligned(16))) float smem[NS * STAGE];
 
     const TileId tid = xcd_tile();
@@ -1314,7 +1316,7 @@ __global__ __launch_bounds__(256, BM * BN > 128 * 128 || BKS > 32 ? 1 : 2) void 
 
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wm = wid >> 1, wn = wid & 1;
+    const int wm = wid / WNW, wn = wid % WNW;
     const int h = lane >> 5, l32 = lane & 31;
 
     f32x16 acc[RM][RN];
@@ -1325,8 +1327,8 @@ __global__ __launch_bounds__(256, BM * BN > 128 * 128 || BKS > 32 ? 1 : 2) void 
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    GldsStream<BM, BKS, true> sa;
-    GldsStream<BN, BKS, true> sb;
+    GldsStream<BM, BKS, true, NWV> sa;
+    GldsStream<BN, BKS, true, NWV> sb;
     sa.init(A, lda, m0, p.M, kbeg, wid, lane);
     sb.init(B, ldb, n0, p.N, kbeg, wid, lane);
     auto issue = [&](int s) {
@@ -1334,15 +1336,15 @@ __global__ __launch_bounds__(256, BM * BN > 128 * 128 || BKS > 32 ? 1 : 2) void 
         const int k = kbeg + s * BKS;
         if (s >= nst) {
             if (NS > 2) {  // keep the per-wave DMA count uniform past the last stage
-                glds_stage<BM, BKS, true, 0>(st, A, lda, m0, p.M, k, kend, 0, 0, 0, 0, wid, lane, true);
-                glds_stage<BN, BKS, true, 0>(st + BM * BKS, B, ldb, n0, p.N, k, kend, 0, 0, 0, 0, wid, lane, true);
+                glds_stage<BM, BKS, true, 0, NWV>(st, A, lda, m0, p.M, k, kend, 0, 0, 0, 0, wid, lane, true);
+                glds_stage<BN, BKS, true, 0, NWV>(st + BM * BKS, B, ldb, n0, p.N, k, kend, 0, 0, 0, 0, wid, lane, true);
             }
         } else if (k + BKS <= kend) {
             glds_stream_issue(sa, st, wid);
             glds_stream_issue(sb, st + BM * BKS, wid);
         } else {
-            glds_stage<BM, BKS, true, 0>(st, A, lda, m0, p.M, k, kend, 0, 0, 0, 0, wid, lane, false);
-            glds_stage<BN, BKS, true, 0>(st + BM * BKS, B, ldb, n0, p.N, k, kend, 0, 0, 0, 0, wid, lane, false);
+            glds_stage<BM, BKS, true, 0, NWV>(st, A, lda, m0, p.M, k, kend, 0, 0, 0, 0, wid, lane, false);
+            glds_stage<BN, BKS, true, 0, NWV>(st + BM * BKS, B, ldb, n0, p.N, k, kend, 0, 0, 0, 0, wid, lane, false);
         }
     };
     auto frag = [&](const float* lds, int row, int kc) {
@@ -1386,9 +1388,9 @@ __global__ __launch_bounds__(256, BM * BN > 128 * 128 || BKS > 32 ? 1 : 2) void 
                                      m0 + BM <= p.M && n0 + BN <= p.N, tid.z);
 }
 
-template <int BM, int BN, int NS, int BKS = 32>
+template <int BM, int BN, int NS, int BKS = 32, int NWV = 4>
 void launch_hb(const GemmParams& p, dim3 grid, hipStream_t st) {
-    hipLaunchKernelGGL((gemm_hb_kernel<BM, BN, NS, BKS>), grid, dim3(256), 0, st, p);
+    hipLaunchKernelGGL((gemm_hb_kernel<BM, BN, NS, BKS, NWV>), grid, dim3(64 * NWV), 0, st, p);
 }
 
 }  // namespace

@@ -43,10 +43,11 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    const int tiles[] = {0, 4};
+    const int variants[][2] = {{0, 2}, {0, 3}, {0, 4}, {4, 2}, {5, 2}};  // (tile, ns)  // (tile, ns) -- gemm_run_hb
     for (auto& s : shapes) {
-        for (int ti : tiles)
-            for (int ns = 2; ns <= 3; ++ns) {
+        for (auto& vt : variants) {
+            const int ti = vt[0], ns = vt[1];
+            {
                 GemmParams p;
                 gemm_init(p);
                 p.mode = 2;
@@ -79,6 +80,7 @@ int main(int argc, char** argv) {
                 printf("%s tile %d ns %d: %.4f ms %.1f TF maxerr %.2e\n", s.name, ti, ns, ms, tf, err);
                 fflush(stdout);
             }
+    }
     }
     return 0;
 }
