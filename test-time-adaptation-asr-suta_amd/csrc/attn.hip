@@ -182,6 +182,7 @@ constexpr float LOG2E = 1.4426950408889634f;
 // ------------------------------------------------------------------------------------------------
 constexpr int FK = 64;
 constexpr int FK_LDT = FK + 4;  // transposed V tile row stride
+constexpr int FF_NW_BF = 4;     // waves per block of the bf16 forward
 
 template <int NW, bool BF16>
 __global__ __launch_bounds__(NW * 64) void flash_fwd_kernel(const float* __restrict__ qkv, float* __restrict__ ctx,
@@ -517,6 +518,355 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void flash_bwd_kernel(
         }
 }
 
+// ------------------------------------------------------------------------------------------------
+// bf16 mode (config C4): the same two kernels with every LDS image in bf16.  The bf16 MFMAs are 16x the
+// fp32 rate, so the fp32-image forms were bound by LDS bytes and the per-element conversions (each
+// product read fp32 rows and converted them in registers, the transposed contractions 8 scalar reads per
+// MFMA).  Here the staging pass rounds once (RNE, the same rounding the MFMA operands had), row images
+// feed 16-B fragment reads and transposed images 8-B reads of 4 consecutive contraction rows.
+// ------------------------------------------------------------------------------------------------
+typedef __bf16 fbf16x2 __attribute__((ext_vector_type(2)));
+constexpr int FB_RS = 72;  // bf16 row image [row][64 + 8]: 144-B rows, 8 consecutive rows on distinct banks
+
+__device__ __forceinline__ fbf16x4 cvt4(f32x4 v) {
+    fbf16x4 b;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) b[e] = (__bf16)v[e];
+    return b;
+}
+
+// acc[r8(v,h)][l32] += sum_d L[i][d] X[l32][d], L a bf16 row image (stride FB_RS), X the lane's bf16 row
+__device__ __forceinline__ void prod_rows_b(f32x16& acc, const __bf16* __restrict__ L, const RowReg<true>& x, int l32,
+                                            int h) {
+    const __bf16* lr = L + l32 * FB_RS + 8 * h;
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const fbf16x8*>(lr + 16 * s), x.v[s], acc, 0,
+                                                      0, 0);
+}
+
+// o[t][32t + r8(v,h)][l32] += sum_r L[r][n] pv[r], L given transposed (Lt[n][r], stride LDT bf16): MFMA c
+// takes rows 16c + 4h + 0..3 and 16c + 8 + 4h + 0..3 (accumulator registers 8c .. 8c + 7)
+template <int LDT>
+__device__ __forceinline__ void apply_cols_b(f32x16 (&o)[2], const __bf16* __restrict__ Lt, const f32x16& pv, int l32,
+                                             int h) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        fbf16x8 b;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) b[j] = (__bf16)pv[8 * c + j];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const __bf16* lr = Lt + (32 * t + l32) * LDT + 16 * c + 4 * h;
+            const fbf16x4 lo = *reinterpret_cast<const fbf16x4*>(lr), hi = *reinterpret_cast<const fbf16x4*>(lr + 8);
+            fbf16x8 a;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                a[j] = lo[j];
+                a[4 + j] = hi[j];
+            }
+            o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, o[t], 0, 0, 0);
+        }
+    }
+}
+
+constexpr int FBK_LDT = FK + 8;  // transposed bf16 V image [64][64 keys + 8]
+
+__global__ __launch_bounds__(FF_NW_BF * 64) void flash_fwd_bf16_kernel(
+    const float* __restrict__ qkv, float* __restrict__ ctx, float* __restrict__ lse, int T, int NH, int H, float scale,
+    const int* __restrict__ tlen, int nqb, __bf16* __restrict__ ctxb) {
+    constexpr int NW = FF_NW_BF, NT = NW * 64;
+    constexpr int ITEMS = FK * 16, NPT = (ITEMS + NT - 1) / NT;
+    __shared__ __attribute__((aligned(16))) __bf16 Ks[2][FK * FB_RS];
+    __shared__ __attribute__((aligned(16))) __bf16 Vt[2][64 * FBK_LDT];
+    const int id = xcd_block();
+    const int qb = id % nqb, bh = id / nqb, hd = bh % NH, u = bh / NH;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, l32 = lane & 31, h = lane >> 5;
+    const int tl = tlen ? tlen[u] : T;
+    const long ld = 3L * H;
+    const float* Qb = qkv + (long)u * T * ld + hd * 64;
+    const float* Kb = Qb + H;
+    const float* Vb = Qb + 2 * H;
+    const int q0 = (qb * NW + w) * 32;
+    const bool active = q0 < T;
+    const float sl2 = scale * LOG2E;
+    RowReg<true> qv;
+    qv.load(Qb + (long)min(q0 + l32, T - 1) * ld, h);
+    auto vmap = [](int it, int& key, int& c4) {
+        const int l = it & 63, wi = it >> 6;
+        key = (l & 15) + 16 * (wi & 3);
+        c4 = 4 * ((l >> 4) + 4 * (wi >> 2));
+    };
+    f32x4 kr[NPT], vr[NPT];
+    auto fetch = [&](int kt) {
+#pragma unroll
+        for (int n = 0; n < NPT; ++n) {
+            const int it = threadIdx.x + n * NT, row = it >> 4, c4 = (it & 15) * 4, key = kt * FK + row;
+            int vk, vc;
+            vmap(it, vk, vc);
+            kr[n] = vr[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (it < ITEMS && key < T) kr[n] = *reinterpret_cast<const f32x4*>(Kb + (long)key * ld + c4);
+            if (it < ITEMS && kt * FK + vk < T) vr[n] = *reinterpret_cast<const f32x4*>(Vb + (long)(kt * FK + vk) * ld + vc);
+        }
+    };
+    auto put = [&](int buf) {
+#pragma unroll
+        for (int n = 0; n < NPT; ++n) {
+            const int it = threadIdx.x + n * NT, row = it >> 4, c4 = (it & 15) * 4;
+            int vk, vc;
+            vmap(it, vk, vc);
+            if (it < ITEMS) {
+                *reinterpret_cast<fbf16x4*>(&Ks[buf][row * FB_RS + c4]) = cvt4(kr[n]);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) Vt[buf][(vc + e) * FBK_LDT + vk] = (__bf16)vr[n][e];
+            }
+        }
+    };
+    const int nkt = (tl + FK - 1) / FK;
+    f32x16 o[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) o[t][v] = 0.f;
+    float m_run = -INFINITY, l_run = 0.f;
+    fetch(0);
+    put(0);
+    __syncthreads();
+    for (int kt = 0; kt < nkt; ++kt) {
+        const int buf = kt & 1;
+        if (kt + 1 < nkt) fetch(kt + 1);
+        if (active) {
+            f32x16 s[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+#pragma unroll
+                for (int v = 0; v < 16; ++v) s[j][v] = 0.f;
+                prod_rows_b(s[j], Ks[buf] + 32 * j * FB_RS, qv, l32, h);
+            }
+            float mx = -INFINITY;
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int v = 0; v < 16; ++v) {
+                    const bool ok = kt * FK + 32 * j + r8(v, h) < tl;
+                    s[j][v] = ok ? sl2 * s[j][v] : -INFINITY;
+                    mx = fmaxf(mx, s[j][v]);
+                }
+            mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+            const float m_new = fmaxf(m_run, mx);
+            float ls = 0.f;
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int v = 0; v < 16; ++v) {
+                    s[j][v] = __builtin_amdgcn_exp2f(s[j][v] - m_new);
+                    ls += s[j][v];
+                }
+            if (m_new != m_run) {
+                const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+                l_run *= alpha;
+#pragma unroll
+                for (int t = 0; t < 2; ++t)
+#pragma unroll
+                    for (int v = 0; v < 16; ++v) o[t][v] *= alpha;
+                m_run = m_new;
+            }
+            l_run += ls;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) apply_cols_b<FBK_LDT>(o, Vt[buf] + 32 * j, s[j], l32, h);
+        }
+        if (kt + 1 < nkt) put(buf ^ 1);
+        __syncthreads();
+    }
+    if (!active) return;
+    const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+    const int q = q0 + l32;
+    if (q >= T) return;
+    const float inv = 1.0f / l_tot;
+    float* cr = ctx + ((long)u * T + q) * H + hd * 64 + 4 * h;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+            f32x4 r;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) r[b] = o[t][4 * a + b] * inv;
+            *reinterpret_cast<f32x4*>(cr + 32 * t + 8 * a) = r;
+            if (ctxb)
+                *reinterpret_cast<fbf16x4*>(ctxb + ((long)u * T + q) * H + hd * 64 + 4 * h + 32 * t + 8 * a) = cvt4(r);
+        }
+    if (h == 0) lse[(long)bh * T + q] = (m_run + log2f(l_tot)) * (1.0f / LOG2E);
+}
+
+// backward, bf16 images: Q / dO tiles row-major (S, dP) and transposed (dV, dK), dS and K^T in bf16
+constexpr int FBB_NW = 8;
+constexpr int FBB_KB = FBB_NW * 32 + 8;   // bf16 row stride of the dS tile and the K^T image
+constexpr int FBB_QT = 32 + 8;            // bf16 row stride of the transposed Q / dO tiles
+constexpr size_t fbb_lds_bytes() {
+    return 2 * ((size_t)(64 + 32) * FBB_KB + 2 * (2 * 32 * FB_RS + 2 * 64 * FBB_QT)) + 4 * 128;
+}
+
+__global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16_kernel(
+    const float* __restrict__ qkv, const float* __restrict__ dctx, const float* __restrict__ lse,
+    const float* __restrict__ delta, float* __restrict__ dqkv, float* __restrict__ dqp, int T, int NH, int H,
+    float scale, const int* __restrict__ tlen, int nkb, int gpb, int B, __bf16* __restrict__ dqkvb) {
+    constexpr int NW = FBB_NW, NT = NW * 64;
+    constexpr int QPT = 512 / NT;
+    extern __shared__ __attribute__((aligned(16))) __bf16 sm16[];
+    __bf16* Kt = sm16;                            // [64][FBB_KB]
+    __bf16* Ss = Kt + 64 * FBB_KB;                // [32][FBB_KB]
+    __bf16* Qr = Ss + 32 * FBB_KB;                // [2][32][FB_RS]   Q rows
+    __bf16* Dr = Qr + 2 * 32 * FB_RS;             // [2][32][FB_RS]   dO rows
+    __bf16* Qc = Dr + 2 * 32 * FB_RS;             // [2][64][FBB_QT]  Q transposed
+    __bf16* Dc = Qc + 2 * 64 * FBB_QT;            // [2][64][FBB_QT]  dO transposed
+    float* Ls = reinterpret_cast<float*>(Dc + 2 * 64 * FBB_QT);  // [2][32]
+    float* Dl = Ls + 64;                          // [2][32]
+    const int id = xcd_block();
+    const int kb = id % nkb, bh = id / nkb, hd = bh % NH, u = bh / NH;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, l32 = lane & 31, h = lane >> 5;
+    const int tl = tlen ? tlen[u] : T;
+    const int ng = (T + 31) >> 5;
+    const int g0 = kb * gpb, ngb = min(gpb, ng - g0);
+    const int kbase = g0 * 32;
+    const long ld = 3L * H;
+    const float* Qb = qkv + (long)u * T * ld + hd * 64;
+    const float* Kb = Qb + H;
+    const float* Vb = Qb + 2 * H;
+    const float* Ob = dctx + (long)u * T * H + hd * 64;
+    const float* lb = lse + (long)bh * T;
+    const float* db = delta + (long)bh * T;
+    const bool active = w < ngb && kbase + 32 * w < tl;
+    const int key = kbase + 32 * w + l32;
+    const float sl2 = scale * LOG2E;
+    RowReg<true> kv, vv;
+    kv.load(Kb + (long)min(key, T - 1) * ld, h);
+    vv.load(Vb + (long)min(key, T - 1) * ld, h);
+    for (int it = threadIdx.x; it < ngb * 32 * 16; it += NT) {
+        const int row = it >> 4, c4 = (it & 15) * 4, k = kbase + row;
+        f32x4 x = {0.f, 0.f, 0.f, 0.f};
+        if (k < T) x = *reinterpret_cast<const f32x4*>(Kb + (long)k * ld + c4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) Kt[(c4 + e) * FBB_KB + row] = (__bf16)x[e];
+    }
+    f32x4 qr[QPT], orr[QPT];
+    float lr = 0.f;
+    auto fetch = [&](int qt) {
+#pragma unroll
+        for (int n = 0; n < QPT; ++n) {
+            const int it = threadIdx.x + n * NT, row = it >> 4, c4 = (it & 15) * 4, q = qt * 32 + row;
+            qr[n] = orr[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (q < T) {
+                qr[n] = *reinterpret_cast<const f32x4*>(Qb + (long)q * ld + c4);
+                orr[n] = *reinterpret_cast<const f32x4*>(Ob + (long)q * H + c4);
+            }
+        }
+        lr = 0.f;
+        const int qq = qt * 32 + (threadIdx.x & 31);
+        if (threadIdx.x < 64 && qq < T) lr = threadIdx.x < 32 ? lb[qq] : db[qq];
+    };
+    auto put = [&](int buf) {
+#pragma unroll
+        for (int n = 0; n < QPT; ++n) {
+            const int it = threadIdx.x + n * NT, row = it >> 4, c4 = (it & 15) * 4;
+            *reinterpret_cast<fbf16x4*>(Qr + (buf * 32 + row) * FB_RS + c4) = cvt4(qr[n]);
+            *reinterpret_cast<fbf16x4*>(Dr + (buf * 32 + row) * FB_RS + c4) = cvt4(orr[n]);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                Qc[(buf * 64 + c4 + e) * FBB_QT + row] = (__bf16)qr[n][e];
+                Dc[(buf * 64 + c4 + e) * FBB_QT + row] = (__bf16)orr[n][e];
+            }
+        }
+        if (threadIdx.x < 32) Ls[buf * 32 + threadIdx.x] = lr;
+        else if (threadIdx.x < 64) Dl[buf * 32 + threadIdx.x - 32] = lr;
+    };
+    f32x16 dv[2], dk[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) dv[t][v] = dk[t][v] = 0.f;
+    const int g = lane >> 4, l16 = lane & 15;
+    const int qi = w & 1, di = w >> 1;
+    const int kq = ngb * 32;
+    const long dq_stride = (long)B * NH * T * 64;
+    float* dqb = dqp + kb * dq_stride + (long)bh * T * 64;
+    const int nqt = (tl + 31) >> 5;
+    if (!active && w < ngb)
+        for (int r = 0; r < 32; ++r)
+            if (h == 0) Ss[r * FBB_KB + 32 * w + l32] = (__bf16)0.f;
+    fetch(0);
+    put(0);
+    __syncthreads();
+    for (int qt = 0; qt < nqt; ++qt) {
+        const int q0 = qt * 32, buf = qt & 1;
+        if (qt + 1 < nqt) fetch(qt + 1);
+        const float* Lt = Ls + buf * 32;
+        const float* Dlt = Dl + buf * 32;
+        if (active) {
+            f32x16 s, dp;
+#pragma unroll
+            for (int v = 0; v < 16; ++v) s[v] = dp[v] = 0.f;
+            prod_rows_b(s, Qr + buf * 32 * FB_RS, kv, l32, h);
+            prod_rows_b(dp, Dr + buf * 32 * FB_RS, vv, l32, h);
+            const bool kok = key < tl;
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                const int r = r8(v, h);
+                const bool ok = kok && q0 + r < T;
+                const float p = ok ? __builtin_amdgcn_exp2f(sl2 * s[v] - LOG2E * Lt[r]) : 0.f;
+                s[v] = p;
+                dp[v] = scale * (p * (dp[v] - Dlt[r]));
+            }
+            apply_cols_b<FBB_QT>(dv, Dc + buf * 64 * FBB_QT, s, l32, h);   // dV^T += dO^T P
+            apply_cols_b<FBB_QT>(dk, Qc + buf * 64 * FBB_QT, dp, l32, h);  // dK^T += Q^T dS
+#pragma unroll
+            for (int v = 0; v < 16; ++v) Ss[r8(v, h) * FBB_KB + 32 * w + l32] = (__bf16)dp[v];
+        }
+        __syncthreads();  // dS tile complete
+        {
+            const __bf16* ar = Ss + (16 * qi + l16) * FBB_KB + 8 * g;
+            const __bf16* br = Kt + (16 * di + l16) * FBB_KB + 8 * g;
+            f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
+            int kc = 0;
+            for (; kc + 64 <= kq; kc += 64) {
+                c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const fbf16x8*>(ar + kc),
+                                                             *reinterpret_cast<const fbf16x8*>(br + kc), c0, 0, 0, 0);
+                c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const fbf16x8*>(ar + kc + 32),
+                                                             *reinterpret_cast<const fbf16x8*>(br + kc + 32), c1, 0, 0, 0);
+            }
+            if (kc < kq)
+                c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const fbf16x8*>(ar + kc),
+                                                             *reinterpret_cast<const fbf16x8*>(br + kc), c0, 0, 0, 0);
+            float* dr = dqb + (long)(q0 + 16 * qi + 4 * g) * 64 + 16 * di + l16;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (q0 + 16 * qi + 4 * g + r < T) dr[r * 64] = c0[r] + c1[r];
+        }
+        if (qt + 1 < nqt) put(buf ^ 1);
+        __syncthreads();
+    }
+    if (w >= ngb || key >= T) return;
+    float* dkr = dqkv + ((long)u * T + key) * ld + H + hd * 64 + 4 * h;
+    float* dvr = dkr + H;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+            f32x4 x, y;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                x[b] = dk[t][4 * a + b];
+                y[b] = dv[t][4 * a + b];
+            }
+            *reinterpret_cast<f32x4*>(dkr + 32 * t + 8 * a) = x;
+            *reinterpret_cast<f32x4*>(dvr + 32 * t + 8 * a) = y;
+            if (dqkvb) {
+                __bf16* kb2 = dqkvb + ((long)u * T + key) * ld + H + hd * 64 + 4 * h + 32 * t + 8 * a;
+                *reinterpret_cast<fbf16x4*>(kb2) = cvt4(x);
+                *reinterpret_cast<fbf16x4*>(kb2 + H) = cvt4(y);
+            }
+        }
+}
+
 // dQ = sum over key blocks in order (query rows < tl; rows past it get 0, as their dS is 0)
 __global__ __launch_bounds__(256) void flash_dq_reduce(const float* __restrict__ dqp, float* __restrict__ dqkv, int B,
                                                        int T, int NH, int H, int nkb, const int* __restrict__ tlen,
@@ -558,6 +908,13 @@ static int fb_nw() {
     return g_fb_nw;
 }
 
+// bf16 mode: LDS images in bf16 (flash_*_bf16_kernel; env SUTA_FLASH_BF16_IMG=0 selects the fp32-image
+// instantiations for A/B runs; read at every launch, so one process can run both)
+static bool fb_img() {
+    const char* e = std::getenv("SUTA_FLASH_BF16_IMG");
+    return !(e && atoi(e) == 0);
+}
+
 long flash_dq_scratch_floats(int B, int T, int NH) {
     const int ng = (T + 31) / 32, nkb = (ng + fb_nw() - 1) / fb_nw();
     return (long)nkb * B * NH * T * 64;
@@ -569,7 +926,11 @@ bool launch_flash_fwd(const float* qkv, float* ctx, float* lse, int B, int T, in
     if (dh != 64 || T < 1 || H % 4) return false;
     const int ng = (T + 31) / 32, nqb = (ng + FF_NW - 1) / FF_NW;
     const dim3 grid((unsigned)((long)B * NH * nqb));
-    if (bf16)
+    if (bf16 && fb_img()) {
+        static_assert(FF_NW_BF == FF_NW, "the bf16 forward shares the query-block grid");
+        hipLaunchKernelGGL(flash_fwd_bf16_kernel, grid, dim3(FF_NW_BF * 64), 0, st, qkv, ctx, lse, T, NH, H, scale,
+                           tlen, nqb, ctxb);
+    } else if (bf16)
         hipLaunchKernelGGL((flash_fwd_kernel<FF_NW, true>), grid, dim3(FF_NW * 64), 0, st, qkv, ctx, lse, T, NH, H,
                            scale, tlen, nqb, ctxb);
     else
@@ -604,7 +965,18 @@ bool launch_flash_bwd(const float* qkv, const float* dctx, const float* lse, con
     const int nkb = (ng + nw - 1) / nw;   // key blocks per head
     const int gpb = (ng + nkb - 1) / nkb;  // key groups per block (balanced)
     const dim3 grid((unsigned)((long)B * NH * nkb));
-    if (nw == 4) {
+    if (bf16 && nw == FBB_NW && fb_img()) {
+        constexpr size_t lds = fbb_lds_bytes();
+        static bool attr = false;
+        if (!attr) {
+            if (hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_bwd_bf16_kernel),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+                throw std::runtime_error("hipFuncSetAttribute(flash_bwd_bf16_kernel) failed");
+            attr = true;
+        }
+        hipLaunchKernelGGL(flash_bwd_bf16_kernel, grid, dim3(FBB_NW * 64), lds, st, qkv, dctx, lse, delta, dqkv, dqp,
+                           T, NH, H, scale, tlen, nkb, gpb, B, dqkvb);
+    } else if (nw == 4) {
         if (bf16) flash_bwd_go<4, true>(grid, st, qkv, dctx, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb);
         else flash_bwd_go<4, false>(grid, st, qkv, dctx, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb);
     } else {

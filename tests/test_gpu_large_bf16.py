@@ -129,3 +129,23 @@ def test_bf16_planes_equal_fp32_staged_path(monkeypatch):
         for u in range(2):
             assert_bf16_close(out["1"][r][u], out["0"][r][u], 0.97, f"planes vs fp32-staged step {r} utt {u}",
                               rtol=BF16_LOGITS_RTOL_LARGE)
+
+
+def test_bf16_flash_images_equal_fp32_image_kernels(monkeypatch):
+    """bf16 mode's flash kernels stage K / V / Q / dO / dS / K^T as bf16 LDS images (default) instead of
+    fp32 images converted per MFMA operand (SUTA_FLASH_BF16_IMG=0).  Same RNE roundings, same MFMA order
+    in the forward: step-0 logits bitwise equal; after backward steps only the dQ partial's summation
+    order differs, so adapted logits agree to bf16 tolerance.  Ragged pair, T = 399 and 239."""
+    cfg = get_config("wav2vec2-base")
+    eng = SutaEngine(cfg, synth_weights(cfg), max_batch=2, max_samples=128000)
+    eng.set_precision("bf16")
+    waves = [synth.wave(128000, 70), synth.wave(76800, 71)]
+    out = {}
+    for img in ("1", "0"):
+        monkeypatch.setenv("SUTA_FLASH_BF16_IMG", img)
+        out[img], _, _ = eng.adapt_varlen(waves, 3, SutaHParams(), record=[0, 3])
+    eng.close()
+    for u in range(2):
+        assert np.array_equal(out["1"][0][u], out["0"][0][u]), f"step 0 utt {u}"
+        assert_bf16_close(out["1"][3][u], out["0"][3][u], 0.97, f"bf16 images step 3 utt {u}",
+                          rtol=BF16_LOGITS_RTOL_LARGE)
