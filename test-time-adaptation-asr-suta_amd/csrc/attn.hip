@@ -255,12 +255,15 @@ __global__ __launch_bounds__(NW * 64) void flash_fwd_kernel(const float* __restr
         const int buf = kt & 1;
         if (kt + 1 < nkt) fetch(kt + 1);
         if (active) {
+            // the second 32-key half of a tile holding no valid key (the tail of the last tile) is skipped:
+            // its probabilities are exactly 0
+            const bool two = kt * FK + 32 < tl;
             f32x16 s[2];
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
 #pragma unroll
                 for (int v = 0; v < 16; ++v) s[j][v] = 0.f;
-                prod_rows<BF16>(s[j], Ks[buf] + 32 * j * FA_LD, qv, l32, h);  // S^T: key r8(v,h), query l32
+                if (j == 0 || two) prod_rows<BF16>(s[j], Ks[buf] + 32 * j * FA_LD, qv, l32, h);  // S^T: key r8(v,h), query l32
             }
             float mx = -INFINITY;
 #pragma unroll
@@ -291,9 +294,8 @@ __global__ __launch_bounds__(NW * 64) void flash_fwd_kernel(const float* __restr
                 m_run = m_new;
             }
             l_run += ls;
-#pragma unroll
-            for (int j = 0; j < 2; ++j)  // O^T[n][q] += sum_key V[key][n] P[q][key]
-                apply_cols<BF16, FK_LDT>(o, Vt[buf] + 32 * j, s[j], l32, h);
+            apply_cols<BF16, FK_LDT>(o, Vt[buf], s[0], l32, h);  // O^T[n][q] += sum_key V[key][n] P[q][key]
+            if (two) apply_cols<BF16, FK_LDT>(o, Vt[buf] + 32, s[1], l32, h);
         }
         if (kt + 1 < nkt) put(buf ^ 1);
         __syncthreads();
@@ -636,12 +638,13 @@ __global__ __launch_bounds__(FF_NW_BF * 64) void flash_fwd_bf16_kernel(
         const int buf = kt & 1;
         if (kt + 1 < nkt) fetch(kt + 1);
         if (active) {
+            const bool two = kt * FK + 32 < tl;  // as in flash_fwd_kernel
             f32x16 s[2];
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
 #pragma unroll
                 for (int v = 0; v < 16; ++v) s[j][v] = 0.f;
-                prod_rows_b(s[j], Ks[buf] + 32 * j * FB_RS, qv, l32, h);
+                if (j == 0 || two) prod_rows_b(s[j], Ks[buf] + 32 * j * FB_RS, qv, l32, h);
             }
             float mx = -INFINITY;
 #pragma unroll
@@ -672,8 +675,8 @@ __global__ __launch_bounds__(FF_NW_BF * 64) void flash_fwd_bf16_kernel(
                 m_run = m_new;
             }
             l_run += ls;
-#pragma unroll
-            for (int j = 0; j < 2; ++j) apply_cols_b<FBK_LDT>(o, Vt[buf] + 32 * j, s[j], l32, h);
+            apply_cols_b<FBK_LDT>(o, Vt[buf], s[0], l32, h);
+            if (two) apply_cols_b<FBK_LDT>(o, Vt[buf] + 32, s[1], l32, h);
         }
         if (kt + 1 < nkt) put(buf ^ 1);
         __syncthreads();

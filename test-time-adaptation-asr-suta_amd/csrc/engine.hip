@@ -344,6 +344,7 @@ struct suta_engine {
                 return;
             }
         }
+        if (!p.C) throw SutaError(SUTA_ERR_UNSUPPORTED, "gemm: fp32 output skipped on a plane-less GEMM");
         p.Ab = nullptr;  // (plane-less GEMM: a plane given for a non-frozen B is ignored)
         p.Cb = nullptr;
         timed(F_GEMM, [&] { gemm_launch(p, st, plan.splitws, plan.splitws_floats); }, ab);
@@ -667,13 +668,17 @@ void suta_engine::forward(int B) {
     // bf16 mode: producers of the linears' A operands also write bf16 planes (P0 / P1, ping-pong)
     void* P0 = plane(0);
     void* P1 = plane(1);
+    // with bf16 planes, fp32 activations read only as a frozen linear's A operand are not written (the linear
+    // reads the plane; no weight gradient reads them): stable-LN outputs and gelu(FFN1).  Only where every
+    // producer and consumer takes its plane path (the vectorised LayerNorm widths, K % 8 == 0).
+    const bool dead = P0 && (H == 512 || H == 768 || H == 1024) && k.F % 8 == 0;
     for (int l = 0; l < k.L; ++l) {
         LayerBufs& lb = pl.lay[l];
         const float* attn_in = lb.x_in;
         if (k.stable) {
             timed(F_NORM, [&] {
-                launch_layernorm_fwd(lb.x_in, P + o_l1g[l], P + o_l1b[l], Pn, T, lb.y1, lb.xhat1, lb.rstd1, (int)BT, H,
-                                     k.eps, 0, st, P0, lb.mean1);
+                launch_layernorm_fwd(lb.x_in, P + o_l1g[l], P + o_l1b[l], Pn, T, dead ? nullptr : lb.y1, lb.xhat1,
+                                     lb.rstd1, (int)BT, H, k.eps, 0, st, P0, lb.mean1);
             });
             attn_in = lb.y1;
         }
@@ -781,8 +786,8 @@ void suta_engine::forward(int B) {
         float* ffn_out;
         if (k.stable) {
             timed(F_NORM, [&] {
-                launch_layernorm_fwd(lb.hmid, P + o_l2g[l], P + o_l2b[l], Pn, T, lb.y2, lb.xhat2, lb.rstd2, (int)BT, H,
-                                     k.eps, 0, st, P0, lb.mean2);
+                launch_layernorm_fwd(lb.hmid, P + o_l2g[l], P + o_l2b[l], Pn, T, dead ? nullptr : lb.y2, lb.xhat2,
+                                     lb.rstd2, (int)BT, H, k.eps, 0, st, P0, lb.mean2);
             });
             ffn_in = lb.y2;
             ffn_res = lb.hmid;
@@ -808,7 +813,7 @@ void suta_engine::forward(int B) {
             g.B = w1[l];
             g.tb = 1;
             g.ldb = H;
-            g.C = pl.gu;
+            g.C = dead ? nullptr : pl.gu;  // with planes FFN2 reads only the bf16 plane (no weight gradient)
             g.ldc = k.F;
             g.M = (int)BT;
             g.N = k.F;
@@ -850,8 +855,8 @@ void suta_engine::forward(int B) {
     const float* hfin = pl.lay[k.L - 1].x_out;
     if (k.stable) {
         timed(F_NORM, [&] {
-            launch_layernorm_fwd(hfin, P + o_eg, P + o_eb, Pn, T, pl.enc_y, pl.enc_xhat, pl.enc_rstd, (int)BT, H, k.eps,
-                                 0, st, P0, pl.enc_mean);
+            launch_layernorm_fwd(hfin, P + o_eg, P + o_eb, Pn, T, dead ? nullptr : pl.enc_y, pl.enc_xhat, pl.enc_rstd,
+                                 (int)BT, H, k.eps, 0, st, P0, pl.enc_mean);
         });
         hfin = pl.enc_y;
     }

@@ -1,6 +1,7 @@
 // GEMM dispatcher: tile choice, split-K, precision mode -> kernel family (gemm_kernels.h).
 #include "gemm_kernels.h"
 #include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 
 namespace {
@@ -105,6 +106,24 @@ static int choose_tile_hb(long M, long N) {
     return best;
 }
 
+// 160 x 128 tile (exact mode, LDS-DMA kernel, 1 x 4 waves): on the M = B*T linears whose 128 x 128 grid
+// ends in a mostly empty round of the 512 resident blocks (N = 768: 1200 tiles = 2.34 rounds; N = 2304:
+// 3600 = 7.03), the 160-row tile covers the same padded area in fewer rounds (960 = 1.88; 2880 = 5.6).
+// Measured (tools/gemm_bench, same box): equal to 128 x 128 within 1.4 % on every such shape (ffn2 1.123 vs
+// 1.138 ms, dqkv->dx 0.870 vs 0.876) and the bench within noise (35.70 vs 35.78 utt/s): the linears are not
+// tail-bound.  Opt-in: SUTA_GEMM160=1.
+static bool use_tile160(long M, long N, long Z) {
+    static int env = -1;
+    if (env < 0) {
+        const char* e = std::getenv("SUTA_GEMM160");
+        env = (e && atoi(e) == 1) ? 1 : 0;
+    }
+    if (!env) return false;
+    const long t128 = ((M + 127) / 128) * ((N + 127) / 128) * Z;
+    const long t160 = ((M + 159) / 160) * ((N + 127) / 128) * Z;
+    return t128 >= 512 && (t160 + 511) / 512 < (t128 + 511) / 512;
+}
+
 void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
     if (p.M <= 0 || p.N <= 0 || p.Z <= 0) return;
     const int second = ((p.epi & EPI_RESID) != 0) + ((p.epi & EPI_ACCUM) != 0) + ((p.epi & EPI_SMBWD) != 0);
@@ -123,13 +142,17 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
     if (hb && (p.Z != 1 || p.K % 8 || p.ldab % 8 || p.ldbb % 8 || !aligned16(p.Ab) || !aligned16(p.Bb)))
         throw std::invalid_argument("gemm: bf16 planes need Z == 1, K, ld % 8 == 0 and 16-B alignment");
     const bool bf16_gbf = p.mode == 2 && glds_ok && p.ta;  // bf16 weight gradients: LDS-DMA fp32 stages
-    const int tile = g_force_tile >= 0 ? g_force_tile
-                     : hb            ? choose_tile_hb(p.M, p.N)
-                     : p.mode == 2   ? choose_tile_bf16(p.M, p.N, p.Z, !bf16_gbf)
-                                     : choose_tile(p.M, p.N, p.Z, p.K, p.mode);
-    // tiles 0 = 128x128, 1 = 128x64, 2 = 64x128, 3 = 64x64; bf16 mode also 4 = 256x128, 5 = 128x256
-    const int BM = (tile == 4 || tile == 6) ? 256 : (tile == 0 || tile == 1 || tile == 5) ? 128 : 64;
-    const int BN = (tile == 5 || tile == 6) ? 256 : (tile == 0 || tile == 2 || tile == 4) ? 128 : 64;
+    int tile = g_force_tile >= 0 ? g_force_tile
+               : hb            ? choose_tile_hb(p.M, p.N)
+               : p.mode == 2   ? choose_tile_bf16(p.M, p.N, p.Z, !bf16_gbf)
+                               : choose_tile(p.M, p.N, p.Z, p.K, p.mode);
+    const bool glds_path = p.mode == 0 && g_nbuf == 3 && glds_ok;
+    if (tile == 7 && !glds_path) tile = 0;  // the 160-row tile exists only in the default LDS-DMA kernel
+    if (g_force_tile < 0 && tile == 0 && glds_path && use_tile160(p.M, p.N, p.Z)) tile = 7;
+    // tiles 0 = 128x128, 1 = 128x64, 2 = 64x128, 3 = 64x64, 7 = 160x128; bf16 mode also 4 = 256x128,
+    // 5 = 128x256
+    const int BM = tile == 7 ? 160 : (tile == 4 || tile == 6) ? 256 : (tile == 0 || tile == 1 || tile == 5) ? 128 : 64;
+    const int BN = (tile == 5 || tile == 6) ? 256 : (tile == 0 || tile == 2 || tile == 4 || tile == 7) ? 128 : 64;
     const int gx = (p.N + BN - 1) / BN, gy = (p.M + BM - 1) / BM;
     const long blocks = (long)gx * gy * p.Z;
 

@@ -302,7 +302,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, const f32x16 
                     const int row = rbase + i * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * h;
                     if (interior || (row < p.M && col < p.N)) {
                         const float o = row < rlim ? v[r] : 0.f;
-                        C[(long)row * p.ldc + col] = o;
+                        if (!CB || p.C) C[(long)row * p.ldc + col] = o;  // bf16-plane GEMMs: C may be dead
                         if (CB) reinterpret_cast<__bf16*>(p.Cb)[(long)row * p.ldcb + col] = (__bf16)o;
                     }
                 }
@@ -828,7 +828,7 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmParams p) {
         const long row = idx / p.N, col = idx % p.N;
         const float v = epi_value(p, s, row, col, bias, R, aux, C2, C, rowv);
         const float o = ((p.epi & EPI_ROWMASK) && row >= p.zrows[z1]) ? 0.f : v;
-        C[row * p.ldc + col] = o;
+        if (p.C) C[row * p.ldc + col] = o;  // null: a bf16-plane GEMM whose fp32 output is dead
         if (p.Cb) reinterpret_cast<__bf16*>(p.Cb)[row * p.ldcb + col] = (__bf16)o;
     }
 }
@@ -974,8 +974,12 @@ __device__ __forceinline__ void wait_vm() {
 // read (never vmcnt(0) inside the loop).
 template <int BM, int BN, bool TA, bool TB, bool CONV, bool SEGB, int BKS, int NS>
 __global__ __launch_bounds__(256, 2) void gemm_glds_kernel(GemmParams p) {
-    constexpr int WTM = BM / 2, WTN = BN / 2;
+    // waves 2 x 2 (wave tile BM/2 x BN/2), or 1 x 4 when BM is not a multiple of 64 (the 160-row tile:
+    // wave tile 160 x BN/4, five A fragments against one B fragment)
+    constexpr int WGM = (BM % 64 == 0) ? 2 : 1, WGN = 4 / WGM;
+    constexpr int WTM = BM / WGM, WTN = BN / WGN;
     constexpr int RM = WTM / 32, RN = WTN / 32;
+    static_assert(RM * 32 == WTM && RN * 32 == WTN, "wave tile must be whole 32x32 fragments");
     constexpr bool AKC = !TA, BKC = TB;
     constexpr int STAGE = (BM + BN) * BKS;  // floats per LDS stage
     constexpr int NPW = (BM + BN) * BKS / 1024;  // DMA instructions per wave per stage
@@ -1000,7 +1004,7 @@ __global__ __launch_bounds__(256, 2) void gemm_glds_kernel(GemmParams p) {
 
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wm = wid >> 1, wn = wid & 1;
+    const int wm = wid / WGN, wn = wid % WGN;
     const int h = lane >> 5, l32 = lane & 31;
 
     f32x16 acc[RM][RN];
@@ -1259,6 +1263,10 @@ void launch_glds(const GemmParams& p, dim3 grid, hipStream_t st) {
 template <int BKS, int NS>
 void launch_glds_tile(int tile, const GemmParams& p, dim3 grid, hipStream_t st) {
     if (tile == 0) launch_glds<128, 128, BKS, NS>(p, grid, st);
+    else if (tile == 7) {
+        if constexpr (BKS == 32 && NS == 2) launch_glds<160, 128, BKS, NS>(p, grid, st);  // default variant only
+        else launch_glds<128, 128, BKS, NS>(p, grid, st);
+    }
     else if (tile == 1) launch_glds<128, 64, BKS, NS>(p, grid, st);
     else if (tile == 2) launch_glds<64, 128, BKS, NS>(p, grid, st);
     else launch_glds<64, 64, BKS, NS>(p, grid, st);

@@ -133,8 +133,10 @@ __global__ __launch_bounds__(256) void gn_bwd_final(const double* __restrict__ p
 // (read/written in the backward).  Block: F0_ROWS frames x all channels, waveform segment in LDS.
 //   MODE 0: per-channel partial sum / sum of squares of z (double)          -> part
 //   MODE 1: a = gelu(((z - mean) * rstd) * g + beta)                         -> a
-//   MODE 2: dg = da * gelu'(xhat * g + beta) (in place), partial sum(dg), sum(dg * xhat)
-//   MODE 3: dz = rstd*g*(dg - S/L - xhat*Q/L); partial dW[k][c] = sum_t dz[t][c] x[s t + k]
+//   MODE 2: dg = da * gelu'(xhat * g + beta): partial sum(dg), sum(dg * xhat) (read-only pass)
+//   MODE 3: dg recomputed from da as in MODE 2, dz = rstd*g*(dg - S/L - xhat*Q/L); partial
+//           dW[k][c] = sum_t dz[t][c] x[s t + k]   (the backward reads da twice and writes nothing
+//           activation-sized: dg is never stored)
 // ------------------------------------------------------------------------------------------
 constexpr int F0_ROWS = 128;
 // KT/ST: compile-time taps/stride (every wav2vec2 conv0 is K = 10, S = 5) -- keeps the filter in
@@ -207,11 +209,11 @@ __global__ __launch_bounds__(256) void conv0_gn_kernel(const float* __restrict__
                     iob[o] = gelu_f(xh * gg + bt);
                 } else if (MODE == 2) {
                     const float dg = iob[o] * dgelu_f(xh * gg + bt);
-                    iob[o] = dg;
                     a0 += dg;
                     a1 += (double)dg * xh;
                 } else {
-                    const float dz = rs * gg * (iob[o] - sS - xh * sQ);
+                    const float dg = iob[o] * dgelu_f(xh * gg + bt);  // recomputed bitwise, as in MODE 2
+                    const float dz = rs * gg * (dg - sS - xh * sQ);
 #pragma unroll
                     for (int k = 0; k < (KT > 0 ? KT : 16); ++k)
                         if (KT > 0 || k < K) dw[k] = fmaf(dz, xs[r * S + k], dw[k]);
@@ -385,7 +387,7 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* __restr
 // Vectorised LayerNorm forward for D = 256 * NV: one wave per row, lane l owns the 16-B column
 // groups l + 64 i.  gamma / beta are read as scalars (their offsets in the flat parameter buffer need
 // not be 16-B aligned).
-template <int NV>
+template <int NV, bool GV>
 __global__ __launch_bounds__(256) void layernorm_fwd_vec_kernel(const float* __restrict__ x,
                                                                 const float* __restrict__ g,
                                                                 const float* __restrict__ beta, long pstride,
@@ -422,15 +424,25 @@ __global__ __launch_bounds__(256) void layernorm_fwd_vec_kernel(const float* __r
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
         const int c = 4 * (lane + 64 * i);
-        f32x4 xh, o;
+        f32x4 xh, o, gg, bb;
+        if constexpr (GV) {  // 16-B aligned gamma / beta (the launcher checks): one load each per 4 columns
+            gg = *reinterpret_cast<const f32x4*>(gu + c);
+            bb = *reinterpret_cast<const f32x4*>(bu + c);
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                gg[e] = gu[c + e];
+                bb[e] = bu[c + e];
+            }
+        }
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             xh[e] = (v[i][e] - mean) * rs;
-            const float t = xh[e] * gu[c + e] + bu[c + e];
+            const float t = xh[e] * gg[e] + bb[e];
             o[e] = gelu_out ? gelu_f(t) : t;
         }
         if (xhat) reinterpret_cast<f32x4*>(xhat + row * D)[lane + 64 * i] = xh;
-        reinterpret_cast<f32x4*>(y + row * D)[lane + 64 * i] = o;
+        if (y) reinterpret_cast<f32x4*>(y + row * D)[lane + 64 * i] = o;  // null: only the bf16 plane is read
         if (yb) store_bf16x4(yb + row * D + c, o);  // the bf16 plane of the next GEMM's A operand
     }
     if (lane == 0) {
@@ -442,7 +454,7 @@ __global__ __launch_bounds__(256) void layernorm_fwd_vec_kernel(const float* __r
 // Vectorised LayerNorm backward for D = 256 * NV: lane l owns the 16-B column groups l + 64 i
 // (i < NV) of every row, so every row access is a fully coalesced 1-KiB wave load.  Same arithmetic,
 // order and partial layout as layernorm_bwd_kernel.
-template <int NV>
+template <int NV, bool GV>
 __global__ __launch_bounds__(256) void layernorm_bwd_vec_kernel(
     const float* __restrict__ dy, const float* __restrict__ xhat, const float* __restrict__ rstd,
     const float* __restrict__ g, const float* __restrict__ beta, long pstride, int rows_per_utt, int gelu_in,
@@ -459,10 +471,16 @@ __global__ __launch_bounds__(256) void layernorm_bwd_vec_kernel(
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
         const int c = 4 * (lane + 64 * i);
+        if constexpr (GV) {
+            gam[i] = *reinterpret_cast<const f32x4*>(gu + c);
+            bet[i] = *reinterpret_cast<const f32x4*>(bu + c);
+        }
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            gam[i][e] = gu[c + e];
-            bet[i][e] = bu[c + e];
+            if constexpr (!GV) {
+                gam[i][e] = gu[c + e];
+                bet[i][e] = bu[c + e];
+            }
             pg[i][e] = pb[i][e] = 0.f;
         }
     }
@@ -1143,18 +1161,19 @@ void launch_layernorm_fwd(const float* x, const float* g, const float* beta, lon
                           hipStream_t st, void* yb_, float* mean) {
     __bf16* yb = reinterpret_cast<__bf16*>(yb_);
     if (!xhat && !mean) throw std::runtime_error("layernorm_fwd: x-hat or the row means must be stored");
+    if (!y && !(yb && (D == 768 || D == 1024 || D == 512)))
+        throw std::runtime_error("layernorm_fwd: the fp32 output may be skipped only beside a bf16 plane");
     dim3 grid(cdiv(rows, 4));
     auto a16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
-    const bool vec = a16(x) && a16(y) && a16(xhat);
-    if (vec && D == 768)
-        hipLaunchKernelGGL(layernorm_fwd_vec_kernel<3>, grid, dim3(256), 0, st, x, g, beta, pstride, rows_per_utt, y,
-                           xhat, rstd, rows, eps, gelu_out, yb, mean);
-    else if (vec && D == 1024)
-        hipLaunchKernelGGL(layernorm_fwd_vec_kernel<4>, grid, dim3(256), 0, st, x, g, beta, pstride, rows_per_utt, y,
-                           xhat, rstd, rows, eps, gelu_out, yb, mean);
-    else if (vec && D == 512)
-        hipLaunchKernelGGL(layernorm_fwd_vec_kernel<2>, grid, dim3(256), 0, st, x, g, beta, pstride, rows_per_utt, y,
-                           xhat, rstd, rows, eps, gelu_out, yb, mean);
+    const bool vec = a16(x) && a16(y) && (xhat == nullptr || a16(xhat));
+    const bool gv = a16(g) && a16(beta) && pstride % 4 == 0;
+#define LNF(NV_)                                                                                                    \
+    hipLaunchKernelGGL((gv ? layernorm_fwd_vec_kernel<NV_, true> : layernorm_fwd_vec_kernel<NV_, false>), grid,       \
+                       dim3(256), 0, st, x, g, beta, pstride, rows_per_utt, y, xhat, rstd, rows, eps, gelu_out, yb, mean)
+    if (vec && D == 768) LNF(3);
+    else if (vec && D == 1024) LNF(4);
+    else if (vec && D == 512) LNF(2);
+#undef LNF
     else if (D <= 256)
         hipLaunchKernelGGL(layernorm_fwd_kernel<4>, grid, dim3(256), 0, st, x, g, beta, pstride, rows_per_utt, y, xhat,
                            rstd, rows, D, eps, gelu_out, mean);
@@ -1178,15 +1197,15 @@ void launch_layernorm_bwd(const float* dy, const float* xhat, const float* rstd,
     dim3 grid(nchunk, B);
     auto a16 = [](const void* q) { return q == nullptr || (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
     const bool vec = a16(dy) && a16(xhat) && a16(x) && a16(dx) && a16(post_aux) && a16(resid) && a16(part);
-    if (vec && D == 768)
-        hipLaunchKernelGGL(layernorm_bwd_vec_kernel<3>, grid, dim3(256), 0, st, dy, xhat, rstd, g, beta, pstride,
-                           rows_per_utt, gelu_in, post_aux, resid, dx, pp, nchunk, dxb, x, mean);
-    else if (vec && D == 1024)
-        hipLaunchKernelGGL(layernorm_bwd_vec_kernel<4>, grid, dim3(256), 0, st, dy, xhat, rstd, g, beta, pstride,
-                           rows_per_utt, gelu_in, post_aux, resid, dx, pp, nchunk, dxb, x, mean);
-    else if (vec && D == 512)
-        hipLaunchKernelGGL(layernorm_bwd_vec_kernel<2>, grid, dim3(256), 0, st, dy, xhat, rstd, g, beta, pstride,
-                           rows_per_utt, gelu_in, post_aux, resid, dx, pp, nchunk, dxb, x, mean);
+    const bool gv = a16(g) && a16(beta) && pstride % 4 == 0;
+#define LNB(NV_)                                                                                                   \
+    hipLaunchKernelGGL((gv ? layernorm_bwd_vec_kernel<NV_, true> : layernorm_bwd_vec_kernel<NV_, false>), grid,      \
+                       dim3(256), 0, st, dy, xhat, rstd, g, beta, pstride, rows_per_utt, gelu_in, post_aux, resid, dx, \
+                       pp, nchunk, dxb, x, mean)
+    if (vec && D == 768) LNB(3);
+    else if (vec && D == 1024) LNB(4);
+    else if (vec && D == 512) LNB(2);
+#undef LNB
     else if (D <= 256)
         hipLaunchKernelGGL(layernorm_bwd_kernel<4>, grid, dim3(256), 0, st, dy, xhat, rstd, g, beta, pstride,
                            rows_per_utt, D, gelu_in, post_aux, resid, dx, pp, nchunk, x, mean);
