@@ -37,6 +37,7 @@ namespace {
 
 typedef __bf16 fbf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 fbf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // [row][64] tiles padded to 72 floats: 16-B row reads of 8 consecutive rows hit 8 distinct 4-bank groups,
 // and the column reads of rows r and r + 4 (lane halves of apply_rows) land 32 banks apart
@@ -440,19 +441,35 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void flash_bwd_kernel(
             for (int v = 0; v < 16; ++v) s[v] = dp[v] = 0.f;
             prod_rows<BF16>(s, Qt, kv, l32, h);   // S[q][key]: query r8(v,h), key on the lane
             prod_rows<BF16>(dp, Dt, vv, l32, h);  // dP[q][key]
+            f32x4 lq[4], dq[4];  // LSE / delta of the lane's rows r8(v, h): 4 runs of 4 consecutive rows
+#pragma unroll
+            for (int a = 0; a < 4; ++a) {
+                lq[a] = *reinterpret_cast<const f32x4*>(Lt + 8 * a + 4 * h);
+                dq[a] = *reinterpret_cast<const f32x4*>(Dlt + 8 * a + 4 * h);
+            }
             const bool kok = key < tl;
 #pragma unroll
             for (int v = 0; v < 16; ++v) {
                 const int r = r8(v, h);
                 const bool ok = kok && q0 + r < T;
-                const float p = ok ? __builtin_amdgcn_exp2f(sl2 * s[v] - LOG2E * Lt[r]) : 0.f;
+                const float p = ok ? __builtin_amdgcn_exp2f(sl2 * s[v] - LOG2E * lq[v >> 2][v & 3]) : 0.f;
                 s[v] = p;
-                dp[v] = scale * (p * (dp[v] - Dlt[r]));
+                dp[v] = scale * (p * (dp[v] - dq[v >> 2][v & 3]));
             }
             apply_rows<BF16>(dv, Dt, s, l32, h);   // dV^T[n][key] += sum_q dO[q][n] P[q][key]
             apply_rows<BF16>(dk, Qt, dp, l32, h);  // dK^T[d][key] += sum_q Q[q][d] dS[q][key]
+            // dS pairs (as in flash_bwd_bf16_kernel): lanes 2i / 2i + 1 swap one value, 8-B writes
+            const bool odd = lane & 1;
 #pragma unroll
-            for (int v = 0; v < 16; ++v) Ss[r8(v, h) * KBP + 32 * w + l32] = dp[v];
+            for (int v = 0; v < 16; v += 2) {
+                const float a = dp[v], b = dp[v + 1];
+                const float recv = __int_as_float(
+                    __builtin_amdgcn_mov_dpp(__float_as_int(odd ? a : b), 0xB1, 0xF, 0xF, false));
+                f32x2 pr;
+                pr[0] = odd ? recv : a;
+                pr[1] = odd ? b : recv;
+                *reinterpret_cast<f32x2*>(Ss + (r8(v, h) + (odd ? 1 : 0)) * KBP + 32 * w + (l32 & ~1)) = pr;
+            }
         }
         __syncthreads();  // dS tile complete
 #pragma unroll
@@ -799,6 +816,13 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16_kernel(
     fetch(0);
     put(0);
     __syncthreads();
+    // the wave's dQ B operand (K^T rows 16 di + l16 over the block's keys) is the same for every query
+    // tile: held in registers (kq <= 256 keys = 8 fragments) instead of re-read from LDS per tile
+    fbf16x8 kfr[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        if (32 * j < kq) kfr[j] = *reinterpret_cast<const fbf16x8*>(Kt + (16 * di + l16) * FBB_KB + 32 * j + 8 * g);
+    const bool odd = lane & 1;
     for (int qt = 0; qt < nqt; ++qt) {
         const int q0 = qt * 32, buf = qt & 1;
         if (qt + 1 < nqt) fetch(qt + 1);
@@ -810,35 +834,48 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16_kernel(
             for (int v = 0; v < 16; ++v) s[v] = dp[v] = 0.f;
             prod_rows_b(s, Qr + buf * 32 * FB_RS, kv, l32, h);
             prod_rows_b(dp, Dr + buf * 32 * FB_RS, vv, l32, h);
+            // the lane's 16 rows r8(v, h) are 4 runs of 4 consecutive rows: 16-B reads of LSE and delta
+            f32x4 lq[4], dq[4];
+#pragma unroll
+            for (int a = 0; a < 4; ++a) {
+                lq[a] = *reinterpret_cast<const f32x4*>(Lt + 8 * a + 4 * h);
+                dq[a] = *reinterpret_cast<const f32x4*>(Dlt + 8 * a + 4 * h);
+            }
             const bool kok = key < tl;
 #pragma unroll
             for (int v = 0; v < 16; ++v) {
                 const int r = r8(v, h);
                 const bool ok = kok && q0 + r < T;
-                const float p = ok ? __builtin_amdgcn_exp2f(sl2 * s[v] - LOG2E * Lt[r]) : 0.f;
+                const float p = ok ? __builtin_amdgcn_exp2f(sl2 * s[v] - LOG2E * lq[v >> 2][v & 3]) : 0.f;
                 s[v] = p;
-                dp[v] = scale * (p * (dp[v] - Dlt[r]));
+                dp[v] = scale * (p * (dp[v] - dq[v >> 2][v & 3]));
             }
             apply_cols_b<FBB_QT>(dv, Dc + buf * 64 * FBB_QT, s, l32, h);   // dV^T += dO^T P
             apply_cols_b<FBB_QT>(dk, Qc + buf * 64 * FBB_QT, dp, l32, h);  // dK^T += Q^T dS
+            // dS into LDS as bf16 pairs: lanes 2i / 2i + 1 (keys k, k + 1) swap one value (DPP quad_perm
+            // [1,0,3,2]) so the even lane writes row r keys (k, k+1) and the odd lane row r + 1 (rows r8(v, h)
+            // and r8(v + 1, h) = r + 1 for even v): 8 four-byte writes per lane instead of 16 two-byte ones
 #pragma unroll
-            for (int v = 0; v < 16; ++v) Ss[r8(v, h) * FBB_KB + 32 * w + l32] = (__bf16)dp[v];
+            for (int v = 0; v < 16; v += 2) {
+                const float a = dp[v], b = dp[v + 1];
+                const float recv = __int_as_float(
+                    __builtin_amdgcn_mov_dpp(__float_as_int(odd ? a : b), 0xB1, 0xF, 0xF, false));
+                fbf16x2 pr;
+                pr[0] = (__bf16)(odd ? recv : a);
+                pr[1] = (__bf16)(odd ? b : recv);
+                *reinterpret_cast<fbf16x2*>(Ss + (r8(v, h) + (odd ? 1 : 0)) * FBB_KB + 32 * w + (l32 & ~1)) = pr;
+            }
         }
         __syncthreads();  // dS tile complete
         {
             const __bf16* ar = Ss + (16 * qi + l16) * FBB_KB + 8 * g;
-            const __bf16* br = Kt + (16 * di + l16) * FBB_KB + 8 * g;
-            f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
-            int kc = 0;
-            for (; kc + 64 <= kq; kc += 64) {
-                c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const fbf16x8*>(ar + kc),
-                                                             *reinterpret_cast<const fbf16x8*>(br + kc), c0, 0, 0, 0);
-                c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const fbf16x8*>(ar + kc + 32),
-                                                             *reinterpret_cast<const fbf16x8*>(br + kc + 32), c1, 0, 0, 0);
-            }
-            if (kc < kq)
-                c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const fbf16x8*>(ar + kc),
-                                                             *reinterpret_cast<const fbf16x8*>(br + kc), c0, 0, 0, 0);
+            f32x4 c[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+            for (int j = 0; j < 8; ++j)  // same split of the key chunks over two chains as before (j even / odd)
+                if (32 * j < kq)
+                    c[j & 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                        *reinterpret_cast<const fbf16x8*>(ar + 32 * j), kfr[j], c[j & 1], 0, 0, 0);
+            const f32x4 c0 = c[0], c1 = c[1];
             float* dr = dqb + (long)(q0 + 16 * qi + 4 * g) * 64 + 16 * di + l16;
 #pragma unroll
             for (int r = 0; r < 4; ++r)

@@ -89,6 +89,7 @@ struct GemmParams {
     float* ws;  // split-K workspace
     int va, vb; // vector (16 B) loads legal
     int mode;   // 0 exact fp32 MFMA, 1 x6 (fp32-accurate bf16 split), 2 bf16 products; gemm_init takes the default
+    int order;  // LDS-DMA kernel tile order within an XCD's range: 0 n fastest (A panel reuse), 1 m fastest (B band reuse)
     // bf16 mode with bf16 operand planes (Z == 1, both k-contiguous): A(m,k) = Ab[m*ldab + k],
     // B(k,n) = Bb[n*ldbb + k] (16-B aligned, ldab % 8 == ldbb % 8 == K % 8 == 0) -> gemm_hb_kernel
     const void* Ab;

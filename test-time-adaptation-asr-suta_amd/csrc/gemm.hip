@@ -167,6 +167,14 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
     if (splits > 1) splits = (p.K + p.kchunk - 1) / p.kchunk;
     p.splits = splits;
     p.ws = ws;
+    {
+        static int ord = -1;  // SUTA_GEMM_ORDER=1: m-fastest tile order for single-batch GEMMs (A/B runs)
+        if (ord < 0) {
+            const char* e = std::getenv("SUTA_GEMM_ORDER");
+            ord = (e && atoi(e) == 1) ? 1 : 0;
+        }
+        p.order = (ord == 1 && p.Z == 1 && splits == 1) ? 1 : 0;
+    }
     dim3 grid(gx, gy, p.Z * splits);
     if (hb) {
         gemm_run_hb(tile, g_force_tile >= 0 ? g_nbuf : 2, p, grid, st);

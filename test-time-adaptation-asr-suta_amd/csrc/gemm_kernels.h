@@ -178,12 +178,13 @@ __device__ __forceinline__ float epi_value(const GemmParams& p, float acc, long 
 struct TileId {
     int x, y, z;
 };
-__device__ __forceinline__ TileId xcd_tile() {
+__device__ __forceinline__ TileId xcd_tile(int order = 0) {
     const int gx = gridDim.x, gy = gridDim.y;
     const int nwg = gx * gy * gridDim.z;
     const int orig = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
     const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
     const int id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+    if (order == 1) return TileId{(id / gy) % gx, id % gy, id / (gx * gy)};  // m fastest: an XCD keeps a B band
     return TileId{id % gx, (id / gx) % gy, id / (gx * gy)};
 }
 
@@ -985,7 +986,7 @@ __global__ __launch_bounds__(256, 2) void gemm_glds_kernel(GemmParams p) {
     constexpr int NPW = (BM + BN) * BKS / 1024;  // DMA instructions per wave per stage
     __shared__ __attribute__((aligned(16))) float smem[NS * STAGE];
 
-    const TileId tid = xcd_tile();
+    const TileId tid = xcd_tile(p.order);
     int zz = tid.z;
     int split = 0;
     if (p.splits > 1) {
@@ -1311,7 +1312,7 @@ __global__ __launch_bounds__(64 * NWV, (BM * BN > 128 * 128 || BKS > 32) ? 1 : 2
     constexpr int NPW = (BM + BN) * BKS / (256 * NWV);  // DMA instructions per wave per stage
     __shared__ __attribute__((aligned(16))) float smem[NS * STAGE];
 
-    const TileId tid = xcd_tile();
+    const TileId tid = xcd_tile(p.order);
     const int split = p.splits > 1 ? tid.z : 0;
     const float* A = reinterpret_cast<const float*>(p.Ab);
     const float* B = reinterpret_cast<const float*>(p.Bb);
