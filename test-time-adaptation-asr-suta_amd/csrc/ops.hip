@@ -489,13 +489,22 @@ __global__ __launch_bounds__(256) void layernorm_bwd_vec_kernel(
         const long row = (long)u * rows_per_utt + r;
         const f32x4* xr = reinterpret_cast<const f32x4*>((xhat ? xhat : xin) + row * D);
         const f32x4* dr = reinterpret_cast<const f32x4*>(dy + row * D);
-        f32x4 gi[NV], xh[NV];
+        f32x4 gi[NV], xh[NV], pa[NV], rr[NV];
         float s1 = 0.f, s2 = 0.f;
         const float rs = rstd[row];
 #pragma unroll
         for (int i = 0; i < NV; ++i) {
             xh[i] = xr[lane + 64 * i];
             gi[i] = dr[lane + 64 * i];
+        }
+        // every load of the row in flight together (the epilogue operands used to wait behind the reductions)
+        if (post_aux) {
+#pragma unroll
+            for (int i = 0; i < NV; ++i) pa[i] = reinterpret_cast<const f32x4*>(post_aux + row * D)[lane + 64 * i];
+        }
+        if (resid) {
+#pragma unroll
+            for (int i = 0; i < NV; ++i) rr[i] = reinterpret_cast<const f32x4*>(resid + row * D)[lane + 64 * i];
         }
         if (!xhat) {  // x-hat recomputed from the LayerNorm input: bitwise the forward's value
             const float mu = meanp[row];
@@ -520,15 +529,6 @@ __global__ __launch_bounds__(256) void layernorm_bwd_vec_kernel(
         s1 = wave_sum(s1);
         s2 = wave_sum(s2);
         const float m1 = s1 / D, m2 = s2 / D;
-        f32x4 pa[NV], rr[NV];
-        if (post_aux) {
-#pragma unroll
-            for (int i = 0; i < NV; ++i) pa[i] = reinterpret_cast<const f32x4*>(post_aux + row * D)[lane + 64 * i];
-        }
-        if (resid) {
-#pragma unroll
-            for (int i = 0; i < NV; ++i) rr[i] = reinterpret_cast<const f32x4*>(resid + row * D)[lane + 64 * i];
-        }
 #pragma unroll
         for (int i = 0; i < NV; ++i) {
             f32x4 o;

@@ -1,0 +1,13 @@
+# Round-2 final evidence, part 2: C4 kernel trace, PMC traffic passes (headline, C4).
+set -e
+export TMPDIR=/tmp
+O=gpurun_out/prof2e
+mkdir -p $O
+B="python3 bench.py --steps 1 --warmup 0 --no-split --no-cpu-baseline --no-timing --no-c4"
+C="python3 bench.py --only-c4 --steps 2 --no-timing"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_c4 -- $C > $O/kt_c4.log 2>&1
+timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -- $B > $O/pmc_fetch.log 2>&1
+timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -- $B > $O/pmc_write.log 2>&1
+timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_c4_fetch -- $C > $O/pmc_c4_fetch.log 2>&1
+timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_c4_write -- $C > $O/pmc_c4_write.log 2>&1
+echo done
