@@ -636,8 +636,21 @@ __global__ __launch_bounds__(FF_NW_BF * 64) void flash_fwd_bf16_kernel(
             vmap(it, vk, vc);
             if (it < ITEMS) {
                 *reinterpret_cast<fbf16x4*>(&Ks[buf][row * FB_RS + c4]) = cvt4(kr[n]);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) Vt[buf][(vc + e) * FBK_LDT + vk] = (__bf16)vr[n][e];
+                // V^T as key pairs: lanes 2i / 2i + 1 hold keys k / k + 1 of the same 4 columns; each swaps two
+                // values (DPP quad_perm [1,0,3,2]) so the even lane writes columns 0-1 and the odd lane columns
+                // 2-3 as (k, k+1) words: 2 writes per lane instead of 4
+                const bool odd = threadIdx.x & 1;
+                const float s0 = odd ? vr[n][0] : vr[n][2], s1 = odd ? vr[n][1] : vr[n][3];
+                const float q0 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(s0), 0xB1, 0xF, 0xF, false));
+                const float q1 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(s1), 0xB1, 0xF, 0xF, false));
+                fbf16x2 w0, w1;
+                w0[0] = (__bf16)(odd ? q0 : vr[n][0]);
+                w0[1] = (__bf16)(odd ? vr[n][2] : q0);
+                w1[0] = (__bf16)(odd ? q1 : vr[n][1]);
+                w1[1] = (__bf16)(odd ? vr[n][3] : q1);
+                const int e0 = odd ? 2 : 0;
+                *reinterpret_cast<fbf16x2*>(&Vt[buf][(vc + e0) * FBK_LDT + (vk & ~1)]) = w0;
+                *reinterpret_cast<fbf16x2*>(&Vt[buf][(vc + e0 + 1) * FBK_LDT + (vk & ~1)]) = w1;
             }
         }
     };

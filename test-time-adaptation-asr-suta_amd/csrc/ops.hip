@@ -84,6 +84,48 @@ __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x,
     }
 }
 
+// Vectorised form (layer-norm conv stack: conv0 output stored): a thread owns 4 consecutive channels
+// (C / 4 threads per frame, 256 / (C / 4) frames per pass), taps KT / stride ST compile-time, 16-B stores;
+// per-element arithmetic and order as conv0_kernel.  Requires C % 4 == 0 and 256 % (C / 4) == 0.
+constexpr int C0V_ROWS = 64;
+template <int KT, int ST>
+__global__ __launch_bounds__(256) void conv0_vec_kernel(const float* __restrict__ x, long N,
+                                                        const float* __restrict__ W, const float* __restrict__ bias,
+                                                        long wstride, float* __restrict__ z, int L0, int C) {
+    __shared__ float xs[C0V_ROWS * ST + KT + 16];
+    const int b = blockIdx.y;
+    const int t0 = blockIdx.x * C0V_ROWS;
+    const float* xb = x + (long)b * N;
+    const int nx = (C0V_ROWS - 1) * ST + KT;
+    for (int i = threadIdx.x; i < nx; i += 256) {
+        const long gi = (long)t0 * ST + i;
+        xs[i] = gi < N ? xb[gi] : 0.f;
+    }
+    __syncthreads();
+    const int cpr = C / 4, fpp = 256 / cpr;  // threads per frame, frames per pass
+    const int c = 4 * (threadIdx.x % cpr), fr = threadIdx.x / cpr;
+    const float* Wb = W + (long)b * wstride;
+    f32x4 w[KT];
+#pragma unroll
+    for (int k = 0; k < KT; ++k) w[k] = *reinterpret_cast<const f32x4*>(Wb + (long)k * C + c);
+    f32x4 bv = {0.f, 0.f, 0.f, 0.f};
+    if (bias) bv = *reinterpret_cast<const f32x4*>(bias + (long)b * wstride + c);
+    const int rows = min(C0V_ROWS, L0 - t0);
+    float* zb = z + ((long)b * L0 + t0) * C + c;
+    for (int r = fr; r < rows; r += fpp) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < KT; ++k) {
+            const float xv = xs[r * ST + k];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[e] = fmaf(xv, w[k][e], acc[e]);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[e] = acc[e] + bv[e];
+        *reinterpret_cast<f32x4*>(zb + (long)r * C) = acc;
+    }
+}
+
 // ------------------------------------------------------------------------------------------
 // per-utterance column statistics (GroupNorm with groups == channels), double partials
 // ------------------------------------------------------------------------------------------
@@ -1150,6 +1192,13 @@ void launch_wave_normalize(const float* x, float* y, int B, long N, const int* l
 
 void launch_conv0(const float* x, long N, const float* W, const float* bias, long wstride, float* z, int B, int L0,
                   int C, int K, int S, hipStream_t st) {
+    auto a16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+    if (K == 10 && S == 5 && C % 4 == 0 && C / 4 <= 256 && 256 % (C / 4) == 0 && wstride % 4 == 0 && a16(W) &&
+        a16(z) && (!bias || a16(bias))) {  // every wav2vec2 conv0
+        hipLaunchKernelGGL((conv0_vec_kernel<10, 5>), dim3(cdiv(L0, C0V_ROWS), B), dim3(256), 0, st, x, N, W, bias,
+                           wstride, z, L0, C);
+        return;
+    }
     hipLaunchKernelGGL(conv0_kernel, dim3(cdiv(L0, C0_ROWS), B), dim3(256), 0, st, x, N, W, bias, wstride, z, L0, C,
                        K, S);
 }

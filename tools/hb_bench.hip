@@ -43,7 +43,7 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    const int variants[][2] = {{0, 2}, {6, 2}};  // (tile, ns)  // (tile, ns) -- gemm_run_hb
+    const int variants[][2] = {{0, 2}};  // (tile, ns)  // (tile, ns) -- gemm_run_hb
     for (auto& s : shapes) {
         for (auto& vt : variants) {
             const int ti = vt[0], ns = vt[1];
