@@ -190,6 +190,9 @@ struct suta_engine {
     // frozen weights
     std::vector<float*> wqkv, bqkv, wo, bo, w1, b1, w2, b2;
     float *wpos_f = nullptr, *wpos_b = nullptr, *bpos = nullptr, *wlm = nullptr, *blm = nullptr;
+    // bf16 positional-conv weights [G][K][n][k] (fwd: n = c_out, k = c_in; bwd: taps flipped, n = c_in, k = c_out)
+    // for posconv_bf16_kernel (group width 64); null otherwise
+    void *wpos_bf_f = nullptr, *wpos_bf_b = nullptr;
     // trainable
     std::vector<TP> tps;
     std::map<std::string, int> tpi;
@@ -621,7 +624,15 @@ void suta_engine::forward(int B) {
                                 rT(), st))
                 throw SutaError(SUTA_ERR_UNSUPPORTED, "positional conv shape");
         });
-    if (!pc_ok) {  // positional conv: e = h0 + gelu(posconv(h0)); pz = pre-activation
+    // bf16 mode, group width 64 (config C4): posconv_bf16_kernel
+    const bool pcb16 = posconv_kernel && gemm_mode == SUTA_PRECISION_BF16 && wpos_bf_f && k.posK % 4 == 0;
+    if (pcb16)
+        timed(F_GEMM, [&] {
+            if (!launch_posconv_bf16(true, pl.h0, wpos_bf_f, bpos, pl.h0, pl.e, pl.pz, B, T, H, k.posG, k.posK,
+                                     k.posK / 2, rT(), st))
+                throw SutaError(SUTA_ERR_UNSUPPORTED, "positional conv shape");
+        });
+    if (!pc_ok && !pcb16) {  // positional conv: e = h0 + gelu(posconv(h0)); pz = pre-activation
         const int Cg = H / k.posG;
         GemmParams g;
         gemm_init(g);
@@ -1126,7 +1137,14 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
                                 k.posK - 1 - k.posK / 2, rT(), st))
                 throw SutaError(SUTA_ERR_UNSUPPORTED, "positional conv shape");
         });
-    if (!pcb_ok) {  // dh0 = posconv^T(dpz) + de
+    const bool pcb16 = posconv_kernel && gemm_mode == SUTA_PRECISION_BF16 && wpos_bf_b && k.posK % 4 == 0;
+    if (pcb16)
+        timed(F_GEMM, [&] {
+            if (!launch_posconv_bf16(false, dpz, wpos_bf_b, nullptr, de, dh0, nullptr, B, T, H, k.posG, k.posK,
+                                     k.posK - 1 - k.posK / 2, rT(), st))
+                throw SutaError(SUTA_ERR_UNSUPPORTED, "positional conv shape");
+        });
+    if (!pcb_ok && !pcb16) {  // dh0 = posconv^T(dpz) + de
         const int Cg = H / k.posG;
         GemmParams g;
         gemm_init(g);
@@ -1726,6 +1744,13 @@ int32_t suta_create(const suta_model_config* cfg, const char* const* names, cons
             std::vector<float> nf(K);
             for (int q = 0; q < K; ++q) nf[q] = (float)std::sqrt(nrm[q]);
             std::vector<float> wf((size_t)G * K * Cg * Cg), wb((size_t)G * K * Cg * Cg);
+            const bool bfw = Cg == 64;  // bf16-mode kernel weights (group width 64)
+            std::vector<uint16_t> bf_f(bfw ? wf.size() : 0), bf_b(bfw ? wf.size() : 0);
+            auto rne = [](float f) {  // fp32 -> bf16 bits, round to nearest even (finite values), as (__bf16)f
+                uint32_t u;
+                std::memcpy(&u, &f, 4);
+                return (uint16_t)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+            };
             for (int gi = 0; gi < G; ++gi)
                 for (int co = 0; co < Cg; ++co)
                     for (int ci = 0; ci < Cg; ++ci)
@@ -1735,11 +1760,21 @@ int32_t suta_create(const suta_model_config* cfg, const char* const* names, cons
                             // fwd B[(q, ci)][co] ; bwd B[(q', co)][ci] with q' = K-1-q
                             wf[(((size_t)gi * K + q) * Cg + ci) * Cg + co] = wv;
                             wb[(((size_t)gi * K + (K - 1 - q)) * Cg + co) * Cg + ci] = wv;
+                            if (bfw) {  // [g][q][n][k]: fwd n = co, k = ci; bwd (q' = K-1-q) n = ci, k = co
+                                bf_f[(((size_t)gi * K + q) * Cg + co) * Cg + ci] = rne(wv);
+                                bf_b[(((size_t)gi * K + (K - 1 - q)) * Cg + ci) * Cg + co] = rne(wv);
+                            }
                         }
             e->wpos_f = e->dalloc((long)wf.size());
             e->wpos_b = e->dalloc((long)wb.size());
             HIPCHK(hipMemcpy(e->wpos_f, wf.data(), wf.size() * 4, hipMemcpyHostToDevice));
             HIPCHK(hipMemcpy(e->wpos_b, wb.data(), wb.size() * 4, hipMemcpyHostToDevice));
+            if (bfw) {
+                e->wpos_bf_f = e->dalloc((long)(bf_f.size() + 1) / 2);
+                e->wpos_bf_b = e->dalloc((long)(bf_b.size() + 1) / 2);
+                HIPCHK(hipMemcpy(e->wpos_bf_f, bf_f.data(), bf_f.size() * 2, hipMemcpyHostToDevice));
+                HIPCHK(hipMemcpy(e->wpos_bf_b, bf_b.data(), bf_b.size() * 2, hipMemcpyHostToDevice));
+            }
             e->bpos = up(b + "bias", H);
         }
         e->reset_slots(max_batch, true);

@@ -61,6 +61,9 @@ bool launch_flash_bwd(const float* qkv, const float* dctx, const float* lse, con
 // bwd: C = conv + R (rows >= tlen -> 0).  false (nothing launched) outside the supported shapes
 bool launch_posconv(bool fwd, const float* x, const float* W, const float* bias, const float* R, float* C, float* C2,
                     int B, int T, int H, int G, int K, int pad, const int* tlen, hipStream_t st);
+// bf16 mode, group width 64: Wt = bf16 weights [G][K][n][k] (n = output channel, k = input channel)
+bool launch_posconv_bf16(bool fwd, const float* x, const void* Wt, const float* bias, const float* R, float* C,
+                         float* C2, int B, int T, int H, int G, int K, int pad, const int* tlen, hipStream_t st);
 // In-place row softmax of `nrows` rows of length T (row stride ld).  tlen (device, may be null):
 // ragged batch, rows of utterance row / rows_per_utt use their first tlen[u] keys; the rest get 0.
 // (GEMM attention path: head dims other than 64)

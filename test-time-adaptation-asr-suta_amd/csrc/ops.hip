@@ -772,6 +772,127 @@ __global__ __launch_bounds__(WB * 64, 1) void posconv_kernel(const float* __rest
 }
 
 // ------------------------------------------------------------------------------------------
+// Positional conv in bf16 mode (config C4, group width 64): the same contraction as posconv_kernel
+// with the operands rounded to bf16 (RNE) on v_mfma_f32_32x32x16_bf16, fp32 accumulation and epilogue.
+// Block = WB waves = 32*WB output frames x 64 channels of one (group, utterance, frame tile); the input
+// window (32*WB + K - 1 frames) is staged once as a bf16 image [row][64 + 8] (144-B rows: the 16-B
+// fragment reads of 32 consecutive rows are conflict-free); the group's bf16 weights Wt[tap][n][k]
+// (n = output channel, k = input channel, built once at suta_create) stream through two LDS chunks of
+// PCB_CHT taps, register-staged.  Wave = 32 frames x 64 channels = two 32x32 accumulators; per tap 4
+// k-steps x 2 MFMAs.  FWD / BWD epilogues as posconv_kernel.
+// ------------------------------------------------------------------------------------------
+constexpr int PCB_CHT = 4;   // taps per weight chunk
+constexpr int PCB_RS = 72;   // bf16 row stride of the window and weight images
+template <int WB, bool FWD>
+__global__ __launch_bounds__(WB * 64, 1) void posconv_bf16_kernel(const float* __restrict__ x,
+                                                                  const __bf16* __restrict__ Wt,
+                                                                  const float* __restrict__ bias,
+                                                                  const float* __restrict__ R, float* __restrict__ C,
+                                                                  float* __restrict__ C2, int T, int H, int G, int K,
+                                                                  int pad, const int* __restrict__ tlen, int ntile,
+                                                                  int nutt) {
+    constexpr int CG = 64, NT = WB * 64, WROWS = 32 * WB;
+    constexpr int CHUNK = PCB_CHT * CG * CG / 8;  // 16-B items per weight chunk
+    constexpr int LPT = (CHUNK + NT - 1) / NT;
+    extern __shared__ __attribute__((aligned(16))) __bf16 pcb_smem[];
+    __bf16* win = pcb_smem;                             // [WROWS + K - 1][PCB_RS]
+    __bf16* wbuf = pcb_smem + (WROWS + K - 1) * PCB_RS;  // 2 x [PCB_CHT * 64][PCB_RS]
+    typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+    typedef __bf16 b4 __attribute__((ext_vector_type(4)));
+
+    const int nb = gridDim.x;
+    int L = blockIdx.x;
+    if ((nb & 7) == 0) L = (L & 7) * (nb >> 3) + (L >> 3);  // a group's blocks on one XCD
+    const int tile = L % ntile;
+    const int u = (L / ntile) % nutt;
+    const int gi = L / (ntile * nutt);
+    const int t0 = tile * WROWS;
+    const int tl = tlen ? tlen[u] : T;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, l32 = lane & 31, h = lane >> 5;
+    const float* xb = x + (long)u * T * H + gi * CG;
+    const __bf16* wg = Wt + (long)gi * K * CG * CG;
+
+    const int nwin = (WROWS + K - 1) * (CG / 4);
+    for (int it = threadIdx.x; it < nwin; it += NT) {
+        const int row = it / (CG / 4), c4 = (it % (CG / 4)) * 4;
+        const int t = t0 - pad + row;
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        if (t >= 0 && t < tl) v = *reinterpret_cast<const f32x4*>(xb + (long)t * H + c4);
+        b4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = (__bf16)v[e];
+        *reinterpret_cast<b4*>(win + row * PCB_RS + c4) = o;
+    }
+    b8 st[LPT];
+    auto load_chunk = [&](int c) {
+        const b8* src = reinterpret_cast<const b8*>(wg + (long)c * PCB_CHT * CG * CG);
+#pragma unroll
+        for (int n = 0; n < LPT; ++n) {
+            const int it = threadIdx.x + n * NT;
+            if (it < CHUNK) st[n] = src[it];
+        }
+    };
+    auto store_chunk = [&](int buf) {
+        __bf16* dst = wbuf + buf * (PCB_CHT * CG * PCB_RS);
+#pragma unroll
+        for (int n = 0; n < LPT; ++n) {
+            const int it = threadIdx.x + n * NT;
+            if (it < CHUNK) *reinterpret_cast<b8*>(dst + (it >> 3) * PCB_RS + (it & 7) * 8) = st[n];
+        }
+    };
+    f32x16 acc[2];
+#pragma unroll
+    for (int nf = 0; nf < 2; ++nf)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) acc[nf][v] = 0.f;
+    const int nch = K / PCB_CHT;
+    load_chunk(0);
+    store_chunk(0);
+    __syncthreads();
+    const __bf16* arow = win + (32 * w + l32) * PCB_RS + 8 * h;
+    for (int c = 0; c < nch; ++c) {
+        if (c + 1 < nch) load_chunk(c + 1);
+        const __bf16* wb = wbuf + (c & 1) * (PCB_CHT * CG * PCB_RS) + l32 * PCB_RS + 8 * h;
+#pragma unroll
+        for (int qq = 0; qq < PCB_CHT; ++qq) {
+            const __bf16* ap = arow + (c * PCB_CHT + qq) * PCB_RS;
+            const __bf16* bp = wb + qq * CG * PCB_RS;
+#pragma unroll
+            for (int kc = 0; kc < CG / 16; ++kc) {
+                const b8 a = *reinterpret_cast<const b8*>(ap + 16 * kc);
+#pragma unroll
+                for (int nf = 0; nf < 2; ++nf)
+                    acc[nf] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                        a, *reinterpret_cast<const b8*>(bp + 32 * nf * PCB_RS + 16 * kc), acc[nf], 0, 0, 0);
+            }
+        }
+        if (c + 1 < nch) store_chunk((c + 1) & 1);
+        __syncthreads();
+    }
+    // epilogue: acc[nf][v] = out[t0 + 32 w + r8(v, h)][32 nf + l32]
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+        const int t = t0 + 32 * w + 8 * (v >> 2) + 4 * h + (v & 3);
+        if (t >= T) continue;
+        const long o = ((long)u * T + t) * H + gi * CG;
+#pragma unroll
+        for (int nf = 0; nf < 2; ++nf) {
+            const int co = 32 * nf + l32;
+            float val;
+            if (FWD) {
+                val = acc[nf][v] + bias[gi * CG + co];
+                C2[o + co] = val;
+                val = gelu_f(val) + R[o + co];
+            } else {
+                val = acc[nf][v] + R[o + co];
+                if (tlen && t >= tl) val = 0.f;
+            }
+            C[o + co] = val;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // attention softmax over rows of length T (<= 64*NPL), one wave per row
 // ------------------------------------------------------------------------------------------
 template <int NPL>
@@ -1348,6 +1469,54 @@ bool launch_posconv(bool fwd, const float* x, const float* W, const float* bias,
         if (fwd) posconv_go<64, true>(WB, grid, lds, st, x, W, bias, R, C, C2, T, H, G, K, pad, tlen, ntile, B);
         else posconv_go<64, false>(WB, grid, lds, st, x, W, bias, R, C, C2, T, H, G, K, pad, tlen, ntile, B);
     }
+    return true;
+}
+
+template <bool FWD>
+static void posconv_bf16_go(int WB, dim3 grid, size_t lds, hipStream_t st, const float* x, const __bf16* W,
+                            const float* bias, const float* R, float* C, float* C2, int T, int H, int G, int K, int pad,
+                            const int* tlen, int ntile, int B) {
+#define PCB(WB_)                                                                                                  \
+    do {                                                                                                          \
+        static bool attr = false;                                                                                 \
+        if (!attr) {                                                                                              \
+            HIPCHK_OPS(hipFuncSetAttribute(reinterpret_cast<const void*>(&posconv_bf16_kernel<WB_, FWD>),          \
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));              \
+            attr = true;                                                                                          \
+        }                                                                                                         \
+        hipLaunchKernelGGL((posconv_bf16_kernel<WB_, FWD>), grid, dim3(WB_ * 64), lds, st, x, W, bias, R, C, C2, T, \
+                           H, G, K, pad, tlen, ntile, B);                                                         \
+    } while (0)
+    switch (WB) {
+        case 4: PCB(4); break;
+        case 5: PCB(5); break;
+        case 6: PCB(6); break;
+        case 7: PCB(7); break;
+        default: PCB(8); break;
+    }
+#undef PCB
+}
+
+bool launch_posconv_bf16(bool fwd, const float* x, const void* Wt, const float* bias, const float* R, float* C,
+                         float* C2, int B, int T, int H, int G, int K, int pad, const int* tlen, hipStream_t st) {
+    if (H / G != 64 || H % G || K % PCB_CHT || !Wt) return false;
+    int WB = 8;  // waves per block: fewest padded frames over ceil(T / (32 WB)) tiles (T = 399 -> 7 waves)
+    long best = 1L << 40;
+    for (int wb = 8; wb >= 4; --wb) {
+        const long tiles = (T + 32 * wb - 1) / (32 * wb);
+        const long waste = tiles * 32 * wb - T;
+        if (waste < best) {
+            best = waste;
+            WB = wb;
+        }
+    }
+    const int ntile = (T + 32 * WB - 1) / (32 * WB);
+    const size_t lds = ((size_t)(32 * WB + K - 1) * PCB_RS + 2 * PCB_CHT * 64 * PCB_RS) * sizeof(__bf16);
+    if (lds > 160 * 1024) return false;
+    const dim3 grid((unsigned)((long)G * B * ntile));
+    const __bf16* W = reinterpret_cast<const __bf16*>(Wt);
+    if (fwd) posconv_bf16_go<true>(WB, grid, lds, st, x, W, bias, R, C, C2, T, H, G, K, pad, tlen, ntile, B);
+    else posconv_bf16_go<false>(WB, grid, lds, st, x, W, bias, R, C, C2, T, H, G, K, pad, tlen, ntile, B);
     return true;
 }
 

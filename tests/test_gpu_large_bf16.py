@@ -149,3 +149,34 @@ def test_bf16_flash_images_equal_fp32_image_kernels(monkeypatch):
         assert np.array_equal(out["1"][0][u], out["0"][0][u]), f"step 0 utt {u}"
         assert_bf16_close(out["1"][3][u], out["0"][3][u], 0.97, f"bf16 images step 3 utt {u}",
                           rtol=BF16_LOGITS_RTOL_LARGE)
+
+
+def test_bf16_posconv_kernel_equals_conv_a_path(monkeypatch):
+    """posconv_bf16_kernel (config C4's positional conv, 16 groups of 64 channels, 128 taps) against the
+    conv-A GEMM path it replaces (SUTA_POSCONV=0): the same bf16 operand rounding with fp32 accumulation
+    in another order (fp32 noise that flips bf16 roundings downstream, as between any two bf16 schedules),
+    so both agree within the bf16 tolerance, and reruns are bitwise identical; a ragged batch covers the
+    backward's zeroed padding rows.  (test_bf16_large_tracks_reference pins the kernel against the fp32
+    reference goldens.)"""
+    cfg = get_config("wav2vec2-large")
+    sd = synth_weights(cfg)
+    monkeypatch.setenv("SUTA_POSCONV", "0")
+    ref = SutaEngine(cfg, sd, max_batch=2, max_samples=64000)
+    monkeypatch.delenv("SUTA_POSCONV")
+    eng = SutaEngine(cfg, sd, max_batch=2, max_samples=64000)
+    ref.set_precision("bf16")
+    eng.set_precision("bf16")
+    x = synth.wave(48000, 41)
+    a, _, _ = ref.adapt(x, 3, SutaHParams(), record=[0, 3])
+    b, _, _ = eng.adapt(x, 3, SutaHParams(), record=[0, 3])
+    b2, _, _ = eng.adapt(x, 3, SutaHParams(), record=[0, 3])
+    assert np.array_equal(b[3], b2[3])
+    for r in (0, 3):
+        assert_bf16_close(b[r][0], a[r][0], 0.97, f"step {r}", rtol=BF16_LOGITS_RTOL_LARGE)
+    waves = [synth.wave(40000, 42), synth.wave(23000, 43)]
+    a, _, _ = ref.adapt_varlen(waves, 2, SutaHParams(), record=[2])
+    b, _, _ = eng.adapt_varlen(waves, 2, SutaHParams(), record=[2])
+    for u in range(2):
+        assert_bf16_close(b[2][u], a[2][u], 0.97, f"ragged utterance {u}", rtol=BF16_LOGITS_RTOL_LARGE)
+    ref.close()
+    eng.close()
