@@ -168,12 +168,16 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
     p.splits = splits;
     p.ws = ws;
     {
-        static int ord = -1;  // SUTA_GEMM_ORDER=1: m-fastest tile order for single-batch GEMMs (A/B runs)
+        static int ord = -1;  // SUTA_GEMM_ORDER=1: m-fastest; =G >= 2: bands of G tile rows (A/B runs)
         if (ord < 0) {
             const char* e = std::getenv("SUTA_GEMM_ORDER");
-            ord = (e && atoi(e) == 1) ? 1 : 0;
+            ord = e ? std::max(0, atoi(e)) : 0;
         }
-        p.order = (ord == 1 && p.Z == 1 && splits == 1) ? 1 : 0;
+        p.order = (ord >= 1 && p.Z == 1 && splits == 1) ? ord : 0;
+        // bf16-plane GEMMs: bands of 8 tile rows (N >= 2048) or 4 walked column by column keep both operand
+        // panels L2-resident (tools/hb_bench, M = 25 536: qkv 543 -> 598 TF, ffn1 525 -> 590, the N = 1024
+        // shapes within +-2 %); the fp32 kernels measured neutral and keep the n-fastest order
+        if (hb && ord == 0 && splits == 1) p.order = gx >= 16 ? 8 : 4;
     }
     dim3 grid(gx, gy, p.Z * splits);
     if (hb) {

@@ -185,6 +185,11 @@ __device__ __forceinline__ TileId xcd_tile(int order = 0) {
     const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
     const int id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
     if (order == 1) return TileId{(id / gy) % gx, id % gy, id / (gx * gy)};  // m fastest: an XCD keeps a B band
+    if (order >= 2) {  // grouped: bands of `order` tile rows walked column by column (A and B panels both reused)
+        const int zid = id / (gx * gy), i2 = id % (gx * gy);
+        const int per = order * gx, fm = (i2 / per) * order, gsz = min(gy - fm, order), loc = i2 % per;
+        return TileId{loc / gsz, fm + loc % gsz, zid};
+    }
     return TileId{id % gx, (id / gx) % gy, id / (gx * gy)};
 }
 
