@@ -946,6 +946,10 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
     };
     void* P0 = plane(0);  // bf16 planes of the linears' A operands (ping-pong), null outside bf16 mode
     void* P1 = plane(1);
+    // with bf16 planes (the forward's condition) dU = dH W2 * gelu'(u) is read only through its plane by the
+    // FFN1 input-gradient GEMM (no weight gradient): its fp32 copy is not written
+    const bool dead = P0 && (H == 512 || H == 768 || H == 1024) && k.F % 8 == 0;
+    float* du32 = dead ? nullptr : pl.du;
     // d hfin = dlogits @ Wlm
     nn_gemm(pl.dlogits, k.V, wlm, H, pl.d1, H, (int)BT, H, k.V, 0, nullptr, 0, nullptr, 0);
     float* dx = pl.d1;  // grad wrt current residual stream
@@ -968,7 +972,7 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
                                      nullptr, t1, G + o_l2g[l], G + o_l2b[l], Pn, pl.lnpart, st, P0);
             });
             // du = (dr2 @ W2) * gelu'(u)
-            nn_gemm(t1, H, w2[l], k.F, pl.du, k.F, (int)BT, k.F, H, EPI_DGELU, nullptr, 0, lb.u, k.F, P0, P1);
+            nn_gemm(t1, H, w2[l], k.F, du32, k.F, (int)BT, k.F, H, EPI_DGELU, nullptr, 0, lb.u, k.F, P0, P1);
             // dh1 = du @ W1 + dr2
             nn_gemm(pl.du, k.F, w1[l], H, t2, H, (int)BT, H, k.F, EPI_RESID, t1, H, nullptr, 0, P1);
             // dr1 = LN1 bwd(dh1)
@@ -979,7 +983,7 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
             dhres = t1;  // dr1
         } else {
             // du = (dx @ W2) * gelu'(u); dy2 = du @ W1; dhmid = LN2 bwd(dy2) + dx
-            nn_gemm(dx, H, w2[l], k.F, pl.du, k.F, (int)BT, k.F, H, EPI_DGELU, nullptr, 0, lb.u, k.F, P0, P1);
+            nn_gemm(dx, H, w2[l], k.F, du32, k.F, (int)BT, k.F, H, EPI_DGELU, nullptr, 0, lb.u, k.F, P0, P1);
             nn_gemm(pl.du, k.F, w1[l], H, t2, H, (int)BT, H, k.F, 0, nullptr, 0, nullptr, 0, P1);
             timed(F_NORM, [&] {
                 launch_layernorm_bwd(t2, lb.xhat2, lb.rstd2, P + o_l2g[l], P + o_l2b[l], Pn, T, B, H, 0, nullptr, dx,

@@ -309,7 +309,28 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, const f32x16 
                     if (interior || (row < p.M && col < p.N)) {
                         const float o = row < rlim ? v[r] : 0.f;
                         if (!CB || p.C) C[(long)row * p.ldc + col] = o;  // bf16-plane GEMMs: C may be dead
-                        if (CB) reinterpret_cast<__bf16*>(p.Cb)[(long)row * p.ldcb + col] = (__bf16)o;
+                        if (CB && !(interior && (p.ldcb & 1) == 0))
+                            reinterpret_cast<__bf16*>(p.Cb)[(long)row * p.ldcb + col] = (__bf16)o;
+                    }
+                }
+                if (CB && interior && (p.ldcb & 1) == 0) {
+                    // bf16 copy as (column, column + 1) pairs: lanes 2i / 2i + 1 swap one value (DPP quad_perm
+                    // [1,0,3,2]); the even lane writes row r, the odd lane row r + 1 (registers rr, rr + 1 hold
+                    // consecutive rows): half the store instructions of one 2-byte store per element
+                    typedef __bf16 cb2 __attribute__((ext_vector_type(2)));
+                    const bool odd = l32 & 1;
+#pragma unroll
+                    for (int r = 0; r < CH; r += 2) {
+                        const int rr = r0 + r;
+                        const int row = rbase + i * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * h;
+                        const float a = row < rlim ? v[r] : 0.f, b = row + 1 < rlim ? v[r + 1] : 0.f;
+                        const float q = __int_as_float(
+                            __builtin_amdgcn_mov_dpp(__float_as_int(odd ? a : b), 0xB1, 0xF, 0xF, false));
+                        cb2 pr;
+                        pr[0] = (__bf16)(odd ? q : a);
+                        pr[1] = (__bf16)(odd ? b : q);
+                        *reinterpret_cast<cb2*>(reinterpret_cast<__bf16*>(p.Cb) + (long)(row + (odd ? 1 : 0)) * p.ldcb +
+                                                (col & ~1)) = pr;
                     }
                 }
             }
