@@ -124,6 +124,16 @@ static bool use_tile160(long M, long N, long Z) {
     return t128 >= 512 && (t160 + 511) / 512 < (t128 + 511) / 512;
 }
 
+// 256 x 256 ping-pong bf16-plane kernel (gemm_hb8_kernel): K % 64 == 0 and a grid of >= 256 tiles (one block
+// per CU, no split-K).  SUTA_HB8=0 keeps the 128 x 128 two-stage kernel everywhere, =2 forces the 256 x 256
+// kernel on every eligible K (tests: small grids, edge tiles).  Read per launch so tests can switch it.
+static int use_hb8(long M, long N, long K) {
+    const char* e = std::getenv("SUTA_HB8");
+    const int mode = e ? atoi(e) : 0;
+    if (K % 64 != 0 || mode == 0) return 0;
+    return mode == 2 || ((M + 255) / 256) * ((N + 255) / 256) >= 256;
+}
+
 void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
     if (p.M <= 0 || p.N <= 0 || p.Z <= 0) return;
     const int second = ((p.epi & EPI_RESID) != 0) + ((p.epi & EPI_ACCUM) != 0) + ((p.epi & EPI_SMBWD) != 0);
@@ -143,11 +153,12 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
         throw std::invalid_argument("gemm: bf16 planes need Z == 1, K, ld % 8 == 0 and 16-B alignment");
     const bool bf16_gbf = p.mode == 2 && glds_ok && p.ta;  // bf16 weight gradients: LDS-DMA fp32 stages
     int tile = g_force_tile >= 0 ? g_force_tile
-               : hb            ? choose_tile_hb(p.M, p.N)
+               : hb            ? (use_hb8(p.M, p.N, p.K) ? 6 : choose_tile_hb(p.M, p.N))
                : p.mode == 2   ? choose_tile_bf16(p.M, p.N, p.Z, !bf16_gbf)
                                : choose_tile(p.M, p.N, p.Z, p.K, p.mode);
     const bool glds_path = p.mode == 0 && g_nbuf == 3 && glds_ok;
     if (tile == 7 && !glds_path) tile = 0;  // the 160-row tile exists only in the default LDS-DMA kernel
+    if (tile == 6 && !(hb && p.K % 64 == 0)) tile = 0;  // the 256 x 256 tile is the bf16-plane ping-pong kernel only
     if (g_force_tile < 0 && tile == 0 && glds_path && use_tile160(p.M, p.N, p.Z)) tile = 7;
     // tiles 0 = 128x128, 1 = 128x64, 2 = 64x128, 3 = 64x64, 7 = 160x128; bf16 mode also 4 = 256x128,
     // 5 = 128x256
@@ -158,7 +169,7 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
 
     // split-K when the grid cannot fill 256 CUs and K is long
     int splits = 1;
-    if (ws && p.K >= 1024 && blocks < 256) {
+    if (ws && p.K >= 1024 && blocks < 256 && tile != 6) {
         splits = (int)std::min<long>(16, (512 + blocks - 1) / blocks);
         while (splits > 1 && (long)splits * p.Z * p.M * (long)p.N > ws_floats) --splits;
         splits = std::min(splits, std::max(1, (p.K + 255) / 256));  // >= 256 K per split

@@ -180,3 +180,36 @@ def test_bf16_posconv_kernel_equals_conv_a_path(monkeypatch):
         assert_bf16_close(b[2][u], a[2][u], 0.97, f"ragged utterance {u}", rtol=BF16_LOGITS_RTOL_LARGE)
     ref.close()
     eng.close()
+
+
+def test_bf16_hb8_pingpong_kernel(monkeypatch):
+    """gemm_hb8_kernel (256 x 256 tile, two wave groups one barrier apart) forced on every bf16-plane linear
+    with K % 64 == 0 (SUTA_HB8=2; by default it runs only where the grid has >= 256 tiles, i.e. config C4's
+    64 x 8 s batches): the large model's 20-step SUTA against the reference goldens g7, reruns bitwise
+    identical, and a ragged pair (edge tiles: 198 and 124 rows of a 256-row tile) against the 128 x 128
+    kernel (SUTA_HB8=0) to bf16 tolerance (same operand roundings, another fp32 summation order)."""
+    z = _load("g7_large_16000.npz")
+    cfg = get_config("wav2vec2-large")
+    sd = synth_weights(cfg)
+    steps = [int(s) for s in z["steps"]]
+    waves = [synth.wave(32000, 80), synth.wave(20000, 81)]
+    out = {}
+    for mode in ("2", "0"):
+        monkeypatch.setenv("SUTA_HB8", mode)
+        eng = SutaEngine(cfg, sd, max_batch=2, max_samples=32000)
+        eng.set_precision("bf16")
+        if mode == "2":
+            logits, _, _ = eng.adapt(_g7_wave(), 20, SutaHParams(), record=steps)
+            for j, s in enumerate(steps):
+                assert_bf16_close(logits[s][0], z["logits"][j], 0.97, f"hb8 large step {s}",
+                                  rtol=BF16_LOGITS_RTOL_LARGE)
+        a, _, _ = eng.adapt_varlen(waves, 3, SutaHParams(), record=[0, 3])
+        b, _, _ = eng.adapt_varlen(waves, 3, SutaHParams(), record=[0, 3])
+        for u in range(2):
+            assert np.array_equal(a[3][u], b[3][u]), (mode, u)
+        out[mode] = a
+        eng.close()
+    for r in (0, 3):
+        for u in range(2):
+            assert_bf16_close(out["2"][r][u], out["0"][r][u], 0.97, f"hb8 vs 128x128 step {r} utt {u}",
+                              rtol=BF16_LOGITS_RTOL_LARGE)

@@ -30,7 +30,7 @@ int main(int argc, char** argv) {
     const int M = 25536;
     struct S { const char* name; int N, K; } shapes[] = {
         {"qkv  N3072 K1024", 3072, 1024}, {"out  N1024 K1024", 1024, 1024}, {"ffn1 N4096 K1024", 4096, 1024},
-        {"ffn2 N1024 K4096", 1024, 4096}, {"dqkv N1024 K3072", 1024, 3072}};
+        {"ffn2 N1024 K4096", 1024, 4096}, {"dqkv N1024 K3072", 1024, 3072}, {"edge N1000 K1024", 1000, 1024}};
     const int reps = argc > 1 ? atoi(argv[1]) : 20;
     __bf16 *A, *B;
     float *C, *R;
@@ -43,7 +43,9 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    const int variants[][2] = {{0, 2}};  // (tile, ns)  // (tile, ns) -- gemm_run_hb
+    const int variants[][2] = {{0, 2}, {6, 2}, {0, 2}, {6, 2}};  // (tile, ns) -- gemm_run_hb (6: 256x256 ping-pong)
+    __bf16* Cb;
+    CK(hipMalloc(&Cb, (size_t)M * 4096 * 2));
     for (auto& s : shapes) {
         for (auto& vt : variants) {
             const int ti = vt[0], ns = vt[1];
@@ -73,11 +75,20 @@ int main(int argc, char** argv) {
                 std::vector<float> hc((size_t)M * s.N), hr((size_t)rows * s.N);
                 CK(hipMemcpy(hc.data(), C, hc.size() * 4, hipMemcpyDeviceToHost));
                 CK(hipMemcpy(hr.data(), R, hr.size() * 4, hipMemcpyDeviceToHost));
-                double err = 0;
+                double err = 0, errb = 0;
+                {   // the bf16 copy of C (epilogue CB path): one extra launch with the plane on
+                    GemmParams q = p;
+                    q.Cb = Cb; q.ldcb = s.N;
+                    gemm_launch(q, 0, nullptr, 0);
+                    CK(hipDeviceSynchronize());
+                    std::vector<__bf16> hb((size_t)M * s.N);
+                    CK(hipMemcpy(hb.data(), Cb, hb.size() * 2, hipMemcpyDeviceToHost));
+                    for (size_t i = 0; i < hb.size(); i += 13) errb = fmax(errb, fabs((float)hb[i] - hc[i]) / (fabs(hc[i]) + 1.0));
+                }
                 for (int r = 0; r < rows; ++r)
                     for (int n = 0; n < s.N; ++n)
                         err = fmax(err, fabs(hc[(size_t)r * rstep * s.N + n] - hr[(size_t)r * s.N + n]));
-                printf("%s tile %d ns %d: %.4f ms %.1f TF maxerr %.2e\n", s.name, ti, ns, ms, tf, err);
+                printf("%s tile %d ns %d: %.4f ms %.1f TF maxerr %.2e bf16-copy relerr %.2e\n", s.name, ti, ns, ms, tf, err, errb);
                 fflush(stdout);
             }
     }
