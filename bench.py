@@ -131,7 +131,7 @@ def bench_c4(args, dev):
         gms, gn = t["gemm"]
         ach = flops_utt * B / (gms / 1000.0) / 1e12
         res["roofline"] = {"bound": "mfma", "achieved": round(ach, 3), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                           "frac": round(ach / BF16_PEAK_TFLOPS, 4), "kernel": "bf16 GEMM family (gemm_x6_kernel one-plane form + gemm_gbf_kernel for weight gradients + flash attention kernels on bf16 MFMA)",
+                           "frac": round(ach / BF16_PEAK_TFLOPS, 4), "kernel": "bf16 GEMM family (bf16-plane linears: gemm_hb_kernel / gemm_hb8_kernel; layer-norm conv stack: gemm_x6_kernel one-plane form; weight gradients: gemm_gbf_kernel; posconv_bf16_kernel; flash attention on bf16 MFMA)",
                            "launches": int(gn), "avg_launch_ms": round(gms / max(1, gn), 5)}
         res["time_breakdown_ms"] = {k: round(v[0], 2) for k, v in t.items()}
     eng.close()

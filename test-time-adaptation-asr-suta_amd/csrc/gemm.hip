@@ -124,14 +124,21 @@ static bool use_tile160(long M, long N, long Z) {
     return t128 >= 512 && (t160 + 511) / 512 < (t128 + 511) / 512;
 }
 
-// 256 x 256 ping-pong bf16-plane kernel (gemm_hb8_kernel): K % 64 == 0 and a grid of >= 256 tiles (one block
-// per CU, no split-K).  SUTA_HB8=0 keeps the 128 x 128 two-stage kernel everywhere, =2 forces the 256 x 256
-// kernel on every eligible K (tests: small grids, edge tiles).  Read per launch so tests can switch it.
-static int use_hb8(long M, long N, long K) {
+// 256 x 256 ping-pong bf16-plane kernel (gemm_hb8_kernel): K % 32 == 0 and a grid of >= 256 tiles (one block
+// per CU, no split-K).  Opt-in (tools/hb_bench: 5-13 % faster than 128 x 128 on the bare C4 shapes, yet config
+// C4 measured 1.3 % slower with it on every eligible linear -- at one block per CU the fused epilogues are
+// exposed).  SUTA_HB8=1: every eligible GEMM; =2: forced on every K % 32 == 0 (tests: small grids, edge tiles);
+// =3: only GEMMs whose epilogue reads no second operand and writes no extra output; =4: only without a bf16 C
+// copy.  Read per launch so tests can switch it.
+static int use_hb8(const GemmParams& p) {
     const char* e = std::getenv("SUTA_HB8");
     const int mode = e ? atoi(e) : 0;
-    if (K % 64 != 0 || mode == 0) return 0;
-    return mode == 2 || ((M + 255) / 256) * ((N + 255) / 256) >= 256;
+    if (p.K % 32 != 0 || mode == 0) return 0;
+    if (mode == 2) return 1;
+    if (mode == 3 && ((p.epi & (EPI_GELU | EPI_RESID | EPI_STORE_PRE | EPI_DGELU | EPI_ACCUM | EPI_SMBWD)) || p.Cb))
+        return 0;
+    if (mode == 4 && p.Cb) return 0;
+    return ((p.M + 255) / 256) * ((p.N + 255) / 256) >= 256;
 }
 
 void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
@@ -153,12 +160,12 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
         throw std::invalid_argument("gemm: bf16 planes need Z == 1, K, ld % 8 == 0 and 16-B alignment");
     const bool bf16_gbf = p.mode == 2 && glds_ok && p.ta;  // bf16 weight gradients: LDS-DMA fp32 stages
     int tile = g_force_tile >= 0 ? g_force_tile
-               : hb            ? (use_hb8(p.M, p.N, p.K) ? 6 : choose_tile_hb(p.M, p.N))
+               : hb            ? (use_hb8(p) ? 6 : choose_tile_hb(p.M, p.N))
                : p.mode == 2   ? choose_tile_bf16(p.M, p.N, p.Z, !bf16_gbf)
                                : choose_tile(p.M, p.N, p.Z, p.K, p.mode);
     const bool glds_path = p.mode == 0 && g_nbuf == 3 && glds_ok;
     if (tile == 7 && !glds_path) tile = 0;  // the 160-row tile exists only in the default LDS-DMA kernel
-    if (tile == 6 && !(hb && p.K % 64 == 0)) tile = 0;  // the 256 x 256 tile is the bf16-plane ping-pong kernel only
+    if (tile == 6 && !(hb && p.K % 32 == 0)) tile = 0;  // the 256 x 256 tile is the bf16-plane ping-pong kernel only
     if (g_force_tile < 0 && tile == 0 && glds_path && use_tile160(p.M, p.N, p.Z)) tile = 7;
     // tiles 0 = 128x128, 1 = 128x64, 2 = 64x128, 3 = 64x64, 7 = 160x128; bf16 mode also 4 = 256x128,
     // 5 = 128x256

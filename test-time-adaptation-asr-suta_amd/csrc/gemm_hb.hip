@@ -4,7 +4,7 @@
 // ns: 2 (default) | 3 = three LDS stages | 4 = 128-deep bf16 K-steps, two stages (benchmark variants,
 // tools/hb_bench); tile 4 = 256x128, 5 = 128x256 (benchmark only)
 void gemm_run_hb(int tile, int ns, const GemmParams& p, dim3 grid, hipStream_t st) {
-    if (tile == 6) {  // 256 x 256 ping-pong (K % 64 == 0, no split-K)
+    if (tile == 6) {  // 256 x 256 ping-pong (K % 32 == 0, no split-K)
         launch_hb8(p, grid, st);
         return;
     }

@@ -1431,28 +1431,31 @@ void launch_hb(const GemmParams& p, dim3 grid, hipStream_t st) {
 // 256 x 256 bf16-plane GEMM on one block per CU with a ping-pong schedule (cdna_hip_programming.md,
 // "256^2 8-phase template": wave groups offset by one barrier).  8 waves = 2 groups (wr: A rows
 // 128 wr..) x 4 (wc: B rows 64 wc..), wave tile 128 x 64 = 4 x 2 fragments of v_mfma_f32_32x32x16_bf16;
-// two 64-deep K-tile buffers (A 256 x 64 + B 256 x 64 bf16 = 64 KB each, the hb stage image).
+// four 32-deep K-tile buffers (A 256 x 32 + B 256 x 32 bf16 = 32 KB each, the hb stage image), three
+// K-tiles of LDS-DMA in flight ahead of the one being read.
 // Every 16-deep K slice is one phase: ds_read the slice's 6 fragments, [LDS-DMA], barrier, 8 MFMAs at
 // raised priority, barrier.  Group 1 enters one barrier late, so each barrier releases one group into
 // its MFMAs and the other into its reads: a SIMD's two waves (one per group) alternate on the matrix
 // pipe.  Hazards, with group 0's phase-p barriers numbered 2p+1 / 2p+2 and group 1's 2p+2 / 2p+3:
-//   WAR -- K-tile s+1 is staged into the buffer of tile s-1 in phase kc = 1 of tile s (phase 4s+1):
-//          group 0 has passed barrier 8s+2, so group 1 has finished phase 4s-1 (its last read of s-1);
-//   RAW -- every wave retires its DMA (vmcnt(0)) before its first barrier of phase 4s+3; group 0 reads
-//          tile s+1 after barrier 8s+8 (group 1's first barrier of 4s+3), group 1 after 8s+9.
-// Requires K % 64 == 0, no split-K (the dispatcher guarantees both).
+//   WAR -- K-tile s+3 is staged into the buffer of tile s-1 in phase kc = 1 of tile s (phase 2s+1):
+//          group 0 has passed barrier 4s+2, so group 1 has finished phase 2s-1 (its last read of s-1);
+//   RAW -- every wave retires tile s+1's DMA (counted vmcnt: tiles s+2, s+3 may stay in flight) before
+//          its first barrier of phase 2s+1; group 0 reads tile s+1 after barrier 4s+4 (group 1's first
+//          barrier of 2s+1), group 1 after 4s+5.
+// Requires K % 32 == 0, no split-K (the dispatcher guarantees both).
 template <bool CB>
 __global__ __launch_bounds__(512, 1) void gemm_hb8_kernel(GemmParams p) {
-    constexpr int BM = 256, BN = 256, BKS = 32, NWV = 8;
-    constexpr int BUF = (BM + BN) * BKS;  // 4-byte units per K-tile buffer
-    __shared__ __attribute__((aligned(16))) float smem[2 * BUF];
+    constexpr int BM = 256, BN = 256, BKS = 16, NWV = 8, NB = 4;
+    constexpr int NPW = (BM + BN) * BKS / (256 * NWV);  // DMA instructions per wave per K-tile (4)
+    constexpr int BUF = (BM + BN) * BKS;                 // 4-byte units per K-tile buffer
+    __shared__ __attribute__((aligned(16))) float smem[NB * BUF];
 
     const TileId tid = xcd_tile(p.order);
     const float* A = reinterpret_cast<const float*>(p.Ab);
     const float* B = reinterpret_cast<const float*>(p.Bb);
     const long lda = p.ldab / 2, ldb = p.ldbb / 2;  // in 4-byte units
     const int m0 = tid.y * BM, n0 = tid.x * BN;
-    const int nst = p.K / 64;
+    const int nst = p.K / 32;
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wr = wid >> 2, wc = wid & 3;
@@ -1470,9 +1473,15 @@ __global__ __launch_bounds__(512, 1) void gemm_hb8_kernel(GemmParams p) {
     GldsStream<BN, BKS, true, NWV> sb;
     sa.init(A, lda, m0, p.M, 0, wid, lane);
     sb.init(B, ldb, n0, p.N, 0, wid, lane);
-    glds_stream_issue(sa, smem, wid);
-    glds_stream_issue(sb, smem + BM * BKS, wid);
-    wait_vm<0>();
+#pragma unroll
+    for (int t = 0; t < NB - 1; ++t)
+        if (t < nst) {
+            glds_stream_issue(sa, smem + t * BUF, wid);
+            glds_stream_issue(sb, smem + t * BUF + BM * BKS, wid);
+        }
+    if (nst >= 3) wait_vm<2 * NPW>();
+    else if (nst == 2) wait_vm<NPW>();
+    else wait_vm<0>();
     __builtin_amdgcn_s_barrier();
     if (wr == 1) __builtin_amdgcn_s_barrier();  // the stagger
     __builtin_amdgcn_sched_barrier(0);
@@ -1482,21 +1491,27 @@ __global__ __launch_bounds__(512, 1) void gemm_hb8_kernel(GemmParams p) {
         return *reinterpret_cast<const bf16x8*>(lds + row * BKS + ((c ^ glds_swz<BKS>(row)) * 4));
     };
     for (int s = 0; s < nst; ++s) {
-        const float* As = smem + (s & 1) * BUF;
+        const float* As = smem + (s % NB) * BUF;
         const float* Bs = As + BM * BKS;
-        float* nxt = smem + ((s + 1) & 1) * BUF;
 #pragma unroll
-        for (int kc = 0; kc < 4; ++kc) {
+        for (int kc = 0; kc < 2; ++kc) {
             bf16x8 af[4], bf[2];
 #pragma unroll
             for (int j = 0; j < 2; ++j) bf[j] = frag(Bs, wc * 64 + j * 32 + l32, kc);
 #pragma unroll
             for (int i = 0; i < 4; ++i) af[i] = frag(As, wr * 128 + i * 32 + l32, kc);
-            if (kc == 1 && s + 1 < nst) {
-                glds_stream_issue(sa, nxt, wid);
-                glds_stream_issue(sb, nxt + BM * BKS, wid);
+            if (kc == 1) {
+                if (s + 3 < nst) {
+                    float* nxt = smem + ((s + 3) % NB) * BUF;
+                    glds_stream_issue(sa, nxt, wid);
+                    glds_stream_issue(sb, nxt + BM * BKS, wid);
+                    wait_vm<2 * NPW>();  // tile s+1 landed; s+2, s+3 in flight
+                } else if (s + 2 < nst) {
+                    wait_vm<NPW>();
+                } else {
+                    wait_vm<0>();
+                }
             }
-            if (kc == 3) wait_vm<0>();
             __builtin_amdgcn_sched_barrier(0);
             __builtin_amdgcn_s_barrier();
             __builtin_amdgcn_sched_barrier(0);

@@ -184,7 +184,7 @@ def test_bf16_posconv_kernel_equals_conv_a_path(monkeypatch):
 
 def test_bf16_hb8_pingpong_kernel(monkeypatch):
     """gemm_hb8_kernel (256 x 256 tile, two wave groups one barrier apart) forced on every bf16-plane linear
-    with K % 64 == 0 (SUTA_HB8=2; by default it runs only where the grid has >= 256 tiles, i.e. config C4's
+    with K % 32 == 0 (SUTA_HB8=2; by default it runs only where the grid has >= 256 tiles, i.e. config C4's
     64 x 8 s batches): the large model's 20-step SUTA against the reference goldens g7, reruns bitwise
     identical, and a ragged pair (edge tiles: 198 and 124 rows of a 256-row tile) against the 128 x 128
     kernel (SUTA_HB8=0) to bf16 tolerance (same operand roundings, another fp32 summation order)."""
