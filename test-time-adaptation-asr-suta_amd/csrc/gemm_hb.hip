@@ -1,11 +1,13 @@
 // bf16 GEMM on bf16 operand planes (LDS-DMA staging, 64-deep K-steps) + the fp32 -> bf16 plane conversion.
 #include "gemm_kernels.h"
+#include <cstdlib>
 
 // ns: 2 (default) | 3 = three LDS stages | 4 = 128-deep bf16 K-steps, two stages (benchmark variants,
 // tools/hb_bench); tile 4 = 256x128, 5 = 128x256 (benchmark only)
 void gemm_run_hb(int tile, int ns, const GemmParams& p, dim3 grid, hipStream_t st) {
     if (tile == 6) {  // 256 x 256 ping-pong (K % 32 == 0, no split-K)
-        launch_hb8(p, grid, st);
+        const char* e = std::getenv("SUTA_HB8_PF");  // 1: fragments read one phase ahead
+        launch_hb8(p, grid, st, e && atoi(e) == 1);
         return;
     }
     if (tile == 4) {

@@ -1443,7 +1443,9 @@ void launch_hb(const GemmParams& p, dim3 grid, hipStream_t st) {
 //          its first barrier of phase 2s+1; group 0 reads tile s+1 after barrier 4s+4 (group 1's first
 //          barrier of 2s+1), group 1 after 4s+5.
 // Requires K % 32 == 0, no split-K (the dispatcher guarantees both).
-template <bool CB>
+// PF: fragments read one phase ahead (after the phase's first barrier, into a second register set) so the
+// MFMAs never wait on this phase's LDS reads; tile s+1 is then retired one phase earlier (kc = 0 of tile s).
+template <bool CB, bool PF>
 __global__ __launch_bounds__(512, 1) void gemm_hb8_kernel(GemmParams p) {
     constexpr int BM = 256, BN = 256, BKS = 16, NWV = 8, NB = 4;
     constexpr int NPW = (BM + BN) * BKS / (256 * NWV);  // DMA instructions per wave per K-tile (4)
@@ -1490,41 +1492,100 @@ __global__ __launch_bounds__(512, 1) void gemm_hb8_kernel(GemmParams p) {
         const int c = 2 * kc + h;
         return *reinterpret_cast<const bf16x8*>(lds + row * BKS + ((c ^ glds_swz<BKS>(row)) * 4));
     };
-    for (int s = 0; s < nst; ++s) {
-        const float* As = smem + (s % NB) * BUF;
-        const float* Bs = As + BM * BKS;
+    if constexpr (PF) {
+        bf16x8 xa[4], xb[2], ya[4], yb[2];  // X: slice kc = 0, Y: slice kc = 1 of the current tile
 #pragma unroll
-        for (int kc = 0; kc < 2; ++kc) {
-            bf16x8 af[4], bf[2];
+        for (int j = 0; j < 2; ++j) xb[j] = frag(smem + BM * BKS, wc * 64 + j * 32 + l32, 0);
 #pragma unroll
-            for (int j = 0; j < 2; ++j) bf[j] = frag(Bs, wc * 64 + j * 32 + l32, kc);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) af[i] = frag(As, wr * 128 + i * 32 + l32, kc);
-            if (kc == 1) {
-                if (s + 3 < nst) {
-                    float* nxt = smem + ((s + 3) % NB) * BUF;
-                    glds_stream_issue(sa, nxt, wid);
-                    glds_stream_issue(sb, nxt + BM * BKS, wid);
-                    wait_vm<2 * NPW>();  // tile s+1 landed; s+2, s+3 in flight
-                } else if (s + 2 < nst) {
-                    wait_vm<NPW>();
-                } else {
-                    wait_vm<0>();
-                }
-            }
+        for (int i = 0; i < 4; ++i) xa[i] = frag(smem, wr * 128 + i * 32 + l32, 0);
+        for (int s = 0; s < nst; ++s) {
+            const float* As = smem + (s % NB) * BUF;
+            const float* Bs = As + BM * BKS;
+            const float* An = smem + ((s + 1) % NB) * BUF;
+            const float* Bn = An + BM * BKS;
+            // phase kc = 0: retire tile s+1 (read from the next phase on), MFMAs on X, read Y
+            if (s + 2 < nst) wait_vm<NPW>();
+            else wait_vm<0>();
             __builtin_amdgcn_sched_barrier(0);
             __builtin_amdgcn_s_barrier();
             __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) yb[j] = frag(Bs, wc * 64 + j * 32 + l32, 1);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) ya[i] = frag(As, wr * 128 + i * 32 + l32, 1);
             __builtin_amdgcn_s_setprio(1);
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
                 for (int j = 0; j < 2; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa[i], xb[j], acc[i][j], 0, 0, 0);
             __builtin_amdgcn_s_setprio(0);
             __builtin_amdgcn_sched_barrier(0);
             __builtin_amdgcn_s_barrier();
             __builtin_amdgcn_sched_barrier(0);
+            // phase kc = 1: stage tile s+3, MFMAs on Y, read X of tile s+1
+            if (s + 3 < nst) {
+                float* nxt = smem + ((s + 3) % NB) * BUF;
+                glds_stream_issue(sa, nxt, wid);
+                glds_stream_issue(sb, nxt + BM * BKS, wid);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+            if (s + 1 < nst) {
+#pragma unroll
+                for (int j = 0; j < 2; ++j) xb[j] = frag(Bn, wc * 64 + j * 32 + l32, 0);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) xa[i] = frag(An, wr * 128 + i * 32 + l32, 0);
+            }
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ya[i], yb[j], acc[i][j], 0, 0, 0);
+            __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    } else {
+    for (int s = 0; s < nst; ++s) {
+            const float* As = smem + (s % NB) * BUF;
+            const float* Bs = As + BM * BKS;
+    #pragma unroll
+            for (int kc = 0; kc < 2; ++kc) {
+                bf16x8 af[4], bf[2];
+    #pragma unroll
+                for (int j = 0; j < 2; ++j) bf[j] = frag(Bs, wc * 64 + j * 32 + l32, kc);
+    #pragma unroll
+                for (int i = 0; i < 4; ++i) af[i] = frag(As, wr * 128 + i * 32 + l32, kc);
+                if (kc == 1) {
+                    if (s + 3 < nst) {
+                        float* nxt = smem + ((s + 3) % NB) * BUF;
+                        glds_stream_issue(sa, nxt, wid);
+                        glds_stream_issue(sb, nxt + BM * BKS, wid);
+                        wait_vm<2 * NPW>();  // tile s+1 landed; s+2, s+3 in flight
+                    } else if (s + 2 < nst) {
+                        wait_vm<NPW>();
+                    } else {
+                        wait_vm<0>();
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_s_barrier();
+                __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_s_setprio(1);
+    #pragma unroll
+                for (int i = 0; i < 4; ++i)
+    #pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+                __builtin_amdgcn_s_setprio(0);
+                __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_s_barrier();
+                __builtin_amdgcn_sched_barrier(0);
+            }
         }
     }
     if (wr == 0) __builtin_amdgcn_s_barrier();  // equal barrier counts in both groups
@@ -1537,9 +1598,14 @@ __global__ __launch_bounds__(512, 1) void gemm_hb8_kernel(GemmParams p) {
                             n0 + wc * 64, h, l32, interior, tid.z);
 }
 
-inline void launch_hb8(const GemmParams& p, dim3 grid, hipStream_t st) {
-    if (p.Cb) hipLaunchKernelGGL(gemm_hb8_kernel<true>, grid, dim3(512), 0, st, p);
-    else hipLaunchKernelGGL(gemm_hb8_kernel<false>, grid, dim3(512), 0, st, p);
+inline void launch_hb8(const GemmParams& p, dim3 grid, hipStream_t st, bool pf) {
+    if (pf) {
+        if (p.Cb) hipLaunchKernelGGL((gemm_hb8_kernel<true, true>), grid, dim3(512), 0, st, p);
+        else hipLaunchKernelGGL((gemm_hb8_kernel<false, true>), grid, dim3(512), 0, st, p);
+    } else {
+        if (p.Cb) hipLaunchKernelGGL((gemm_hb8_kernel<true, false>), grid, dim3(512), 0, st, p);
+        else hipLaunchKernelGGL((gemm_hb8_kernel<false, false>), grid, dim3(512), 0, st, p);
+    }
 }
 
 }  // namespace

@@ -43,12 +43,14 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    const int variants[][2] = {{0, 2}, {6, 2}, {0, 2}, {6, 2}};  // (tile, ns) -- gemm_run_hb (6: 256x256 ping-pong)
+    // (tile, ns, pf) -- gemm_run_hb (6: 256x256 ping-pong; pf: SUTA_HB8_PF, fragments read one phase ahead)
+    const int variants[][3] = {{0, 2, 0}, {6, 2, 0}, {6, 2, 1}, {0, 2, 0}, {6, 2, 0}, {6, 2, 1}};
     __bf16* Cb;
     CK(hipMalloc(&Cb, (size_t)M * 4096 * 2));
     for (auto& s : shapes) {
         for (auto& vt : variants) {
             const int ti = vt[0], ns = vt[1];
+            setenv("SUTA_HB8_PF", vt[2] ? "1" : "0", 1);
             {
                 GemmParams p;
                 gemm_init(p);
@@ -88,7 +90,7 @@ int main(int argc, char** argv) {
                 for (int r = 0; r < rows; ++r)
                     for (int n = 0; n < s.N; ++n)
                         err = fmax(err, fabs(hc[(size_t)r * rstep * s.N + n] - hr[(size_t)r * s.N + n]));
-                printf("%s tile %d ns %d: %.4f ms %.1f TF maxerr %.2e bf16-copy relerr %.2e\n", s.name, ti, ns, ms, tf, err, errb);
+                printf("%s tile %d ns %d pf %d: %.4f ms %.1f TF maxerr %.2e bf16-copy relerr %.2e\n", s.name, ti, ns, vt[2], ms, tf, err, errb);
                 fflush(stdout);
             }
     }
