@@ -1,0 +1,9 @@
+# Final tree check: GPU suite + smoke + default bench on the shipped libsuta.so.
+set -e
+export TMPDIR=/tmp
+O=gpurun_out/final
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+timeout -k 10 500 python bench.py > $O/bench.json 2> $O/bench.err
+echo done
