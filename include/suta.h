@@ -177,6 +177,14 @@ int32_t suta_get_timing(suta_engine* e, double* ms_out /*[6]*/, int64_t* launche
 int32_t suta_get_timing_ex(suta_engine* e, int32_t nfam, double* ms_out, int64_t* launches_out,
                            double* alg_bytes_out);
 
+/* GEMM launch census (process-wide; not in the reference, test/bench instrumentation): while enabled,
+ * every GEMM launch the engine issues (eagerly or while capturing a graph; replays issue none) is
+ * counted per "<kernel> <BMxBN> z=<batch> split=<k> <A/B form>" key.  suta_set_census(1) clears and
+ * starts it, suta_get_census copies "key count\n" lines (needed = bytes incl. the NUL).  Used by
+ * tests/test_gpu_bench_scale.py to assert which tile and weight-gradient schedule a layout reaches. */
+int32_t suta_set_census(int32_t enable);
+int32_t suta_get_census(char* buf, int64_t cap, int64_t* needed);
+
 /* GEMM arithmetic.  The first two are fp32-accurate; results agree to fp32 rounding
  * (tests/test_gpu_parity.py):
  *   SUTA_PRECISION_FP32_MFMA        v_mfma_f32_32x32x2_f32: exact fp32 products, fp32 accumulation
@@ -187,8 +195,8 @@ int32_t suta_get_timing_ex(suta_engine* e, int32_t nfam, double* ms_out, int64_t
  *                                   operand rounded to bf16 (RNE) as it enters the MFMA, fp32
  *                                   accumulation; activations, norms, softmax, loss, AdamW and the
  *                                   trainable master tensors stay fp32 (torch.autocast(bf16)
- *                                   semantics for the matmuls) -- tests/test_gpu_bf16.py states the
- *                                   tolerance */
+ *                                   semantics for the matmuls) -- tests/parity.py (assert_bf16_close) states the
+ *                                   tolerance, tests/test_gpu_large_bf16.py applies it */
 #define SUTA_PRECISION_FP32_MFMA 0
 #define SUTA_PRECISION_FP32_SPLIT_BF16 1
 #define SUTA_PRECISION_BF16 2

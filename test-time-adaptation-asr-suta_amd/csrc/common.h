@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string>
 
 #define SUTA_WAVE 64
 
@@ -111,3 +112,6 @@ void gemm_set_mode(int mode);
 // with row stride K: the A plane of a bf16-plane GEMM.
 void launch_to_bf16(const float* src, long lds, long rows, int K, void* dst, hipStream_t st);
 int gemm_get_mode();
+// launch census per (kernel, tile, Z, splits, operand form): suta_set_census / suta_get_census
+void gemm_census_enable(bool on);
+std::string gemm_census_text();

@@ -337,6 +337,7 @@ struct suta_engine {
                     timed(F_GEMM, [&] { gemm_launch(p, st, plan.splitws, plan.splitws_floats); }, ab);
                     return;
                 }
+                if (!p.A) throw SutaError(SUTA_ERR_UNSUPPORTED, "gemm: neither an fp32 A nor its bf16 plane");
                 if (abuf.alloc((size_t)p.M * p.K * 2 + 256)) drop_graph();
                 p.Ab = abuf.p;
                 p.ldab = p.K;
@@ -348,6 +349,7 @@ struct suta_engine {
             }
         }
         if (!p.C) throw SutaError(SUTA_ERR_UNSUPPORTED, "gemm: fp32 output skipped on a plane-less GEMM");
+        if (!p.A) throw SutaError(SUTA_ERR_UNSUPPORTED, "gemm: fp32 A not written (bf16-plane producer) on a plane-less GEMM");
         p.Ab = nullptr;  // (plane-less GEMM: a plane given for a non-frozen B is ignored)
         p.Cb = nullptr;
         timed(F_GEMM, [&] { gemm_launch(p, st, plan.splitws, plan.splitws_floats); }, ab);
@@ -691,7 +693,7 @@ void suta_engine::forward(int B) {
                 launch_layernorm_fwd(lb.x_in, P + o_l1g[l], P + o_l1b[l], Pn, T, dead ? nullptr : lb.y1, lb.xhat1,
                                      lb.rstd1, (int)BT, H, k.eps, 0, st, P0, lb.mean1);
             });
-            attn_in = lb.y1;
+            attn_in = dead ? nullptr : lb.y1;  // (dead: the QKV GEMM reads the LN1 plane only)
         }
         {  // fused QKV
             GemmParams g;
@@ -800,7 +802,7 @@ void suta_engine::forward(int B) {
                 launch_layernorm_fwd(lb.hmid, P + o_l2g[l], P + o_l2b[l], Pn, T, dead ? nullptr : lb.y2, lb.xhat2,
                                      lb.rstd2, (int)BT, H, k.eps, 0, st, P0, lb.mean2);
             });
-            ffn_in = lb.y2;
+            ffn_in = dead ? nullptr : lb.y2;
             ffn_res = lb.hmid;
             ffn_out = lb.x_out;
         } else {
@@ -838,7 +840,7 @@ void suta_engine::forward(int B) {
         {  // out = gu W2^T + b2 + residual
             GemmParams g;
             gemm_init(g);
-            g.A = pl.gu;
+            g.A = dead ? nullptr : pl.gu;
             g.lda = k.F;
             g.Ab = P1;
             g.ldab = k.F;
@@ -869,7 +871,7 @@ void suta_engine::forward(int B) {
             launch_layernorm_fwd(hfin, P + o_eg, P + o_eb, Pn, T, dead ? nullptr : pl.enc_y, pl.enc_xhat, pl.enc_rstd,
                                  (int)BT, H, k.eps, 0, st, P0, pl.enc_mean);
         });
-        hfin = pl.enc_y;
+        hfin = dead ? nullptr : pl.enc_y;
     }
     {  // lm_head
         GemmParams g;
@@ -974,7 +976,7 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
             // du = (dr2 @ W2) * gelu'(u)
             nn_gemm(t1, H, w2[l], k.F, du32, k.F, (int)BT, k.F, H, EPI_DGELU, nullptr, 0, lb.u, k.F, P0, P1);
             // dh1 = du @ W1 + dr2
-            nn_gemm(pl.du, k.F, w1[l], H, t2, H, (int)BT, H, k.F, EPI_RESID, t1, H, nullptr, 0, P1);
+            nn_gemm(du32, k.F, w1[l], H, t2, H, (int)BT, H, k.F, EPI_RESID, t1, H, nullptr, 0, P1);
             // dr1 = LN1 bwd(dh1)
             timed(F_NORM, [&] {
                 launch_layernorm_bwd(t2, lb.xhat1, lb.rstd1, P + o_l1g[l], P + o_l1b[l], Pn, T, B, H, 0, nullptr,
@@ -984,7 +986,7 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
         } else {
             // du = (dx @ W2) * gelu'(u); dy2 = du @ W1; dhmid = LN2 bwd(dy2) + dx
             nn_gemm(dx, H, w2[l], k.F, du32, k.F, (int)BT, k.F, H, EPI_DGELU, nullptr, 0, lb.u, k.F, P0, P1);
-            nn_gemm(pl.du, k.F, w1[l], H, t2, H, (int)BT, H, k.F, 0, nullptr, 0, nullptr, 0, P1);
+            nn_gemm(du32, k.F, w1[l], H, t2, H, (int)BT, H, k.F, 0, nullptr, 0, nullptr, 0, P1);
             timed(F_NORM, [&] {
                 launch_layernorm_bwd(t2, lb.xhat2, lb.rstd2, P + o_l2g[l], P + o_l2b[l], Pn, T, B, H, 0, nullptr, dx,
                                      t1, G + o_l2g[l], G + o_l2b[l], Pn, pl.lnpart, st, P0, lb.hmid, lb.mean2);
@@ -2049,6 +2051,19 @@ int32_t suta_set_precision(suta_engine* e, int32_t mode) {
 
 int32_t suta_set_graphs(suta_engine* e, int32_t enable) {
     return guard([&] { e->use_graphs = enable != 0; });
+}
+
+int32_t suta_set_census(int32_t enable) {
+    return guard([&] { gemm_census_enable(enable != 0); });
+}
+
+int32_t suta_get_census(char* buf, int64_t cap, int64_t* needed) {
+    return guard([&] {
+        const std::string t = gemm_census_text();
+        if (needed) *needed = (int64_t)t.size() + 1;
+        if (!buf || cap < (int64_t)t.size() + 1) throw SutaError(SUTA_ERR_ARG, "census buffer too small");
+        memcpy(buf, t.c_str(), t.size() + 1);
+    });
 }
 
 }  // extern "C"

@@ -1,8 +1,12 @@
 // GEMM dispatcher: tile choice, split-K, precision mode -> kernel family (gemm_kernels.h).
 #include "gemm_kernels.h"
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
+#include <map>
+#include <mutex>
 #include <stdexcept>
+#include <string>
 
 namespace {
 
@@ -17,6 +21,35 @@ int g_mode = 0;  // 0 = exact fp32 MFMA, 1 = x6 (fp32-accurate bf16 split), 2 = 
 void gemm_set_variant(int tile, int nbuf) {
     g_force_tile = tile;
     g_nbuf = nbuf;
+}
+
+// Kernel census (suta_set_census / suta_get_census): host-side count of GEMM launches per
+// (kernel, tile, batch count, split count, operand form), so a test can assert which instantiation a
+// layout reaches.  Counted when a launch is issued (eager or while a graph is captured), not on replay.
+static std::mutex g_census_mu;
+static std::map<std::string, long> g_census;
+static bool g_census_on = false;
+
+void gemm_census_enable(bool on) {
+    std::lock_guard<std::mutex> lk(g_census_mu);
+    g_census_on = on;
+    g_census.clear();
+}
+
+std::string gemm_census_text() {
+    std::lock_guard<std::mutex> lk(g_census_mu);
+    std::string out;
+    for (const auto& kv : g_census) out += kv.first + " " + std::to_string(kv.second) + "\n";
+    return out;
+}
+
+static void census(const char* kernel, int BM, int BN, const GemmParams& p, int splits) {
+    if (!g_census_on) return;
+    char key[160];
+    snprintf(key, sizeof key, "%s %dx%d z=%ld split=%d %s%s", kernel, BM, BN, (long)p.Z, splits, p.ta ? "T" : "N",
+             p.tb ? "T" : "N");
+    std::lock_guard<std::mutex> lk(g_census_mu);
+    ++g_census[key];
 }
 
 void gemm_set_mode(int mode) { g_mode = mode; }
@@ -199,23 +232,29 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
     }
     dim3 grid(gx, gy, p.Z * splits);
     if (hb) {
+        census(tile == 6 ? "hb8" : "hb", BM, BN, p, splits);
         gemm_run_hb(tile, g_force_tile >= 0 ? g_nbuf : 2, p, grid, st);
     } else if (p.mode == 2) {
         // bf16: register-staged one-plane kernel; weight gradients (and benchmark variants 3 / 8) on
         // register-converted LDS-DMA stages (8 = BK64 x 2)
         const bool gbf = glds_ok && tile < 4 && (g_force_tile >= 0 ? (g_nbuf == 3 || g_nbuf == 8) : bf16_gbf);
+        census(gbf ? "gbf" : "x6_1plane", BM, BN, p, splits);
         if (gbf) gemm_run_gbf(g_nbuf == 8, 1, tile, p, grid, st);
         else gemm_run_x6(tile, 0, 1, p, grid, st);
     } else if (p.mode == 1 && glds_ok && g_nbuf >= 9) {
         // x6 with register splits on LDS-DMA stages (benchmark variants 9 = BK32 x 2, 10 = BK64 x 2)
+        census("gbf_x6", BM, BN, p, splits);
         gemm_run_gbf(g_nbuf == 10, 6, tile, p, grid, st);
     } else if (p.mode == 1) {
         // x6 planes: g_nbuf 2 -> BK 16 double-buffered; else BK 32 single LDS stage
+        census("x6", BM, BN, p, splits);
         gemm_run_x6(tile, g_nbuf == 2, 3, p, grid, st);
     } else if (g_nbuf >= 3 && glds_ok) {
         // LDS-DMA variants: 3 = BK32 x 2 stages, 4 = BK16 x 4, 5 = BK16 x 3, 6 = BK32 x 3, 7 = BK64 x 2
+        census("glds", BM, BN, p, splits);
         gemm_run_glds(g_nbuf, tile, p, grid, st);
     } else {
+        census("f32", BM, BN, p, splits);
         gemm_run_f32(tile, g_nbuf == 2 ? 2 : 1, p, grid, st);
     }
     if (splits > 1) {

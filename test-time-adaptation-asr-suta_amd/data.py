@@ -9,11 +9,14 @@ Behaviour kept from the reference:
   * audio_reader (data.py:13-25): decode, resample to 16 kHz, truncate at 600 000 samples,
     add extra_noise * N(0, 1) noise
   * collate (data.py:27-45): sort a bucket by audio length, descending
-Deviations (documented in DESIGN.md): torchaudio/soundfile are not installed in this image, so
-WAV is decoded with the standard-library `wave` module when neither is present (FLAC then needs
-soundfile or torchaudio); resampling falls back to scipy's polyphase filter; the noise comes from
-a torch.Generator seeded 0 in the reading process (the reference's draw depends on DataLoader
-worker seeding and on transformers consuming the global RNG).
+Deviations (documented in DESIGN.md): torchaudio/soundfile are not installed in this image, so FLAC
+is decoded by the from-spec decoder in libsuta_audio (csrc/flac.cpp), WAV by the standard-library
+`wave` module, and resampling restates torchaudio's Hann-windowed sinc resampler (`resample`).  The
+noise of utterance i comes from its own torch.Generator seeded `seed * 1_000_003 + i` (i = its index in
+the sorted dataset), so every rank of a sharded run draws exactly the audio a single process draws
+(the reference's draw depends on DataLoader worker seeding and on transformers consuming the global
+RNG, SURVEY.md Appendix B.3, so noise parity with it is statistical either way).
+Under torchrun only rank 0 prints the loaders' [INFO] lines.
 """
 from __future__ import annotations
 
@@ -124,6 +127,7 @@ class CVDataset(_Corpus):
         df = pd.read_csv(path + "/test.tsv", sep="\t")
         texts = list(df["sentence"].apply(preprocess_cv_text).values)
         files = [os.path.join(path + "/clips", f) for f in df["path"].values]
+        _say(len(files), len(texts))   # commonvoice.py:40
         self._finish(files, texts, ascending)
 
 
@@ -154,6 +158,12 @@ class TedDataset(_Corpus):
                 return line.strip("\n")
 
 
+def _say(*a):
+    """print on rank 0 only (a sharded run is one job: its log reads like the reference's one process)."""
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a)
+
+
 def create_dataset(split, name, path, batch_size=1):
     """data.py:48-68."""
     n = name.lower()
@@ -161,7 +171,7 @@ def create_dataset(split, name, path, batch_size=1):
     if n not in table:
         raise NotImplementedError(name)
     ds = table[n](split, batch_size, path)
-    print(f"[INFO]    There are {len(ds)} samples.")
+    _say(f"[INFO]    There are {len(ds)} samples.")
     return ds, batch_size
 
 
@@ -364,45 +374,68 @@ def resample(x: np.ndarray, sr: int, target: int = SAMPLE_RATE) -> np.ndarray:
     return y[:target_len].numpy()
 
 
+NOISE_SEED_STRIDE = 1_000_003
+
+
 class AudioReader:
-    """data.py:13-25.  decode() is thread-safe (the loader runs it on worker threads); the noise is
-    drawn in load order by noise(), from a torch.Generator seeded 0 (see module docstring)."""
+    """data.py:13-25.  decode() is thread-safe (the loader runs it on worker threads) and returns the
+    utterance with its decoded length; the truncation lines are printed by the caller in load order.
+    noise(x, index) draws utterance `index`'s noise from its own generator (module docstring)."""
 
     def __init__(self, extra_noise: float = 0.0, max_len: int = MAX_LEN, seed: int = 0):
-        import torch
         self.extra_noise = extra_noise
         self.max_len = max_len
-        self.gen = torch.Generator().manual_seed(seed)
+        self.seed = seed
 
-    def decode(self, path: str) -> np.ndarray:
+    def decode(self, path: str) -> Tuple[np.ndarray, int]:
+        """(waveform truncated to max_len, decoded length before truncation)."""
         x, sr = decode_channels(str(path))
         if sr != SAMPLE_RATE:  # the reference resamples the (C, N) tensor per channel, then flattens
             x = np.stack([resample(c, sr) for c in x])
         x = x.reshape(-1)
-        if x.shape[-1] >= self.max_len:
-            print(f"{path} has len {x.shape}, truncate to {self.max_len}")
+        n = int(x.shape[-1])
+        if n >= self.max_len:
             x = x[: self.max_len]
-        return np.ascontiguousarray(x, dtype=np.float32)
+        return np.ascontiguousarray(x, dtype=np.float32), n
 
-    def noise(self, x: np.ndarray) -> np.ndarray:
+    def truncation_lines(self, path: str, n: int) -> List[str]:
+        """What the reference prints for an utterance cut at max_len (data.py:19-21: the message, then
+        wav.shape, both as torch.Size)."""
+        if n < self.max_len:
+            return []
+        return [f"{path} has len torch.Size([{n}]), truncate to {self.max_len}", f"torch.Size([{self.max_len}])"]
+
+    def noise(self, x: np.ndarray, index: int = 0) -> np.ndarray:
         import torch
         w = torch.from_numpy(x)
         if self.extra_noise:
-            w = w + self.extra_noise * torch.randn(w.shape, generator=self.gen)
+            g = torch.Generator().manual_seed(self.seed * NOISE_SEED_STRIDE + int(index))
+            w = w + self.extra_noise * torch.randn(w.shape, generator=g)
         return w.numpy()
 
-    def __call__(self, path: str) -> np.ndarray:
-        return self.noise(self.decode(path))
+    def __call__(self, path: str, index: int = 0) -> np.ndarray:
+        x, n = self.decode(path)
+        for ln in self.truncation_lines(str(path), n):
+            print(ln)
+        return self.noise(x, index)
 
 
-def collect_audio_batch(batch, reader: AudioReader, decoded=None):
+def collect_audio_batch(batch, reader: AudioReader, decoded=None, indices=None, log=None):
     """data.py:9-45: read a bucket, sort by audio length descending.  `decoded`: the bucket's
-    waveforms already decoded (by loader threads); noise is still drawn here, in load order."""
+    (waveform, decoded length) pairs already decoded by loader threads; `indices`: the items' dataset
+    indices (their noise seeds; default 0..len-1); `log`: a list collecting the truncation lines in load
+    order (printed here when None)."""
     if type(batch[0]) is not tuple:
         batch = batch[0]
     if decoded is None:
         decoded = [reader.decode(str(b[0])) for b in batch]
-    feats = [(reader.noise(w), str(b[0]).split("/")[-1].split(".")[0], b[1]) for w, b in zip(decoded, batch)]
+    if indices is None:
+        indices = range(len(batch))
+    feats = []
+    for (w, n), b, i in zip(decoded, batch, indices):
+        for ln in reader.truncation_lines(str(b[0]), n):
+            print(ln) if log is None else log.append(ln)
+        feats.append((reader.noise(w, i), str(b[0]).split("/")[-1].split(".")[0], b[1]))
     feats = sorted(((len(f), n, f, t) for f, n, t in feats), reverse=True, key=lambda x: x[0])
     lens, files, wavs, texts = zip(*feats)
     return lens, wavs, texts, files
@@ -426,17 +459,37 @@ def load_dataset(split=None, name="librispeech", path=None, batch_size=1, extra_
                 out.append(list(it) if isinstance(it, list) else [it])
             return out
 
-        def collate(self, items, decoded=None):
-            return collect_audio_batch(items, reader, decoded)
+        def batch_indices(self) -> List[List[int]]:
+            """dataset index of every item of raw_batches() (a bucket starting past len - bucket_size
+            is moved back, as _Corpus.__getitem__ does)."""
+            out, every = [], list(range(len(ds)))
+            for i in range(0, len(ds), bs):
+                start = min(len(ds) - bs, i) if bs > 1 else i
+                out.append(every[start:start + bs] if bs > 1 else [i])
+            return out
 
-        def iter_collated(self, indices: Sequence[int], workers: int = 0, window: int = 32):
+        def collate(self, items, decoded=None, indices=None, log=None):
+            return collect_audio_batch(items, reader, decoded, indices, log)
+
+        def iter_collated(self, indices: Sequence[int], workers: int = 0, window: int = 32, log=None):
             """(index, collated batch) for the given loader batches, in order.  workers > 1 decodes
             ahead on a thread pool (the FLAC decoder and file reads release the GIL), at most
-            `window` batches in flight; the noise draw stays sequential (deterministic)."""
+            `window` batches in flight; noise is keyed on each item's dataset index, so the result
+            does not depend on which batches this process loads or in what order.  `log`: a callable
+            taking (loader batch index, truncation lines) instead of printing them."""
             batches = self.raw_batches()
+            didx = self.batch_indices()
+
+            def coll(i, decoded=None):
+                lines = [] if log is not None else None
+                out = self.collate(batches[i], decoded, didx[i], lines)
+                if log is not None:
+                    log(i, lines)
+                return out
+
             if workers <= 1:
                 for i in indices:
-                    yield i, self.collate(batches[i])
+                    yield i, coll(i)
                 return
             from collections import deque
             from concurrent.futures import ThreadPoolExecutor
@@ -449,7 +502,7 @@ def load_dataset(split=None, name="librispeech", path=None, batch_size=1, extra_
                         break
                 while pending:
                     i, futs = pending.popleft()
-                    yield i, self.collate(batches[i], [f.result() for f in futs])
+                    yield i, coll(i, [f.result() for f in futs])
                     nxt = next(it, None)
                     if nxt is not None:
                         pending.append((nxt, [ex.submit(reader.decode, str(f)) for f, _ in batches[nxt]]))

@@ -20,7 +20,8 @@ MAX_CONV = 8
 # exported symbols (kept in sync with include/suta.h; tests/test_abi.py checks both)
 EXPORTS = ("suta_create", "suta_destroy", "suta_reset", "suta_num_frames", "suta_forward", "suta_step",
            "suta_adapt", "suta_adapt_varlen", "suta_loss_grad", "suta_get_param", "suta_param_info", "suta_sync", "suta_stream", "suta_set_timing",
-           "suta_get_timing", "suta_get_timing_ex", "suta_set_precision", "suta_set_graphs", "suta_last_error")
+           "suta_get_timing", "suta_get_timing_ex", "suta_set_precision", "suta_set_graphs", "suta_set_census",
+           "suta_get_census", "suta_last_error")
 
 
 class ModelConfigC(C.Structure):
@@ -102,6 +103,9 @@ def load_library(path: str = LIB_PATH):
     if hasattr(lib, "suta_get_timing_ex"):
         lib.suta_get_timing_ex.argtypes = [C.c_void_p, C.c_int32, P(C.c_double), i64p, P(C.c_double)]
     lib.suta_set_graphs.argtypes = [C.c_void_p, C.c_int32]
+    if hasattr(lib, "suta_set_census"):
+        lib.suta_set_census.argtypes = [C.c_int32]
+        lib.suta_get_census.argtypes = [C.c_char_p, C.c_int64, i64p]
     lib.suta_set_precision.argtypes = [C.c_void_p, C.c_int32]
     lib.suta_last_error.restype = C.c_char_p
     for name in EXPORTS:
@@ -328,3 +332,19 @@ class SutaEngine:
 
     def set_graphs(self, enable: bool):
         _check(self.lib.suta_set_graphs(self.handle, int(enable)))
+
+    def set_census(self, enable: bool):
+        """Start (clear) or stop the process-wide GEMM launch census (suta_set_census)."""
+        _check(self.lib.suta_set_census(int(enable)))
+
+    def get_census(self) -> Dict[str, int]:
+        """{"<kernel> <BMxBN> z=<Z> split=<k> <form>": launches} since set_census(True)."""
+        need = C.c_int64()
+        self.lib.suta_get_census(None, 0, C.byref(need))
+        buf = C.create_string_buffer(int(need.value))
+        _check(self.lib.suta_get_census(buf, need.value, C.byref(need)))
+        out = {}
+        for ln in buf.value.decode().splitlines():
+            key, n = ln.rsplit(" ", 1)
+            out[key] = int(n)
+        return out

@@ -197,6 +197,16 @@ def main(argv=None, sdpl: bool = False):
         say(line)
 
     cfg, weights = load_model(a.asr, a.synthetic_weights)
+    # collect_params (main.py:79-80 prints every module name; main_SDPL.py's copy does not), setup_optimizer
+    # (main.py:19-20), then print(param_names) (main.py:314, main_SDPL.py:321)
+    from .modules import collect_params
+    printed, param_names = collect_params(cfg, a.bias_only, a.train_feature)
+    if not sdpl:
+        for nm in printed:
+            say(nm)
+    say(f"[INFO]    optimizer: {getattr(torch.optim, a.opt)}")
+    say(f"[INFO]    scheduler: {a.scheduler}")
+    say(param_names)
     gb = max(1, a.gpu_batch) if a.episodic else 1  # non-episodic adaptation is sequential
     engine = SutaEngine(cfg, weights, device=device, max_batch=gb)
     engine.set_precision(a.precision)
@@ -243,8 +253,9 @@ def main(argv=None, sdpl: bool = False):
             print(*ln)
 
     def flush():
-        for (bi, x, text), ids in zip(window, adapt_window(window)):
-            rec = {"idx": bi, "text": text, "duration": len(x) / SAMPLE_RATE, "hyp": {}, "lines": []}
+        for (bi, x, text, pre), ids in zip(window, adapt_window(window)):
+            rec = {"idx": bi, "text": text, "duration": len(x) / SAMPLE_RATE, "hyp": {},
+                   "lines": [(ln,) for ln in pre]}
             ori = batch_decode(ids[0][None])
             rec["hyp"][0] = ori[0]
             ori_wer = wer([text], ori)
@@ -263,9 +274,11 @@ def main(argv=None, sdpl: bool = False):
             results.append(rec)
         window.clear()
 
-    for bi, (lens, wavs, texts, files) in dataset.iter_collated(mine, a.num_workers):
-        for wav, text in zip(wavs, texts):
-            window.append((bi, normalize(wav), text))
+    truncated = {}   # loader batch -> the reader's truncation lines (data.py:19-21), printed before its WER lines
+    for bi, (lens, wavs, texts, files) in dataset.iter_collated(mine, a.num_workers,
+                                                                log=lambda i, lines: truncated.__setitem__(i, lines)):
+        for j, (wav, text) in enumerate(zip(wavs, texts)):
+            window.append((bi, normalize(wav), text, truncated.pop(bi, []) if j == 0 else []))
         if len(window) >= 8 * gb:
             flush()
     flush()

@@ -22,6 +22,9 @@ Fixtures written next to this file:
   g6_sdpl_loss.npz   SDPL pseudo-label CTC loss + dL/dlogits through the reference
                      main_SDPL.forward_and_adapt (main_SDPL.py:143-209) with a fake model
   g6_sdpl_tiny_<variant>.npz  tiny-config episodic SDPL runs (main_SDPL.py:327-349)
+  g8_collect_params.json  the module names reference collect_params prints (main.py:79-80) and
+                     the param_names list it returns (main.py:312-314) for the tiny / base / large
+                     geometries under every (bias_only, train_feature) flag pair
   g7_large_16000.npz large-960h-lv60 shapes (layer-norm feature encoder, conv bias, stable
                      pre-LN encoder), 20 SUTA steps (config C4's step count), scripts/LS.sh flags:
                      logits at steps 0,1,5,10,20 + digests of the adapted tensors
@@ -370,6 +373,30 @@ def g6(ref):
                 res[f"N{n}/final/{k}"] = sdf[k].numpy().copy()
         np.savez_compressed(os.path.join(HERE, f"g6_sdpl_tiny_{vname}.npz"), **res)
         print("g6", vname, "done")
+
+
+def g8(ref):
+    """collect_params stdout (every named_modules() name, main.py:79-80) and its param_names."""
+    import json
+    from transformers import Wav2Vec2Config, Wav2Vec2ForCTC
+    out = {}
+    for name in ("tiny-group", "tiny-layer", "wav2vec2-base", "wav2vec2-large"):
+        cfg = get_config(name)
+        torch.manual_seed(0)
+        model = Wav2Vec2ForCTC(Wav2Vec2Config(**cfg)).eval()
+        ent = {"param_names": {}}
+        for bias_only in (False, True):
+            for train_feature in (False, True):
+                buf = io.StringIO()
+                with contextlib.redirect_stdout(buf):
+                    _, names = ref.collect_params(model, bias_only, train_feature, False, True)
+                ent["printed"] = buf.getvalue().split("\n")[:-1]
+                ent["param_names"][f"bias_only={bias_only},train_feature={train_feature}"] = names
+        out[name] = ent
+        del model
+    with open(os.path.join(HERE, "g8_collect_params.json"), "w") as f:
+        json.dump(out, f, indent=0)
+    print("g8 done")
 
 
 if __name__ == "__main__":

@@ -104,3 +104,71 @@ def test_ragged_long_utterances_equal_singles():
         for n, v in p1.items():
             assert_params_close(finals[b][n], v, hp.lr, 2, name=f"utt {b} {n}")
     eng.close()
+
+
+def test_ragged_ted_lengths_equal_singles():
+    """Config C5's longest ragged batch at logits level: T = 531 / 812 / 1874 (the 600 000-sample cap) in
+    one suta_adapt_varlen call against each utterance adapted alone (reference main.py:347-348 adapts one
+    utterance per call)."""
+    cfg = get_config("wav2vec2-base")
+    eng = SutaEngine(cfg, synth_weights(cfg), device=0, max_batch=3, max_samples=600000)
+    hp = SutaHParams()
+    rec = [0, 1, 3]
+    waves = [synth.wave(n, 340 + i) for i, n in enumerate((170000, 260000, 600000))]
+    lv, iv, tv = eng.adapt_varlen(waves, 3, hp, record=rec)
+    assert list(tv) == [531, 812, 1874]
+    finals = [{n: eng.get_param(b, n) for n in eng.trainable_names()} for b in range(3)]
+    for b, (l1, p1, t1) in enumerate(_singles(eng, waves, 3, hp, rec)):
+        assert tv[b] == t1
+        for r in rec:
+            np.testing.assert_allclose(lv[r][b], l1[r], rtol=0, atol=logits_tol(hp.lr), err_msg=f"utt {b} step {r}")
+            np.testing.assert_array_equal(iv[r][b], lv[r][b].argmax(-1))
+        for n, v in p1.items():
+            assert_params_close(finals[b][n], v, hp.lr, 3, name=f"utt {b} {n}")
+    eng.close()
+
+
+def test_c4_bench_layout_bf16():
+    """Config C4 exactly as bench.py --only-c4 runs it: wav2vec2-large, 64 x 128 000 samples, 20 SUTA steps,
+    bf16 GEMMs, the second call of the layout (every step a graph replay).  Slots 0 / 31 / 63 against the
+    exact-fp32 engine adapting each utterance alone (bf16 tolerance of tests/parity.py: 2.5 % of max|ref|,
+    greedy ids on >= 97 % of frames) at steps 0 / 1 / 5 / 20, and slot 0 against the CPU oracle at steps 0
+    and 20.  The launch census of the capturing call shows the schedules this layout reaches: the 256 x 128
+    one-plane bf16 tile and the per-utterance (Z = 64) weight-gradient GEMMs."""
+    from oracle import w2v2_cpu as W
+    import os
+    from tests.parity import BF16_LOGITS_RTOL_LARGE, assert_bf16_close
+    torch.set_num_threads(min(16, len(os.sched_getaffinity(0))))
+    cfg = get_config("wav2vec2-large")
+    sd = synth_weights(cfg)
+    B, N, S = 64, 128000, 20
+    rec = [0, 1, 5, 20]
+    eng = SutaEngine(cfg, sd, device=0, max_batch=B, max_samples=N)
+    eng.set_precision("bf16")
+    hp = SutaHParams()
+    warm = torch.from_numpy(synth.batch(N, B, start=0)).cuda()
+    x = synth.batch(N, B, start=B)
+    eng.set_census(True)
+    eng.adapt(warm, S, hp, record=rec, want_logits=False)                 # captures the loop
+    census = eng.get_census()
+    eng.set_census(False)
+    logits, ids, T = eng.adapt(torch.from_numpy(x).cuda(), S, hp, record=rec)   # replayed
+    assert T == 399
+    txt = "\n".join(f"{k}: {v}" for k, v in sorted(census.items()))
+    assert any(k.startswith("x6_1plane 256x128") for k in census), txt
+    assert any(" z=64 " in k and k.startswith(("gbf", "x6_1plane")) for k in census), txt
+    assert any(k.startswith("hb ") for k in census), txt
+    eng.set_precision("fp32")
+    for slot in (0, 31, 63):
+        ref, _, _ = eng.adapt(x[slot], S, hp, record=rec)
+        for r in rec:
+            assert_bf16_close(logits[r][slot], ref[r][0], 0.97, f"C4 slot {slot} step {r}", rtol=BF16_LOGITS_RTOL_LARGE)
+            np.testing.assert_array_equal(ids[r][slot], logits[r][slot].argmax(-1))
+        if slot == 0:
+            o, _ = W.run_suta({k: torch.from_numpy(v) for k, v in sd.items()}, cfg, torch.from_numpy(x[0])[None], S,
+                              record=[0, 20])
+            for r in (0, 20):
+                np.testing.assert_allclose(ref[r][0], o[r][0].numpy(), rtol=0, atol=5e-5, err_msg=f"fp32 vs oracle {r}")
+                assert_bf16_close(logits[r][0], o[r][0].numpy(), 0.97, f"C4 slot 0 step {r} vs oracle",
+                                  rtol=BF16_LOGITS_RTOL_LARGE)
+    eng.close()

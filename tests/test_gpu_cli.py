@@ -112,8 +112,8 @@ def _oracle_counts(ds_files, ds_texts, cfg_name, steps, lr, extra_noise=0.0):
     reader = AudioReader(extra_noise)
     rec = [0] + [c for c in (1, 3, 5, 10) if c <= steps]
     hyps = {k: [] for k in rec}
-    for f in ds_files:
-        x = torch.from_numpy(normalize(reader(str(f))))[None]
+    for i, f in enumerate(ds_files):   # i = dataset index = the utterance's noise key
+        x = torch.from_numpy(normalize(reader(str(f), i)))[None]
         lg, _ = W.run_suta(sd, cfg, x, steps, lr=lr, record=rec)
         for k in rec:
             hyps[k].append(batch_decode(lg[k].argmax(-1).numpy())[0])
@@ -144,9 +144,12 @@ def test_cli_world2_gloo_on_one_gpu(tmp_path):
 
 def test_cli_librispeech_flac_ls_flags(tmp_path, capsys):
     """scripts/LS.sh (LS + 0.01 noise) flags on a LibriSpeech-layout FLAC corpus (FLAC decoded by
-    libsuta_audio): the driver's corpus WER counts equal the CPU oracle's on the same decoded, noised,
-    normalised audio (w2v2-base shapes, seeded weights)."""
+    libsuta_audio), w2v2-base shapes with seeded weights: the driver's corpus WER counts equal the CPU
+    oracle's on the same decoded, noised, normalised audio -- run in-process (world 1) and as 2 gloo
+    ranks sharing device 0 (config C2/C3's sharded path: LPT shards, per-utterance noise keyed on the
+    dataset index, count all_reduce); rank 1 prints nothing of the job's log."""
     from tests import corpus_fixtures as CF
+    from tests.multirank import run_ranks
     from suta_amd.data import LibriDataset
     CF.librispeech(tmp_path)
     args = (f"--asr facebook/wav2vec2-base-960h --synthetic_weights --steps 10 --dataset_name librispeech "
@@ -157,6 +160,30 @@ def test_cli_librispeech_flac_ls_flags(tmp_path, capsys):
     assert out.count("original WER: ") >= 5 and "TTA-10 WER:" in out
     ds = LibriDataset(None, 1, str(tmp_path))
     ref = _oracle_counts(ds.file_list, ds.text, "wav2vec2-base", 10, 2e-5, extra_noise=0.01)
+    for k, v in ref.items():
+        assert tuple(counts[str(k)]) == v, k
+    c2, o2 = run_ranks(2, args + "--gpu_batch 2 --device 0 --dist_backend gloo".split(), tmp_path, fake=False)
+    assert c2[0] == c2[1] == {k: tuple(v) for k, v in counts.items()}
+    per = lambda o: [ln for ln in o.splitlines() if ln.startswith(("original WER:", "adapt-"))]  # noqa: E731
+    assert per(o2[0]) == per(out) and per(o2[1]) == [] and "[INFO]" not in o2[1]
+
+
+def test_cli_chime_base_world2(tmp_path, capsys):
+    """Config C3 (w2v2-base on the CHiME layout, utterance-sharded): 2 gloo ranks on device 0 give the
+    world-1 counts, which equal the oracle's."""
+    from tests import corpus_fixtures as CF
+    from tests.multirank import run_ranks
+    from suta_amd.data import CHiMEDataset
+    CF.chime(tmp_path, n=4)
+    args = (f"--asr facebook/wav2vec2-base-960h --synthetic_weights --steps 10 --dataset_name chime "
+            f"--dataset_dir {tmp_path} --temp 2.5 --episodic --em_coef 0.3 --reweight --log_dir {tmp_path}/exps "
+            f"--lr 2e-5 --non_blank --train_feature --extra_noise 0.005").split()
+    counts = M.main(args)
+    capsys.readouterr()
+    c2, _ = run_ranks(2, args + "--gpu_batch 2 --device 0 --dist_backend gloo".split(), tmp_path, fake=False)
+    assert c2[0] == c2[1] == {k: tuple(v) for k, v in counts.items()}
+    ds = CHiMEDataset(None, 1, str(tmp_path))
+    ref = _oracle_counts(ds.file_list, ds.text, "wav2vec2-base", 10, 2e-5, extra_noise=0.005)
     for k, v in ref.items():
         assert tuple(counts[str(k)]) == v, k
 

@@ -230,6 +230,37 @@ def test_graph_replay_equals_eager(preset, n):
         assert np.array_equal(d[r], e2[r]), r
 
 
+def test_non_episodic_graph_replay_equals_eager():
+    """Non-episodic calls carry the adapted tensors and the Adam state (moments, step counter) from one
+    call to the next (reference main.py:323-348 without --episodic).  Three calls with one key, run with
+    graphs off and with graphs on (the second and third replayed): logits, greedy ids and final tensors
+    bitwise equal, and a following suta_step (which reads the carried Adam moments and step) too."""
+    cfg = get_config("tiny-group")
+    sd = synth_weights(cfg)
+    xs = [synth.batch(11000, 2, start=120 + 2 * i) for i in range(3)]
+    hp = SutaHParams(lr=5e-4, episodic=False)
+    runs = []
+    for graphs in (False, True):
+        eng = SutaEngine(cfg, sd, device=0, max_batch=2)
+        eng.set_graphs(graphs)
+        outs = [eng.adapt(x, 3, hp, record=[0, 1, 3]) for x in xs]
+        names = eng.trainable_names()
+        finals = [{k: eng.get_param(b, k) for k in names} for b in range(2)]
+        nxt, loss = eng.step(xs[0], hp)
+        after = [{k: eng.get_param(b, k) for k in names} for b in range(2)]
+        runs.append((outs, finals, nxt, loss, after))
+        eng.close()
+    (oa, fa, na, la, aa), (ob, fb, nb, lb, ab) = runs
+    for (l1, i1, _), (l2, i2, _) in zip(oa, ob):
+        for r in (0, 1, 3):
+            assert np.array_equal(l1[r], l2[r]) and np.array_equal(i1[r], i2[r]), r
+    assert np.array_equal(na, nb) and np.array_equal(la, lb)
+    for u in range(2):
+        for k in fa[u]:
+            assert np.array_equal(fa[u][k], fb[u][k]) and np.array_equal(aa[u][k], ab[u][k]), (u, k)
+    assert any(not np.array_equal(fa[0][k], aa[0][k]) for k in fa[0])   # the step moved the tensors
+
+
 def test_episodic_reset_restores_pristine_tensors():
     eng, cfg = engine("tiny-layer")
     sd = synth_weights(cfg)

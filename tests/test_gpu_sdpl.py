@@ -78,7 +78,7 @@ def test_sdpl_tiny_adaptation_tracks_reference(variant):
             for key in z.files:
                 if key.startswith(f"N{n}/final/"):
                     name = key[len(f"N{n}/final/"):]
-                    assert_params_close(eng.get_param(0, name), z[key], lr, 5, max_frac=1.0, name=name)
+                    assert_params_close(eng.get_param(0, name), z[key], lr, 5, max_frac=1.0, name=name, factor=2.0)
     assert compared >= 8  # most of the 12 recorded steps share the reference's pseudo labels
 
 

@@ -174,11 +174,14 @@ def _per_utt_lines(out):
     return [ln for ln in out.splitlines() if ln.startswith(("original WER:", "adapt-"))]
 
 
-@pytest.mark.parametrize("corpus", ["chime", "librispeech"])
-def test_driver_world2_gloo_equals_world1(tmp_path, corpus):
-    """The real driver (suta_amd/main.py) as 2 gloo ranks with a deterministic stand-in engine: LPT
-    sharding by decoded length, the count all_reduce and the object gather give the world-1 counts, and
-    rank 0 alone prints every per-utterance line, in the world-1 (dataset) order."""
+@pytest.mark.parametrize("corpus,noise", [("chime", 0.0), ("librispeech", 0.0), ("librispeech", 0.01),
+                                          ("chime", 0.01)])
+def test_driver_world2_gloo_equals_world1(tmp_path, corpus, noise):
+    """The real driver (suta_amd/main.py) as 2 gloo ranks with a deterministic stand-in engine whose ids
+    depend on every sample it is given: LPT sharding by decoded length, the count all_reduce and the
+    object gather give the world-1 counts -- with --extra_noise too, since each utterance's noise is keyed
+    on its dataset index -- and rank 0 alone prints the loader / collect_params / per-utterance lines, in
+    the world-1 (dataset) order."""
     from tests import corpus_fixtures as CF
     from tests.multirank import run_ranks
     if corpus == "chime":
@@ -189,13 +192,70 @@ def test_driver_world2_gloo_equals_world1(tmp_path, corpus):
         flags = f"--dataset_name librispeech --dataset_dir {tmp_path}"
     argv = (f"--asr tiny-group --synthetic_weights --steps 10 {flags} --temp 2.5 --episodic --em_coef 0.3 "
             f"--reweight --log_dir {tmp_path}/exps --lr 5e-4 --non_blank --train_feature --gpu_batch 2 "
-            f"--dist_backend gloo").split()
+            f"--dist_backend gloo --extra_noise {noise}").split()
     (c1,), (o1,) = run_ranks(1, argv, tmp_path, fake=True)
     c2, o2 = run_ranks(2, argv, tmp_path, fake=True)
     assert c2[0] == c2[1] == c1
     assert _per_utt_lines(o2[0]) == _per_utt_lines(o1) and len(_per_utt_lines(o1)) > 0
     assert _per_utt_lines(o2[1]) == []
     assert "TTA-10 WER:" in o2[0] and "TTA-10 WER:" not in o2[1]
+    for marker in ("[INFO]    There are", "wav2vec2.feature_extractor.conv_layers.0.conv", "[INFO]    optimizer:",
+                   "['wav2vec2.feature_extractor.conv_layers.0.conv.weight'"):
+        assert marker in o1 and marker in o2[0] and marker not in o2[1], marker
+
+
+def test_noise_is_keyed_on_dataset_index(tmp_path):
+    """Loading any subset of the loader batches, in any order, gives each utterance the audio a full
+    pass gives it (the multi-rank invariance of --extra_noise)."""
+    from tests import corpus_fixtures as CF
+    CF.librispeech(tmp_path)
+    full = D.load_dataset(None, "librispeech", str(tmp_path), 1, 0.01)
+    ref = {i: b[1][0] for i, b in full.iter_collated(range(len(full)))}
+    part = D.load_dataset(None, "librispeech", str(tmp_path), 1, 0.01)
+    sub = list(range(len(part)))[::-2]
+    got = {i: b[1][0] for i, b in part.iter_collated(sub, workers=3, window=2)}
+    assert sub and all(np.array_equal(got[i], ref[i]) for i in sub)
+    clean = D.load_dataset(None, "librispeech", str(tmp_path), 1, 0.0)
+    c = {i: b[1][0] for i, b in clean.iter_collated(range(len(clean)))}
+    assert all(abs(np.std(ref[i] - c[i]) - 0.01) < 2e-3 for i in ref)
+    assert not np.array_equal(ref[0] - c[0], (ref[1] - c[1])[:len(c[0])])
+
+
+def test_bucket_indices_follow_getitem(tmp_path):
+    from tests import corpus_fixtures as CF
+    CF.chime(tmp_path, n=5)
+    ld = D.load_dataset(None, "chime", str(tmp_path), 2, 0.0)
+    assert ld.batch_indices() == [[0, 1], [2, 3], [3, 4]]   # the last bucket moves back (CHiME.py __getitem__)
+    files = [[str(f) for f, _ in b] for b in ld.raw_batches()]
+    ds = D.CHiMEDataset(None, 1, str(tmp_path))
+    assert files == [[str(ds.file_list[i]) for i in b] for b in ld.batch_indices()]
+
+
+def test_collect_params_names_match_reference_golden():
+    """suta_amd.modules restates named_modules() and the reference collect_params walk: the printed module
+    names and param_names equal what the reference's own collect_params produced on transformers'
+    Wav2Vec2ForCTC (golden g8), for tiny / base / large geometries and all flag pairs."""
+    import json
+    from suta_amd.modules import collect_params
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "g8_collect_params.json")))
+    assert set(g) == {"tiny-group", "tiny-layer", "wav2vec2-base", "wav2vec2-large"}
+    for name, ent in g.items():
+        for key, names in ent["param_names"].items():
+            printed, got = collect_params(get_config(name), "bias_only=True" in key, "train_feature=True" in key)
+            assert printed == ent["printed"], name
+            assert got == names, (name, key)
+
+
+def test_truncation_lines_in_load_order(tmp_path, capsys):
+    """data.py:19-21: the reader prints the cut message and the new shape as torch.Size, in load order."""
+    x = np.random.default_rng(3).standard_normal(650000) * 0.05
+    _write_wav(tmp_path / "a.wav", x)
+    _write_wav(tmp_path / "b.wav", x[:1000])
+    log = []
+    D.collect_audio_batch([(str(tmp_path / "a.wav"), "A"), (str(tmp_path / "b.wav"), "B")], D.AudioReader(), log=log)
+    assert log == [f"{tmp_path / 'a.wav'} has len torch.Size([650000]), truncate to 600000", "torch.Size([600000])"]
+    D.AudioReader()(str(tmp_path / "a.wav"))
+    assert capsys.readouterr().out.splitlines() == log
 
 
 def test_driver_refuses_to_shard_non_episodic(tmp_path):

@@ -190,4 +190,4 @@ def test_g6_sdpl_tiny_oracle_matches_reference(variant):
     for key in z.files:
         if key.startswith("N8000/final/"):
             name = key[len("N8000/final/"):]
-            assert_params_close(final[name].numpy(), z[key], lr, 5, max_frac=1.0, name=name)
+            assert_params_close(final[name].numpy(), z[key], lr, 5, max_frac=1.0, name=name, factor=2.0)

@@ -1,0 +1,9 @@
+# Round-3 opening check: GPU suite + smoke + default bench on the tree as round 2 left it.
+set -e
+export TMPDIR=/tmp
+O=gpurun_out/r3a
+mkdir -p $O
+timeout -k 10 700 python -u -m pytest tests -m gpu -v -rA --timeout 400 --timeout-method thread > $O/gpu_tests.log 2>&1
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+timeout -k 10 500 python bench.py > $O/bench.json 2> $O/bench.err
+echo done
