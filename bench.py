@@ -28,19 +28,26 @@ import torch  # noqa: E402
 from suta_amd import synth  # noqa: E402
 from suta_amd.config import get_config, num_frames  # noqa: E402
 from suta_amd.engine import SutaEngine, SutaHParams  # noqa: E402
-from suta_amd.flops import suta_flops  # noqa: E402
+from suta_amd.flops import reference_schedule_flops, suta_flops  # noqa: E402
 from suta_amd.weights import synth_weights  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
 BF16_PEAK_TFLOPS = 2500.0      # MI355X_MICROARCH.md: bf16 dense MFMA peak
 BF16_SPLIT_PEAK_TFLOPS = BF16_PEAK_TFLOPS / 6
-HBM_PEAK_TBS = 8.0             # MI355X_MICROARCH.md: HBM3E peak  # 6 bf16 products per fp32-equivalent MAC
+HBM_PEAK_TBS = 8.0             # MI355X_MICROARCH.md: HBM3E peak
 RECORD = [0, 1, 3, 5, 10]
 # newest committed rocprofv3 PMC reduction of this workload (tools/pmc_traffic.py; profiles/<round>/README.md)
-PMC_TRAFFIC = next((p for p in (os.path.join(ROOT, "profiles", r, "pmc_traffic.json") for r in ("r2", "r1"))
+PMC_TRAFFIC = next((p for p in (os.path.join(ROOT, "profiles", r, "pmc_traffic.json") for r in ("r3", "r2", "r1"))
                     if os.path.exists(p)), None)
-GEMM_KERNELS = ("gemm_glds_kernel", "gemm_f32_kernel", "attn_fwd_kernel", "attn_bwd_kernel", "posconv_kernel",
-                "flash_fwd_kernel", "flash_bwd_kernel", "flash_dq_kernel")
+PMC_TRAFFIC_C4 = next((p for p in (os.path.join(ROOT, "profiles", r, f) for r, f in
+                                   (("r3", "pmc_traffic_c4.json"), ("r2", "close_pmc_traffic_c4.json")))
+                       if os.path.exists(p)), None)
+GEMM_KERNELS = ("gemm_glds_kernel", "gemm_f32_kernel", "gemm_splitk_reduce", "attn_fwd_kernel", "attn_bwd_kernel",
+                "posconv_kernel", "flash_fwd_kernel", "flash_bwd_kernel", "flash_dq_reduce")
+# config C4's GEMM family (bf16 mode): every kernel its "gemm" + "attention" timing families launch
+GEMM_KERNELS_C4 = ("gemm_hb_kernel", "gemm_hb8_kernel", "gemm_x6_kernel", "gemm_gbf_kernel", "gemm_splitk_reduce",
+                   "to_bf16_kernel", "posconv_bf16_kernel", "flash_fwd_bf16_kernel", "flash_bwd_bf16_kernel",
+                   "flash_dq_reduce")
 FRONT_KERNELS = ("conv0_gn_kernel", "col_stats_final", "gn_bwd_final", "conv0_dw_reduce")
 
 
@@ -52,10 +59,10 @@ def pmc(args):
     return json.load(open(PMC_TRAFFIC))
 
 
-def gemm_traffic(d):
+def gemm_traffic(d, kernels=GEMM_KERNELS):
     """HBM bytes per GEMM-family launch from the PMC passes."""
-    n = sum(d[k]["launches"] for k in GEMM_KERNELS if k in d)
-    b = sum(d[k]["launches"] * d[k]["hbm_bytes_per_launch"] for k in GEMM_KERNELS if k in d)
+    n = sum(d[k]["launches"] for k in kernels if k in d)
+    b = sum(d[k]["launches"] * d[k]["hbm_bytes_per_launch"] for k in kernels if k in d)
     return round(b / n) if n else None
 
 
@@ -93,7 +100,13 @@ def cpu_baseline(cfg, n_samples, suta_steps, budget_s=25.0):
             break
     return {"value": done / el, "unit": "utt/s", "cores": cores, "kind": "port",
             "sample": f"{done} utterance(s) of {n_samples} samples, {suta_steps} SUTA steps each, oracle/w2v2_cpu.py "
-                      f"run_suta (torch {torch.__version__} CPU, {cores} threads), {el:.1f} s"}
+                      f"run_suta (torch {torch.__version__} CPU, {cores} threads), {el:.1f} s; schedule: the minimal "
+                      f"one the engine runs ({suta_steps + 1} forwards + {suta_steps} backwards per utterance, "
+                      f"{suta_flops(cfg, n_samples, suta_steps) / 1e9:.1f} GF), not the reference's "
+                      f"{2 * suta_steps + 1} forwards ({reference_schedule_flops(cfg, n_samples, suta_steps) / 1e9:.1f} GF): "
+                      f"the reference loop itself would take about "
+                      f"{reference_schedule_flops(cfg, n_samples, suta_steps) / suta_flops(cfg, n_samples, suta_steps):.2f}x "
+                      f"this time"}
 
 
 def bench_c4(args, dev):
@@ -120,6 +133,7 @@ def bench_c4(args, dev):
         eng.set_timing(True)
         eng.adapt(waves[1], S, hp, record=rec, want_logits=False)
         eng.sync()
+        tex = eng.get_timing_ex()
     flops_utt = suta_flops(cfg, N, S)
     res = {"workload": f"wav2vec2-large SUTA {S} steps on {N}-sample (8 s) utterances, {B} utterances per step, "
                        "scripts/LS.sh flags, bf16 GEMMs", "config": "C4", "precision": "bf16", "dtype": "bf16",
@@ -133,7 +147,24 @@ def bench_c4(args, dev):
         res["roofline"] = {"bound": "mfma", "achieved": round(ach, 3), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                            "frac": round(ach / BF16_PEAK_TFLOPS, 4), "kernel": "bf16 GEMM family (bf16-plane linears: gemm_hb_kernel / gemm_hb8_kernel; layer-norm conv stack: gemm_x6_kernel one-plane form; weight gradients: gemm_gbf_kernel; posconv_bf16_kernel; flash attention on bf16 MFMA)",
                            "launches": int(gn), "avg_launch_ms": round(gms / max(1, gn), 5)}
-        res["time_breakdown_ms"] = {k: round(v[0], 2) for k, v in t.items()}
+        gx, ax = tex["gemm"], tex["attention"]
+        talg = round((gx[2] + ax[2]) / max(1, gx[1] + ax[1]))
+        d4 = json.load(open(PMC_TRAFFIC_C4)) if (PMC_TRAFFIC_C4 and B == 64 and N == 128000) else None
+        traffic = gemm_traffic(d4, GEMM_KERNELS_C4) if d4 else None
+        res["roofline"].update({
+            "traffic": traffic, "traffic_unit": "HBM bytes per GEMM-family launch",
+            "traffic_source": f"{os.path.relpath(PMC_TRAFFIC_C4, ROOT)} (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE "
+                              "passes of bench.py --only-c4)" if traffic else None,
+            "traffic_alg": talg, "traffic_ratio": round(traffic / talg, 3) if traffic and talg else None})
+        if ax[1]:
+            T = num_frames(cfg, N)
+            af, ab = attention_flops(cfg, T, B)
+            layers = cfg["num_hidden_layers"]
+            nf, nb = (S + 1) * layers, S * layers
+            res["attention"] = {"launches": int(ax[1]), "ms": round(ax[0], 2),
+                                "tflops": round((nf * af + nb * ab) / (ax[0] / 1000) / 1e12, 3),
+                                "frac_bf16_peak": round((nf * af + nb * ab) / (ax[0] / 1000) / 1e12 / BF16_PEAK_TFLOPS, 4)}
+        res["time_breakdown_ms"] = {k: round(v[0], 2) for k, v in tex.items()}
     eng.close()
     return res
 

@@ -46,3 +46,9 @@ def backward_flops(cfg: dict, n_samples: int) -> float:
 
 def suta_flops(cfg: dict, n_samples: int, steps: int) -> float:
     return (steps + 1) * forward_flops(cfg, n_samples) + steps * backward_flops(cfg, n_samples)
+
+
+def reference_schedule_flops(cfg: dict, n_samples: int, steps: int) -> float:
+    """What the reference loop executes per utterance: a vanilla forward, then per step a grad forward,
+    a backward and a no-grad re-inference forward (main.py:172-215, 330-348): (2S+1) F + S B."""
+    return (2 * steps + 1) * forward_flops(cfg, n_samples) + steps * backward_flops(cfg, n_samples)

@@ -1,28 +1,75 @@
-"""Per-kernel SQ stall breakdown from one rocprofv3 --pmc pass (tools/profile_round2.sh).
+"""Per-kernel SQ breakdown from rocprofv3 --pmc passes (one CSV per pass, any number of passes).
+
+Pass A: SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES
+        SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT
+Pass B: SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR
+        SQ_WAIT_INST_LDS SQ_INSTS_VALU_CVT
 WAIT_ANY (parked on s_waitcnt / barrier) + WAIT_INST_ANY (issue stall) + ACTIVE_INST_ANY ~= WAVE_CYCLES
-(MI355X_MICROARCH.md, PMC slots); MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES / (SQ_BUSY_CYCLES x 4 SIMDs) per CU.
-usage: python tools/pmc_sq.py <counter_collection.csv>"""
+(MI355X_MICROARCH.md, PMC slots); MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES / (SQ_BUSY_CYCLES x 4 SIMDs) per CU
+(SQ_BUSY_CYCLES sums the CUs' busy cycles the same way the MFMA counter sums the SIMDs').  Instruction
+counts are per wave-instruction; VALU counts include the MFMAs (SQ_INSTS_VALU), so valu/mfma below
+subtracts them.
+usage: python tools/pmc_sq.py pass_a.csv [pass_b.csv ...] [--json out.json]
+"""
 import collections
 import csv
+import json
 import sys
 
 
+def short(name):
+    return name.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0].split("<")[0]
+
+
 def main():
+    args = sys.argv[1:]
+    out_json = None
+    if "--json" in args:
+        i = args.index("--json")
+        out_json = args[i + 1]
+        args = args[:i] + args[i + 2:]
     acc = collections.defaultdict(lambda: collections.defaultdict(float))
-    n = collections.defaultdict(set)
-    for r in csv.DictReader(open(sys.argv[1])):
-        name = r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0].split("<")[0]
-        acc[name][r["Counter_Name"]] += float(r["Counter_Value"])
-        n[name].add(r.get("Dispatch_Id"))
-    rows = sorted(acc.items(), key=lambda kv: -kv[1].get("SQ_WAVE_CYCLES", 0))
-    print(f"{'kernel':28s} {'launches':>8s} {'parked':>7s} {'stall':>7s} {'active':>7s} {'mfma_busy':>9s} {'lds_conf/inst':>13s}")
+    n = collections.defaultdict(lambda: collections.defaultdict(set))
+    for path in args:
+        for r in csv.DictReader(open(path)):
+            k = short(r["Kernel_Name"])
+            acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
+            n[k][r["Counter_Name"]].add(r.get("Dispatch_Id"))
+    rows = sorted(acc.items(), key=lambda kv: -kv[1].get("SQ_WAVE_CYCLES", kv[1].get("SQ_INSTS_VALU", 0)))
+    res = {}
+    print(f"{'kernel':34s} {'launch':>6s} {'parked':>6s} {'stall':>6s} {'active':>6s} {'mfma_busy':>9s} "
+          f"{'ldsconf/i':>9s} {'valu/mfma':>9s} {'trans/mfma':>10s} {'lds/mfma':>8s} {'vmem/mfma':>9s}")
     for k, c in rows:
-        wc = c.get("SQ_WAVE_CYCLES", 0) or 1
+        launches = max((len(v) for v in n[k].values()), default=0)
+        wc = c.get("SQ_WAVE_CYCLES", 0)
         busy = c.get("SQ_BUSY_CYCLES", 0)
-        mf = c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / (4 * busy) if busy else 0
-        li = c.get("SQ_INSTS_LDS", 0)
-        print(f"{k:28s} {len(n[k]):8d} {c.get('SQ_WAIT_ANY', 0) / wc:7.3f} {c.get('SQ_WAIT_INST_ANY', 0) / wc:7.3f} "
-              f"{c.get('SQ_ACTIVE_INST_ANY', 0) / wc:7.3f} {mf:9.3f} {c.get('SQ_LDS_BANK_CONFLICT', 0) / li if li else 0:13.3f}")
+        mf = c.get("SQ_INSTS_MFMA", 0)
+        e = {"launches": launches}
+        if wc:
+            e.update(parked=c.get("SQ_WAIT_ANY", 0) / wc, stall=c.get("SQ_WAIT_INST_ANY", 0) / wc,
+                     active=c.get("SQ_ACTIVE_INST_ANY", 0) / wc)
+        if busy:
+            e["mfma_busy"] = c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / (4 * busy)
+        if c.get("SQ_INSTS_LDS"):
+            e["lds_conflict_cycles_per_inst"] = c.get("SQ_LDS_BANK_CONFLICT", 0) / c["SQ_INSTS_LDS"]
+        if mf:
+            e["valu_per_mfma"] = (c.get("SQ_INSTS_VALU", 0) - mf) / mf
+            e["trans_per_mfma"] = c.get("SQ_INSTS_VALU_TRANS_F32", 0) / mf
+            e["cvt_per_mfma"] = c.get("SQ_INSTS_VALU_CVT", 0) / mf
+            e["salu_per_mfma"] = c.get("SQ_INSTS_SALU", 0) / mf
+            e["vmem_per_mfma"] = (c.get("SQ_INSTS_VMEM_RD", 0) + c.get("SQ_INSTS_VMEM_WR", 0)) / mf
+            if c.get("SQ_INSTS_LDS"):
+                e["lds_per_mfma"] = c["SQ_INSTS_LDS"] / mf
+        e["raw"] = dict(c)
+        res[k] = e
+
+        def f(key, w, p=3):
+            return f"{e[key]:{w}.{p}f}" if key in e else " " * (w - 1) + "-"
+        print(f"{k[:34]:34s} {launches:6d} {f('parked', 6)} {f('stall', 6)} {f('active', 6)} {f('mfma_busy', 9)} "
+              f"{f('lds_conflict_cycles_per_inst', 9)} {f('valu_per_mfma', 9, 2)} {f('trans_per_mfma', 10, 2)} "
+              f"{f('lds_per_mfma', 8, 2)} {f('vmem_per_mfma', 9, 3)}")
+    if out_json:
+        json.dump(res, open(out_json, "w"), indent=1)
 
 
 if __name__ == "__main__":
