@@ -731,6 +731,173 @@ __global__ __launch_bounds__(FF_NW_BF * 64) void flash_fwd_bf16_kernel(
     if (h == 0) lse[(long)bh * T + q] = (m_run + log2f(l_tot)) * (1.0f / LOG2E);
 }
 
+// ------------------------------------------------------------------------------------------------
+// forward, bf16 operand plane (config C4 with bf16 planes): Q, K and V come from the bf16 plane of qkv
+// that the QKV GEMM writes beside its fp32 output, so the kernel converts nothing.  Per 64-key tile the
+// block copies the K and V rows as 16-B chunks into row-major LDS images; S^T = K Q^T with the K rows read
+// by row (prod_rows_b), and the PV product's V^T operand is read from the ROW-major V image with
+// ds_read_b64_tr_b16 (gfx950 transposed read: per 16-lane group, lane 4q + p addresses row q, columns
+// 4p..4p+3 of a 4 x 16 block and receives column (lane & 15) of the 4 rows), so the staging writes no
+// transposed image.  Masks and address arithmetic only where they are needed: keys past the utterance's
+// length exist only in its last tile, and the per-thread copy addresses advance by one constant per tile.
+// The exponent argument is one fma (scores scaled to the log2 domain, the row maximum taken on raw
+// scores: scaling by a positive constant commutes with max under round-to-nearest).
+// ------------------------------------------------------------------------------------------------
+constexpr int FP_KS = 72;  // K image row stride (bf16): 144 B
+constexpr int FP_VS = 96;  // V image row stride (bf16): 192 B -> the 4 rows x 64 B of a 32-lane tr read hit 64 banks
+
+typedef __attribute__((address_space(3))) fbf16x4* lds_b4p;
+
+// o[t] += V^T(rows 32t..32t+31 = head dims, contraction over 16 keys from kb) P^T: the A operand by two
+// transposed reads of the row-major V image (keys kb + 4h + 0..3 and kb + 8 + 4h + 0..3, as apply_cols_b)
+template <int RS = FP_VS>
+__device__ __forceinline__ void pv_tr(f32x16 (&o)[2], const __bf16* __restrict__ V, int kb, const fbf16x8& b,
+                                      int lane) {
+    const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+    const int k0 = kb + 4 * (g >> 1) + q;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const __bf16* a0 = V + k0 * RS + 32 * t + 16 * (g & 1) + 4 * pp;
+        const fbf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_b4p)(a0));
+        const fbf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_b4p)(a0 + 8 * RS));
+        fbf16x8 a;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            a[j] = lo[j];
+            a[4 + j] = hi[j];
+        }
+        o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, o[t], 0, 0, 0);
+    }
+}
+
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void flash_fwd_bf16p_kernel(
+    const __bf16* __restrict__ qkvb, float* __restrict__ ctx, float* __restrict__ lse, int T, int NH, int H,
+    float scale, const int* __restrict__ tlen, int nqb, __bf16* __restrict__ ctxb) {
+    constexpr int NT = NW * 64;
+    constexpr int NPT = 512 / NT;  // 16-B chunks of a 64 x 64 bf16 tile per thread (each of K and V)
+    __shared__ __attribute__((aligned(16))) __bf16 Ks[2][FK * FP_KS];
+    __shared__ __attribute__((aligned(16))) __bf16 Vs[2][FK * FP_VS];
+    const int id = xcd_block();
+    const int qb = id % nqb, bh = id / nqb, hd = bh % NH, u = bh / NH;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, l32 = lane & 31, h = lane >> 5;
+    const int tl = tlen ? tlen[u] : T;
+    const long ld = 3L * H;
+    const __bf16* Qb = qkvb + (long)u * T * ld + hd * 64;
+    const int q0 = (qb * NW + w) * 32;
+    const bool active = q0 < T;
+    const float sl2 = scale * LOG2E;
+    RowReg<true> qv;
+    {
+        const __bf16* qr = Qb + (long)min(q0 + l32, T - 1) * ld + 8 * h;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) qv.v[s] = *reinterpret_cast<const fbf16x8*>(qr + 16 * s);
+    }
+    // copy map: chunk c = threadIdx.x + n NT of a tile, row c >> 3, columns 8 (c & 7) .. + 7
+    const int crow = threadIdx.x >> 3, ccol = (threadIdx.x & 7) * 8;
+    fbf16x8 kr[NPT], vr[NPT];
+    auto fetch = [&](int kt) {
+#pragma unroll
+        for (int n = 0; n < NPT; ++n) {
+            const int key = min(kt * FK + crow + n * (NT / 8), T - 1);  // rows past T: any finite row (P = 0)
+            const __bf16* src = Qb + (long)key * ld + ccol;
+            kr[n] = *reinterpret_cast<const fbf16x8*>(src + H);
+            vr[n] = *reinterpret_cast<const fbf16x8*>(src + 2 * H);
+        }
+    };
+    auto put = [&](int buf) {
+#pragma unroll
+        for (int n = 0; n < NPT; ++n) {
+            const int row = crow + n * (NT / 8);
+            *reinterpret_cast<fbf16x8*>(&Ks[buf][row * FP_KS + ccol]) = kr[n];
+            *reinterpret_cast<fbf16x8*>(&Vs[buf][row * FP_VS + ccol]) = vr[n];
+        }
+    };
+    const int nkt = (tl + FK - 1) / FK;
+    f32x16 o[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) o[t][v] = 0.f;
+    float m_run = -INFINITY, l_run = 0.f;
+    fetch(0);
+    put(0);
+    __syncthreads();
+    for (int kt = 0; kt < nkt; ++kt) {
+        const int buf = kt & 1;
+        if (kt + 1 < nkt) fetch(kt + 1);
+        if (active) {
+            // both 32-key halves always (a skipped half on the last tile would cost branch-merged register
+            // copies on every tile); keys past the length are masked on the last tile only
+            f32x16 s[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+#pragma unroll
+                for (int v = 0; v < 16; ++v) s[j][v] = 0.f;
+                prod_rows_b(s[j], Ks[buf] + 32 * j * FP_KS, qv, l32, h);
+            }
+            if (kt * FK + FK > tl) {  // the utterance's last tile: keys >= tl get probability 0
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int v = 0; v < 16; ++v)
+                        if (kt * FK + 32 * j + r8(v, h) >= tl) s[j][v] = -INFINITY;
+            }
+            float mx = s[0][0];
+#pragma unroll
+            for (int v = 1; v < 16; ++v) mx = fmaxf(mx, s[0][v]);
+#pragma unroll
+            for (int v = 0; v < 16; ++v) mx = fmaxf(mx, s[1][v]);
+            mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+            const float m_new = fmaxf(m_run, sl2 * mx);
+            float ls = 0.f;
+            fbf16x8 pb[2][2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int v = 0; v < 16; ++v) {
+                    const float pr = __builtin_amdgcn_exp2f(fmaf(s[j][v], sl2, -m_new));
+                    ls += pr;
+                    pb[j][v >> 3][v & 7] = (__bf16)pr;
+                }
+            if (m_new != m_run) {
+                const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+                l_run *= alpha;
+#pragma unroll
+                for (int t = 0; t < 2; ++t)
+#pragma unroll
+                    for (int v = 0; v < 16; ++v) o[t][v] *= alpha;
+                m_run = m_new;
+            }
+            l_run += ls;
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int c = 0; c < 2; ++c) pv_tr(o, Vs[buf], 32 * j + 16 * c, pb[j][c], lane);
+        }
+        if (kt + 1 < nkt) put(buf ^ 1);
+        __syncthreads();
+    }
+    if (!active) return;
+    const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+    const int q = q0 + l32;
+    if (q >= T) return;
+    const float inv = 1.0f / l_tot;
+    float* cr = ctx + ((long)u * T + q) * H + hd * 64 + 4 * h;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+            f32x4 r;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) r[b] = o[t][4 * a + b] * inv;
+            *reinterpret_cast<f32x4*>(cr + 32 * t + 8 * a) = r;
+            if (ctxb)
+                *reinterpret_cast<fbf16x4*>(ctxb + ((long)u * T + q) * H + hd * 64 + 4 * h + 32 * t + 8 * a) = cvt4(r);
+        }
+    if (h == 0) lse[(long)bh * T + q] = (m_run + log2f(l_tot)) * (1.0f / LOG2E);
+}
+
 // backward, bf16 images: Q / dO tiles row-major (S, dP) and transposed (dV, dK), dS and K^T in bf16
 constexpr int FBB_NW = 8;
 constexpr int FBB_KB = FBB_NW * 32 + 8;   // bf16 row stride of the dS tile and the K^T image
@@ -920,6 +1087,192 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16_kernel(
         }
 }
 
+// backward on bf16 operand planes (config C4 with bf16 planes): K and V rows of the wave's keys, the
+// block's K^T image, and the Q / dO query tiles all come from bf16 planes (qkv's, written by the QKV GEMM
+// in the forward; dctx's, written by the out-projection's input-gradient GEMM), so nothing is converted.
+// One row image per query tile serves the S / dP products (row reads) and the dV^T / dK^T products
+// (ds_read_b64_tr_b16 transposed reads, as the forward's PV): no transposed tiles are written.  Masks only
+// on a wave whose keys pass the utterance's length or on a query tile past T.
+constexpr size_t fbbp_lds_bytes() { return 2 * ((size_t)(64 + 32) * FBB_KB + 2 * 2 * 32 * FB_RS) + 4 * 128; }
+
+__global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
+    const __bf16* __restrict__ qkvb, const __bf16* __restrict__ dob, const float* __restrict__ lse,
+    const float* __restrict__ delta, float* __restrict__ dqkv, float* __restrict__ dqp, int T, int NH, int H,
+    float scale, const int* __restrict__ tlen, int nkb, int gpb, int B, __bf16* __restrict__ dqkvb) {
+    constexpr int NW = FBB_NW, NT = NW * 64;
+    extern __shared__ __attribute__((aligned(16))) __bf16 sm16[];
+    __bf16* Kt = sm16;                            // [64][FBB_KB]   K^T of the block's keys
+    __bf16* Ss = Kt + 64 * FBB_KB;                // [32][FBB_KB]   dS of the query tile
+    __bf16* Qr = Ss + 32 * FBB_KB;                // [2][32][FB_RS] Q rows
+    __bf16* Dr = Qr + 2 * 32 * FB_RS;             // [2][32][FB_RS] dO rows
+    float* Ls = reinterpret_cast<float*>(Dr + 2 * 32 * FB_RS);  // [2][32]
+    float* Dl = Ls + 64;                          // [2][32]
+    const int id = xcd_block();
+    const int kb = id % nkb, bh = id / nkb, hd = bh % NH, u = bh / NH;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, l32 = lane & 31, h = lane >> 5;
+    const int tl = tlen ? tlen[u] : T;
+    const int ng = (T + 31) >> 5;
+    const int g0 = kb * gpb, ngb = min(gpb, ng - g0);
+    const int kbase = g0 * 32;
+    const long ld = 3L * H;
+    const __bf16* Qb = qkvb + (long)u * T * ld + hd * 64;
+    const __bf16* Kb = Qb + H;
+    const __bf16* Vb = Qb + 2 * H;
+    const __bf16* Ob = dob + (long)u * T * H + hd * 64;
+    const float* lb = lse + (long)bh * T;
+    const float* db = delta + (long)bh * T;
+    const bool active = w < ngb && kbase + 32 * w < tl;
+    const bool kall = kbase + 32 * w + 32 <= tl;  // every key of the wave inside the length (wave-uniform)
+    const int key = kbase + 32 * w + l32;
+    const float sl2 = scale * LOG2E;
+    RowReg<true> kv, vv;
+    {
+        const long kr = (long)min(key, T - 1) * ld + 8 * h;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            kv.v[s] = *reinterpret_cast<const fbf16x8*>(Kb + kr + 16 * s);
+            vv.v[s] = *reinterpret_cast<const fbf16x8*>(Vb + kr + 16 * s);
+        }
+    }
+    for (int it = threadIdx.x; it < ngb * 32 * 8; it += NT) {  // K^T image of the block's keys (0 past T)
+        const int row = it >> 3, c8 = (it & 7) * 8, k = kbase + row;
+        fbf16x8 x = {};
+        if (k < T) x = *reinterpret_cast<const fbf16x8*>(Kb + (long)k * ld + c8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) Kt[(c8 + e) * FBB_KB + row] = x[e];
+    }
+    // query-tile copy: threads 0..255 one 16-B chunk of the Q rows, 256..511 one of the dO rows
+    const bool isq = threadIdx.x < 256;
+    const int crow = (threadIdx.x & 255) >> 3, ccol = (threadIdx.x & 7) * 8;
+    fbf16x8 xr;
+    float lr = 0.f;
+    auto fetch = [&](int qt) {
+        const int q = qt * 32 + crow;
+        xr = fbf16x8{};
+        if (q < T) xr = *reinterpret_cast<const fbf16x8*>(isq ? Qb + (long)q * ld + ccol : Ob + (long)q * H + ccol);
+        lr = 0.f;
+        const int qq = qt * 32 + (threadIdx.x & 31);
+        if (threadIdx.x < 64 && qq < T) lr = threadIdx.x < 32 ? lb[qq] : db[qq];
+    };
+    auto put = [&](int buf) {
+        *reinterpret_cast<fbf16x8*>((isq ? Qr : Dr) + (buf * 32 + crow) * FB_RS + ccol) = xr;
+        if (threadIdx.x < 32) Ls[buf * 32 + threadIdx.x] = lr;
+        else if (threadIdx.x < 64) Dl[buf * 32 + threadIdx.x - 32] = lr;
+    };
+    f32x16 dv[2], dk[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) dv[t][v] = dk[t][v] = 0.f;
+    const int g = lane >> 4, l16 = lane & 15;
+    const int qi = w & 1, di = w >> 1;
+    const int kq = ngb * 32;
+    const long dq_stride = (long)B * NH * T * 64;
+    float* dqb = dqp + kb * dq_stride + (long)bh * T * 64;
+    const int nqt = (tl + 31) >> 5;
+    if (!active && w < ngb)
+        for (int r = 0; r < 32; ++r)
+            if (h == 0) Ss[r * FBB_KB + 32 * w + l32] = (__bf16)0.f;
+    fetch(0);
+    put(0);
+    __syncthreads();
+    fbf16x8 kfr[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        if (32 * j < kq) kfr[j] = *reinterpret_cast<const fbf16x8*>(Kt + (16 * di + l16) * FBB_KB + 32 * j + 8 * g);
+    const bool odd = lane & 1;
+    for (int qt = 0; qt < nqt; ++qt) {
+        const int q0 = qt * 32, buf = qt & 1;
+        if (qt + 1 < nqt) fetch(qt + 1);
+        const float* Lt = Ls + buf * 32;
+        const float* Dlt = Dl + buf * 32;
+        if (active) {
+            const __bf16* Qt = Qr + buf * 32 * FB_RS;
+            const __bf16* Dt = Dr + buf * 32 * FB_RS;
+            f32x16 s, dp;
+#pragma unroll
+            for (int v = 0; v < 16; ++v) s[v] = dp[v] = 0.f;
+            prod_rows_b(s, Qt, kv, l32, h);
+            prod_rows_b(dp, Dt, vv, l32, h);
+            f32x4 lq[4], dq[4];
+#pragma unroll
+            for (int a = 0; a < 4; ++a) {
+                lq[a] = *reinterpret_cast<const f32x4*>(Lt + 8 * a + 4 * h);
+                dq[a] = *reinterpret_cast<const f32x4*>(Dlt + 8 * a + 4 * h);
+            }
+#pragma unroll
+            for (int v = 0; v < 16; ++v) s[v] = __builtin_amdgcn_exp2f(fmaf(s[v], sl2, -LOG2E * lq[v >> 2][v & 3]));
+            if (!kall || q0 + 32 > T) {  // keys past the length, query rows past T: probability 0
+                const bool kok = key < tl;
+#pragma unroll
+                for (int v = 0; v < 16; ++v)
+                    if (!(kok && q0 + r8(v, h) < T)) s[v] = 0.f;
+            }
+#pragma unroll
+            for (int v = 0; v < 16; ++v) dp[v] = scale * (s[v] * (dp[v] - dq[v >> 2][v & 3]));
+            fbf16x8 pb[2], sb[2];
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                pb[v >> 3][v & 7] = (__bf16)s[v];
+                sb[v >> 3][v & 7] = (__bf16)dp[v];
+            }
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                pv_tr<FB_RS>(dv, Dt, 16 * c, pb[c], lane);  // dV^T += dO^T P
+                pv_tr<FB_RS>(dk, Qt, 16 * c, sb[c], lane);  // dK^T += Q^T dS
+            }
+#pragma unroll
+            for (int v = 0; v < 16; v += 2) {
+                const float a = dp[v], b = dp[v + 1];
+                const float recv = __int_as_float(
+                    __builtin_amdgcn_mov_dpp(__float_as_int(odd ? a : b), 0xB1, 0xF, 0xF, false));
+                fbf16x2 pr;
+                pr[0] = (__bf16)(odd ? recv : a);
+                pr[1] = (__bf16)(odd ? b : recv);
+                *reinterpret_cast<fbf16x2*>(Ss + (r8(v, h) + (odd ? 1 : 0)) * FBB_KB + 32 * w + (l32 & ~1)) = pr;
+            }
+        }
+        __syncthreads();  // dS tile complete
+        {
+            const __bf16* ar = Ss + (16 * qi + l16) * FBB_KB + 8 * g;
+            f32x4 c[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (32 * j < kq)
+                    c[j & 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                        *reinterpret_cast<const fbf16x8*>(ar + 32 * j), kfr[j], c[j & 1], 0, 0, 0);
+            const f32x4 c0 = c[0], c1 = c[1];
+            float* dr = dqb + (long)(q0 + 16 * qi + 4 * g) * 64 + 16 * di + l16;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (q0 + 16 * qi + 4 * g + r < T) dr[r * 64] = c0[r] + c1[r];
+        }
+        if (qt + 1 < nqt) put(buf ^ 1);
+        __syncthreads();
+    }
+    if (w >= ngb || key >= T) return;
+    float* dkr = dqkv + ((long)u * T + key) * ld + H + hd * 64 + 4 * h;
+    float* dvr = dkr + H;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+            f32x4 x, y;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                x[b] = dk[t][4 * a + b];
+                y[b] = dv[t][4 * a + b];
+            }
+            *reinterpret_cast<f32x4*>(dkr + 32 * t + 8 * a) = x;
+            *reinterpret_cast<f32x4*>(dvr + 32 * t + 8 * a) = y;
+            if (dqkvb) {
+                __bf16* kb2 = dqkvb + ((long)u * T + key) * ld + H + hd * 64 + 4 * h + 32 * t + 8 * a;
+                *reinterpret_cast<fbf16x4*>(kb2) = cvt4(x);
+                *reinterpret_cast<fbf16x4*>(kb2 + H) = cvt4(y);
+            }
+        }
+}
+
 // dQ = sum over key blocks in order (query rows < tl; rows past it get 0, as their dS is 0)
 __global__ __launch_bounds__(256) void flash_dq_reduce(const float* __restrict__ dqp, float* __restrict__ dqkv, int B,
                                                        int T, int NH, int H, int nkb, const int* __restrict__ tlen,
@@ -973,13 +1326,24 @@ long flash_dq_scratch_floats(int B, int T, int NH) {
     return (long)nkb * B * NH * T * 64;
 }
 
+// bf16 mode, bf16 qkv plane given: flash_fwd_bf16p_kernel (env SUTA_FLASH_FWD_PLANE=0 keeps the fp32-row
+// kernels for A/B runs; read at every launch)
+static bool ff_plane() {
+    const char* e = std::getenv("SUTA_FLASH_FWD_PLANE");
+    return !(e && atoi(e) == 0);
+}
+
 bool launch_flash_fwd(const float* qkv, float* ctx, float* lse, int B, int T, int NH, int H, int dh, float scale,
-                      const int* tlen, bool bf16, hipStream_t st, void* ctxb_) {
+                      const int* tlen, bool bf16, hipStream_t st, void* ctxb_, const void* qkvb) {
     __bf16* ctxb = reinterpret_cast<__bf16*>(ctxb_);
     if (dh != 64 || T < 1 || H % 4) return false;
     const int ng = (T + 31) / 32, nqb = (ng + FF_NW - 1) / FF_NW;
     const dim3 grid((unsigned)((long)B * NH * nqb));
-    if (bf16 && fb_img()) {
+    if (bf16 && qkvb && H % 8 == 0 && ff_plane()) {
+        if (reinterpret_cast<uintptr_t>(qkvb) & 15) throw std::invalid_argument("flash_fwd: bf16 qkv plane not 16-B aligned");
+        hipLaunchKernelGGL(flash_fwd_bf16p_kernel<FF_NW>, grid, dim3(FF_NW * 64), 0, st,
+                           reinterpret_cast<const __bf16*>(qkvb), ctx, lse, T, NH, H, scale, tlen, nqb, ctxb);
+    } else if (bf16 && fb_img()) {
         static_assert(FF_NW_BF == FF_NW, "the bf16 forward shares the query-block grid");
         hipLaunchKernelGGL(flash_fwd_bf16_kernel, grid, dim3(FF_NW_BF * 64), 0, st, qkv, ctx, lse, T, NH, H, scale,
                            tlen, nqb, ctxb);
@@ -1008,9 +1372,16 @@ static void flash_bwd_go(dim3 grid, hipStream_t st, const float* qkv, const floa
                        T, NH, H, scale, tlen, nkb, gpb, B, dqkvb);
 }
 
+// bf16 mode, bf16 planes of qkv and dctx given: flash_bwd_bf16p_kernel (env SUTA_FLASH_BWD_PLANE=0 keeps the
+// fp32-row kernels for A/B runs; read at every launch)
+static bool fb_plane() {
+    const char* e = std::getenv("SUTA_FLASH_BWD_PLANE");
+    return !(e && atoi(e) == 0);
+}
+
 bool launch_flash_bwd(const float* qkv, const float* dctx, const float* lse, const float* delta, float* dqkv,
                       float* dqp, int B, int T, int NH, int H, int dh, float scale, const int* tlen, bool bf16,
-                      hipStream_t st, void* dqkvb_) {
+                      hipStream_t st, void* dqkvb_, const void* qkvb, const void* dctxb) {
     __bf16* dqkvb = reinterpret_cast<__bf16*>(dqkvb_);
     if (dh != 64 || T < 1 || H % 4) return false;
     const int nw = fb_nw();
@@ -1018,7 +1389,21 @@ bool launch_flash_bwd(const float* qkv, const float* dctx, const float* lse, con
     const int nkb = (ng + nw - 1) / nw;   // key blocks per head
     const int gpb = (ng + nkb - 1) / nkb;  // key groups per block (balanced)
     const dim3 grid((unsigned)((long)B * NH * nkb));
-    if (bf16 && nw == FBB_NW && fb_img()) {
+    if (bf16 && nw == FBB_NW && qkvb && dctxb && H % 8 == 0 && fb_plane()) {
+        if ((reinterpret_cast<uintptr_t>(qkvb) | reinterpret_cast<uintptr_t>(dctxb)) & 15)
+            throw std::invalid_argument("flash_bwd: bf16 planes not 16-B aligned");
+        constexpr size_t lds = fbbp_lds_bytes();
+        static bool attr = false;
+        if (!attr) {
+            if (hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_bwd_bf16p_kernel),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+                throw std::runtime_error("hipFuncSetAttribute(flash_bwd_bf16p_kernel) failed");
+            attr = true;
+        }
+        hipLaunchKernelGGL(flash_bwd_bf16p_kernel, grid, dim3(FBB_NW * 64), lds, st,
+                           reinterpret_cast<const __bf16*>(qkvb), reinterpret_cast<const __bf16*>(dctxb), lse, delta,
+                           dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb);
+    } else if (bf16 && nw == FBB_NW && fb_img()) {
         constexpr size_t lds = fbb_lds_bytes();
         static bool attr = false;
         if (!attr) {

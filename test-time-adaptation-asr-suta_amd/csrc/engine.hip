@@ -315,11 +315,21 @@ struct suta_engine {
     // operand (LayerNorm, flash attention, GEMM epilogue), read by the linear right after
     DevBuf planebuf;
     bool use_planes() const { return gemm_mode == SUTA_PRECISION_BF16 && !wplanes.empty(); }
+    // planes 0 / 1: the ping-pong A planes; plane 2: dctx's plane (the flash backward's dO operand)
     void* plane(int i) {
         if (!use_planes()) return nullptr;
         const size_t half = rup((long)plan.B * plan.T * std::max(3 * c.H, c.F) * 2, 256);
-        if (planebuf.alloc(2 * half)) drop_graph();
+        if (planebuf.alloc(3 * half)) drop_graph();
         return reinterpret_cast<char*>(planebuf.p) + i * half;
+    }
+    // bf16 plane of layer l's qkv [B*T][3H]: written by the QKV GEMM, read by the flash forward and, in the
+    // backward, by the flash backward (kept for every layer, like the fp32 qkv)
+    DevBuf qkvplanes;
+    void* qkv_plane(int l) {
+        if (!use_planes() || c.H % 8) return nullptr;
+        const size_t per = rup((long)plan.B * plan.T * 3 * c.H * 2, 256);
+        if (qkvplanes.alloc(per * c.L)) drop_graph();
+        return reinterpret_cast<char*>(qkvplanes.p) + l * per;
     }
     void build_weight_planes();
     void gemm(const GemmParams& p0) {
@@ -350,6 +360,7 @@ struct suta_engine {
         }
         if (!p.C) throw SutaError(SUTA_ERR_UNSUPPORTED, "gemm: fp32 output skipped on a plane-less GEMM");
         if (!p.A) throw SutaError(SUTA_ERR_UNSUPPORTED, "gemm: fp32 A not written (bf16-plane producer) on a plane-less GEMM");
+        if (p.Cb) throw SutaError(SUTA_ERR_UNSUPPORTED, "gemm: a bf16 C plane (read by the next kernel) requested on a plane-less GEMM");
         p.Ab = nullptr;  // (plane-less GEMM: a plane given for a non-frozen B is ignored)
         p.Cb = nullptr;
         timed(F_GEMM, [&] { gemm_launch(p, st, plan.splitws, plan.splitws_floats); }, ab);
@@ -695,6 +706,7 @@ void suta_engine::forward(int B) {
             });
             attn_in = dead ? nullptr : lb.y1;  // (dead: the QKV GEMM reads the LN1 plane only)
         }
+        void* qkvp = pl.flash ? qkv_plane(l) : nullptr;
         {  // fused QKV
             GemmParams g;
             gemm_init(g);
@@ -712,6 +724,10 @@ void suta_engine::forward(int B) {
             g.K = H;
             g.epi = EPI_BIAS;
             g.bias = bqkv[l];
+            if (qkvp) {  // bf16 plane of qkv: the flash kernels' operands
+                g.Cb = qkvp;
+                g.ldcb = 3 * H;
+            }
             gemm(g);
         }
         // flash attention (head dim 64, any T): ctx and the per-row LSE, no T x T matrix
@@ -719,7 +735,7 @@ void suta_engine::forward(int B) {
         if (fused)
             timed(F_ATTN, [&] {
                 if (!launch_flash_fwd(lb.qkv, lb.ctx, lb.lse, B, T, NH, H, d, scale, rT(),
-                                      gemm_mode == SUTA_PRECISION_BF16, st, P0))
+                                      gemm_mode == SUTA_PRECISION_BF16, st, P0, qkvp))
                     throw SutaError(SUTA_ERR_UNSUPPORTED, "flash attention shape");
             }, 4.0 * BT * (4.0 * H + NH));  // Q, K, V read; ctx and LSE written
         if (!fused) {
@@ -994,7 +1010,10 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
             dhres = t1;  // dhmid
         }
         // dctx = dhres @ Wo
-        nn_gemm(dhres, H, wo[l], H, pl.ctx, H, (int)BT, H, H, 0, nullptr, 0, nullptr, 0, P0);
+        void* dctxp = (pl.flash && P0) ? plane(2) : nullptr;   // dO plane of the flash backward
+        void* qkvp = (pl.flash && P0) ? qkv_plane(l) : nullptr;
+        if (!qkvp) dctxp = nullptr;
+        nn_gemm(dhres, H, wo[l], H, pl.ctx, H, (int)BT, H, H, 0, nullptr, 0, nullptr, 0, P0, dctxp);
         // softmax-backward row term delta = rowsum(dctx * ctx) per head, fused into the dP epilogue
         timed(F_SOFTMAX, [&] { launch_attn_delta(pl.ctx, lb.ctx, pl.delta, B, T, NH, d, st); });
         // flash backward: P recomputed from the LSE, dQ, dK, dV into dqkv (else the GEMM path below)
@@ -1002,7 +1021,7 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
         if (fused_bwd)
             timed(F_ATTN, [&] {
                 if (!launch_flash_bwd(lb.qkv, pl.ctx, lb.lse, pl.delta, pl.dqkv, pl.dqp, B, T, NH, H, d, scale, rT(),
-                                      gemm_mode == SUTA_PRECISION_BF16, st, P1))
+                                      gemm_mode == SUTA_PRECISION_BF16, st, P1, qkvp, dctxp))
                     throw SutaError(SUTA_ERR_UNSUPPORTED, "flash attention shape");
             }, 4.0 * BT * (7.0 * H + 2.0 * NH));  // Q, K, V, dctx, LSE, delta read; dQ, dK, dV written
         if (!fused_bwd) {

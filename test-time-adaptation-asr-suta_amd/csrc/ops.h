@@ -53,10 +53,11 @@ void launch_colsum(const float* x, int B, int rows, int C, float* out, long ostr
 long flash_dq_scratch_floats(int B, int T, int NH);
 // ctxb / dqkvb (may be null): bf16 copies of ctx / dqkv for the bf16-plane GEMMs that consume them.
 bool launch_flash_fwd(const float* qkv, float* ctx, float* lse, int B, int T, int NH, int H, int dh, float scale,
-                      const int* tlen, bool bf16, hipStream_t st, void* ctxb = nullptr);
+                      const int* tlen, bool bf16, hipStream_t st, void* ctxb = nullptr, const void* qkvb = nullptr);
 bool launch_flash_bwd(const float* qkv, const float* dctx, const float* lse, const float* delta, float* dqkv,
                       float* dqp, int B, int T, int NH, int H, int dh, float scale, const int* tlen, bool bf16,
-                      hipStream_t st, void* dqkvb = nullptr);
+                      hipStream_t st, void* dqkvb = nullptr, const void* qkvb = nullptr,
+                      const void* dctxb = nullptr);
 // grouped positional conv (group width 48 or 64, exact fp32 MFMA); fwd: C = R + gelu(conv + bias), C2 = conv + bias;
 // bwd: C = conv + R (rows >= tlen -> 0).  false (nothing launched) outside the supported shapes
 bool launch_posconv(bool fwd, const float* x, const float* W, const float* bias, const float* R, float* C, float* C2,

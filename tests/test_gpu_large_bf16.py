@@ -213,3 +213,58 @@ def test_bf16_hb8_pingpong_kernel(monkeypatch):
         for u in range(2):
             assert_bf16_close(out["2"][r][u], out["0"][r][u], 0.97, f"hb8 vs 128x128 step {r} utt {u}",
                               rtol=BF16_LOGITS_RTOL_LARGE)
+
+
+@pytest.mark.parametrize("preset", ["wav2vec2-base", "wav2vec2-large"])
+def test_flash_fwd_plane_kernel_equals_row_kernel(monkeypatch, preset):
+    """flash_fwd_bf16p_kernel (Q / K / V read from the QKV GEMM's bf16 plane, V^T by transposed LDS reads;
+    default in bf16 mode) against flash_fwd_bf16_kernel (fp32 rows rounded in the kernel,
+    SUTA_FLASH_FWD_PLANE=0): the same RNE-rounded operands; the exponent argument is one fma instead of a
+    multiply and a subtraction, so probabilities differ by fp32 rounding and the adapted logits agree to
+    the bf16 tolerance.  Ragged pair (T = 399 and 239: a partial last key tile, both 32-key halves of it
+    masked differently), reruns bitwise identical."""
+    cfg = get_config(preset)
+    eng = SutaEngine(cfg, synth_weights(cfg), max_batch=2, max_samples=128000)
+    eng.set_precision("bf16")
+    waves = [synth.wave(128000, 80), synth.wave(76800, 81)]
+    out = {}
+    for plane in ("1", "0"):
+        monkeypatch.setenv("SUTA_FLASH_FWD_PLANE", plane)
+        a, _, _ = eng.adapt_varlen(waves, 3, SutaHParams(), record=[0, 3])
+        b, _, _ = eng.adapt_varlen(waves, 3, SutaHParams(), record=[0, 3])
+        for u in range(2):
+            assert np.array_equal(a[3][u], b[3][u]), (plane, u)
+        out[plane] = a
+    eng.close()
+    for r in (0, 3):
+        for u in range(2):
+            assert_bf16_close(out["1"][r][u], out["0"][r][u], 0.97, f"plane fwd step {r} utt {u}",
+                              rtol=BF16_LOGITS_RTOL_LARGE)
+
+
+@pytest.mark.parametrize("preset", ["wav2vec2-base", "wav2vec2-large"])
+def test_flash_bwd_plane_kernel_equals_row_kernel(monkeypatch, preset):
+    """flash_bwd_bf16p_kernel (Q / K / V from the qkv bf16 plane, dO from the plane the out-projection's
+    input-gradient GEMM writes, dV^T / dK^T operands by transposed LDS reads; default in bf16 mode) against
+    flash_bwd_bf16_kernel (fp32 rows rounded in the kernel, transposed LDS images; SUTA_FLASH_BWD_PLANE=0):
+    the same RNE-rounded operands, the exponent argument one fma instead of a multiply and a subtraction
+    -> adapted logits and tensors agree to the bf16 tolerance; the step-0 logits (no backward yet) are
+    bitwise equal; reruns bitwise identical.  Ragged pair (T = 399 / 239: masked keys and rows)."""
+    cfg = get_config(preset)
+    eng = SutaEngine(cfg, synth_weights(cfg), max_batch=2, max_samples=128000)
+    eng.set_precision("bf16")
+    waves = [synth.wave(128000, 82), synth.wave(76800, 83)]
+    out = {}
+    for plane in ("1", "0"):
+        monkeypatch.setenv("SUTA_FLASH_BWD_PLANE", plane)
+        a, _, _ = eng.adapt_varlen(waves, 3, SutaHParams(), record=[0, 1, 3])
+        b, _, _ = eng.adapt_varlen(waves, 3, SutaHParams(), record=[0, 1, 3])
+        for u in range(2):
+            assert np.array_equal(a[3][u], b[3][u]), (plane, u)
+        out[plane] = a
+    eng.close()
+    for u in range(2):
+        assert np.array_equal(out["1"][0][u], out["0"][0][u]), u
+        for r in (1, 3):
+            assert_bf16_close(out["1"][r][u], out["0"][r][u], 0.97, f"plane bwd step {r} utt {u}",
+                              rtol=BF16_LOGITS_RTOL_LARGE)
