@@ -98,6 +98,7 @@ struct GemmParams {
     long ldab, ldbb;
     void* Cb;   // optional bf16 copy of the stored C (Z == 1): the A plane of the next bf16-plane GEMM
     long ldcb;
+    int off32;  // internal: every epilogue operand (rows x ld) within 4 GiB -> 32-bit offset epilogue
 };
 
 void gemm_init(GemmParams& p);

@@ -98,6 +98,13 @@ struct DevBuf {
     }
 };
 
+// SUTA_FUSED_CONV_LN=0: the layer-mode conv stack's LayerNorm backward without the fused bias / conv0 weight
+// gradient sums (separate column-sum pass and GEMM), for A/B runs; read at every call
+static bool fused_conv_ln() {
+    const char* e = std::getenv("SUTA_FUSED_CONV_LN");
+    return !(e && atoi(e) == 0);
+}
+
 struct Arena {
     char* base = nullptr;
     size_t off = 0, cap = 0;
@@ -165,6 +172,7 @@ struct Plan {
     // the conv LNs of layer mode, the feature-projection LN, the encoder LN, and every LN of stable
     // (pre-LN) layers; post-LN layers' LN inputs are transient and keep x-hat
     std::vector<LayerBufs> lay;
+    long lnpart_floats = 0;
     float *ctx, *gu, *rtmp, *logits;
     // backward
     float *dlogits, *d1, *d2, *d3, *dqkv, *dP, *dqp, *du, *dzc, *dzc2, *lnpart, *loss, *loss_scratch, *c0part, *delta;
@@ -492,7 +500,8 @@ void suta_engine::build_plan(int B, long N) {
         pl.dzc = ar.take<float>((size_t)B * maxLC);
         pl.dzc2 = ar.take<float>((size_t)B * maxLC);
         const long lnrows = std::max<long>(pl.Lc[0], T);
-        pl.lnpart = ar.take<float>((size_t)B * ((lnrows + 15) / 16) * 2 * std::max<long>(H, maxLC / pl.Lc[0] + 1) + 64);
+        pl.lnpart_floats = (long)B * ((lnrows + 15) / 16) * 2 * std::max<long>(H, maxLC / pl.Lc[0] + 1) + 64;
+        pl.lnpart = ar.take<float>((size_t)pl.lnpart_floats);
         pl.dpart = ar.take<double>((size_t)B * ((pl.Lc[0] + 127) / 128 + 2) * 2 * k.C[0] + (size_t)B * k.C[0] * 2);
         pl.c0part = ar.take<float>((size_t)B * ((pl.Lc[0] + 127) / 128) * k.K[0] * k.C[0] + 64);
         pl.loss = ar.take<float>(B);
@@ -1257,15 +1266,25 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
     float* other = pl.dzc;
     for (int i = last; i >= 1; --i) {
         // cur: group mode -> dz_i ; layer mode -> da_i
+        bool bias_done = false;
         if (k.layer_mode) {
             timed(F_NORM, [&] {
-                launch_layernorm_bwd(cur, pl.cxhat[i], pl.crstd[i], P + o_cg[i], P + o_cbeta[i], Pn, pl.Lc[i], B,
-                                     k.C[i], 1, nullptr, nullptr, other, G + o_cg[i], G + o_cbeta[i], Pn, pl.lnpart,
-                                     st, nullptr, pl.z[i], pl.cmean[i]);
+                // fused: the LayerNorm backward also sums the conv bias gradient (one read of dz_i)
+                if (!pl.cxhat[i] && fused_conv_ln() &&
+                    layernorm_bwd_conv_part_floats(B, pl.Lc[i], k.C[i], 0) <= pl.lnpart_floats &&
+                    launch_layernorm_bwd_conv(cur, pl.crstd[i], P + o_cg[i], P + o_cbeta[i], Pn, pl.Lc[i], B, k.C[i],
+                                              other, G + o_cg[i], G + o_cbeta[i], k.conv_bias ? G + o_cb[i] : nullptr,
+                                              nullptr, Pn, pl.lnpart, st, pl.z[i], pl.cmean[i], nullptr, 0, 0, 0)) {
+                    bias_done = true;
+                } else {
+                    launch_layernorm_bwd(cur, pl.cxhat[i], pl.crstd[i], P + o_cg[i], P + o_cbeta[i], Pn, pl.Lc[i], B,
+                                         k.C[i], 1, nullptr, nullptr, other, G + o_cg[i], G + o_cbeta[i], Pn, pl.lnpart,
+                                         st, nullptr, pl.z[i], pl.cmean[i]);
+                }
             });
             std::swap(cur, other);
         }
-        if (k.conv_bias)
+        if (k.conv_bias && !bias_done)
             timed(F_NORM, [&] { launch_colsum(cur, B, pl.Lc[i], k.C[i], G + o_cb[i], Pn, pl.lnpart, st); });
         {  // dW_i = im2col(a_{i-1})^T dz_i
             GemmParams g;
@@ -1337,11 +1356,22 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
         }, 4.0 * B * ((double)pl.N + (double)pl.Lc[0] * k.C[0]));  // waveform and activation gradient read
         return;
     }
+    bool fused0 = false;
     timed(F_NORM, [&] {
-        launch_layernorm_bwd(cur, pl.cxhat[0], pl.crstd[0], P + o_cg[0], P + o_cbeta[0], Pn, pl.Lc[0], B, k.C[0], 1,
-                             nullptr, nullptr, other, G + o_cg[0], G + o_cbeta[0], Pn, pl.lnpart, st, nullptr, pl.z[0],
-                             pl.cmean[0]);
+        // fused: the LayerNorm backward also sums the conv0 bias and weight gradients (dz0 read once)
+        if (!pl.cxhat[0] && fused_conv_ln() && k.K[0] == 10 &&
+            layernorm_bwd_conv_part_floats(B, pl.Lc[0], k.C[0], 10) <= pl.lnpart_floats &&
+            launch_layernorm_bwd_conv(cur, pl.crstd[0], P + o_cg[0], P + o_cbeta[0], Pn, pl.Lc[0], B, k.C[0], other,
+                                      G + o_cg[0], G + o_cbeta[0], k.conv_bias ? G + o_cb[0] : nullptr, G + o_cw[0], Pn,
+                                      pl.lnpart, st, pl.z[0], pl.cmean[0], pl.x, pl.N, k.S[0], 10)) {
+            fused0 = true;
+        } else {
+            launch_layernorm_bwd(cur, pl.cxhat[0], pl.crstd[0], P + o_cg[0], P + o_cbeta[0], Pn, pl.Lc[0], B, k.C[0], 1,
+                                 nullptr, nullptr, other, G + o_cg[0], G + o_cbeta[0], Pn, pl.lnpart, st, nullptr,
+                                 pl.z[0], pl.cmean[0]);
+        }
     });
+    if (fused0) return;
     if (k.conv_bias)
         timed(F_NORM, [&] { launch_colsum(other, B, pl.Lc[0], k.C[0], G + o_cb[0], Pn, pl.lnpart, st); });
     {  // dW0[k][c] = sum_t x[S0 t + k] dz0[t][c]

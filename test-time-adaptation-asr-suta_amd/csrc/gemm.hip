@@ -218,6 +218,20 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
     if (splits > 1) splits = (p.K + p.kchunk - 1) / p.kchunk;
     p.splits = splits;
     p.ws = ws;
+    {  // 32-bit epilogue offsets: M x ld elements of every operand the epilogue touches within 4 GiB
+       // (SUTA_EPI_FAST=0: the general epilogue everywhere, for A/B runs)
+        static int fast = -1;
+        if (fast < 0) {
+            const char* ev = std::getenv("SUTA_EPI_FAST");
+            fast = (ev && atoi(ev) == 0) ? 0 : 1;
+        }
+        const double lim = 4294967295.0 - 1024.0;
+        auto fits = [&](long ld, double esz) { return (double)p.M * (double)std::max(ld, (long)p.N) * esz < lim; };
+        p.off32 = fits(p.ldc, 4) && (!(p.epi & EPI_RESID) || fits(p.ldr, 4)) &&
+                  (!(p.epi & (EPI_DGELU | EPI_SMBWD)) || fits(p.ldaux, 4)) && (!(p.epi & EPI_STORE_PRE) || fits(p.ldc2, 4)) &&
+                  (!p.Cb || fits(p.ldcb, 2)) && p.ldc >= 0 && p.ldr >= 0 && p.ldaux >= 0 && p.ldc2 >= 0 && p.ldcb >= 0 &&
+                  fast;
+    }
     {
         static int ord = -1;  // SUTA_GEMM_ORDER=1: m-fastest; =G >= 2: bands of G tile rows (A/B runs)
         if (ord < 0) {

@@ -193,6 +193,151 @@ __device__ __forceinline__ TileId xcd_tile(int order = 0) {
     return TileId{id % gx, (id / gx) % gy, id / (gx * gy)};
 }
 
+// Interior-tile epilogue with 32-bit offsets (p.off32: every operand's rows x leading dimension fits 4 GiB):
+// element r of a fragment sits at row rb + ro(r), ro(r) = (r & 3) + 8 (r >> 2) the same for every lane, so its
+// address is a wave-uniform base (operand + ro(r) x ld, scalar arithmetic) plus the lane's 32-bit byte offset of
+// row rb (one multiply per fragment): the stores and operand loads take the scalar-base + vector-offset form
+// and cost no per-element address arithmetic (the general epilogue below spends ~15 VALU per element on
+// 64-bit addresses).  Same operations in the same order as the general epilogue.
+template <typename T>
+__device__ __forceinline__ T* byte_at(T* base, unsigned off) {
+    return reinterpret_cast<T*>(reinterpret_cast<char*>(base) + off);
+}
+template <typename T>
+__device__ __forceinline__ const T* byte_at(const T* base, unsigned off) {
+    return reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + off);
+}
+
+template <int RM, int RN, bool CB>
+__device__ __forceinline__ void gemm_epilogue_fast(const GemmParams& p, const f32x16 (&acc)[RM][RN], int z1, int z0,
+                                                   int rbase, int cbase, int h, int l32) {
+    const int e = p.epi;
+    float* C = p.C ? p.C + z1 * p.sC1 + z0 * p.sC0 : nullptr;
+    const float* bias = p.bias ? p.bias + z1 * p.sBias1 + z0 * p.sBias0 : nullptr;
+    const float* aux = p.aux ? p.aux + z1 * p.sAux1 + z0 * p.sAux0 : nullptr;
+    const int rlim = (e & EPI_ROWMASK) ? p.zrows[z1] : 0x7fffffff;
+    float* C2 = p.C2 ? p.C2 + z1 * p.sC21 + z0 * p.sC20 : nullptr;
+    const float* Q = nullptr;
+    long ldq = 0;
+    if (e & EPI_RESID) {
+        Q = p.R + z1 * p.sR1 + z0 * p.sR0;
+        ldq = p.ldr;
+    } else if (e & EPI_ACCUM) {
+        Q = C;
+        ldq = p.ldc;
+    } else if (e & EPI_SMBWD) {
+        Q = p.rowv + z1 * p.sRow1 + z0 * p.sRow0;
+    }
+    const float alpha = p.alpha;
+    const bool cbpair = CB && (p.ldcb & 1) == 0;
+    const bool odd = l32 & 1;
+    constexpr int CH = 8;
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j) {
+            const unsigned rb = rbase + i * 32 + 4 * h;
+            const unsigned col = cbase + j * 32 + l32;
+            const unsigned oc = 4u * (rb * (unsigned)p.ldc + col);
+            const unsigned oq = (e & EPI_SMBWD) ? 4u * rb : 4u * (rb * (unsigned)ldq + col);
+            const unsigned oa = 4u * (rb * (unsigned)p.ldaux + col);
+            const unsigned o2 = 4u * (rb * (unsigned)p.ldc2 + col);
+            const unsigned ob = 2u * ((rb + (odd ? 1u : 0u)) * (unsigned)p.ldcb + (col & ~1u));
+            const float bj = (e & EPI_BIAS) ? bias[col] : 0.f;
+#pragma unroll
+            for (int r0 = 0; r0 < 16; r0 += CH) {
+                float v[CH], xa[CH], xq[CH];
+                if (e & (EPI_DGELU | EPI_SMBWD)) {
+#pragma unroll
+                    for (int r = 0; r < CH; ++r) {
+                        const int ro = ((r0 + r) & 3) + 8 * ((r0 + r) >> 2);
+                        xa[r] = *byte_at(aux + ro * p.ldaux, oa);
+                    }
+                }
+                if (Q) {
+#pragma unroll
+                    for (int r = 0; r < CH; ++r) {
+                        const int ro = ((r0 + r) & 3) + 8 * ((r0 + r) >> 2);
+                        xq[r] = (e & EPI_SMBWD) ? *byte_at(Q + ro, oq) : *byte_at(Q + ro * ldq, oq);
+                    }
+                }
+                if (e & EPI_SMBWD) {
+#pragma unroll
+                    for (int r = 0; r < CH; ++r) v[r] = alpha * (xa[r] * (acc[i][j][r0 + r] - xq[r]));
+                } else {
+#pragma unroll
+                    for (int r = 0; r < CH; ++r) v[r] = acc[i][j][r0 + r] * alpha;
+                    if (e & EPI_BIAS) {
+#pragma unroll
+                        for (int r = 0; r < CH; ++r) v[r] += bj;
+                    }
+                    if (e & EPI_ACCUM) {
+#pragma unroll
+                        for (int r = 0; r < CH; ++r) v[r] += xq[r];
+                    }
+                    if (e & EPI_STORE_PRE) {
+#pragma unroll
+                        for (int r = 0; r < CH; ++r) {
+                            const int ro = ((r0 + r) & 3) + 8 * ((r0 + r) >> 2);
+                            *byte_at(C2 + ro * p.ldc2, o2) = v[r];
+                        }
+                    }
+                    if (e & EPI_GELU) {
+#pragma unroll
+                        for (int r = 0; r < CH; ++r) v[r] = gelu_f(v[r]);
+                    }
+                    if (e & EPI_DGELU) {
+#pragma unroll
+                        for (int r = 0; r < CH; ++r) v[r] *= dgelu_f(xa[r]);
+                    }
+                    if (e & EPI_RESID) {
+#pragma unroll
+                        for (int r = 0; r < CH; ++r) v[r] += xq[r];
+                    }
+                }
+                if (e & EPI_ROWMASK) {
+#pragma unroll
+                    for (int r = 0; r < CH; ++r) {
+                        const int ro = ((r0 + r) & 3) + 8 * ((r0 + r) >> 2);
+                        if ((int)rb + ro >= rlim) v[r] = 0.f;
+                    }
+                }
+                if (!CB || C) {
+#pragma unroll
+                    for (int r = 0; r < CH; ++r) {
+                        const int ro = ((r0 + r) & 3) + 8 * ((r0 + r) >> 2);
+                        *byte_at(C + ro * p.ldc, oc) = v[r];
+                    }
+                }
+                if (CB) {
+                    typedef __bf16 cb2 __attribute__((ext_vector_type(2)));
+                    __bf16* Cb = reinterpret_cast<__bf16*>(p.Cb);
+                    if (cbpair) {
+                        // (column, column + 1) pairs: lanes 2i / 2i + 1 swap one value (DPP quad_perm [1,0,3,2]);
+                        // the even lane writes row r, the odd lane row r + 1 (registers r, r + 1: consecutive rows)
+#pragma unroll
+                        for (int r = 0; r < CH; r += 2) {
+                            const int ro = ((r0 + r) & 3) + 8 * ((r0 + r) >> 2);
+                            const float a = v[r], b = v[r + 1];
+                            const float q = __int_as_float(
+                                __builtin_amdgcn_mov_dpp(__float_as_int(odd ? a : b), 0xB1, 0xF, 0xF, false));
+                            cb2 pr;
+                            pr[0] = (__bf16)(odd ? q : a);
+                            pr[1] = (__bf16)(odd ? b : q);
+                            *reinterpret_cast<cb2*>(byte_at(Cb + ro * p.ldcb, ob)) = pr;
+                        }
+                    } else {
+#pragma unroll
+                        for (int r = 0; r < CH; ++r) {
+                            const int ro = ((r0 + r) & 3) + 8 * ((r0 + r) >> 2);
+                            Cb[(long)(rb + ro) * p.ldcb + col] = (__bf16)v[r];
+                        }
+                    }
+                }
+            }
+        }
+}
+
 // Store the wave's RM x RN 32x32 accumulator fragments (MFMA 32x32 output layout: lane -> column,
 // register r -> row (r&3) + 8(r>>2) + 4h).  Flags are block-uniform, so each epilogue step is one
 // uniform branch per fragment rather than per element; operand loads use clamped (always valid)
@@ -214,6 +359,10 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, const f32x16 
                     const int col = cbase + j * 32 + l32;
                     if (interior || (row < p.M && col < p.N)) W[(long)row * p.N + col] = acc[i][j][r];
                 }
+        return;
+    }
+    if (interior && p.off32) {
+        gemm_epilogue_fast<RM, RN, CB>(p, acc, z1, z0, rbase, cbase, h, l32);
         return;
     }
     const int e = p.epi;

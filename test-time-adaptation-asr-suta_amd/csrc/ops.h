@@ -42,6 +42,17 @@ void launch_layernorm_bwd(const float* dy, const float* xhat, const float* rstd,
                           hipStream_t st, void* dxb = nullptr, const float* x = nullptr, const float* mean = nullptr);
 // dxb: optional bf16 copy of dx; xhat null: x-hat = (x - mean) * rstd recomputed from the LayerNorm input
 
+// Layer-mode conv stack (D = 512, GELU after the LayerNorm, x-hat recomputed from the stored conv output x and
+// its row means): the LayerNorm backward that also sums the conv bias gradient (dbias, may be null) and, with
+// ktaps = 10 (conv0), the weight gradient dw[k][c] = sum_t xw[xs t + k] dx[t][c] (xw: the waveform, xws per
+// utterance) -- dgamma / dbeta / dbias / dw per utterance at gstride.  Returns false when the shape is not
+// covered (the caller then runs launch_layernorm_bwd + launch_colsum + its GEMM).  part: >=
+// layernorm_bwd_conv_part_floats(...) floats.
+long layernorm_bwd_conv_part_floats(int B, int rows_per_utt, int D, int ktaps);
+bool launch_layernorm_bwd_conv(const float* dy, const float* rstd, const float* g, const float* beta, long pstride,
+                               int rows_per_utt, int B, int D, float* dx, float* dgamma, float* dbeta, float* dbias,
+                               float* dw, long gstride, float* part, hipStream_t st, const float* x, const float* mean,
+                               const float* xw, long xws, int xs, int ktaps);
 // Column sums per utterance: out[b][c] = sum_{t < rows} x[b][t][c]   (bias gradients).
 void launch_colsum(const float* x, int B, int rows, int C, float* out, long ostride, float* part, hipStream_t st);
 

@@ -599,6 +599,136 @@ __global__ __launch_bounds__(256) void layernorm_bwd_vec_kernel(
     }
 }
 
+// Layer-mode conv stack: LayerNorm backward of conv i (D = 512, NV = 2) that also sums what the layer's
+// other two consumers of dz_i read it for -- the conv bias gradient (column sums of dz_i) and, for conv0
+// (KT = kernel taps), the weight gradient dW0[k][c] = sum_t x[S0 t + k] dz0[t][c] -- so dz_i is read once
+// instead of three times (the separate column-sum pass and the conv0 weight-gradient GEMM, 3.4 GB each
+// at 64 x 8 s on wav2vec2-large).  Rows in chunks of CROWS per block (larger chunks for the long layers
+// keep the partial slabs small); partial layout [B][nchunk][2 + 1 + KT][D]: dgamma, dbeta, dbias, dW0 rows;
+// fixed-order reductions (waves, then chunks in order): deterministic.
+template <int NV, bool GV, int KT>
+__global__ __launch_bounds__(256) void layernorm_bwd_conv_kernel(
+    const float* __restrict__ dy, const float* __restrict__ rstd, const float* __restrict__ g,
+    const float* __restrict__ beta, long pstride, int rows_per_utt, float* __restrict__ dx, float* __restrict__ part,
+    int nchunk, int crows, const float* __restrict__ xin, const float* __restrict__ meanp,
+    const float* __restrict__ xw, long xws, int xs) {
+    constexpr int D = 256 * NV;
+    constexpr int NVEC = 3 + KT;
+    __shared__ f32x4 red[4][2][NV * 64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int u = blockIdx.y, ch = blockIdx.x;
+    const float* gu = g + (long)u * pstride;
+    const float* bu = beta + (long)u * pstride;
+    f32x4 gam[NV], bet[NV], acc[NVEC][NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        const int c = 4 * (lane + 64 * i);
+        if constexpr (GV) {
+            gam[i] = *reinterpret_cast<const f32x4*>(gu + c);
+            bet[i] = *reinterpret_cast<const f32x4*>(bu + c);
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                gam[i][e] = gu[c + e];
+                bet[i][e] = bu[c + e];
+            }
+        }
+#pragma unroll
+        for (int v = 0; v < NVEC; ++v) acc[v][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    const float* xu = xw ? xw + (long)u * xws : nullptr;
+    const int r0 = ch * crows, r1 = min(rows_per_utt, r0 + crows);
+    for (int r = r0 + w; r < r1; r += 4) {
+        const long row = (long)u * rows_per_utt + r;
+        const f32x4* xr = reinterpret_cast<const f32x4*>(xin + row * D);
+        const f32x4* dr = reinterpret_cast<const f32x4*>(dy + row * D);
+        f32x4 gi[NV], xh[NV];
+        float s1 = 0.f, s2 = 0.f;
+        const float rs = rstd[row];
+        const float mu = meanp[row];
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            xh[i] = xr[lane + 64 * i];
+            gi[i] = dr[lane + 64 * i];
+        }
+        float xt[KT > 0 ? KT : 1];
+        if constexpr (KT > 0) {
+#pragma unroll
+            for (int k = 0; k < KT; ++k) xt[k] = xu[(long)xs * r + k];
+        }
+#pragma unroll
+        for (int i = 0; i < NV; ++i)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) xh[i][e] = (xh[i][e] - mu) * rs;  // x-hat recomputed bitwise
+#pragma unroll
+        for (int i = 0; i < NV; ++i)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float d = gi[i][e] * dgelu_f(xh[i][e] * gam[i][e] + bet[i][e]);
+                gi[i][e] = d;
+                acc[0][i][e] += d * xh[i][e];
+                acc[1][i][e] += d;
+                const float dg = d * gam[i][e];
+                s1 += dg;
+                s2 += dg * xh[i][e];
+            }
+        s1 = wave_sum(s1);
+        s2 = wave_sum(s2);
+        const float m1 = s1 / D, m2 = s2 / D;
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            f32x4 o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = rs * (gi[i][e] * gam[i][e] - m1 - xh[i][e] * m2);
+            reinterpret_cast<f32x4*>(dx + row * D)[lane + 64 * i] = o;
+            acc[2][i] += o;
+#pragma unroll
+            for (int k = 0; k < KT; ++k) acc[3 + k][i] += xt[k] * o;
+        }
+    }
+    f32x4* pp = reinterpret_cast<f32x4*>(part + ((long)u * nchunk + ch) * NVEC * D);
+#pragma unroll
+    for (int v = 0; v < NVEC; v += 2) {
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            red[w][0][lane + i * 64] = acc[v][i];
+            if (v + 1 < NVEC) red[w][1][lane + i * 64] = acc[v + 1][i];
+        }
+        __syncthreads();
+        for (int c = threadIdx.x; c < D / 4; c += 256) {
+            pp[v * (D / 4) + c] = red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c];
+            if (v + 1 < NVEC) pp[(v + 1) * (D / 4) + c] = red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
+        }
+    }
+}
+
+// chunk sums of layernorm_bwd_conv_kernel's partials in chunk order: vector 0 -> dgamma, 1 -> dbeta,
+// 2 -> dbias (may be null), 3 + k -> dW row k (w_out + k * D)
+__global__ __launch_bounds__(256) void chunk_reduce_conv(const float* __restrict__ part, int nchunk, int nvec, int D,
+                                                         float* __restrict__ dgam, float* __restrict__ dbet,
+                                                         float* __restrict__ dbias, float* __restrict__ wout,
+                                                         long ostride) {
+    const int b = blockIdx.y, v = blockIdx.z;
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= D) return;
+    float* out = v == 0 ? dgam : v == 1 ? dbet : v == 2 ? dbias : (wout ? wout + (long)(v - 3) * D : nullptr);
+    if (!out) return;
+    const float* q = part + ((long)b * nchunk * nvec + v) * D + c;
+    const long cs = (long)nvec * D;
+    float s = 0.f;
+    int chn = 0;
+    for (; chn + 8 <= nchunk; chn += 8) {
+        float t[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) t[k] = q[(chn + k) * cs];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s += t[k];
+    }
+    for (; chn < nchunk; ++chn) s += q[chn * cs];
+    out[(long)b * ostride + c] = s;
+}
+
 // sum partial slabs [B][nchunk][nvec][D] over chunks in order -> out_v[b*ostride + c]
 // (loads issued 8 chunks at a time, summed in chunk order: the result is that of the serial loop)
 __global__ __launch_bounds__(256) void chunk_reduce(const float* __restrict__ part, int nchunk, int nvec, int D,
@@ -1389,6 +1519,40 @@ void launch_layernorm_bwd(const float* dy, const float* xhat, const float* rstd,
     if (pp)
         hipLaunchKernelGGL(chunk_reduce, dim3(cdiv(D, 256), B), dim3(256), 0, st, pp, nchunk, 2, D, dgamma, dbeta,
                            gstride);
+}
+
+long layernorm_bwd_conv_part_floats(int B, int rows_per_utt, int D, int ktaps) {
+    const int crows = rows_per_utt >= 4096 ? 128 : 16;
+    return (long)B * cdiv(rows_per_utt, crows) * (3 + ktaps) * D;
+}
+
+bool launch_layernorm_bwd_conv(const float* dy, const float* rstd, const float* g, const float* beta, long pstride,
+                               int rows_per_utt, int B, int D, float* dx, float* dgamma, float* dbeta, float* dbias,
+                               float* dw, long gstride, float* part, hipStream_t st, const float* x, const float* mean,
+                               const float* xw, long xws, int xs, int ktaps) {
+    auto a16 = [](const void* q) { return q == nullptr || (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+    if (D != 512 || !(ktaps == 0 || ktaps == 10) || (ktaps && !xw) || !x || !mean || !dgamma || !dbeta ||
+        !(a16(dy) && a16(x) && a16(dx) && a16(part)))
+        return false;
+    const int crows = rows_per_utt >= 4096 ? 128 : 16;
+    const int nchunk = cdiv(rows_per_utt, crows);
+    const bool gv = a16(g) && a16(beta) && pstride % 4 == 0;
+    const dim3 grid(nchunk, B);
+#define LBC(GV_, KT_)                                                                                         \
+    hipLaunchKernelGGL((layernorm_bwd_conv_kernel<2, GV_, KT_>), grid, dim3(256), 0, st, dy, rstd, g, beta, pstride, \
+                       rows_per_utt, dx, part, nchunk, crows, x, mean, xw, xws, xs)
+    if (ktaps == 10) {
+        if (gv) LBC(true, 10);
+        else LBC(false, 10);
+    } else {
+        if (gv) LBC(true, 0);
+        else LBC(false, 0);
+    }
+#undef LBC
+    const int nvec = 3 + ktaps;
+    hipLaunchKernelGGL(chunk_reduce_conv, dim3(cdiv(D, 256), B, nvec), dim3(256), 0, st, part, nchunk, nvec, D, dgamma,
+                       dbeta, dbias, dw, gstride);
+    return true;
 }
 
 void launch_colsum(const float* x, int B, int rows, int C, float* out, long ostride, float* part, hipStream_t st) {
