@@ -18,7 +18,7 @@ from suta_amd import synth
 from suta_amd.config import get_config
 from suta_amd.engine import SutaEngine, SutaHParams
 from suta_amd.weights import synth_weights
-from tests.parity import BF16_LOGITS_RTOL_BASE, BF16_LOGITS_RTOL_LARGE, assert_bf16_close, assert_params_close
+from tests.parity import BF16_LOGITS_RTOL_BASE, BF16_LOGITS_RTOL_LARGE, assert_bf16_close, assert_params_close, logits_tol
 
 pytestmark = pytest.mark.gpu
 
@@ -268,3 +268,34 @@ def test_flash_bwd_plane_kernel_equals_row_kernel(monkeypatch, preset):
         for r in (1, 3):
             assert_bf16_close(out["1"][r][u], out["0"][r][u], 0.97, f"plane bwd step {r} utt {u}",
                               rtol=BF16_LOGITS_RTOL_LARGE)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_fused_conv_layernorm_backward_equals_separate_passes(monkeypatch, precision):
+    """wav2vec2-large's layer-norm conv stack: the LayerNorm backward that also sums the conv bias gradients
+    and conv0's weight gradient (default) against the separate column-sum passes and the conv0 weight-gradient
+    GEMM (SUTA_FUSED_CONV_LN=0).  The same sums in another fixed order (fp32; the GEMM rounded its operands to
+    bf16 in bf16 mode, the fused sum does not): fp32 logits within logits_tol, adapted conv tensors by the
+    Adam budget; bf16 to the bf16 tolerance.  Ragged pair (padding rows carry zero gradient)."""
+    cfg = get_config("wav2vec2-large")
+    eng = SutaEngine(cfg, synth_weights(cfg), max_batch=2, max_samples=48000)
+    eng.set_precision(precision)
+    waves = [synth.wave(48000, 90), synth.wave(30400, 91)]
+    names = [n for n in eng.trainable_names() if "feature_extractor" in n]
+    out, par = {}, {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("SUTA_FUSED_CONV_LN", fused)
+        eng.set_graphs(False)
+        out[fused], _, _ = eng.adapt_varlen(waves, 3, SutaHParams(), record=[1, 3])
+        par[fused] = [{n: eng.get_param(b, n) for n in names} for b in range(2)]
+    eng.close()
+    for u in range(2):
+        for r in (1, 3):
+            if precision == "fp32":
+                np.testing.assert_allclose(out["1"][r][u], out["0"][r][u], rtol=0, atol=logits_tol(2e-5),
+                                           err_msg=f"step {r} utt {u}")
+            else:
+                assert_bf16_close(out["1"][r][u], out["0"][r][u], 0.97, f"step {r} utt {u}", rtol=BF16_LOGITS_RTOL_LARGE)
+        if precision == "fp32":
+            for n in names:
+                assert_params_close(par["1"][u][n], par["0"][u][n], 2e-5, 3, name=f"utt {u} {n}")

@@ -26,9 +26,37 @@ def load(path, counter):
     return per
 
 
+def load_by_grid(path, counter):
+    """GEMM-family dispatches grouped by (kernel template, total grid threads): per-shape traffic."""
+    per = collections.defaultdict(lambda: [0, 0.0])
+    for r in csv.DictReader(open(path)):
+        if r.get("Counter_Name") != counter:
+            continue
+        n = r["Kernel_Name"]
+        if not any(k in n for k in ("gemm_", "flash_", "posconv")):
+            continue
+        base = n.replace("void ", "").replace("(anonymous namespace)::", "")
+        tmpl = base.split("(")[0]
+        key = (tmpl[:90], int(r["Grid_Size"]))
+        per[key][0] += 1
+        per[key][1] += float(r["Counter_Value"])
+    return per
+
+
 def main():
     fetch = load(sys.argv[1], "FETCH_SIZE")
     write = load(sys.argv[2], "WRITE_SIZE")
+    if "--by-grid" in sys.argv:
+        fg, wg = load_by_grid(sys.argv[1], "FETCH_SIZE"), load_by_grid(sys.argv[2], "WRITE_SIZE")
+        rows = []
+        for k in set(fg) | set(wg):
+            n = max(fg[k][0], wg[k][0])
+            rd = 2.0 * fg[k][1] * 1024 / max(1, fg[k][0])
+            wr = wg[k][1] * 1024 / max(1, wg[k][0])
+            rows.append((n * (rd + wr), k, n, rd, wr))
+        for tot, k, n, rd, wr in sorted(rows, reverse=True)[:40]:
+            print(f"{tot/1e9:9.2f} GB total  {n:5d} x  read {rd/1e6:9.2f} MB  write {wr/1e6:9.2f} MB  grid {k[1]:9d}  {k[0]}")
+        return
     out = {}
     for k in sorted(set(fetch) | set(write)):
         n = max(fetch[k][0], write[k][0])
