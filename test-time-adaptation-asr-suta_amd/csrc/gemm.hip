@@ -247,7 +247,12 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
     dim3 grid(gx, gy, p.Z * splits);
     if (hb) {
         census(tile == 6 ? "hb8" : "hb", BM, BN, p, splits);
-        gemm_run_hb(tile, g_force_tile >= 0 ? g_nbuf : 2, p, grid, st);
+        static int hbns = -1;  // SUTA_HB_NS: stage variant of the 128 x 128 bf16-plane kernel (A/B runs; 2 default)
+        if (hbns < 0) {
+            const char* ev = std::getenv("SUTA_HB_NS");
+            hbns = ev ? std::max(2, atoi(ev)) : 2;
+        }
+        gemm_run_hb(tile, g_force_tile >= 0 ? g_nbuf : (tile == 0 ? hbns : 2), p, grid, st);
     } else if (p.mode == 2) {
         // bf16: register-staged one-plane kernel; weight gradients (and benchmark variants 3 / 8) on
         // register-converted LDS-DMA stages (8 = BK64 x 2)

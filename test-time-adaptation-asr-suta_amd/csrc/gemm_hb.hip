@@ -19,6 +19,11 @@ void gemm_run_hb(int tile, int ns, const GemmParams& p, dim3 grid, hipStream_t s
         return;
     }
 
+    if (ns == 5 || ns == 6) {  // 32-deep bf16 K-steps: 4 (ns 5) or 3 (ns 6) LDS stages of 16 KB at 128 x 128
+        if (ns == 5) launch_hb<128, 128, 4, 16>(p, grid, st);
+        else launch_hb<128, 128, 3, 16>(p, grid, st);
+        return;
+    }
     if (ns == 4) {
         if (tile == 0) launch_hb<128, 128, 2, 64>(p, grid, st);
         else if (tile == 1) launch_hb<128, 64, 2, 64>(p, grid, st);

@@ -44,7 +44,7 @@ int main(int argc, char** argv) {
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     // (tile, ns, pf) -- gemm_run_hb (6: 256x256 ping-pong; pf: SUTA_HB8_PF, fragments read one phase ahead)
-    const int variants[][3] = {{0, 2, 0}, {6, 2, 0}, {6, 2, 1}, {0, 2, 0}, {6, 2, 0}, {6, 2, 1}};
+    const int variants[][3] = {{0, 2, 0}, {0, 5, 0}, {0, 6, 0}, {6, 2, 0}, {0, 2, 0}, {0, 5, 0}, {0, 6, 0}, {6, 2, 0}};
     __bf16* Cb;
     CK(hipMalloc(&Cb, (size_t)M * 4096 * 2));
     for (auto& s : shapes) {
