@@ -1341,8 +1341,16 @@ bool launch_flash_fwd(const float* qkv, float* ctx, float* lse, int B, int T, in
     const dim3 grid((unsigned)((long)B * NH * nqb));
     if (bf16 && qkvb && H % 8 == 0 && ff_plane()) {
         if (reinterpret_cast<uintptr_t>(qkvb) & 15) throw std::invalid_argument("flash_fwd: bf16 qkv plane not 16-B aligned");
-        hipLaunchKernelGGL(flash_fwd_bf16p_kernel<FF_NW>, grid, dim3(FF_NW * 64), 0, st,
-                           reinterpret_cast<const __bf16*>(qkvb), ctx, lse, T, NH, H, scale, tlen, nqb, ctxb);
+        // SUTA_FLASH_FWD_NW=8: 8-wave blocks (256 queries share each K / V tile copy); read at every launch
+        const char* ev = std::getenv("SUTA_FLASH_FWD_NW");
+        if (ev && atoi(ev) == 8) {
+            const int nqb8 = (ng + 7) / 8;
+            hipLaunchKernelGGL(flash_fwd_bf16p_kernel<8>, dim3((unsigned)((long)B * NH * nqb8)), dim3(512), 0, st,
+                               reinterpret_cast<const __bf16*>(qkvb), ctx, lse, T, NH, H, scale, tlen, nqb8, ctxb);
+        } else {
+            hipLaunchKernelGGL(flash_fwd_bf16p_kernel<FF_NW>, grid, dim3(FF_NW * 64), 0, st,
+                               reinterpret_cast<const __bf16*>(qkvb), ctx, lse, T, NH, H, scale, tlen, nqb, ctxb);
+        }
     } else if (bf16 && fb_img()) {
         static_assert(FF_NW_BF == FF_NW, "the bf16 forward shares the query-block grid");
         hipLaunchKernelGGL(flash_fwd_bf16_kernel, grid, dim3(FF_NW_BF * 64), 0, st, qkv, ctx, lse, T, NH, H, scale,

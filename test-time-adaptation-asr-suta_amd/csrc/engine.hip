@@ -330,6 +330,35 @@ struct suta_engine {
         if (planebuf.alloc(3 * half)) drop_graph();
         return reinterpret_cast<char*>(planebuf.p) + i * half;
     }
+    // layer-mode conv stack on bf16 planes (bf16 mode): the conv LayerNorm forwards write bf16 activation planes
+    // (ping-pong) that the next conv GEMM reads as its A operand, and the per-slot conv weights are re-laid
+    // [C_out][tap * C_in] in bf16 (the B operand) at the start of every forward; SUTA_CONV_PLANES=0 keeps the
+    // fp32-staged one-plane kernels
+    DevBuf convact, convwt;
+    bool conv_planes() const {
+        if (!use_planes() || !c.layer_mode) return false;
+        const char* e = std::getenv("SUTA_CONV_PLANES");
+        if (e && atoi(e) == 0) return false;
+        for (int i = 0; i < c.nconv; ++i)
+            if (c.C[i] != 512 || (i > 0 && ((long)c.K[i] * c.C[i - 1] % 8 || (long)c.S[i] * c.C[i - 1] % 8))) return false;
+        return true;
+    }
+    void* conv_act_plane(int i) {  // ping-pong: plane i & 1
+        size_t half = 0;
+        for (int j = 0; j + 1 < c.nconv; ++j) half = std::max(half, (size_t)rup((long)plan.B * plan.Lc[j] * c.C[j] * 2, 256));
+        if (convact.alloc(2 * half)) drop_graph();
+        return reinterpret_cast<char*>(convact.p) + (i & 1) * half;
+    }
+    void* conv_wt_plane(int i) {  // layer i >= 1: [B][C_i][K_i * C_{i-1}] bf16
+        size_t off = 0, tot = 0;
+        for (int j = 1; j < c.nconv; ++j) {
+            const size_t n = rup((long)plan.B * c.C[j] * c.K[j] * c.C[j - 1] * 2, 256);
+            if (j < i) off += n;
+            tot += n;
+        }
+        if (convwt.alloc(tot)) drop_graph();
+        return reinterpret_cast<char*>(convwt.p) + off;
+    }
     // bf16 plane of layer l's qkv [B*T][3H]: written by the QKV GEMM, read by the flash forward and, in the
     // backward, by the flash backward (kept for every layer, like the fp32 qkv)
     DevBuf qkvplanes;
@@ -344,6 +373,10 @@ struct suta_engine {
         GemmParams p = p0;
         p.mode = gemm_mode;
         const double ab = timing ? gemm_alg_bytes(p) : 0.0;
+        if (gemm_mode == SUTA_PRECISION_BF16 && p.Ab && p.Bb) {  // both planes given by the caller (conv stack)
+            timed(F_GEMM, [&] { gemm_launch(p, st, plan.splitws, plan.splitws_floats); }, ab);
+            return;
+        }
         if (gemm_mode == SUTA_PRECISION_BF16 && p.segK == 0 && !p.ta && p.Z == 1 && p.K % 8 == 0 && p.lda % 4 == 0 &&
             (reinterpret_cast<uintptr_t>(p.A) & 15) == 0) {
             auto it = wplanes.find(p.B);
@@ -567,9 +600,13 @@ void suta_engine::forward(int B) {
             launch_conv0(pl.x, pl.N, P + o_cw[0], k.conv_bias ? P + o_cb[0] : nullptr, Pn, pl.z[0], B, pl.Lc[0],
                          k.C[0], k.K[0], k.S[0], st);
         }, 4.0 * B * ((double)pl.N + (double)pl.Lc[0] * k.C[0]));
+    }
+    const bool cpl = conv_planes();
+    if (k.layer_mode) {
         timed(F_NORM, [&] {
             launch_layernorm_fwd(pl.z[0], P + o_cg[0], P + o_cbeta[0], Pn, pl.Lc[0], pl.a[0], pl.cxhat[0],
-                                 pl.crstd[0], B * pl.Lc[0], k.C[0], 1e-5f, 1, st, nullptr, pl.cmean[0]);
+                                 pl.crstd[0], B * pl.Lc[0], k.C[0], 1e-5f, 1, st, cpl ? conv_act_plane(0) : nullptr,
+                                 pl.cmean[0]);
         });
     }
     for (int i = 1; i < k.nconv; ++i) {
@@ -586,6 +623,16 @@ void suta_engine::forward(int B) {
         g.sA1 = (long)pl.Lc[i - 1] * k.C[i - 1];
         g.sB1 = Pn;
         g.sC1 = (long)pl.Lc[i] * k.C[i];
+        if (cpl) {  // bf16 planes: activations written by the previous LayerNorm, weights re-laid per slot
+            void* wt = conv_wt_plane(i);
+            timed(F_EW, [&] { launch_transpose_bf16(P + o_cw[i], Pn, B, g.K, g.N, wt, st); });
+            g.Ab = conv_act_plane(i - 1);
+            g.ldab = g.lda;
+            g.Bb = wt;
+            g.ldbb = g.K;
+            g.sB1 = (long)g.N * g.K;
+            // (g.sA1: the same element stride in the bf16 plane)
+        }
         if (k.conv_bias) {
             g.epi |= EPI_BIAS;
             g.bias = P + o_cb[i];
@@ -605,7 +652,8 @@ void suta_engine::forward(int B) {
             gemm(g);
             timed(F_NORM, [&] {
                 launch_layernorm_fwd(pl.z[i], P + o_cg[i], P + o_cbeta[i], Pn, pl.Lc[i], pl.a[i], pl.cxhat[i],
-                                     pl.crstd[i], B * pl.Lc[i], k.C[i], 1e-5f, 1, st, nullptr, pl.cmean[i]);
+                                     pl.crstd[i], B * pl.Lc[i], k.C[i], 1e-5f, 1, st,
+                                     (cpl && i + 1 < k.nconv) ? conv_act_plane(i) : nullptr, pl.cmean[i]);
             });
         }
     }

@@ -120,7 +120,7 @@ static int choose_tile_bf16(long M, long N, long Z, bool big) {
 
 // bf16-plane GEMMs (tools/hb_bench, C4 linears at M = 25536): 128x128 with two LDS stages wins every
 // shape (460-660 TF vs 370-570 for 256x128 at one block per CU); smaller tiles only for small grids.
-static int choose_tile_hb(long M, long N) {
+static int choose_tile_hb(long M, long N, long Z) {
     struct Cand {
         int id, bm, bn;
         double eff;
@@ -129,7 +129,7 @@ static int choose_tile_hb(long M, long N) {
     int best = 0;
     double bt = 1e300;
     for (int i = 0; i < 4; ++i) {
-        const long tiles = ((M + c[i].bm - 1) / c[i].bm) * ((N + c[i].bn - 1) / c[i].bn);
+        const long tiles = ((M + c[i].bm - 1) / c[i].bm) * ((N + c[i].bn - 1) / c[i].bn) * Z;
         const double t = (double)((tiles + 511) / 512) * c[i].bm * c[i].bn / c[i].eff;
         if (t < bt * 0.999) {
             bt = t;
@@ -166,7 +166,7 @@ static bool use_tile160(long M, long N, long Z) {
 static int use_hb8(const GemmParams& p) {
     const char* e = std::getenv("SUTA_HB8");
     const int mode = e ? atoi(e) : 0;
-    if (p.K % 32 != 0 || mode == 0) return 0;
+    if (p.K % 32 != 0 || mode == 0 || p.Z != 1) return 0;
     if (mode == 2) return 1;
     if (mode == 3 && ((p.epi & (EPI_GELU | EPI_RESID | EPI_STORE_PRE | EPI_DGELU | EPI_ACCUM | EPI_SMBWD)) || p.Cb))
         return 0;
@@ -189,11 +189,12 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
     const bool hb = p.mode == 2 && p.Ab && p.Bb;  // bf16 operand planes (gemm_hb_kernel)
     if (p.Cb && (!hb || p.Z != 1 || (reinterpret_cast<uintptr_t>(p.Cb) & 7)))
         throw std::invalid_argument("gemm: a bf16 output plane needs the bf16-plane kernel, Z == 1, 8-B alignment");
-    if (hb && (p.Z != 1 || p.K % 8 || p.ldab % 8 || p.ldbb % 8 || !aligned16(p.Ab) || !aligned16(p.Bb)))
-        throw std::invalid_argument("gemm: bf16 planes need Z == 1, K, ld % 8 == 0 and 16-B alignment");
+    if (hb && (p.K % 8 || p.ldab % 8 || p.ldbb % 8 || !aligned16(p.Ab) || !aligned16(p.Bb) ||
+               (p.Z > 1 && ((p.sA0 | p.sA1 | p.sB0 | p.sB1) % 8))))
+        throw std::invalid_argument("gemm: bf16 planes need K, ld and batch strides % 8 == 0 and 16-B alignment");
     const bool bf16_gbf = p.mode == 2 && glds_ok && p.ta;  // bf16 weight gradients: LDS-DMA fp32 stages
     int tile = g_force_tile >= 0 ? g_force_tile
-               : hb            ? (use_hb8(p) ? 6 : choose_tile_hb(p.M, p.N))
+               : hb            ? (use_hb8(p) ? 6 : choose_tile_hb(p.M, p.N, p.Z))
                : p.mode == 2   ? choose_tile_bf16(p.M, p.N, p.Z, !bf16_gbf)
                                : choose_tile(p.M, p.N, p.Z, p.K, p.mode);
     const bool glds_path = p.mode == 0 && g_nbuf == 3 && glds_ok;

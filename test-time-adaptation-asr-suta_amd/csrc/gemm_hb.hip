@@ -71,3 +71,29 @@ void launch_to_bf16(const float* src, long lds, long rows, int K, void* dst, hip
     hipLaunchKernelGGL(to_bf16_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, src, lds, rows, K,
                        reinterpret_cast<bf16x8*>(dst));
 }
+
+// Per-slot transposed bf16 copy of a trainable [K][N] fp32 matrix (conv weights [tap][C_in][C_out] of every
+// utterance slot): dst[z][n][k] = bf16(src[z * zs + k * N + n]), 64 x 64 tiles through LDS (coalesced both
+// ways).  The B operand of the bf16-plane conv GEMMs ([N][K], k-contiguous), rebuilt after every AdamW step.
+__global__ __launch_bounds__(256) void transpose_bf16_kernel(const float* __restrict__ src, long zs, int K, int N,
+                                                             __bf16* __restrict__ dst) {
+    __shared__ float t[64][65];
+    const int z = blockIdx.z, k0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
+    const float* s = src + (long)z * zs;
+    __bf16* d = dst + (long)z * N * K;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int r = ty; r < 64; r += 4) {
+        const int k = k0 + r, n = n0 + tx;
+        t[r][tx] = (k < K && n < N) ? s[(long)k * N + n] : 0.f;
+    }
+    __syncthreads();
+    for (int r = ty; r < 64; r += 4) {
+        const int n = n0 + r, k = k0 + tx;
+        if (n < N && k < K) d[(long)n * K + k] = (__bf16)t[tx][r];
+    }
+}
+
+void launch_transpose_bf16(const float* src, long zs, int Z, int K, int N, void* dst, hipStream_t st) {
+    hipLaunchKernelGGL(transpose_bf16_kernel, dim3((N + 63) / 64, (K + 63) / 64, Z), dim3(256), 0, st, src, zs, K, N,
+                       reinterpret_cast<__bf16*>(dst));
+}

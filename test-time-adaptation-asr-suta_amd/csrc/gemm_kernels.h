@@ -1488,9 +1488,12 @@ __global__ __launch_bounds__(64 * NWV, (BM * BN > 128 * 128 || BKS > 32) ? 1 : 2
     __shared__ __attribute__((aligned(16))) float smem[NS * STAGE];
 
     const TileId tid = xcd_tile(p.order);
-    const int split = p.splits > 1 ? tid.z : 0;
-    const float* A = reinterpret_cast<const float*>(p.Ab);
-    const float* B = reinterpret_cast<const float*>(p.Bb);
+    // grid z = batch x split (Z-batched planes: batch strides in bf16 elements, even)
+    const int split = p.splits > 1 ? tid.z % p.splits : 0;
+    const int zz = p.splits > 1 ? tid.z / p.splits : tid.z;
+    const int z1 = zz / p.zdiv, z0 = zz % p.zdiv;
+    const float* A = reinterpret_cast<const float*>(p.Ab) + (z1 * p.sA1 + z0 * p.sA0) / 2;
+    const float* B = reinterpret_cast<const float*>(p.Bb) + (z1 * p.sB1 + z0 * p.sB0) / 2;
     const long lda = p.ldab / 2, ldb = p.ldbb / 2;  // in 4-byte units
     const int m0 = tid.y * BM;
     const int n0 = tid.x * BN;
@@ -1565,10 +1568,10 @@ __global__ __launch_bounds__(64 * NWV, (BM * BN > 128 * 128 || BKS > 32) ? 1 : 2
     wait_vm<0>();
     // only the bf16-plane GEMMs write a bf16 copy of C (the template keeps the other kernels' epilogue as it was)
     if (p.Cb)
-        gemm_epilogue<RM, RN, true>(p, acc, 0, 0, m0 + wm * WTM, n0 + wn * WTN, h, l32,
+        gemm_epilogue<RM, RN, true>(p, acc, z1, z0, m0 + wm * WTM, n0 + wn * WTN, h, l32,
                                     m0 + BM <= p.M && n0 + BN <= p.N, tid.z);
     else
-        gemm_epilogue<RM, RN, false>(p, acc, 0, 0, m0 + wm * WTM, n0 + wn * WTN, h, l32,
+        gemm_epilogue<RM, RN, false>(p, acc, z1, z0, m0 + wm * WTM, n0 + wn * WTN, h, l32,
                                      m0 + BM <= p.M && n0 + BN <= p.N, tid.z);
 }
 

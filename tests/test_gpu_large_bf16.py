@@ -299,3 +299,27 @@ def test_fused_conv_layernorm_backward_equals_separate_passes(monkeypatch, preci
         if precision == "fp32":
             for n in names:
                 assert_params_close(par["1"][u][n], par["0"][u][n], 2e-5, 3, name=f"utt {u} {n}")
+
+
+def test_conv_stack_on_bf16_planes_equals_fp32_staged(monkeypatch):
+    """wav2vec2-large's conv stack in bf16 mode: the forward conv GEMMs on bf16 planes (activation planes written
+    by the conv LayerNorms, per-slot transposed bf16 weights rebuilt after each AdamW step; default) against the
+    fp32-staged one-plane kernels (SUTA_CONV_PLANES=0).  The same RNE-rounded operands, another accumulation
+    order: adapted logits agree to the bf16 tolerance; reruns bitwise identical.  Ragged pair."""
+    cfg = get_config("wav2vec2-large")
+    eng = SutaEngine(cfg, synth_weights(cfg), max_batch=2, max_samples=48000)
+    eng.set_precision("bf16")
+    waves = [synth.wave(48000, 92), synth.wave(30400, 93)]
+    out = {}
+    for cp in ("1", "0"):
+        monkeypatch.setenv("SUTA_CONV_PLANES", cp)
+        a, _, _ = eng.adapt_varlen(waves, 3, SutaHParams(), record=[0, 3])
+        b, _, _ = eng.adapt_varlen(waves, 3, SutaHParams(), record=[0, 3])
+        for u in range(2):
+            assert np.array_equal(a[3][u], b[3][u]), (cp, u)
+        out[cp] = a
+    eng.close()
+    for r in (0, 3):
+        for u in range(2):
+            assert_bf16_close(out["1"][r][u], out["0"][r][u], 0.97, f"conv planes step {r} utt {u}",
+                              rtol=BF16_LOGITS_RTOL_LARGE)

@@ -23,7 +23,7 @@ def main():
     for n, t, gx, gy, gz, v in rows(sys.argv[1]):
         base = n.replace('void ', '').replace('(anonymous namespace)::', '')
         fam[base.split('(')[0].split('<')[0]] += t
-        if 'gemm_f32_kernel' in n or 'gemm_x6_kernel' in n or 'gemm_glds_kernel' in n:
+        if any(q in n for q in ('gemm_f32_kernel', 'gemm_x6_kernel', 'gemm_glds_kernel', 'gemm_hb_kernel', 'gemm_gbf_kernel', 'gemm_hb8_kernel')):
             tmpl = base.split("<")[0][5:9] + ":" + n[n.find('<') + 1:n.find('>')]
             k = (tmpl, gx // 256, gy, gz)
             g[k][0] += 1
