@@ -29,6 +29,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <stdexcept>
+#include <type_traits>
 
 #include "common.h"
 #include "ops.h"
@@ -252,13 +253,17 @@ __global__ __launch_bounds__(NW * 64) void flash_fwd_kernel(const float* __restr
     fetch(0);
     put(0);
     __syncthreads();
-    for (int kt = 0; kt < nkt; ++kt) {
+    // full tiles (every key valid, both 32-key halves) run a body without masks or branches; the utterance's
+    // last tile, with the masks and the skipped empty half, is peeled (same arithmetic per element: bitwise the
+    // single-body loop)
+    auto tile = [&](int kt, auto last_tag) {
+        constexpr bool LAST = decltype(last_tag)::value;
         const int buf = kt & 1;
-        if (kt + 1 < nkt) fetch(kt + 1);
+        if (!LAST) fetch(kt + 1);
         if (active) {
             // the second 32-key half of a tile holding no valid key (the tail of the last tile) is skipped:
             // its probabilities are exactly 0
-            const bool two = kt * FK + 32 < tl;
+            const bool two = !LAST || kt * FK + 32 < tl;
             f32x16 s[2];
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
@@ -271,7 +276,7 @@ __global__ __launch_bounds__(NW * 64) void flash_fwd_kernel(const float* __restr
             for (int j = 0; j < 2; ++j)
 #pragma unroll
                 for (int v = 0; v < 16; ++v) {
-                    const bool ok = kt * FK + 32 * j + r8(v, h) < tl;
+                    const bool ok = !LAST || kt * FK + 32 * j + r8(v, h) < tl;
                     s[j][v] = ok ? sl2 * s[j][v] : -INFINITY;
                     mx = fmaxf(mx, s[j][v]);
                 }
@@ -298,9 +303,11 @@ __global__ __launch_bounds__(NW * 64) void flash_fwd_kernel(const float* __restr
             apply_cols<BF16, FK_LDT>(o, Vt[buf], s[0], l32, h);  // O^T[n][q] += sum_key V[key][n] P[q][key]
             if (two) apply_cols<BF16, FK_LDT>(o, Vt[buf] + 32, s[1], l32, h);
         }
-        if (kt + 1 < nkt) put(buf ^ 1);
+        if (!LAST) put(buf ^ 1);
         __syncthreads();
-    }
+    };
+    for (int kt = 0; kt + 1 < nkt; ++kt) tile(kt, std::false_type{});
+    tile(nkt - 1, std::true_type{});
     if (!active) return;
     const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
     const int q = q0 + l32;
@@ -823,20 +830,27 @@ __global__ __launch_bounds__(NW * 64) void flash_fwd_bf16p_kernel(
     fetch(0);
     put(0);
     __syncthreads();
-    for (int kt = 0; kt < nkt; ++kt) {
+    // full tiles run a body without masks; the utterance's last tile (masks, the empty second half skipped) is
+    // peeled, so neither costs the full tiles a branch-merged register copy
+    auto tile = [&](int kt, auto last_tag) {
+        constexpr bool LAST = decltype(last_tag)::value;
         const int buf = kt & 1;
-        if (kt + 1 < nkt) fetch(kt + 1);
+        if (!LAST) fetch(kt + 1);
         if (active) {
-            // both 32-key halves always (a skipped half on the last tile would cost branch-merged register
-            // copies on every tile); keys past the length are masked on the last tile only
+            const bool two = !LAST || kt * FK + 32 < tl;
             f32x16 s[2];
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
 #pragma unroll
-                for (int v = 0; v < 16; ++v) s[j][v] = 0.f;
-                prod_rows_b(s[j], Ks[buf] + 32 * j * FP_KS, qv, l32, h);
+                for (int v = 0; v < 16; ++v) s[j][v] = LAST ? -INFINITY : 0.f;
+                if (j == 0 || two) {
+                    if (LAST)
+#pragma unroll
+                        for (int v = 0; v < 16; ++v) s[j][v] = 0.f;
+                    prod_rows_b(s[j], Ks[buf] + 32 * j * FP_KS, qv, l32, h);
+                }
             }
-            if (kt * FK + FK > tl) {  // the utterance's last tile: keys >= tl get probability 0
+            if (LAST) {  // keys >= tl get probability 0
 #pragma unroll
                 for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -846,8 +860,9 @@ __global__ __launch_bounds__(NW * 64) void flash_fwd_bf16p_kernel(
             float mx = s[0][0];
 #pragma unroll
             for (int v = 1; v < 16; ++v) mx = fmaxf(mx, s[0][v]);
+            if (two)
 #pragma unroll
-            for (int v = 0; v < 16; ++v) mx = fmaxf(mx, s[1][v]);
+                for (int v = 0; v < 16; ++v) mx = fmaxf(mx, s[1][v]);
             mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
             const float m_new = fmaxf(m_run, sl2 * mx);
             float ls = 0.f;
@@ -871,13 +886,16 @@ __global__ __launch_bounds__(NW * 64) void flash_fwd_bf16p_kernel(
             }
             l_run += ls;
 #pragma unroll
-            for (int j = 0; j < 2; ++j)
+            for (int c = 0; c < 2; ++c) pv_tr(o, Vs[buf], 16 * c, pb[0][c], lane);
+            if (two)
 #pragma unroll
-                for (int c = 0; c < 2; ++c) pv_tr(o, Vs[buf], 32 * j + 16 * c, pb[j][c], lane);
+                for (int c = 0; c < 2; ++c) pv_tr(o, Vs[buf], 32 + 16 * c, pb[1][c], lane);
         }
-        if (kt + 1 < nkt) put(buf ^ 1);
+        if (!LAST) put(buf ^ 1);
         __syncthreads();
-    }
+    };
+    for (int kt = 0; kt + 1 < nkt; ++kt) tile(kt, std::false_type{});
+    tile(nkt - 1, std::true_type{});
     if (!active) return;
     const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
     const int q = q0 + l32;

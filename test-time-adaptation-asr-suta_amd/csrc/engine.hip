@@ -343,11 +343,22 @@ struct suta_engine {
             if (c.C[i] != 512 || (i > 0 && ((long)c.K[i] * c.C[i - 1] % 8 || (long)c.S[i] * c.C[i - 1] % 8))) return false;
         return true;
     }
-    void* conv_act_plane(int i) {  // ping-pong: plane i & 1
-        size_t half = 0;
-        for (int j = 0; j + 1 < c.nconv; ++j) half = std::max(half, (size_t)rup((long)plan.B * plan.Lc[j] * c.C[j] * 2, 256));
-        if (convact.alloc(2 * half)) drop_graph();
-        return reinterpret_cast<char*>(convact.p) + (i & 1) * half;
+    void* conv_act_plane(int i) {  // layer i < nconv - 1: [B][L_i][C_i] bf16, kept for the weight gradients
+        size_t off = 0, tot = 0;
+        for (int j = 0; j + 1 < c.nconv; ++j) {
+            const size_t n = rup((long)plan.B * plan.Lc[j] * c.C[j] * 2, 256);
+            if (j < i) off += n;
+            tot += n;
+        }
+        if (convact.alloc(tot)) drop_graph();
+        return reinterpret_cast<char*>(convact.p) + off;
+    }
+    DevBuf convdz;
+    void* conv_dz_plane() {  // bf16 plane of the current conv layer's dz (the weight gradient's B operand)
+        size_t n = 0;
+        for (int j = 1; j < c.nconv; ++j) n = std::max(n, (size_t)rup((long)plan.B * plan.Lc[j] * c.C[j] * 2, 256));
+        if (convdz.alloc(n)) drop_graph();
+        return convdz.p;
     }
     void* conv_wt_plane(int i) {  // layer i >= 1: [B][C_i][K_i * C_{i-1}] bf16
         size_t off = 0, tot = 0;
@@ -604,9 +615,10 @@ void suta_engine::forward(int B) {
     const bool cpl = conv_planes();
     if (k.layer_mode) {
         timed(F_NORM, [&] {
-            launch_layernorm_fwd(pl.z[0], P + o_cg[0], P + o_cbeta[0], Pn, pl.Lc[0], pl.a[0], pl.cxhat[0],
-                                 pl.crstd[0], B * pl.Lc[0], k.C[0], 1e-5f, 1, st, cpl ? conv_act_plane(0) : nullptr,
-                                 pl.cmean[0]);
+            // with conv planes only the bf16 activation is read (the next conv GEMM and its weight gradient)
+            launch_layernorm_fwd(pl.z[0], P + o_cg[0], P + o_cbeta[0], Pn, pl.Lc[0], cpl ? nullptr : pl.a[0],
+                                 pl.cxhat[0], pl.crstd[0], B * pl.Lc[0], k.C[0], 1e-5f, 1, st,
+                                 cpl ? conv_act_plane(0) : nullptr, pl.cmean[0]);
         });
     }
     for (int i = 1; i < k.nconv; ++i) {
@@ -651,9 +663,10 @@ void suta_engine::forward(int B) {
             g.ldc = k.C[i];
             gemm(g);
             timed(F_NORM, [&] {
-                launch_layernorm_fwd(pl.z[i], P + o_cg[i], P + o_cbeta[i], Pn, pl.Lc[i], pl.a[i], pl.cxhat[i],
-                                     pl.crstd[i], B * pl.Lc[i], k.C[i], 1e-5f, 1, st,
-                                     (cpl && i + 1 < k.nconv) ? conv_act_plane(i) : nullptr, pl.cmean[i]);
+                const bool pln = cpl && i + 1 < k.nconv;
+                launch_layernorm_fwd(pl.z[i], P + o_cg[i], P + o_cbeta[i], Pn, pl.Lc[i], pln ? nullptr : pl.a[i],
+                                     pl.cxhat[i], pl.crstd[i], B * pl.Lc[i], k.C[i], 1e-5f, 1, st,
+                                     pln ? conv_act_plane(i) : nullptr, pl.cmean[i]);
             });
         }
     }
@@ -1315,14 +1328,16 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
     for (int i = last; i >= 1; --i) {
         // cur: group mode -> dz_i ; layer mode -> da_i
         bool bias_done = false;
+        const bool cpl = conv_planes();
         if (k.layer_mode) {
             timed(F_NORM, [&] {
                 // fused: the LayerNorm backward also sums the conv bias gradient (one read of dz_i)
-                if (!pl.cxhat[i] && fused_conv_ln() &&
+                if (!pl.cxhat[i] && (fused_conv_ln() || cpl) &&
                     layernorm_bwd_conv_part_floats(B, pl.Lc[i], k.C[i], 0) <= pl.lnpart_floats &&
                     launch_layernorm_bwd_conv(cur, pl.crstd[i], P + o_cg[i], P + o_cbeta[i], Pn, pl.Lc[i], B, k.C[i],
                                               other, G + o_cg[i], G + o_cbeta[i], k.conv_bias ? G + o_cb[i] : nullptr,
-                                              nullptr, Pn, pl.lnpart, st, pl.z[i], pl.cmean[i], nullptr, 0, 0, 0)) {
+                                              nullptr, Pn, pl.lnpart, st, pl.z[i], pl.cmean[i], nullptr, 0, 0, 0,
+                                              cpl ? conv_dz_plane() : nullptr)) {
                     bias_done = true;
                 } else {
                     launch_layernorm_bwd(cur, pl.cxhat[i], pl.crstd[i], P + o_cg[i], P + o_cbeta[i], Pn, pl.Lc[i], B,
@@ -1351,6 +1366,15 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
             g.sA1 = (long)pl.Lc[i - 1] * k.C[i - 1];
             g.sB1 = (long)pl.Lc[i] * k.C[i];
             g.sC1 = Pn;
+            if (cpl) {  // bf16 planes: the forward's activation plane and the LayerNorm-written dz plane (the fp32
+                        // activation was not stored)
+                if (!bias_done) throw SutaError(SUTA_ERR_UNSUPPORTED, "conv planes: dz plane not written");
+                g.A = nullptr;
+                g.Ab = conv_act_plane(i - 1);
+                g.ldab = g.lda;
+                g.Bb = conv_dz_plane();
+                g.ldbb = g.ldb;
+            }
             gemm(g);
         }
         {  // da_{i-1} = conv_i^T(dz_i): one GEMM per output-row residue rho (rows S*m + rho), whose K

@@ -186,14 +186,21 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
     p.vb = vec_ok(p.B, p.ldb, p.sB0, p.sB1) && (!p.segB || (p.sBseg % 4 == 0 && p.segK % 4 == 0));
 
     const bool glds_ok = p.va && p.vb && (p.ta || p.K % 4 == 0) && (!p.tb || p.K % 4 == 0);
-    const bool hb = p.mode == 2 && p.Ab && p.Bb;  // bf16 operand planes (gemm_hb_kernel)
+    const bool hbt = p.mode == 2 && p.Ab && p.Bb && p.ta && !p.tb;  // MN-contiguous bf16 planes (gemm_hbt_kernel)
+    const bool hb = p.mode == 2 && p.Ab && p.Bb && !p.ta;            // k-contiguous bf16 planes (gemm_hb_kernel)
+    if (p.mode == 2 && p.Ab && p.Bb && !hb && !hbt)
+        throw std::invalid_argument("gemm: bf16 planes: A and B both k-contiguous ([M][K], [N][K]) or both MN-contiguous");
+    if (hbt && (p.M % 8 || p.N % 8 || p.ldab % 8 || p.ldbb % 8 || !aligned16(p.Ab) || !aligned16(p.Bb) || p.Cb ||
+                ((p.sA0 | p.sA1 | p.sB0 | p.sB1) % 8)))
+        throw std::invalid_argument("gemm: MN-contiguous bf16 planes need M, N, ld, batch strides % 8 == 0, 16-B alignment");
     if (p.Cb && (!hb || p.Z != 1 || (reinterpret_cast<uintptr_t>(p.Cb) & 7)))
         throw std::invalid_argument("gemm: a bf16 output plane needs the bf16-plane kernel, Z == 1, 8-B alignment");
     if (hb && (p.K % 8 || p.ldab % 8 || p.ldbb % 8 || !aligned16(p.Ab) || !aligned16(p.Bb) ||
                (p.Z > 1 && ((p.sA0 | p.sA1 | p.sB0 | p.sB1) % 8))))
         throw std::invalid_argument("gemm: bf16 planes need K, ld and batch strides % 8 == 0 and 16-B alignment");
     const bool bf16_gbf = p.mode == 2 && glds_ok && p.ta;  // bf16 weight gradients: LDS-DMA fp32 stages
-    int tile = g_force_tile >= 0 ? g_force_tile
+    int tile = hbt             ? 0
+               : g_force_tile >= 0 ? g_force_tile
                : hb            ? (use_hb8(p) ? 6 : choose_tile_hb(p.M, p.N, p.Z))
                : p.mode == 2   ? choose_tile_bf16(p.M, p.N, p.Z, !bf16_gbf)
                                : choose_tile(p.M, p.N, p.Z, p.K, p.mode);
@@ -244,9 +251,18 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
         // panels L2-resident (tools/hb_bench, M = 25 536: qkv 543 -> 598 TF, ffn1 525 -> 590, the N = 1024
         // shapes within +-2 %); the fp32 kernels measured neutral and keep the n-fastest order
         if (hb && ord == 0 && splits == 1) p.order = gx >= 16 ? 8 : 4;
+        // fp32 linears with >= 16 column tiles (QKV, FFN1 and their input-gradient GEMMs): their weight panels do
+        // not stay in an XCD's 4 MB L2 across a band of rows in n-fastest order; bands of 8 tile rows walked
+        // column by column halve their HBM reads (FFN1 forward 1.43 -> 0.72 GB per launch, PMC) at equal time
+        // (37.05 vs 37.13 utt/s, within noise); narrow GEMMs (6 column tiles) keep the n-fastest order, which
+        // reads less for them
+        if (!hb && p.mode == 0 && ord == 0 && splits == 1 && p.Z == 1 && gx >= 16) p.order = 8;
     }
     dim3 grid(gx, gy, p.Z * splits);
-    if (hb) {
+    if (hbt) {
+        census("hbt", BM, BN, p, splits);
+        gemm_run_hbt(p, grid, st);
+    } else if (hb) {
         census(tile == 6 ? "hb8" : "hb", BM, BN, p, splits);
         static int hbns = -1;  // SUTA_HB_NS: stage variant of the 128 x 128 bf16-plane kernel (A/B runs; 2 default)
         if (hbns < 0) {

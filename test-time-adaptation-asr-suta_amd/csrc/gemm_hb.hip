@@ -97,3 +97,7 @@ void launch_transpose_bf16(const float* src, long zs, int Z, int K, int N, void*
     hipLaunchKernelGGL(transpose_bf16_kernel, dim3((N + 63) / 64, (K + 63) / 64, Z), dim3(256), 0, st, src, zs, K, N,
                        reinterpret_cast<__bf16*>(dst));
 }
+
+void gemm_run_hbt(const GemmParams& p, dim3 grid, hipStream_t st) {
+    hipLaunchKernelGGL((gemm_hbt_kernel<128, 128>), grid, dim3(256), 0, st, p);
+}

@@ -627,6 +627,7 @@ __global__ __launch_bounds__(256, GEMM_F32_MINB) void gemm_f32_kernel(GemmParams
 // ds_read_b128 fragment reads are conflict-free without padding.
 // ============================================================================================
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 fbf16x4_t __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
@@ -1766,5 +1767,132 @@ inline void launch_hb8(const GemmParams& p, dim3 grid, hipStream_t st, bool pf) 
 void gemm_run_f32(int tile, int nbuf, const GemmParams& p, dim3 grid, hipStream_t st);      // gemm_f32.hip
 void gemm_run_x6(int tile, int bk16, int npl, const GemmParams& p, dim3 grid, hipStream_t st);  // gemm_x6.hip
 void gemm_run_glds(int variant, int tile, const GemmParams& p, dim3 grid, hipStream_t st);  // gemm_glds.hip
+// ============================================================================================
+// bf16 GEMM on MN-contiguous bf16 planes ("hbt"; the conv weight gradients of config C4):
+//   A(m, k) = Ab[k * ldab + m], B(k, n) = Bb[k * ldbb + n]   (both row-major over k: im2col(a)^T and dz)
+// Stages of 64 k-rows of both operands arrive by LDS-DMA as [k][BM] / [k][BN] bf16 images (one 256-B row per k at
+// 128 columns); the MFMA operands (8 consecutive k of one column) come from two ds_read_b64_tr_b16 transposed reads
+// per fragment.  Conflict-free: the 16-B chunk c of image row r sits in slot c ^ 4 (r & 3) (applied to the DMA
+// SOURCE, as the glds swizzle), so the 4 rows x 64 B a 32-lane half reads land in 64 distinct banks.  Two stages,
+// one barrier per stage; the general epilogues (fast 32-bit path on interior tiles).  M % 8 == N % 8 == 0.
+// ============================================================================================
+template <int BM, int BN>
+__global__ __launch_bounds__(256, 2) void gemm_hbt_kernel(GemmParams p) {
+    constexpr int BKR = 64;                    // k rows per stage
+    constexpr int ASZ = BKR * BM * 2, BSZ = BKR * BN * 2;  // bytes per stage
+    constexpr int STAGE = ASZ + BSZ;
+    constexpr int APC = ASZ / 1024 / 4, BPC = BSZ / 1024 / 4;  // 1-KiB DMA pieces per wave per stage
+    constexpr int ACPR = BM / 8, BCPR = BN / 8;  // 16-B chunks per image row
+    constexpr int WTM = BM / 2, WTN = BN / 2, RM = WTM / 32, RN = WTN / 32;
+    static_assert(ACPR == 16 && BCPR == 16, "hbt: 128-column images (the swizzle assumes 16 chunks per row)");
+    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+
+    const TileId tid = xcd_tile(p.order);
+    const int split = p.splits > 1 ? tid.z % p.splits : 0;
+    const int zz = p.splits > 1 ? tid.z / p.splits : tid.z;
+    const int z1 = zz / p.zdiv, z0 = zz % p.zdiv;
+    const __bf16* A = reinterpret_cast<const __bf16*>(p.Ab) + z1 * p.sA1 + z0 * p.sA0;
+    const __bf16* B = reinterpret_cast<const __bf16*>(p.Bb) + z1 * p.sB1 + z0 * p.sB0;
+    const int m0 = tid.y * BM, n0 = tid.x * BN;
+    const int kbeg = split * p.kchunk, kend = min(p.K, kbeg + p.kchunk);
+    const int nst = (kend - kbeg + BKR - 1) / BKR;
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wid >> 1, wn = wid & 1;
+    const int h = lane >> 5, l32 = lane & 31;
+
+    f32x16 acc[RM][RN];
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    // DMA sources: piece c (wave-uniform) covers image rows 4c .. 4c + 3; lane j: row 4c + j / 16, slot j % 16
+    // holding global chunk (j % 16) ^ 4 (row & 3)
+    const __bf16* asrc[APC];
+    const __bf16* bsrc[BPC];
+    int arow[APC], brow[BPC];
+    bool aok[APC], bok[BPC];
+#pragma unroll
+    for (int i = 0; i < APC; ++i) {
+        const int c = i * 4 + wid, r = 4 * c + lane / 16, gc = (lane % 16) ^ (4 * (r & 3));
+        arow[i] = r;
+        aok[i] = m0 + 8 * gc < p.M;
+        asrc[i] = A + (long)(kbeg + r) * p.ldab + m0 + 8 * gc;
+    }
+#pragma unroll
+    for (int i = 0; i < BPC; ++i) {
+        const int c = i * 4 + wid, r = 4 * c + lane / 16, gc = (lane % 16) ^ (4 * (r & 3));
+        brow[i] = r;
+        bok[i] = n0 + 8 * gc < p.N;
+        bsrc[i] = B + (long)(kbeg + r) * p.ldbb + n0 + 8 * gc;
+    }
+    auto issue = [&](int s) {
+        if (s >= nst) return;
+        char* st = smem + (s & 1) * STAGE;
+        const int kb = kbeg + s * BKR;
+#pragma unroll
+        for (int i = 0; i < APC; ++i) {
+            const void* g = (aok[i] && kb + arow[i] < kend) ? (const void*)(asrc[i] + (long)s * BKR * p.ldab)
+                                                            : (const void*)g_zero16;
+            __builtin_amdgcn_global_load_lds(g, (lds_ptr_t)(st + (i * 4 + wid) * 1024), 16, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < BPC; ++i) {
+            const void* g = (bok[i] && kb + brow[i] < kend) ? (const void*)(bsrc[i] + (long)s * BKR * p.ldbb)
+                                                            : (const void*)g_zero16;
+            __builtin_amdgcn_global_load_lds(g, (lds_ptr_t)(st + ASZ + (i * 4 + wid) * 1024), 16, 0, 0);
+        }
+    };
+    // fragment of 8 consecutive k (16 ks + 8 h + 0..7) of column col0 + lane-column: two transposed reads
+    const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+    auto frag = [&](const char* img, int col0, int ks) {
+        const int c = col0 + 16 * (g & 1) + 4 * pp;   // the column block this lane addresses (4 columns)
+        const int gc = c >> 3, half = (c & 7) * 2;
+        const int r0 = 16 * ks + 8 * (g >> 1) + q;    // rows r0 and r0 + 4: row & 3 == q for both
+        const int off = (gc ^ (4 * q)) * 16 + half;
+        typedef __attribute__((address_space(3))) fbf16x4_t* lp4;
+        const fbf16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lp4)(img + r0 * 256 + off));
+        const fbf16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lp4)(img + (r0 + 4) * 256 + off));
+        bf16x8 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            v[e] = lo[e];
+            v[4 + e] = hi[e];
+        }
+        return v;
+    };
+    auto compute = [&](int s) {
+        const char* As = smem + (s & 1) * STAGE;
+        const char* Bs = As + ASZ;
+#pragma unroll
+        for (int ks = 0; ks < BKR / 16; ++ks) {
+            bf16x8 af[RM], bfr[RN];
+#pragma unroll
+            for (int i = 0; i < RM; ++i) af[i] = frag(As, wm * WTM + i * 32, ks);
+#pragma unroll
+            for (int j = 0; j < RN; ++j) bfr[j] = frag(Bs, wn * WTN + j * 32, ks);
+#pragma unroll
+            for (int i = 0; i < RM; ++i)
+#pragma unroll
+                for (int j = 0; j < RN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        }
+    };
+    issue(0);
+    for (int s = 0; s < nst; ++s) {
+        wait_vm<0>();
+        __builtin_amdgcn_s_barrier();
+        issue(s + 1);
+        compute(s);
+    }
+    wait_vm<0>();
+    gemm_epilogue<RM, RN, false>(p, acc, z1, z0, m0 + wm * WTM, n0 + wn * WTN, h, l32,
+                                 m0 + BM <= p.M && n0 + BN <= p.N, tid.z);
+}
+
 void gemm_run_gbf(int bk64, int nprod, int tile, const GemmParams& p, dim3 grid, hipStream_t st);  // gemm_gbf.hip
 void gemm_run_hb(int tile, int ns, const GemmParams& p, dim3 grid, hipStream_t st);                         // gemm_hb.hip
+void gemm_run_hbt(const GemmParams& p, dim3 grid, hipStream_t st);                                          // gemm_hb.hip

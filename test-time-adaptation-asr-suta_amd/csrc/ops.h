@@ -52,7 +52,7 @@ long layernorm_bwd_conv_part_floats(int B, int rows_per_utt, int D, int ktaps);
 bool launch_layernorm_bwd_conv(const float* dy, const float* rstd, const float* g, const float* beta, long pstride,
                                int rows_per_utt, int B, int D, float* dx, float* dgamma, float* dbeta, float* dbias,
                                float* dw, long gstride, float* part, hipStream_t st, const float* x, const float* mean,
-                               const float* xw, long xws, int xs, int ktaps);
+                               const float* xw, long xws, int xs, int ktaps, void* dxb = nullptr);
 // Column sums per utterance: out[b][c] = sum_{t < rows} x[b][t][c]   (bias gradients).
 void launch_colsum(const float* x, int B, int rows, int C, float* out, long ostride, float* part, hipStream_t st);
 

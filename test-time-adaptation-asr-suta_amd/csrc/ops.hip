@@ -611,7 +611,7 @@ __global__ __launch_bounds__(256) void layernorm_bwd_conv_kernel(
     const float* __restrict__ dy, const float* __restrict__ rstd, const float* __restrict__ g,
     const float* __restrict__ beta, long pstride, int rows_per_utt, float* __restrict__ dx, float* __restrict__ part,
     int nchunk, int crows, const float* __restrict__ xin, const float* __restrict__ meanp,
-    const float* __restrict__ xw, long xws, int xs) {
+    const float* __restrict__ xw, long xws, int xs, __bf16* __restrict__ dxb) {
     constexpr int D = 256 * NV;
     constexpr int NVEC = 3 + KT;
     __shared__ f32x4 red[4][2][NV * 64];
@@ -681,6 +681,7 @@ __global__ __launch_bounds__(256) void layernorm_bwd_conv_kernel(
 #pragma unroll
             for (int e = 0; e < 4; ++e) o[e] = rs * (gi[i][e] * gam[i][e] - m1 - xh[i][e] * m2);
             reinterpret_cast<f32x4*>(dx + row * D)[lane + 64 * i] = o;
+            if (dxb) store_bf16x4(dxb + row * D + 4 * (lane + 64 * i), o);  // the weight gradient's B plane
             acc[2][i] += o;
 #pragma unroll
             for (int k = 0; k < KT; ++k) acc[3 + k][i] += xt[k] * o;
@@ -1529,7 +1530,7 @@ long layernorm_bwd_conv_part_floats(int B, int rows_per_utt, int D, int ktaps) {
 bool launch_layernorm_bwd_conv(const float* dy, const float* rstd, const float* g, const float* beta, long pstride,
                                int rows_per_utt, int B, int D, float* dx, float* dgamma, float* dbeta, float* dbias,
                                float* dw, long gstride, float* part, hipStream_t st, const float* x, const float* mean,
-                               const float* xw, long xws, int xs, int ktaps) {
+                               const float* xw, long xws, int xs, int ktaps, void* dxb) {
     auto a16 = [](const void* q) { return q == nullptr || (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
     if (D != 512 || !(ktaps == 0 || ktaps == 10) || (ktaps && !xw) || !x || !mean || !dgamma || !dbeta ||
         !(a16(dy) && a16(x) && a16(dx) && a16(part)))
@@ -1540,7 +1541,7 @@ bool launch_layernorm_bwd_conv(const float* dy, const float* rstd, const float* 
     const dim3 grid(nchunk, B);
 #define LBC(GV_, KT_)                                                                                         \
     hipLaunchKernelGGL((layernorm_bwd_conv_kernel<2, GV_, KT_>), grid, dim3(256), 0, st, dy, rstd, g, beta, pstride, \
-                       rows_per_utt, dx, part, nchunk, crows, x, mean, xw, xws, xs)
+                       rows_per_utt, dx, part, nchunk, crows, x, mean, xw, xws, xs, reinterpret_cast<__bf16*>(dxb))
     if (ktaps == 10) {
         if (gv) LBC(true, 10);
         else LBC(false, 10);

@@ -226,6 +226,7 @@ def test_flash_fwd_plane_kernel_equals_row_kernel(monkeypatch, preset):
     cfg = get_config(preset)
     eng = SutaEngine(cfg, synth_weights(cfg), max_batch=2, max_samples=128000)
     eng.set_precision("bf16")
+    eng.set_graphs(False)  # eager: a replayed graph would keep the kernels it was captured with
     waves = [synth.wave(128000, 80), synth.wave(76800, 81)]
     out = {}
     for plane in ("1", "0"):
@@ -253,6 +254,7 @@ def test_flash_bwd_plane_kernel_equals_row_kernel(monkeypatch, preset):
     cfg = get_config(preset)
     eng = SutaEngine(cfg, synth_weights(cfg), max_batch=2, max_samples=128000)
     eng.set_precision("bf16")
+    eng.set_graphs(False)  # eager: a replayed graph would keep the kernels it was captured with
     waves = [synth.wave(128000, 82), synth.wave(76800, 83)]
     out = {}
     for plane in ("1", "0"):
@@ -309,6 +311,7 @@ def test_conv_stack_on_bf16_planes_equals_fp32_staged(monkeypatch):
     cfg = get_config("wav2vec2-large")
     eng = SutaEngine(cfg, synth_weights(cfg), max_batch=2, max_samples=48000)
     eng.set_precision("bf16")
+    eng.set_graphs(False)  # eager: a replayed graph would keep the kernels it was captured with
     waves = [synth.wave(48000, 92), synth.wave(30400, 93)]
     out = {}
     for cp in ("1", "0"):
