@@ -528,8 +528,10 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void flash_bwd_kernel(
                 x[b] = dk[t][4 * a + b];
                 y[b] = dv[t][4 * a + b];
             }
-            *reinterpret_cast<f32x4*>(dkr + 32 * t + 8 * a) = x;
-            *reinterpret_cast<f32x4*>(dvr + 32 * t + 8 * a) = y;
+            if (dqkv) {
+                *reinterpret_cast<f32x4*>(dkr + 32 * t + 8 * a) = x;
+                *reinterpret_cast<f32x4*>(dvr + 32 * t + 8 * a) = y;
+            }
             if (dqkvb) {
                 fbf16x4 bx, by;
 #pragma unroll
@@ -1095,8 +1097,10 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16_kernel(
                 x[b] = dk[t][4 * a + b];
                 y[b] = dv[t][4 * a + b];
             }
-            *reinterpret_cast<f32x4*>(dkr + 32 * t + 8 * a) = x;
-            *reinterpret_cast<f32x4*>(dvr + 32 * t + 8 * a) = y;
+            if (dqkv) {  // null in bf16 mode when only the bf16 plane is read (the QKV input-gradient GEMM)
+                *reinterpret_cast<f32x4*>(dkr + 32 * t + 8 * a) = x;
+                *reinterpret_cast<f32x4*>(dvr + 32 * t + 8 * a) = y;
+            }
             if (dqkvb) {
                 __bf16* kb2 = dqkvb + ((long)u * T + key) * ld + H + hd * 64 + 4 * h + 32 * t + 8 * a;
                 *reinterpret_cast<fbf16x4*>(kb2) = cvt4(x);
@@ -1281,8 +1285,10 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
                 x[b] = dk[t][4 * a + b];
                 y[b] = dv[t][4 * a + b];
             }
-            *reinterpret_cast<f32x4*>(dkr + 32 * t + 8 * a) = x;
-            *reinterpret_cast<f32x4*>(dvr + 32 * t + 8 * a) = y;
+            if (dqkv) {  // null in bf16 mode when only the bf16 plane is read (the QKV input-gradient GEMM)
+                *reinterpret_cast<f32x4*>(dkr + 32 * t + 8 * a) = x;
+                *reinterpret_cast<f32x4*>(dvr + 32 * t + 8 * a) = y;
+            }
             if (dqkvb) {
                 __bf16* kb2 = dqkvb + ((long)u * T + key) * ld + H + hd * 64 + 4 * h + 32 * t + 8 * a;
                 *reinterpret_cast<fbf16x4*>(kb2) = cvt4(x);
@@ -1310,7 +1316,7 @@ __global__ __launch_bounds__(256) void flash_dq_reduce(const float* __restrict__
         const f32x4* p = reinterpret_cast<const f32x4*>(dqp + row * 64 + c4);
         for (int k = 0; k < nkb; ++k) s += p[k * (stride / 4)];
     }
-    *reinterpret_cast<f32x4*>(dqkv + ((long)u * T + q) * 3 * H + hd * 64 + c4) = s;
+    if (dqkv) *reinterpret_cast<f32x4*>(dqkv + ((long)u * T + q) * 3 * H + hd * 64 + c4) = s;
     if (dqkvb) {
         fbf16x4 b;
 #pragma unroll

@@ -1088,10 +1088,12 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
         timed(F_SOFTMAX, [&] { launch_attn_delta(pl.ctx, lb.ctx, pl.delta, B, T, NH, d, st); });
         // flash backward: P recomputed from the LSE, dQ, dK, dV into dqkv (else the GEMM path below)
         const bool fused_bwd = pl.flash;
+        // with bf16 planes the QKV input-gradient GEMM reads only dqkv's bf16 plane: the fp32 copy is not written
+        const bool dqkv_dead = fused_bwd && P1 && dead;
         if (fused_bwd)
             timed(F_ATTN, [&] {
-                if (!launch_flash_bwd(lb.qkv, pl.ctx, lb.lse, pl.delta, pl.dqkv, pl.dqp, B, T, NH, H, d, scale, rT(),
-                                      gemm_mode == SUTA_PRECISION_BF16, st, P1, qkvp, dctxp))
+                if (!launch_flash_bwd(lb.qkv, pl.ctx, lb.lse, pl.delta, dqkv_dead ? nullptr : pl.dqkv, pl.dqp, B, T,
+                                      NH, H, d, scale, rT(), gemm_mode == SUTA_PRECISION_BF16, st, P1, qkvp, dctxp))
                     throw SutaError(SUTA_ERR_UNSUPPORTED, "flash attention shape");
             }, 4.0 * BT * (7.0 * H + 2.0 * NH));  // Q, K, V, dctx, LSE, delta read; dQ, dK, dV written
         if (!fused_bwd) {
@@ -1198,12 +1200,13 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
         }
         if (!k.stable) {
             // dx_in = dqkv @ Wqkv + dr1
-            nn_gemm(pl.dqkv, 3 * H, wqkv[l], H, t2, H, (int)BT, H, 3 * H, EPI_RESID, dhres, H, nullptr, 0,
+            nn_gemm(dqkv_dead ? nullptr : pl.dqkv, 3 * H, wqkv[l], H, t2, H, (int)BT, H, 3 * H, EPI_RESID, dhres, H,
+                    nullptr, 0,
                     fused_bwd ? P1 : nullptr);
             std::swap(dx, t2);
         } else {
             // dy1 = dqkv @ Wqkv ; dx_in = LN1 bwd(dy1) + dhmid
-            nn_gemm(pl.dqkv, 3 * H, wqkv[l], H, t2, H, (int)BT, H, 3 * H, 0, nullptr, 0, nullptr, 0,
+            nn_gemm(dqkv_dead ? nullptr : pl.dqkv, 3 * H, wqkv[l], H, t2, H, (int)BT, H, 3 * H, 0, nullptr, 0, nullptr, 0,
                     fused_bwd ? P1 : nullptr);
             timed(F_NORM, [&] {
                 launch_layernorm_bwd(t2, lb.xhat1, lb.rstd1, P + o_l1g[l], P + o_l1b[l], Pn, T, B, H, 0, nullptr, dhres,
