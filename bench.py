@@ -45,7 +45,8 @@ PMC_TRAFFIC_C4 = next((p for p in (os.path.join(ROOT, "profiles", r, f) for r, f
 GEMM_KERNELS = ("gemm_glds_kernel", "gemm_f32_kernel", "gemm_splitk_reduce", "attn_fwd_kernel", "attn_bwd_kernel",
                 "posconv_kernel", "flash_fwd_kernel", "flash_bwd_kernel", "flash_dq_reduce")
 # config C4's GEMM family (bf16 mode): every kernel its "gemm" + "attention" timing families launch
-GEMM_KERNELS_C4 = ("gemm_hb_kernel", "gemm_hb8_kernel", "gemm_x6_kernel", "gemm_gbf_kernel", "gemm_splitk_reduce",
+GEMM_KERNELS_C4 = ("gemm_hb_kernel", "gemm_hb8_kernel", "gemm_hbt_kernel", "gemm_x6_kernel", "gemm_gbf_kernel",
+                   "gemm_splitk_reduce",
                    "to_bf16_kernel", "posconv_bf16_kernel", "flash_fwd_bf16_kernel", "flash_bwd_bf16_kernel",
                    "flash_dq_reduce")
 FRONT_KERNELS = ("conv0_gn_kernel", "col_stats_final", "gn_bwd_final", "conv0_dw_reduce")
@@ -145,7 +146,7 @@ def bench_c4(args, dev):
         gms, gn = t["gemm"]
         ach = flops_utt * B / (gms / 1000.0) / 1e12
         res["roofline"] = {"bound": "mfma", "achieved": round(ach, 3), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                           "frac": round(ach / BF16_PEAK_TFLOPS, 4), "kernel": "bf16 GEMM family (bf16-plane linears: gemm_hb_kernel / gemm_hb8_kernel; layer-norm conv stack: gemm_x6_kernel one-plane form; weight gradients: gemm_gbf_kernel; posconv_bf16_kernel; flash attention on bf16 MFMA)",
+                           "frac": round(ach / BF16_PEAK_TFLOPS, 4), "kernel": "bf16 GEMM family (bf16-plane linears and the layer-norm conv stack's forward / input gradients: gemm_hb_kernel; conv weight gradients: gemm_hbt_kernel; per-utterance projection GEMMs: gemm_x6_kernel one-plane form / gemm_gbf_kernel; posconv_bf16_kernel; flash attention on bf16 MFMA)",
                            "launches": int(gn), "avg_launch_ms": round(gms / max(1, gn), 5)}
         gx, ax = tex["gemm"], tex["attention"]
         talg = round((gx[2] + ax[2]) / max(1, gx[1] + ax[1]))

@@ -1357,13 +1357,17 @@ static bool ff_plane() {
     return !(e && atoi(e) == 0);
 }
 
+bool flash_fwd_reads_plane(bool bf16, const void* qkvb, int H) { return bf16 && qkvb && H % 8 == 0 && ff_plane(); }
+
 bool launch_flash_fwd(const float* qkv, float* ctx, float* lse, int B, int T, int NH, int H, int dh, float scale,
                       const int* tlen, bool bf16, hipStream_t st, void* ctxb_, const void* qkvb) {
     __bf16* ctxb = reinterpret_cast<__bf16*>(ctxb_);
     if (dh != 64 || T < 1 || H % 4) return false;
     const int ng = (T + 31) / 32, nqb = (ng + FF_NW - 1) / FF_NW;
     const dim3 grid((unsigned)((long)B * NH * nqb));
-    if (bf16 && qkvb && H % 8 == 0 && ff_plane()) {
+    const bool on_plane = flash_fwd_reads_plane(bf16, qkvb, H);
+    if (!qkv && !on_plane) throw std::invalid_argument("flash_fwd: fp32 qkv not written and the plane kernel not taken");
+    if (on_plane) {
         if (reinterpret_cast<uintptr_t>(qkvb) & 15) throw std::invalid_argument("flash_fwd: bf16 qkv plane not 16-B aligned");
         // SUTA_FLASH_FWD_NW=8: 8-wave blocks (256 queries share each K / V tile copy); read at every launch
         const char* ev = std::getenv("SUTA_FLASH_FWD_NW");
@@ -1411,6 +1415,10 @@ static bool fb_plane() {
     return !(e && atoi(e) == 0);
 }
 
+bool flash_bwd_reads_planes(bool bf16, const void* qkvb, const void* dctxb, int H) {
+    return bf16 && fb_nw() == FBB_NW && qkvb && dctxb && H % 8 == 0 && fb_plane();
+}
+
 bool launch_flash_bwd(const float* qkv, const float* dctx, const float* lse, const float* delta, float* dqkv,
                       float* dqp, int B, int T, int NH, int H, int dh, float scale, const int* tlen, bool bf16,
                       hipStream_t st, void* dqkvb_, const void* qkvb, const void* dctxb) {
@@ -1421,7 +1429,9 @@ bool launch_flash_bwd(const float* qkv, const float* dctx, const float* lse, con
     const int nkb = (ng + nw - 1) / nw;   // key blocks per head
     const int gpb = (ng + nkb - 1) / nkb;  // key groups per block (balanced)
     const dim3 grid((unsigned)((long)B * NH * nkb));
-    if (bf16 && nw == FBB_NW && qkvb && dctxb && H % 8 == 0 && fb_plane()) {
+    const bool on_planes = flash_bwd_reads_planes(bf16, qkvb, dctxb, H);
+    if (!qkv && !on_planes) throw std::invalid_argument("flash_bwd: fp32 qkv not written and the plane kernel not taken");
+    if (on_planes) {
         if ((reinterpret_cast<uintptr_t>(qkvb) | reinterpret_cast<uintptr_t>(dctxb)) & 15)
             throw std::invalid_argument("flash_bwd: bf16 planes not 16-B aligned");
         constexpr size_t lds = fbbp_lds_bytes();

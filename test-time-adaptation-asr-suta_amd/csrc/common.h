@@ -113,8 +113,11 @@ void gemm_set_mode(int mode);
 // with row stride K: the A plane of a bf16-plane GEMM.
 void launch_to_bf16(const float* src, long lds, long rows, int K, void* dst, hipStream_t st);
 // dst[z][n][k] = bf16(src[z * zs + k * N + n]) (per-slot transposed bf16 weights)
-void launch_transpose_bf16(const float* src, long zs, int Z, int K, int N, void* dst, hipStream_t st);
+void launch_transpose_bf16(const float* src, long zs, int Z, int K, int N, void* dst, hipStream_t st,
+                          void* dstn = nullptr);
 int gemm_get_mode();
 // launch census per (kernel, tile, Z, splits, operand form): suta_set_census / suta_get_census
 void gemm_census_enable(bool on);
 std::string gemm_census_text();
+bool gemm_census_is_on();
+void gemm_census_time(const std::string& shape, double ms);

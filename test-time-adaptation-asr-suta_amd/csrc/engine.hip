@@ -302,18 +302,24 @@ struct suta_engine {
         fn();
         HIPCHK(hipEventRecord(b, st));
         pending.push_back({fam, {a, b}});
+        pending_shape.push_back(fam == F_GEMM ? gemm_shape : std::string());
     }
+    std::vector<std::string> pending_shape;  // per pending pair: the GEMM shape (census on), else empty
+    std::string gemm_shape;
     void collect_timing() {
-        for (auto& pe : pending) {
+        for (size_t i = 0; i < pending.size(); ++i) {
+            auto& pe = pending[i];
             float ms = 0.f;
             HIPCHK(hipEventSynchronize(pe.second.second));
             HIPCHK(hipEventElapsedTime(&ms, pe.second.first, pe.second.second));
             fam_ms[pe.first] += ms;
             fam_n[pe.first] += 1;
+            if (i < pending_shape.size() && !pending_shape[i].empty()) gemm_census_time(pending_shape[i], ms);
             evpool.push_back(pe.second.first);
             evpool.push_back(pe.second.second);
         }
         pending.clear();
+        pending_shape.clear();
     }
     // bf16 mode: bf16 planes of the frozen linear weights, {[N][K] for x W^T, [in][out] for dY W}, keyed by
     // the fp32 weight pointer (built once when the mode is selected), and the A plane of the current GEMM
@@ -360,15 +366,23 @@ struct suta_engine {
         if (convdz.alloc(n)) drop_graph();
         return convdz.p;
     }
-    void* conv_wt_plane(int i) {  // layer i >= 1: [B][C_i][K_i * C_{i-1}] bf16
+    // layer i >= 1, native = 0: [B][C_i][K_i * C_{i-1}] bf16 (forward B operand); native = 1: the source layout
+    // [B][K_i][C_{i-1}][C_i] (the input gradient's per-tap B segments)
+    void* conv_wt_plane(int i, int native = 0) {
         size_t off = 0, tot = 0;
         for (int j = 1; j < c.nconv; ++j) {
             const size_t n = rup((long)plan.B * c.C[j] * c.K[j] * c.C[j - 1] * 2, 256);
             if (j < i) off += n;
             tot += n;
         }
-        if (convwt.alloc(tot)) drop_graph();
-        return reinterpret_cast<char*>(convwt.p) + off;
+        if (convwt.alloc(2 * tot)) drop_graph();
+        return reinterpret_cast<char*>(convwt.p) + native * tot + off;
+    }
+    // conv input gradients on the bf16 planes too (SUTA_CONV_DX_PLANES=0: fp32-staged x6 kernels, for A/B runs)
+    bool conv_dx_planes() const {
+        if (!conv_planes()) return false;
+        const char* e = std::getenv("SUTA_CONV_DX_PLANES");
+        return !(e && atoi(e) == 0);
     }
     // bf16 plane of layer l's qkv [B*T][3H]: written by the QKV GEMM, read by the flash forward and, in the
     // backward, by the flash backward (kept for every layer, like the fp32 qkv)
@@ -384,6 +398,14 @@ struct suta_engine {
         GemmParams p = p0;
         p.mode = gemm_mode;
         const double ab = timing ? gemm_alg_bytes(p) : 0.0;
+        gemm_shape.clear();
+        if (timing && gemm_census_is_on()) {  // per-shape time table (census + timing: tools/gemm_shapes.py)
+            char key[200];
+            snprintf(key, sizeof key, "M=%d N=%d K=%d z=%d %s%s epi=%d%s%s%s%s", p.M, p.N, p.K, p.Z, p.ta ? "T" : "N",
+                     p.tb ? "T" : "N", p.epi, p.segK > 0 ? " conv" : "", p.Ab ? " Ab" : "", p.C ? " C" : "",
+                     p.Cb ? " Cb" : "");
+            gemm_shape = key;
+        }
         if (gemm_mode == SUTA_PRECISION_BF16 && p.Ab && p.Bb) {  // both planes given by the caller (conv stack)
             timed(F_GEMM, [&] { gemm_launch(p, st, plan.splitws, plan.splitws_floats); }, ab);
             return;
@@ -637,7 +659,9 @@ void suta_engine::forward(int B) {
         g.sC1 = (long)pl.Lc[i] * k.C[i];
         if (cpl) {  // bf16 planes: activations written by the previous LayerNorm, weights re-laid per slot
             void* wt = conv_wt_plane(i);
-            timed(F_EW, [&] { launch_transpose_bf16(P + o_cw[i], Pn, B, g.K, g.N, wt, st); });
+            timed(F_EW, [&] {
+                launch_transpose_bf16(P + o_cw[i], Pn, B, g.K, g.N, wt, st, conv_dx_planes() ? conv_wt_plane(i, 1) : nullptr);
+            });
             g.Ab = conv_act_plane(i - 1);
             g.ldab = g.lda;
             g.Bb = wt;
@@ -777,6 +801,9 @@ void suta_engine::forward(int B) {
             attn_in = dead ? nullptr : lb.y1;  // (dead: the QKV GEMM reads the LN1 plane only)
         }
         void* qkvp = pl.flash ? qkv_plane(l) : nullptr;
+        // both flash kernels read qkv's bf16 plane only (the backward's dO plane is plane 2): no fp32 qkv
+        const bool bf = gemm_mode == SUTA_PRECISION_BF16;
+        const bool qkv_dead = qkvp && P0 && flash_fwd_reads_plane(bf, qkvp, H) && flash_bwd_reads_planes(bf, qkvp, plane(2), H);
         {  // fused QKV
             GemmParams g;
             gemm_init(g);
@@ -787,7 +814,7 @@ void suta_engine::forward(int B) {
             g.B = wqkv[l];
             g.tb = 1;
             g.ldb = H;
-            g.C = lb.qkv;
+            g.C = qkv_dead ? nullptr : lb.qkv;
             g.ldc = 3 * H;
             g.M = (int)BT;
             g.N = 3 * H;
@@ -804,7 +831,7 @@ void suta_engine::forward(int B) {
         const bool fused = pl.flash;
         if (fused)
             timed(F_ATTN, [&] {
-                if (!launch_flash_fwd(lb.qkv, lb.ctx, lb.lse, B, T, NH, H, d, scale, rT(),
+                if (!launch_flash_fwd(qkv_dead ? nullptr : lb.qkv, lb.ctx, lb.lse, B, T, NH, H, d, scale, rT(),
                                       gemm_mode == SUTA_PRECISION_BF16, st, P0, qkvp))
                     throw SutaError(SUTA_ERR_UNSUPPORTED, "flash attention shape");
             }, 4.0 * BT * (4.0 * H + NH));  // Q, K, V read; ctx and LSE written
@@ -1092,7 +1119,10 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
         const bool dqkv_dead = fused_bwd && P1 && dead;
         if (fused_bwd)
             timed(F_ATTN, [&] {
-                if (!launch_flash_bwd(lb.qkv, pl.ctx, lb.lse, pl.delta, dqkv_dead ? nullptr : pl.dqkv, pl.dqp, B, T,
+                // (the forward's test: the fp32 qkv was not written when both flash kernels read its plane)
+                const bool bf = gemm_mode == SUTA_PRECISION_BF16;
+                const bool qkv_dead = qkvp && flash_fwd_reads_plane(bf, qkvp, H) && flash_bwd_reads_planes(bf, qkvp, dctxp, H);
+                if (!launch_flash_bwd(qkv_dead ? nullptr : lb.qkv, pl.ctx, lb.lse, pl.delta, dqkv_dead ? nullptr : pl.dqkv, pl.dqp, B, T,
                                       NH, H, d, scale, rT(), gemm_mode == SUTA_PRECISION_BF16, st, P1, qkvp, dctxp))
                     throw SutaError(SUTA_ERR_UNSUPPORTED, "flash attention shape");
             }, 4.0 * BT * (7.0 * H + 2.0 * NH));  // Q, K, V, dctx, LSE, delta read; dQ, dK, dV written
@@ -1338,7 +1368,9 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
                 if (!pl.cxhat[i] && (fused_conv_ln() || cpl) &&
                     layernorm_bwd_conv_part_floats(B, pl.Lc[i], k.C[i], 0) <= pl.lnpart_floats &&
                     launch_layernorm_bwd_conv(cur, pl.crstd[i], P + o_cg[i], P + o_cbeta[i], Pn, pl.Lc[i], B, k.C[i],
-                                              other, G + o_cg[i], G + o_cbeta[i], k.conv_bias ? G + o_cb[i] : nullptr,
+                                              // both conv GEMMs read dz_i from its plane: no fp32 copy
+                                              cpl && conv_dx_planes() ? nullptr : other, G + o_cg[i], G + o_cbeta[i],
+                                              k.conv_bias ? G + o_cb[i] : nullptr,
                                               nullptr, Pn, pl.lnpart, st, pl.z[i], pl.cmean[i], nullptr, 0, 0, 0,
                                               cpl ? conv_dz_plane() : nullptr)) {
                     bias_done = true;
@@ -1416,6 +1448,18 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
                     g.aux = zprev + (long)rho * Cin;
                     g.ldaux = (long)S_ * Cin;
                     g.sAux1 = (long)Lin * Cin;
+                }
+                if (cpl && conv_dx_planes()) {  // bf16 planes: the LayerNorm-written dz plane and the forward's
+                                                // source-layout bf16 weights (strides in bf16 elements)
+                    if (!bias_done) throw SutaError(SUTA_ERR_UNSUPPORTED, "conv planes: dz plane not written");
+                    g.A = nullptr;
+                    g.B = nullptr;
+                    g.Ab = conv_dz_plane();
+                    g.ldab = Cout;
+                    g.Bb = static_cast<char*>(conv_wt_plane(i, 1)) + (long)(rho + S_ * (nj - 1)) * Cin * Cout * 2;
+                    g.ldbb = Cout;
+                    g.tb = 0;
+                    g.sB1 = (long)Kt * Cin * Cout;
                 }
                 gemm(g);
             }

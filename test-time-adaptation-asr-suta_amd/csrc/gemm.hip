@@ -29,25 +29,41 @@ void gemm_set_variant(int tile, int nbuf) {
 static std::mutex g_census_mu;
 static std::map<std::string, long> g_census;
 static bool g_census_on = false;
+// with engine timing on as well: per GEMM shape, the summed HIP-event time of its launches ("ms|<shape>|n=<n>"
+// entries, value in microseconds)
+static std::map<std::string, std::pair<double, long>> g_census_ms;
 
 void gemm_census_enable(bool on) {
     std::lock_guard<std::mutex> lk(g_census_mu);
     g_census_on = on;
     g_census.clear();
+    g_census_ms.clear();
+}
+
+bool gemm_census_is_on() { return g_census_on; }
+
+void gemm_census_time(const std::string& shape, double ms) {
+    std::lock_guard<std::mutex> lk(g_census_mu);
+    auto& e = g_census_ms[shape];
+    e.first += ms;
+    e.second += 1;
 }
 
 std::string gemm_census_text() {
     std::lock_guard<std::mutex> lk(g_census_mu);
     std::string out;
     for (const auto& kv : g_census) out += kv.first + " " + std::to_string(kv.second) + "\n";
+    for (const auto& kv : g_census_ms)
+        out += "ms|" + kv.first + "|n=" + std::to_string(kv.second.second) + " " +
+               std::to_string((long)(kv.second.first * 1000.0)) + "\n";
     return out;
 }
 
 static void census(const char* kernel, int BM, int BN, const GemmParams& p, int splits) {
     if (!g_census_on) return;
     char key[160];
-    snprintf(key, sizeof key, "%s %dx%d z=%ld split=%d %s%s", kernel, BM, BN, (long)p.Z, splits, p.ta ? "T" : "N",
-             p.tb ? "T" : "N");
+    snprintf(key, sizeof key, "%s %dx%d z=%ld split=%d %s%s%s", kernel, BM, BN, (long)p.Z, splits, p.ta ? "T" : "N",
+             p.tb ? "T" : "N", p.segK > 0 ? (p.segB ? " conv-seg" : " conv") : "");
     std::lock_guard<std::mutex> lk(g_census_mu);
     ++g_census[key];
 }
@@ -166,7 +182,7 @@ static bool use_tile160(long M, long N, long Z) {
 static int use_hb8(const GemmParams& p) {
     const char* e = std::getenv("SUTA_HB8");
     const int mode = e ? atoi(e) : 0;
-    if (p.K % 32 != 0 || mode == 0 || p.Z != 1) return 0;
+    if (p.K % 32 != 0 || mode == 0 || p.Z != 1 || p.segK > 0) return 0;
     if (mode == 2) return 1;
     if (mode == 3 && ((p.epi & (EPI_GELU | EPI_RESID | EPI_STORE_PRE | EPI_DGELU | EPI_ACCUM | EPI_SMBWD)) || p.Cb))
         return 0;
@@ -199,7 +215,9 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
                (p.Z > 1 && ((p.sA0 | p.sA1 | p.sB0 | p.sB1) % 8))))
         throw std::invalid_argument("gemm: bf16 planes need K, ld and batch strides % 8 == 0 and 16-B alignment");
     const bool bf16_gbf = p.mode == 2 && glds_ok && p.ta;  // bf16 weight gradients: LDS-DMA fp32 stages
-    int tile = hbt             ? 0
+    if (hb && p.segK > 0 && (p.segK % 8 || p.pad < 0 || (p.segB && (p.sBseg % 8))))
+        throw std::invalid_argument("gemm: conv-A bf16 planes need segK and the tap stride % 8 == 0");
+    int tile = hbt || (hb && p.segK > 0) ? 0
                : g_force_tile >= 0 ? g_force_tile
                : hb            ? (use_hb8(p) ? 6 : choose_tile_hb(p.M, p.N, p.Z))
                : p.mode == 2   ? choose_tile_bf16(p.M, p.N, p.Z, !bf16_gbf)

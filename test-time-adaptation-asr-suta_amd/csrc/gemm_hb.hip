@@ -5,6 +5,11 @@
 // ns: 2 (default) | 3 = three LDS stages | 4 = 128-deep bf16 K-steps, two stages (benchmark variants,
 // tools/hb_bench); tile 4 = 256x128, 5 = 128x256 (benchmark only)
 void gemm_run_hb(int tile, int ns, const GemmParams& p, dim3 grid, hipStream_t st) {
+    if (p.segK > 0) {  // conv input gradient on bf16 planes (128 x 128, conv-A rows, per-tap B segments)
+        if (p.segB) launch_hb<128, 128, 2, 32, 4, true, true>(p, grid, st);
+        else launch_hb<128, 128, 2, 32, 4, true, false>(p, grid, st);
+        return;
+    }
     if (tile == 6) {  // 256 x 256 ping-pong (K % 32 == 0, no split-K)
         const char* e = std::getenv("SUTA_HB8_PF");  // 1: fragments read one phase ahead
         launch_hb8(p, grid, st, e && atoi(e) == 1);
@@ -75,8 +80,10 @@ void launch_to_bf16(const float* src, long lds, long rows, int K, void* dst, hip
 // Per-slot transposed bf16 copy of a trainable [K][N] fp32 matrix (conv weights [tap][C_in][C_out] of every
 // utterance slot): dst[z][n][k] = bf16(src[z * zs + k * N + n]), 64 x 64 tiles through LDS (coalesced both
 // ways).  The B operand of the bf16-plane conv GEMMs ([N][K], k-contiguous), rebuilt after every AdamW step.
+// dstn (optional): the same values in the source layout, dstn[z][k][n] (the conv input gradient's B operand),
+// from the same read.
 __global__ __launch_bounds__(256) void transpose_bf16_kernel(const float* __restrict__ src, long zs, int K, int N,
-                                                             __bf16* __restrict__ dst) {
+                                                             __bf16* __restrict__ dst, __bf16* __restrict__ dstn) {
     __shared__ float t[64][65];
     const int z = blockIdx.z, k0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
     const float* s = src + (long)z * zs;
@@ -84,7 +91,9 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const float* __rest
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
     for (int r = ty; r < 64; r += 4) {
         const int k = k0 + r, n = n0 + tx;
-        t[r][tx] = (k < K && n < N) ? s[(long)k * N + n] : 0.f;
+        const float v = (k < K && n < N) ? s[(long)k * N + n] : 0.f;
+        t[r][tx] = v;
+        if (dstn && k < K && n < N) dstn[(long)z * N * K + (long)k * N + n] = (__bf16)v;
     }
     __syncthreads();
     for (int r = ty; r < 64; r += 4) {
@@ -93,9 +102,9 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const float* __rest
     }
 }
 
-void launch_transpose_bf16(const float* src, long zs, int Z, int K, int N, void* dst, hipStream_t st) {
+void launch_transpose_bf16(const float* src, long zs, int Z, int K, int N, void* dst, hipStream_t st, void* dstn) {
     hipLaunchKernelGGL(transpose_bf16_kernel, dim3((N + 63) / 64, (K + 63) / 64, Z), dim3(256), 0, st, src, zs, K, N,
-                       reinterpret_cast<__bf16*>(dst));
+                       reinterpret_cast<__bf16*>(dst), reinterpret_cast<__bf16*>(dstn));
 }
 
 void gemm_run_hbt(const GemmParams& p, dim3 grid, hipStream_t st) {

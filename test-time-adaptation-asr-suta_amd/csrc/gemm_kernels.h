@@ -1479,7 +1479,9 @@ void launch_tile(const GemmParams& p, dim3 grid, hipStream_t st) {
 // Half the operand bytes of the fp32-staged bf16 kernels, no conversion in the K-loop.
 // ============================================================================================
 // NWV = 4 waves (2 x 2) or 8 waves (2 x 4, the 256 x 256 tile: 128 x 64 per wave, 128 KB of LDS)
-template <int BM, int BN, int NS, int BKS = 32, int NWV = 4>  // BKS: stage depth in 4-byte units (32 = 64 bf16)
+// CONV / SEGB: the conv input-gradient form (conv-A rows of A, per-tap B segments; glds_stage modes 1 / 2 in
+// 4-byte units: segK, pad, sBseg given in bf16 elements, even)
+template <int BM, int BN, int NS, int BKS = 32, int NWV = 4, bool CONV = false, bool SEGB = false>  // BKS: 4-byte units
 __global__ __launch_bounds__(64 * NWV, (BM * BN > 128 * 128 || BKS > 32) ? 1 : 2) void gemm_hb_kernel(GemmParams p) {
     constexpr int WNW = NWV / 2;                 // waves along N
     constexpr int WTM = BM / 2, WTN = BN / WNW;
@@ -1519,6 +1521,9 @@ __global__ __launch_bounds__(64 * NWV, (BM * BN > 128 * 128 || BKS > 32) ? 1 : 2
     GldsStream<BN, BKS, true, NWV> sb;
     sa.init(A, lda, m0, p.M, kbeg, wid, lane);
     sb.init(B, ldb, n0, p.N, kbeg, wid, lane);
+    const int segK2 = p.segK / 2, pad = p.pad;
+    const int Mv = p.zmvalid ? p.zmvalid[z1] : p.Mvalid;
+    const long sseg2 = p.sBseg / 2;
     auto issue = [&](int s) {
         float* st = smem + (s % NS) * STAGE;
         const int k = kbeg + s * BKS;
@@ -1527,6 +1532,11 @@ __global__ __launch_bounds__(64 * NWV, (BM * BN > 128 * 128 || BKS > 32) ? 1 : 2
                 glds_stage<BM, BKS, true, 0, NWV>(st, A, lda, m0, p.M, k, kend, 0, 0, 0, 0, wid, lane, true);
                 glds_stage<BN, BKS, true, 0, NWV>(st + BM * BKS, B, ldb, n0, p.N, k, kend, 0, 0, 0, 0, wid, lane, true);
             }
+        } else if (CONV || SEGB) {  // conv input gradient: per-lane addresses from the row / segment maps
+            glds_stage<BM, BKS, true, CONV ? 1 : 0, NWV>(st, A, lda, m0, p.M, k, kend, segK2, pad, Mv, 0, wid, lane,
+                                                          false);
+            glds_stage<BN, BKS, true, SEGB ? 2 : 0, NWV>(st + BM * BKS, B, ldb, n0, p.N, k, kend, segK2, 0, 0, sseg2,
+                                                          wid, lane, false);
         } else if (k + BKS <= kend) {
             glds_stream_issue(sa, st, wid);
             glds_stream_issue(sb, st + BM * BKS, wid);
@@ -1576,9 +1586,9 @@ __global__ __launch_bounds__(64 * NWV, (BM * BN > 128 * 128 || BKS > 32) ? 1 : 2
                                      m0 + BM <= p.M && n0 + BN <= p.N, tid.z);
 }
 
-template <int BM, int BN, int NS, int BKS = 32, int NWV = 4>
+template <int BM, int BN, int NS, int BKS = 32, int NWV = 4, bool CONV = false, bool SEGB = false>
 void launch_hb(const GemmParams& p, dim3 grid, hipStream_t st) {
-    hipLaunchKernelGGL((gemm_hb_kernel<BM, BN, NS, BKS, NWV>), grid, dim3(64 * NWV), 0, st, p);
+    hipLaunchKernelGGL((gemm_hb_kernel<BM, BN, NS, BKS, NWV, CONV, SEGB>), grid, dim3(64 * NWV), 0, st, p);
 }
 
 // 256 x 256 bf16-plane GEMM on one block per CU with a ping-pong schedule (cdna_hip_programming.md,

@@ -63,6 +63,10 @@ void launch_colsum(const float* x, int B, int rows, int C, float* out, long ostr
 // MFMAs (config C4).  false (nothing launched) when dh != 64.
 long flash_dq_scratch_floats(int B, int T, int NH);
 // ctxb / dqkvb (may be null): bf16 copies of ctx / dqkv for the bf16-plane GEMMs that consume them.
+// qkv may be null when the launch takes the bf16-plane kernel (flash_*_reads_plane[s]: the engine's test for
+// leaving the fp32 qkv unwritten); the launch throws otherwise.
+bool flash_fwd_reads_plane(bool bf16, const void* qkvb, int H);
+bool flash_bwd_reads_planes(bool bf16, const void* qkvb, const void* dctxb, int H);
 bool launch_flash_fwd(const float* qkv, float* ctx, float* lse, int B, int T, int NH, int H, int dh, float scale,
                       const int* tlen, bool bf16, hipStream_t st, void* ctxb = nullptr, const void* qkvb = nullptr);
 bool launch_flash_bwd(const float* qkv, const float* dctx, const float* lse, const float* delta, float* dqkv,

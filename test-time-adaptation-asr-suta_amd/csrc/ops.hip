@@ -680,8 +680,8 @@ __global__ __launch_bounds__(256) void layernorm_bwd_conv_kernel(
             f32x4 o;
 #pragma unroll
             for (int e = 0; e < 4; ++e) o[e] = rs * (gi[i][e] * gam[i][e] - m1 - xh[i][e] * m2);
-            reinterpret_cast<f32x4*>(dx + row * D)[lane + 64 * i] = o;
-            if (dxb) store_bf16x4(dxb + row * D + 4 * (lane + 64 * i), o);  // the weight gradient's B plane
+            if (dx) reinterpret_cast<f32x4*>(dx + row * D)[lane + 64 * i] = o;  // (null: only the plane is read)
+            if (dxb) store_bf16x4(dxb + row * D + 4 * (lane + 64 * i), o);  // the conv GEMMs' bf16 operand plane
             acc[2][i] += o;
 #pragma unroll
             for (int k = 0; k < KT; ++k) acc[3 + k][i] += xt[k] * o;
@@ -1532,7 +1532,7 @@ bool launch_layernorm_bwd_conv(const float* dy, const float* rstd, const float* 
                                float* dw, long gstride, float* part, hipStream_t st, const float* x, const float* mean,
                                const float* xw, long xws, int xs, int ktaps, void* dxb) {
     auto a16 = [](const void* q) { return q == nullptr || (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
-    if (D != 512 || !(ktaps == 0 || ktaps == 10) || (ktaps && !xw) || !x || !mean || !dgamma || !dbeta ||
+    if (D != 512 || !(ktaps == 0 || ktaps == 10) || (ktaps && !xw) || !x || !mean || !dgamma || !dbeta || !(dx || dxb) ||
         !(a16(dy) && a16(x) && a16(dx) && a16(part)))
         return false;
     const int crows = rows_per_utt >= 4096 ? 128 : 16;

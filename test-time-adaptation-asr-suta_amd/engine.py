@@ -338,7 +338,8 @@ class SutaEngine:
         _check(self.lib.suta_set_census(int(enable)))
 
     def get_census(self) -> Dict[str, int]:
-        """{"<kernel> <BMxBN> z=<Z> split=<k> <form>": launches} since set_census(True)."""
+        """{"<kernel> <BMxBN> z=<Z> split=<k> <form>": launches} since set_census(True) (and, with timing on,
+        "ms|<shape>|n=<launches>": microseconds entries: get_gemm_shape_times)."""
         need = C.c_int64()
         self.lib.suta_get_census(None, 0, C.byref(need))
         buf = C.create_string_buffer(int(need.value))
@@ -347,4 +348,13 @@ class SutaEngine:
         for ln in buf.value.decode().splitlines():
             key, n = ln.rsplit(" ", 1)
             out[key] = int(n)
+        return out
+
+    def get_gemm_shape_times(self) -> Dict[str, tuple]:
+        """With the census and timing both on: {"M=.. N=.. K=.. z=.. <form> epi=..": (launches, total ms)}."""
+        out = {}
+        for k, v in self.get_census().items():
+            if k.startswith("ms|"):
+                _, shape, n = k.split("|")
+                out[shape] = (int(n[2:]), v / 1000.0)
         return out

@@ -133,8 +133,10 @@ def test_c4_bench_layout_bf16():
     bf16 GEMMs, the second call of the layout (every step a graph replay).  Slots 0 / 31 / 63 against the
     exact-fp32 engine adapting each utterance alone (bf16 tolerance of tests/parity.py: 2.5 % of max|ref|,
     greedy ids on >= 97 % of frames) at steps 0 / 1 / 5 / 20, and slot 0 against the CPU oracle at steps 0
-    and 20.  The launch census of the capturing call shows the schedules this layout reaches: the 256 x 128
-    one-plane bf16 tile and the per-utterance (Z = 64) weight-gradient GEMMs."""
+    and 20.  The launch census of the capturing call shows the schedules this layout reaches: the linears on
+    the bf16-plane kernel (hb), the conv stack's per-utterance (Z = 64) GEMMs on bf16 planes -- forward and
+    input gradients (conv-A rows, per-tap weight segments) on hb, weight gradients on the MN-contiguous hbt
+    kernel -- and the per-utterance feature-projection weight gradient."""
     from oracle import w2v2_cpu as W
     import os
     from tests.parity import BF16_LOGITS_RTOL_LARGE, assert_bf16_close
@@ -155,9 +157,12 @@ def test_c4_bench_layout_bf16():
     logits, ids, T = eng.adapt(torch.from_numpy(x).cuda(), S, hp, record=rec)   # replayed
     assert T == 399
     txt = "\n".join(f"{k}: {v}" for k, v in sorted(census.items()))
-    assert any(k.startswith("x6_1plane 256x128") for k in census), txt
+    print(txt)
+    assert any(k.startswith("hb ") and " z=1 " in k for k in census), txt
+    assert any(k.startswith("hb 128x128 z=64 ") and k.endswith(" conv-seg") for k in census), txt   # conv dX
+    assert any(k.startswith("hb ") and " z=64 " in k and "conv" not in k for k in census), txt     # conv forward
+    assert any(k.startswith("hbt ") and " z=64 " in k for k in census), txt                        # conv dW
     assert any(" z=64 " in k and k.startswith(("gbf", "x6_1plane")) for k in census), txt
-    assert any(k.startswith("hb ") for k in census), txt
     eng.set_precision("fp32")
     for slot in (0, 31, 63):
         ref, _, _ = eng.adapt(x[slot], S, hp, record=rec)
