@@ -19,6 +19,39 @@ __device__ __forceinline__ float dgelu_f(float x) {
     return cdf + x * pdf;
 }
 
+// Branch-free erf for the bf16-plane GEMM epilogues (config C4, whose outputs are rounded to bf16): erfc(z),
+// z = |x|, as t exp(-z^2 + P(t)), t = 1 / (1 + z / 2), with the 9-term Chebyshev fit of Numerical Recipes
+// 2nd ed. section 6.2 (fractional error < 1.2e-7 for every z >= 0).  ~18 VALU operations against ~40 for the
+// two-range erff; the exact-fp32 paths keep erff.
+__device__ __forceinline__ float erfc_t(float z, float t, float ez2) {  // ez2 = exp(-z^2)
+    float p = 0.17087277f;
+    p = fmaf(p, t, -0.82215223f);
+    p = fmaf(p, t, 1.48851587f);
+    p = fmaf(p, t, -1.13520398f);
+    p = fmaf(p, t, 0.27886807f);
+    p = fmaf(p, t, -0.18628806f);
+    p = fmaf(p, t, 0.09678418f);
+    p = fmaf(p, t, 0.37409196f);
+    p = fmaf(p, t, 1.00002368f);
+    p = fmaf(p, t, -1.26551223f);
+    return t * ez2 * __expf(p);
+}
+__device__ __forceinline__ float gelu_fast(float x) {
+    const float z = fabsf(x) * 0.70710678118654752f;
+    const float t = __builtin_amdgcn_rcpf(fmaf(0.5f, z, 1.0f));
+    const float erfc = erfc_t(z, t, __expf(-z * z));
+    // x Phi(x) = x (1 + erf(x / sqrt 2)) / 2, erf = sign(x) (1 - erfc)
+    return 0.5f * x * (x >= 0.f ? 2.0f - erfc : erfc);
+}
+__device__ __forceinline__ float dgelu_fast(float x) {
+    const float z = fabsf(x) * 0.70710678118654752f;
+    const float t = __builtin_amdgcn_rcpf(fmaf(0.5f, z, 1.0f));
+    const float e = __expf(-z * z);  // exp(-x^2 / 2): the normal density's exponential too
+    const float erfc = erfc_t(z, t, e);
+    const float cdf = 0.5f * (x >= 0.f ? 2.0f - erfc : erfc);
+    return cdf + x * (0.39894228040143268f * e);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -99,6 +132,12 @@ struct GemmParams {
     void* Cb;   // optional bf16 copy of the stored C (Z == 1): the A plane of the next bf16-plane GEMM
     long ldcb;
     int off32;  // internal: every epilogue operand (rows x ld) within 4 GiB -> 32-bit offset epilogue
+    // bf16-plane GEMMs (Cb given, gemm_hb_kernel, no split-K): C2 (EPI_STORE_PRE) and aux (EPI_DGELU) hold bf16
+    // elements (ld and batch strides in elements; ldc2 even) -- the FFN pre-activation u of config C4
+    int preb;
+    // internal: bf16-plane epilogues (Cb given) evaluate GELU / GELU' with gelu_fast / dgelu_fast (SUTA_FAST_GELU=0:
+    // erff, for A/B runs)
+    int fgelu;
 };
 
 void gemm_init(GemmParams& p);
@@ -111,6 +150,8 @@ void gemm_set_variant(int tile, int nbuf);
 void gemm_set_mode(int mode);
 // dst[r][0:K] = bf16(src[r * lds + 0:K]) (RNE) for r < rows; K % 8 == 0, src/lds 16-B aligned, dst 16-B aligned
 // with row stride K: the A plane of a bf16-plane GEMM.
+// the 128 x 128 bf16-plane GEMM specialised on its epilogue class (false: no class covers p.epi)
+bool gemm_run_hb_class(const GemmParams& p, dim3 grid, hipStream_t st);
 void launch_to_bf16(const float* src, long lds, long rows, int K, void* dst, hipStream_t st);
 // dst[z][n][k] = bf16(src[z * zs + k * N + n]) (per-slot transposed bf16 weights)
 void launch_transpose_bf16(const float* src, long zs, int Z, int K, int N, void* dst, hipStream_t st,

@@ -378,6 +378,20 @@ struct suta_engine {
         if (convwt.alloc(2 * tot)) drop_graph();
         return reinterpret_cast<char*>(convwt.p) + native * tot + off;
     }
+    // with bf16 planes, fp32 activations read only as a frozen linear's A operand are not written (the linear
+    // reads the plane; no weight gradient reads them): stable-LN outputs, gelu(FFN1), dU.  Only where every
+    // producer and consumer takes its plane path (the vectorised LayerNorm widths, K % 8 == 0).  One predicate
+    // for the forward and the backward.
+    bool fp32_acts_dead() const {
+        return use_planes() && (c.H == 512 || c.H == 768 || c.H == 1024) && c.F % 8 == 0;
+    }
+    // bf16 mode with planes: the FFN pre-activation u (stored by FFN1, read by the FFN2 input gradient's gelu')
+    // kept in bf16 (SUTA_PRE_BF16=0: fp32, for A/B runs)
+    bool pre_bf16() const {
+        if (!use_planes()) return false;
+        const char* e = std::getenv("SUTA_PRE_BF16");
+        return !(e && atoi(e) == 0);
+    }
     // conv input gradients on the bf16 planes too (SUTA_CONV_DX_PLANES=0: fp32-staged x6 kernels, for A/B runs)
     bool conv_dx_planes() const {
         if (!conv_planes()) return false;
@@ -786,10 +800,7 @@ void suta_engine::forward(int B) {
     // bf16 mode: producers of the linears' A operands also write bf16 planes (P0 / P1, ping-pong)
     void* P0 = plane(0);
     void* P1 = plane(1);
-    // with bf16 planes, fp32 activations read only as a frozen linear's A operand are not written (the linear
-    // reads the plane; no weight gradient reads them): stable-LN outputs and gelu(FFN1).  Only where every
-    // producer and consumer takes its plane path (the vectorised LayerNorm widths, K % 8 == 0).
-    const bool dead = P0 && (H == 512 || H == 768 || H == 1024) && k.F % 8 == 0;
+    const bool dead = fp32_acts_dead();  // (P0 non-null exactly then)
     for (int l = 0; l < k.L; ++l) {
         LayerBufs& lb = pl.lay[l];
         const float* attn_in = lb.x_in;
@@ -946,8 +957,9 @@ void suta_engine::forward(int B) {
             g.K = H;
             g.epi = EPI_BIAS | EPI_STORE_PRE | EPI_GELU;
             g.bias = b1[l];
-            g.C2 = lb.u;
+            g.C2 = lb.u;  // (dead: bf16 elements, the first half of the fp32 buffer)
             g.ldc2 = k.F;
+            g.preb = dead && pre_bf16();
             gemm(g);
         }
         {  // out = gu W2^T + b2 + residual
@@ -1036,9 +1048,10 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
     // Ab: bf16 plane of A written by its producer; Cb: bf16 plane of C for the next linear (bf16 mode)
     auto nn_gemm = [&](const float* A, int lda, const float* Bm, int ldb, float* C, int ldc, int M, int N, int K,
                        int epi, const float* R, int ldr, const float* aux, int ldaux, const void* Ab = nullptr,
-                       void* Cb = nullptr) {
+                       void* Cb = nullptr, int preb = 0) {
         GemmParams g;
         gemm_init(g);
+        g.preb = preb;
         g.A = A;
         g.lda = lda;
         g.Ab = Ab;
@@ -1063,7 +1076,7 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
     void* P1 = plane(1);
     // with bf16 planes (the forward's condition) dU = dH W2 * gelu'(u) is read only through its plane by the
     // FFN1 input-gradient GEMM (no weight gradient): its fp32 copy is not written
-    const bool dead = P0 && (H == 512 || H == 768 || H == 1024) && k.F % 8 == 0;
+    const bool dead = fp32_acts_dead();
     float* du32 = dead ? nullptr : pl.du;
     // d hfin = dlogits @ Wlm
     nn_gemm(pl.dlogits, k.V, wlm, H, pl.d1, H, (int)BT, H, k.V, 0, nullptr, 0, nullptr, 0);
@@ -1087,7 +1100,8 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
                                      nullptr, t1, G + o_l2g[l], G + o_l2b[l], Pn, pl.lnpart, st, P0);
             });
             // du = (dr2 @ W2) * gelu'(u)
-            nn_gemm(t1, H, w2[l], k.F, du32, k.F, (int)BT, k.F, H, EPI_DGELU, nullptr, 0, lb.u, k.F, P0, P1);
+            nn_gemm(t1, H, w2[l], k.F, du32, k.F, (int)BT, k.F, H, EPI_DGELU, nullptr, 0, lb.u, k.F, P0, P1,
+                    dead && pre_bf16());
             // dh1 = du @ W1 + dr2
             nn_gemm(du32, k.F, w1[l], H, t2, H, (int)BT, H, k.F, EPI_RESID, t1, H, nullptr, 0, P1);
             // dr1 = LN1 bwd(dh1)
@@ -1098,7 +1112,8 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
             dhres = t1;  // dr1
         } else {
             // du = (dx @ W2) * gelu'(u); dy2 = du @ W1; dhmid = LN2 bwd(dy2) + dx
-            nn_gemm(dx, H, w2[l], k.F, du32, k.F, (int)BT, k.F, H, EPI_DGELU, nullptr, 0, lb.u, k.F, P0, P1);
+            nn_gemm(dx, H, w2[l], k.F, du32, k.F, (int)BT, k.F, H, EPI_DGELU, nullptr, 0, lb.u, k.F, P0, P1,
+                    dead && pre_bf16());
             nn_gemm(du32, k.F, w1[l], H, t2, H, (int)BT, H, k.F, 0, nullptr, 0, nullptr, 0, P1);
             timed(F_NORM, [&] {
                 launch_layernorm_bwd(t2, lb.xhat2, lb.rstd2, P + o_l2g[l], P + o_l2b[l], Pn, T, B, H, 0, nullptr, dx,

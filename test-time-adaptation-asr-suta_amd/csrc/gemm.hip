@@ -215,6 +215,16 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
                (p.Z > 1 && ((p.sA0 | p.sA1 | p.sB0 | p.sB1) % 8))))
         throw std::invalid_argument("gemm: bf16 planes need K, ld and batch strides % 8 == 0 and 16-B alignment");
     const bool bf16_gbf = p.mode == 2 && glds_ok && p.ta;  // bf16 weight gradients: LDS-DMA fp32 stages
+    {
+        static int fg = -1;
+        if (fg < 0) {
+            const char* ev = std::getenv("SUTA_FAST_GELU");
+            fg = (ev && atoi(ev) == 0) ? 0 : 1;
+        }
+        p.fgelu = fg;
+    }
+    if (p.preb && (!hb || !p.Cb || (p.ldc2 & 1)))  // (gemm_hb8_kernel shares the epilogue)
+        throw std::invalid_argument("gemm: bf16 pre-activation operands need the bf16-plane kernel with a Cb plane, ldc2 even");
     if (hb && p.segK > 0 && (p.segK % 8 || p.pad < 0 || (p.segB && (p.sBseg % 8))))
         throw std::invalid_argument("gemm: conv-A bf16 planes need segK and the tap stride % 8 == 0");
     int tile = hbt || (hb && p.segK > 0) ? 0
@@ -235,7 +245,7 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
 
     // split-K when the grid cannot fill 256 CUs and K is long
     int splits = 1;
-    if (ws && p.K >= 1024 && blocks < 256 && tile != 6) {
+    if (ws && p.K >= 1024 && blocks < 256 && tile != 6 && !p.preb) {  // (the split-K reduce has no bf16 pre store)
         splits = (int)std::min<long>(16, (512 + blocks - 1) / blocks);
         while (splits > 1 && (long)splits * p.Z * p.M * (long)p.N > ws_floats) --splits;
         splits = std::min(splits, std::max(1, (p.K + 255) / 256));  // >= 256 K per split
@@ -281,13 +291,14 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
         census("hbt", BM, BN, p, splits);
         gemm_run_hbt(p, grid, st);
     } else if (hb) {
-        census(tile == 6 ? "hb8" : "hb", BM, BN, p, splits);
         static int hbns = -1;  // SUTA_HB_NS: stage variant of the 128 x 128 bf16-plane kernel (A/B runs; 2 default)
         if (hbns < 0) {
             const char* ev = std::getenv("SUTA_HB_NS");
             hbns = ev ? std::max(2, atoi(ev)) : 2;
         }
-        gemm_run_hb(tile, g_force_tile >= 0 ? g_nbuf : (tile == 0 ? hbns : 2), p, grid, st);
+        const int ns = g_force_tile >= 0 ? g_nbuf : (tile == 0 ? hbns : 2);
+        census(tile == 6 ? "hb8" : "hb", BM, BN, p, splits);
+        gemm_run_hb(tile, ns, p, grid, st);
     } else if (p.mode == 2) {
         // bf16: register-staged one-plane kernel; weight gradients (and benchmark variants 3 / 8) on
         // register-converted LDS-DMA stages (8 = BK64 x 2)

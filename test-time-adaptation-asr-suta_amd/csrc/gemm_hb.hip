@@ -43,6 +43,7 @@ void gemm_run_hb(int tile, int ns, const GemmParams& p, dim3 grid, hipStream_t s
         else launch_hb<64, 64, 3>(p, grid, st);
         return;
     }
+    if (tile == 0 && gemm_run_hb_class(p, grid, st)) return;
     if (tile == 0) launch_hb<128, 128, 2>(p, grid, st);
     else if (tile == 1) launch_hb<128, 64, 2>(p, grid, st);
     else if (tile == 2) launch_hb<64, 128, 2>(p, grid, st);

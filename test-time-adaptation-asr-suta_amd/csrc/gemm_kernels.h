@@ -208,10 +208,12 @@ __device__ __forceinline__ const T* byte_at(const T* base, unsigned off) {
     return reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + off);
 }
 
-template <int RM, int RN, bool CB>
+// EM: the epilogue flags a kernel instantiation can see (p.epi & EM; -1 = all): class-specialised kernels carry
+// only their own epilogue code
+template <int RM, int RN, bool CB, int EM = -1>
 __device__ __forceinline__ void gemm_epilogue_fast(const GemmParams& p, const f32x16 (&acc)[RM][RN], int z1, int z0,
                                                    int rbase, int cbase, int h, int l32) {
-    const int e = p.epi;
+    const int e = p.epi & EM;
     float* C = p.C ? p.C + z1 * p.sC1 + z0 * p.sC0 : nullptr;
     const float* bias = p.bias ? p.bias + z1 * p.sBias1 + z0 * p.sBias0 : nullptr;
     const float* aux = p.aux ? p.aux + z1 * p.sAux1 + z0 * p.sAux0 : nullptr;
@@ -231,6 +233,10 @@ __device__ __forceinline__ void gemm_epilogue_fast(const GemmParams& p, const f3
     const float alpha = p.alpha;
     const bool cbpair = CB && (p.ldcb & 1) == 0;
     const bool odd = l32 & 1;
+    const bool preb = CB && p.preb;  // bf16 pre-activation store / DGELU operand
+    const __bf16* auxh = preb && p.aux ? reinterpret_cast<const __bf16*>(p.aux) + z1 * p.sAux1 + z0 * p.sAux0 : nullptr;
+    __bf16* C2h = preb && p.C2 ? reinterpret_cast<__bf16*>(p.C2) + z1 * p.sC21 + z0 * p.sC20 : nullptr;
+    typedef __bf16 cb2 __attribute__((ext_vector_type(2)));
     constexpr int CH = 8;
 #pragma unroll
     for (int i = 0; i < RM; ++i)
@@ -243,11 +249,21 @@ __device__ __forceinline__ void gemm_epilogue_fast(const GemmParams& p, const f3
             const unsigned oa = 4u * (rb * (unsigned)p.ldaux + col);
             const unsigned o2 = 4u * (rb * (unsigned)p.ldc2 + col);
             const unsigned ob = 2u * ((rb + (odd ? 1u : 0u)) * (unsigned)p.ldcb + (col & ~1u));
+            const unsigned oah = 2u * (rb * (unsigned)p.ldaux + col);
+            const unsigned o2h = 2u * ((rb + (odd ? 1u : 0u)) * (unsigned)p.ldc2 + (col & ~1u));
             const float bj = (e & EPI_BIAS) ? bias[col] : 0.f;
 #pragma unroll
             for (int r0 = 0; r0 < 16; r0 += CH) {
                 float v[CH], xa[CH], xq[CH];
-                if (e & (EPI_DGELU | EPI_SMBWD)) {
+                // (the bf16 / fp32 choice is hoisted out of the element loop: a per-element select branches around
+                // every load and waits for each one)
+                if ((e & EPI_DGELU) && preb) {
+#pragma unroll
+                    for (int r = 0; r < CH; ++r) {
+                        const int ro = ((r0 + r) & 3) + 8 * ((r0 + r) >> 2);
+                        xa[r] = (float)*byte_at(auxh + ro * p.ldaux, oah);
+                    }
+                } else if (e & (EPI_DGELU | EPI_SMBWD)) {
 #pragma unroll
                     for (int r = 0; r < CH; ++r) {
                         const int ro = ((r0 + r) & 3) + 8 * ((r0 + r) >> 2);
@@ -275,18 +291,37 @@ __device__ __forceinline__ void gemm_epilogue_fast(const GemmParams& p, const f3
 #pragma unroll
                         for (int r = 0; r < CH; ++r) v[r] += xq[r];
                     }
-                    if (e & EPI_STORE_PRE) {
+                    if ((e & EPI_STORE_PRE) && preb) {
+                        // (column, column + 1) bf16 pairs, as the Cb store below
+#pragma unroll
+                        for (int r = 0; r < CH; r += 2) {
+                            const int ro = ((r0 + r) & 3) + 8 * ((r0 + r) >> 2);
+                            const float a = v[r], b = v[r + 1];
+                            const float q = __int_as_float(
+                                __builtin_amdgcn_mov_dpp(__float_as_int(odd ? a : b), 0xB1, 0xF, 0xF, false));
+                            cb2 pr;
+                            pr[0] = (__bf16)(odd ? q : a);
+                            pr[1] = (__bf16)(odd ? b : q);
+                            *reinterpret_cast<cb2*>(byte_at(C2h + ro * p.ldc2, o2h)) = pr;
+                        }
+                    } else if (e & EPI_STORE_PRE) {
 #pragma unroll
                         for (int r = 0; r < CH; ++r) {
                             const int ro = ((r0 + r) & 3) + 8 * ((r0 + r) >> 2);
                             *byte_at(C2 + ro * p.ldc2, o2) = v[r];
                         }
                     }
-                    if (e & EPI_GELU) {
+                    if ((e & EPI_GELU) && CB && p.fgelu) {  // (uniform choice hoisted out of the element loop)
+#pragma unroll
+                        for (int r = 0; r < CH; ++r) v[r] = gelu_fast(v[r]);
+                    } else if (e & EPI_GELU) {
 #pragma unroll
                         for (int r = 0; r < CH; ++r) v[r] = gelu_f(v[r]);
                     }
-                    if (e & EPI_DGELU) {
+                    if ((e & EPI_DGELU) && CB && p.fgelu) {  // (uniform choice hoisted out of the element loop)
+#pragma unroll
+                        for (int r = 0; r < CH; ++r) v[r] *= dgelu_fast(xa[r]);
+                    } else if (e & EPI_DGELU) {
 #pragma unroll
                         for (int r = 0; r < CH; ++r) v[r] *= dgelu_f(xa[r]);
                     }
@@ -310,7 +345,6 @@ __device__ __forceinline__ void gemm_epilogue_fast(const GemmParams& p, const f3
                     }
                 }
                 if (CB) {
-                    typedef __bf16 cb2 __attribute__((ext_vector_type(2)));
                     __bf16* Cb = reinterpret_cast<__bf16*>(p.Cb);
                     if (cbpair) {
                         // (column, column + 1) pairs: lanes 2i / 2i + 1 swap one value (DPP quad_perm [1,0,3,2]);
@@ -344,7 +378,7 @@ __device__ __forceinline__ void gemm_epilogue_fast(const GemmParams& p, const f3
 // indices so they are unpredicated, and every operand of a fragment is in registers before its first
 // store (C may alias aux / R in place).  Only the stores are predicated, and only on edge tiles.
 // gemm_launch guarantees RESID, ACCUM and SMBWD are mutually exclusive (they share xq).
-template <int RM, int RN, bool CB = false>
+template <int RM, int RN, bool CB = false, int EM = -1>
 __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, const f32x16 (&acc)[RM][RN], int z1, int z0,
                                               int rbase, int cbase, int h, int l32, bool interior, int tz) {
     if (p.splits > 1) {
@@ -362,15 +396,18 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, const f32x16 
         return;
     }
     if (interior && p.off32) {
-        gemm_epilogue_fast<RM, RN, CB>(p, acc, z1, z0, rbase, cbase, h, l32);
+        gemm_epilogue_fast<RM, RN, CB, EM>(p, acc, z1, z0, rbase, cbase, h, l32);
         return;
     }
-    const int e = p.epi;
+    const int e = p.epi & EM;
     float* C = p.C + z1 * p.sC1 + z0 * p.sC0;
     const float* bias = p.bias ? p.bias + z1 * p.sBias1 + z0 * p.sBias0 : nullptr;
     const float* aux = p.aux ? p.aux + z1 * p.sAux1 + z0 * p.sAux0 : nullptr;
     const int rlim = (e & EPI_ROWMASK) ? p.zrows[z1] : p.M;
     float* C2 = p.C2 ? p.C2 + z1 * p.sC21 + z0 * p.sC20 : nullptr;
+    const bool preb = CB && p.preb;  // bf16 pre-activation store / DGELU operand
+    const __bf16* auxh = preb && p.aux ? reinterpret_cast<const __bf16*>(p.aux) + z1 * p.sAux1 + z0 * p.sAux0 : nullptr;
+    __bf16* C2h = preb && p.C2 ? reinterpret_cast<__bf16*>(p.C2) + z1 * p.sC21 + z0 * p.sC20 : nullptr;
     // second operand: R (RESID), old C (ACCUM) or the row vector (SMBWD)
     const float* Q = nullptr;
     long ldq = 0, colq = 1;
@@ -399,7 +436,14 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, const f32x16 
                 const int col = cbase + j * 32 + l32;
                 const long colc = min(col, p.N - 1);
                 float v[CH], xa[CH], xq[CH];
-                if (e & (EPI_DGELU | EPI_SMBWD)) {
+                if ((e & EPI_DGELU) && preb) {
+#pragma unroll
+                    for (int r = 0; r < CH; ++r) {
+                        const int rr = r0 + r;
+                        const long row = min(rbase + i * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * h, p.M - 1);
+                        xa[r] = (float)auxh[row * p.ldaux + colc];
+                    }
+                } else if (e & (EPI_DGELU | EPI_SMBWD)) {
 #pragma unroll
                     for (int r = 0; r < CH; ++r) {
                         const int rr = r0 + r;
@@ -435,14 +479,23 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, const f32x16 
                         for (int r = 0; r < CH; ++r) {
                             const int rr = r0 + r;
                             const int row = rbase + i * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * h;
-                            if (interior || (row < p.M && col < p.N)) C2[(long)row * p.ldc2 + col] = v[r];
+                            if (interior || (row < p.M && col < p.N)) {
+                                if (preb) C2h[(long)row * p.ldc2 + col] = (__bf16)v[r];
+                                else C2[(long)row * p.ldc2 + col] = v[r];
+                            }
                         }
                     }
-                    if (e & EPI_GELU) {
+                    if ((e & EPI_GELU) && CB && p.fgelu) {  // (uniform choice hoisted out of the element loop)
+#pragma unroll
+                        for (int r = 0; r < CH; ++r) v[r] = gelu_fast(v[r]);
+                    } else if (e & EPI_GELU) {
 #pragma unroll
                         for (int r = 0; r < CH; ++r) v[r] = gelu_f(v[r]);
                     }
-                    if (e & EPI_DGELU) {
+                    if ((e & EPI_DGELU) && CB && p.fgelu) {  // (uniform choice hoisted out of the element loop)
+#pragma unroll
+                        for (int r = 0; r < CH; ++r) v[r] *= dgelu_fast(xa[r]);
+                    } else if (e & EPI_DGELU) {
 #pragma unroll
                         for (int r = 0; r < CH; ++r) v[r] *= dgelu_f(xa[r]);
                     }
@@ -1481,7 +1534,9 @@ void launch_tile(const GemmParams& p, dim3 grid, hipStream_t st) {
 // NWV = 4 waves (2 x 2) or 8 waves (2 x 4, the 256 x 256 tile: 128 x 64 per wave, 128 KB of LDS)
 // CONV / SEGB: the conv input-gradient form (conv-A rows of A, per-tap B segments; glds_stage modes 1 / 2 in
 // 4-byte units: segK, pad, sBseg given in bf16 elements, even)
-template <int BM, int BN, int NS, int BKS = 32, int NWV = 4, bool CONV = false, bool SEGB = false>  // BKS: 4-byte units
+// CBT: -1 = the bf16 C plane chosen at run time (p.Cb), 0 / 1 = fixed; EM: epilogue flag class (gemm_epilogue)
+template <int BM, int BN, int NS, int BKS = 32, int NWV = 4, bool CONV = false, bool SEGB = false, int CBT = -1,
+          int EM = -1>  // BKS: 4-byte units
 __global__ __launch_bounds__(64 * NWV, (BM * BN > 128 * 128 || BKS > 32) ? 1 : 2) void gemm_hb_kernel(GemmParams p) {
     constexpr int WNW = NWV / 2;                 // waves along N
     constexpr int WTM = BM / 2, WTN = BN / WNW;
@@ -1578,17 +1633,18 @@ __global__ __launch_bounds__(64 * NWV, (BM * BN > 128 * 128 || BKS > 32) ? 1 : 2
     }
     wait_vm<0>();
     // only the bf16-plane GEMMs write a bf16 copy of C (the template keeps the other kernels' epilogue as it was)
-    if (p.Cb)
-        gemm_epilogue<RM, RN, true>(p, acc, z1, z0, m0 + wm * WTM, n0 + wn * WTN, h, l32,
-                                    m0 + BM <= p.M && n0 + BN <= p.N, tid.z);
+    if (CBT == 1 || (CBT < 0 && p.Cb))
+        gemm_epilogue<RM, RN, true, EM>(p, acc, z1, z0, m0 + wm * WTM, n0 + wn * WTN, h, l32,
+                                        m0 + BM <= p.M && n0 + BN <= p.N, tid.z);
     else
-        gemm_epilogue<RM, RN, false>(p, acc, z1, z0, m0 + wm * WTM, n0 + wn * WTN, h, l32,
-                                     m0 + BM <= p.M && n0 + BN <= p.N, tid.z);
+        gemm_epilogue<RM, RN, false, EM>(p, acc, z1, z0, m0 + wm * WTM, n0 + wn * WTN, h, l32,
+                                         m0 + BM <= p.M && n0 + BN <= p.N, tid.z);
 }
 
-template <int BM, int BN, int NS, int BKS = 32, int NWV = 4, bool CONV = false, bool SEGB = false>
+template <int BM, int BN, int NS, int BKS = 32, int NWV = 4, bool CONV = false, bool SEGB = false, int CBT = -1,
+          int EM = -1>
 void launch_hb(const GemmParams& p, dim3 grid, hipStream_t st) {
-    hipLaunchKernelGGL((gemm_hb_kernel<BM, BN, NS, BKS, NWV, CONV, SEGB>), grid, dim3(64 * NWV), 0, st, p);
+    hipLaunchKernelGGL((gemm_hb_kernel<BM, BN, NS, BKS, NWV, CONV, SEGB, CBT, EM>), grid, dim3(64 * NWV), 0, st, p);
 }
 
 // 256 x 256 bf16-plane GEMM on one block per CU with a ping-pong schedule (cdna_hip_programming.md,

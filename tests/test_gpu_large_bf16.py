@@ -326,3 +326,28 @@ def test_conv_stack_on_bf16_planes_equals_fp32_staged(monkeypatch):
         for u in range(2):
             assert_bf16_close(out["1"][r][u], out["0"][r][u], 0.97, f"conv planes step {r} utt {u}",
                               rtol=BF16_LOGITS_RTOL_LARGE)
+
+
+@pytest.mark.parametrize("model", ["wav2vec2-large", "wav2vec2-base"])
+def test_ffn_preactivation_bf16_equals_fp32(monkeypatch, model):
+    """bf16 mode: the FFN pre-activation u stored in bf16 by the FFN1 GEMM epilogue and read back in bf16 by the
+    FFN2 input gradient's gelu' (default) against u kept in fp32 (SUTA_PRE_BF16=0).  Stable-LN (large) and
+    post-LN (base) layer paths, ragged pair: adapted logits agree to the bf16 tolerance; reruns bitwise."""
+    cfg = get_config(model)
+    eng = SutaEngine(cfg, synth_weights(cfg), max_batch=2, max_samples=48000)
+    eng.set_precision("bf16")
+    eng.set_graphs(False)  # eager: a replayed graph would keep the kernels it was captured with
+    waves = [synth.wave(48000, 94), synth.wave(30400, 95)]
+    out = {}
+    for pb in ("1", "0"):
+        monkeypatch.setenv("SUTA_PRE_BF16", pb)
+        a, _, _ = eng.adapt_varlen(waves, 3, SutaHParams(), record=[0, 3])
+        b, _, _ = eng.adapt_varlen(waves, 3, SutaHParams(), record=[0, 3])
+        for u in range(2):
+            assert np.array_equal(a[3][u], b[3][u]), (pb, u)
+        out[pb] = a
+    eng.close()
+    rtol = BF16_LOGITS_RTOL_LARGE if model == "wav2vec2-large" else BF16_LOGITS_RTOL_BASE
+    for u in range(2):
+        np.testing.assert_array_equal(out["1"][0][u], out["0"][0][u])  # step 0: the forward does not read u
+        assert_bf16_close(out["1"][3][u], out["0"][3][u], 0.97, f"pre bf16 step 3 utt {u}", rtol=rtol)
