@@ -16,6 +16,16 @@
  *                      (STREAMINFO; 0 = unknown) — the driver's LPT cost model uses it
  *   suta_flac_decode   decode a whole in-memory file
  *
+ * MPEG-1 / 2 / 2.5 audio Layer III (CommonVoice clips/<name>.mp3, reference corpus/commonvoice.py:32-38 via
+ * torchaudio.load at reference data.py:15), decoded from ISO/IEC 11172-3 / 13818-3 (csrc/mp3.cpp): bit
+ * reservoir, MPEG-1 and LSF scale factors, all Huffman tables, long / short / mixed blocks, mid/side and
+ * intensity stereo, IMDCT and polyphase synthesis in double precision.  torchaudio's MP3 backend is FFmpeg, so
+ * the output follows FFmpeg: float32 in the decoder's native scale, the Xing / Info frame not decoded, and with an
+ * encoder tag (LAME / Lavf / Lavc) the first enc_delay + 529 and the last max(0, enc_padding - 529) samples
+ * dropped (gapless).  Free-format streams and Layers I / II are refused (SUTA_AUDIO_ERR_FORMAT).
+ *   suta_mp3_info      header walk only: sample rate, channels, samples per channel after trimming
+ *   suta_mp3_decode    decode a whole in-memory file
+ *
  * Conventions: plain pointers and sizes, int32 status codes (0 = OK), a thread-local message via
  * suta_audio_last_error().  Thread-safe: no global state besides the per-thread message, so a loader
  * may decode several files concurrently (ctypes releases the GIL during the call).
@@ -45,6 +55,19 @@ int32_t suta_flac_info(const uint8_t* buf, int64_t len, int32_t* sample_rate, in
  * requirement in *n_out).  verify_crc != 0 checks every frame's CRC-8 and CRC-16. */
 int32_t suta_flac_decode(const uint8_t* buf, int64_t len, float* out, int64_t out_capacity,
                          int32_t verify_crc, int64_t* n_out);
+
+/* Frame walk of the MP3 file in buf[0..len): sample rate, channels and the samples per channel that
+ * suta_mp3_decode will return. */
+int32_t suta_mp3_info(const uint8_t* buf, int64_t len, int32_t* sample_rate, int32_t* channels,
+                      int64_t* total_samples);
+
+/* Decode every frame into out (float32, channels x out_capacity, channel-major as suta_flac_decode).
+ * strict != 0: SUTA_AUDIO_ERR_FORMAT when a granule's Huffman data runs past its part2_3_length (a damaged or
+ * mis-parsed stream; decoders otherwise drop the crossing count1 quadruple).  stats (may be NULL) receives
+ * 5 int64: frames decoded, granule-channels, of those ending exactly at part2_3_length, overrunning it, and
+ * frames whose bit reservoir was not available (decoded as silence). */
+int32_t suta_mp3_decode(const uint8_t* buf, int64_t len, float* out, int64_t out_capacity, int32_t strict,
+                        int64_t* n_out, int64_t* stats);
 
 const char* suta_audio_last_error(void);
 

@@ -245,6 +245,11 @@ const int kBps[8] = {0, 8, 12, -1, 16, 20, 24, 32};
 
 }  // namespace
 
+// shared with mp3.cpp (the other decoder of libsuta_audio.so): one per-thread message for both
+namespace suta_audio_internal {
+void set_error(const char* msg) { g_err = msg; }
+}  // namespace suta_audio_internal
+
 extern "C" {
 
 int32_t suta_flac_info(const uint8_t* buf, int64_t len, int32_t* sample_rate, int32_t* channels,

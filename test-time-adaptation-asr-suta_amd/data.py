@@ -10,8 +10,8 @@ Behaviour kept from the reference:
     add extra_noise * N(0, 1) noise
   * collate (data.py:27-45): sort a bucket by audio length, descending
 Deviations (documented in DESIGN.md): torchaudio/soundfile are not installed in this image, so FLAC
-is decoded by the from-spec decoder in libsuta_audio (csrc/flac.cpp), WAV by the standard-library
-`wave` module, and resampling restates torchaudio's Hann-windowed sinc resampler (`resample`).  The
+and MP3 (CommonVoice clips) are decoded by the from-spec decoders in libsuta_audio (csrc/flac.cpp,
+csrc/mp3.cpp), WAV by the standard-library `wave` module, and resampling restates torchaudio's Hann-windowed sinc resampler (`resample`).  The
 noise of utterance i comes from its own torch.Generator seeded `seed * 1_000_003 + i` (i = its index in
 the sorted dataset), so every rank of a sharded run draws exactly the audio a single process draws
 (the reference's draw depends on DataLoader worker seeding and on transformers consuming the global
@@ -183,7 +183,7 @@ AUDIO_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsu
 
 
 def _audio_lib():
-    """libsuta_audio.so (include/suta_audio.h): the from-spec FLAC decoder, host C++."""
+    """libsuta_audio.so (include/suta_audio.h): the from-spec FLAC and MP3 decoders, host C++."""
     global _AUDIO_LIB
     if _AUDIO_LIB is None:
         import ctypes as C
@@ -195,6 +195,10 @@ def _audio_lib():
         lib.suta_flac_info.restype = C.c_int32
         lib.suta_flac_decode.argtypes = [u8p, C.c_int64, C.POINTER(C.c_float), C.c_int64, C.c_int32, i64p]
         lib.suta_flac_decode.restype = C.c_int32
+        lib.suta_mp3_info.argtypes = [u8p, C.c_int64, i32p, i32p, i64p]
+        lib.suta_mp3_info.restype = C.c_int32
+        lib.suta_mp3_decode.argtypes = [u8p, C.c_int64, C.POINTER(C.c_float), C.c_int64, C.c_int32, i64p, i64p]
+        lib.suta_mp3_decode.restype = C.c_int32
         lib.suta_audio_last_error.restype = C.c_char_p
         _AUDIO_LIB = lib
     return _AUDIO_LIB
@@ -244,11 +248,48 @@ def flac_decode(src, verify_crc: bool = True) -> Tuple[np.ndarray, int]:
     return out[:, :n.value], sr.value
 
 
+def mp3_info(src):
+    """(sample_rate, channels, samples per channel after FFmpeg's gapless trim) by a header walk."""
+    import ctypes as C
+    lib = _audio_lib()
+    buf = np.frombuffer(_as_bytes(src), dtype=np.uint8)
+    sr, ch, n = C.c_int32(), C.c_int32(), C.c_int64()
+    st = lib.suta_mp3_info(buf.ctypes.data_as(C.POINTER(C.c_uint8)), buf.size, C.byref(sr), C.byref(ch), C.byref(n))
+    if st:
+        raise RuntimeError(f"MP3: {lib.suta_audio_last_error().decode()}")
+    return sr.value, ch.value, n.value
+
+
+def mp3_decode(src, strict: bool = False, stats: bool = False):
+    """torchaudio.load semantics for an MPEG audio Layer III file (reference data.py:15 on CommonVoice
+    clips/*.mp3, corpus/commonvoice.py:32-38): ((C, N) float32, sample_rate), FFmpeg's decoder delay and
+    gapless trimming.  strict: fail on Huffman data that runs past part2_3_length.  stats=True also returns
+    [frames, granule-channels, ending exactly at part2_3_length, overrunning, without bit reservoir]."""
+    import ctypes as C
+    lib = _audio_lib()
+    buf = np.frombuffer(_as_bytes(src), dtype=np.uint8)
+    bp = buf.ctypes.data_as(C.POINTER(C.c_uint8))
+    sr, ch, total = mp3_info(buf.tobytes())
+    cap = max(1, total)
+    out = np.empty((ch, cap), np.float32)
+    n = C.c_int64()
+    st_arr = np.zeros(5, np.int64)
+    st = lib.suta_mp3_decode(bp, buf.size, out.ctypes.data_as(C.POINTER(C.c_float)), cap, int(strict), C.byref(n),
+                             st_arr.ctypes.data_as(C.POINTER(C.c_int64)))
+    if st:
+        raise RuntimeError(f"MP3: {lib.suta_audio_last_error().decode()}")
+    res = (out[:, :n.value], sr)
+    return res + (st_arr,) if stats else res
+
+
 def audio_info(path: str) -> Tuple[int, int]:
-    """(samples per channel, sample rate) from the file header without decoding (WAV, FLAC), or by
+    """(samples per channel, sample rate) from the file header without decoding (WAV, FLAC, MP3), or by
     decoding for other formats.  The driver's LPT cost model uses it."""
     p = str(path)
     low = p.lower()
+    if low.endswith(".mp3"):
+        sr, ch, n = mp3_info(p)
+        return n, sr
     if low.endswith(".flac"):
         sr, ch, bps, n = flac_info(p)
         if n > 0:
@@ -270,6 +311,8 @@ def decoded_length(path: str, max_len: int = MAX_LEN) -> int:
     if p.lower().endswith(".flac"):
         sr, ch, bps, n = flac_info(p)
         per = n
+    elif p.lower().endswith(".mp3"):
+        sr, ch, per = mp3_info(p)
     elif p.lower().endswith(".wav"):
         with _wave.open(p, "rb") as f:
             sr, ch, per = f.getframerate(), f.getnchannels(), f.getnframes()
@@ -290,13 +333,15 @@ def _decode_audio(path: str) -> Tuple[np.ndarray, int]:
 
 
 def decode_channels(path: str) -> Tuple[np.ndarray, int]:
-    """torchaudio.load(path) (reference data.py:15): ((C, N) float32, sample rate).  FLAC: libsuta_audio;
-    WAV: the standard library; anything else (CommonVoice MP3) needs soundfile or torchaudio, neither of
+    """torchaudio.load(path) (reference data.py:15): ((C, N) float32, sample rate).  FLAC and MP3:
+    libsuta_audio; WAV: the standard library; anything else needs soundfile or torchaudio, neither of
     which is in this image."""
     path = str(path)
     low = path.lower()
     if low.endswith(".flac"):
         return flac_decode(path)
+    if low.endswith(".mp3"):
+        return mp3_decode(path)
     if not low.endswith(".wav"):
         try:
             import soundfile as sf
@@ -310,7 +355,7 @@ def decode_channels(path: str) -> Tuple[np.ndarray, int]:
             return w.numpy().astype(np.float32), sr
         except ImportError:
             pass
-        raise RuntimeError(f"cannot decode {path}: FLAC and WAV are built in; other formats need soundfile or "
+        raise RuntimeError(f"cannot decode {path}: FLAC, MP3 and WAV are built in; other formats need soundfile or "
                            "torchaudio (not installed)")
     with _wave.open(path, "rb") as f:
         sr, ch, sw, n = f.getframerate(), f.getnchannels(), f.getsampwidth(), f.getnframes()

@@ -3,12 +3,15 @@
 * chime(root): CHiME-3 enhanced 16 kHz WAVs + .trn transcripts (reference corpus/CHiME.py:9-49)
 * librispeech(root): LibriSpeech test-other FLAC files + <spk>-<chapter>.trans.txt
   (reference corpus/librispeech.py:8-39), encoded by tests/flac_spec_encoder.py
+* commonvoice(root): CommonVoice test.tsv + clips/*.mp3 (reference corpus/commonvoice.py:27-42), MPEG-1
+  Layer III 44.1 kHz mono frames written by tests/mp3_builder.py
 """
 import wave
 
 import numpy as np
 
 from tests import flac_spec_encoder as E
+from tests import mp3_builder as M
 
 WORDS = ["HELLO", "WORLD", "THE", "CAT", "SAT", "ON", "A", "MAT"]
 
@@ -63,3 +66,21 @@ def ted(root, lengths=(170000, 260000, 600000, 640000), seed=13):
             f.setframerate(16000)
             f.writeframes((np.clip(x, -1, 1) * 32767).astype("<i2").tobytes())
         (tpath / f"talk{i}.txt").write_text(" ".join(rng.choice(WORDS, size=4 + 3 * i)) + "\n")
+
+
+def commonvoice(root, frames=(4, 7, 5, 9, 3), seed=14):
+    """test.tsv (client_id, path, sentence, ...) and clips/<name>.mp3; sentences with the punctuation and
+    abbreviations preprocess_cv_text rewrites (corpus/commonvoice.py:12-24)."""
+    rng = np.random.default_rng(seed)
+    (root / "clips").mkdir(parents=True)
+    rows = ["client_id\tpath\tsentence\tup_votes\tdown_votes"]
+    for i, nf in enumerate(frames):
+        data = b"".join(M.write_frame([[M.random_granule(rng, int(rng.choice([0, 0, 1, 2, 3])))] for _ in range(2)], 1)
+                        for _ in range(nf))
+        name = f"common_voice_en_{1000 + i}.mp3"
+        (root / "clips" / name).write_bytes(data)
+        words = list(rng.choice(WORDS, size=2 + i))
+        words[0] = words[0].capitalize() + ","
+        sentence = " ".join(words) + (" e.g. Dr. Who-ever." if i % 2 else ".")
+        rows.append(f"c{i}\t{name}\t{sentence}\t2\t0")
+    (root / "test.tsv").write_text("\n".join(rows) + "\n")

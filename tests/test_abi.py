@@ -60,11 +60,12 @@ AUDIO_HEADER = os.path.join(REPO, "include", "suta_audio.h")
 
 
 def test_audio_library_exports_every_symbol():
-    """libsuta_audio.so (host FLAC decoder) exports what include/suta_audio.h declares."""
+    """libsuta_audio.so (host FLAC and MP3 decoders) exports what include/suta_audio.h declares."""
     from suta_amd import data as D
     src = re.sub(r"/\*.*?\*/", "", open(AUDIO_HEADER).read(), flags=re.S)
     names = sorted(set(re.findall(r"\b(suta_[a-z_0-9]+)\s*\(", src)))
-    assert names == ["suta_audio_last_error", "suta_flac_decode", "suta_flac_info"]
+    assert names == ["suta_audio_last_error", "suta_flac_decode", "suta_flac_info", "suta_mp3_decode",
+                     "suta_mp3_info"]
     lib = ctypes.CDLL(D.AUDIO_LIB_PATH)
     for name in names:
         assert hasattr(lib, name), name

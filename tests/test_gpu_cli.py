@@ -168,6 +168,28 @@ def test_cli_librispeech_flac_ls_flags(tmp_path, capsys):
     assert per(o2[0]) == per(out) and per(o2[1]) == [] and "[INFO]" not in o2[1]
 
 
+def test_cli_commonvoice_mp3_cv_flags(tmp_path, capsys):
+    """scripts/CV.sh flags on a CommonVoice-layout corpus (test.tsv + clips/*.mp3, MPEG-1 Layer III 44.1 kHz decoded
+    by libsuta_audio's MP3 decoder and resampled to 16 kHz), w2v2-base shapes with seeded weights: corpus WER counts
+    equal the CPU oracle's on the same decoded audio, in-process and as 2 gloo ranks sharing device 0."""
+    from tests import corpus_fixtures as CF
+    from tests.multirank import run_ranks
+    from suta_amd.data import CVDataset
+    CF.commonvoice(tmp_path)
+    args = (f"--asr facebook/wav2vec2-base-960h --synthetic_weights --steps 10 --dataset_name commonvoice "
+            f"--dataset_dir {tmp_path} --temp 2.5 --episodic --em_coef 0.3 --reweight --log_dir {tmp_path}/exps "
+            f"--lr 2e-5 --non_blank --train_feature --extra_noise 0").split()
+    counts = M.main(args)
+    out = capsys.readouterr().out
+    assert out.count("original WER: ") >= 5 and "TTA-10 WER:" in out
+    ds = CVDataset(None, 1, str(tmp_path))
+    ref = _oracle_counts(ds.file_list, ds.text, "wav2vec2-base", 10, 2e-5)
+    for k, v in ref.items():
+        assert tuple(counts[str(k)]) == v, k
+    c2, _ = run_ranks(2, args + "--gpu_batch 2 --device 0 --dist_backend gloo".split(), tmp_path, fake=False)
+    assert c2[0] == c2[1] == {k: tuple(v) for k, v in counts.items()}
+
+
 def test_cli_chime_base_world2(tmp_path, capsys):
     """Config C3 (w2v2-base on the CHiME layout, utterance-sharded): 2 gloo ranks on device 0 give the
     world-1 counts, which equal the oracle's."""

@@ -175,7 +175,7 @@ def _per_utt_lines(out):
 
 
 @pytest.mark.parametrize("corpus,noise", [("chime", 0.0), ("librispeech", 0.0), ("librispeech", 0.01),
-                                          ("chime", 0.01)])
+                                          ("chime", 0.01), ("commonvoice", 0.01)])
 def test_driver_world2_gloo_equals_world1(tmp_path, corpus, noise):
     """The real driver (suta_amd/main.py) as 2 gloo ranks with a deterministic stand-in engine whose ids
     depend on every sample it is given: LPT sharding by decoded length, the count all_reduce and the
@@ -187,6 +187,9 @@ def test_driver_world2_gloo_equals_world1(tmp_path, corpus, noise):
     if corpus == "chime":
         CF.chime(tmp_path, n=5)
         flags = f"--dataset_name chime --dataset_dir {tmp_path}"
+    elif corpus == "commonvoice":
+        CF.commonvoice(tmp_path)
+        flags = f"--dataset_name commonvoice --dataset_dir {tmp_path}"
     else:
         CF.librispeech(tmp_path)
         flags = f"--dataset_name librispeech --dataset_dir {tmp_path}"
