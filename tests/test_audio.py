@@ -237,3 +237,19 @@ def test_threaded_loader_equals_serial(tmp_path):
     assert [i for i, _ in a] == [i for i, _ in b] == list(range(6))
     for (_, x), (_, y) in zip(a, b):
         assert x[2] == y[2] and np.array_equal(x[1][0], y[1][0])
+
+
+def test_flac_rfc9639_example_1_known_answer():
+    """RFC 9639 Appendix D.1 (decoding example 1), the byte-exact stream of the specification: a stereo 16-bit
+    44.1 kHz file of one sample per channel.  Its frame-header CRC-8 and frame CRC-16 pass, it decodes to the
+    samples the RFC states (25588, 10416), and the MD5 of the decoded samples equals the one in its STREAMINFO,
+    so the stream typed here is the RFC's own (a typing slip would fail a CRC or the MD5)."""
+    import hashlib
+    import struct
+    stream = bytes.fromhex("664c6143800000221000100000000f00000f0ac442f0000000013e84b41807dc690307586a3dad1a2e0f"
+                           "fff869180000bf0358fd03128baa9a")
+    x, sr = D.flac_decode(stream, verify_crc=True)
+    assert sr == 44100 and x.shape == (2, 1)
+    ints = [int(round(v * 32768)) for v in x[:, 0]]
+    assert ints == [25588, 10416]
+    assert hashlib.md5(struct.pack("<2h", *ints)).digest() == stream[26:42]
