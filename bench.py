@@ -42,6 +42,8 @@ PMC_TRAFFIC = next((p for p in (os.path.join(ROOT, "profiles", r, "pmc_traffic.j
 PMC_TRAFFIC_C4 = next((p for p in (os.path.join(ROOT, "profiles", r, f) for r, f in
                                    (("r3", "pmc_traffic_c4.json"), ("r2", "close_pmc_traffic_c4.json")))
                        if os.path.exists(p)), None)
+BATCH = 164      # utterances per engine call (see --batch)
+PMC_BATCH = 164  # the batch the committed PMC passes (profiles/r3/pmc_traffic*.json) were taken at
 GEMM_KERNELS = ("gemm_glds_kernel", "gemm_f32_kernel", "gemm_splitk_reduce", "attn_fwd_kernel", "attn_bwd_kernel",
                 "posconv_kernel", "flash_fwd_kernel", "flash_bwd_kernel", "flash_dq_reduce")
 # config C4's GEMM family (bf16 mode): every kernel its "gemm" + "attention" timing families launch
@@ -53,8 +55,8 @@ FRONT_KERNELS = ("conv0_gn_kernel", "col_stats_final", "gn_bwd_final", "conv0_dw
 
 
 def pmc(args):
-    """The committed PMC reduction when this run is its workload (w2v2-base, 64 x 8 s, 10 steps)."""
-    if not (args.model == "wav2vec2-base" and args.batch == 64 and args.n_samples == 128000 and args.suta_steps == 10
+    """The committed PMC reduction when this run is its workload (w2v2-base, PMC_BATCH x 8 s, 10 steps)."""
+    if not (args.model == "wav2vec2-base" and args.batch == PMC_BATCH and args.n_samples == 128000 and args.suta_steps == 10
             and PMC_TRAFFIC):
         return None
     return json.load(open(PMC_TRAFFIC))
@@ -150,7 +152,7 @@ def bench_c4(args, dev):
                            "launches": int(gn), "avg_launch_ms": round(gms / max(1, gn), 5)}
         gx, ax = tex["gemm"], tex["attention"]
         talg = round((gx[2] + ax[2]) / max(1, gx[1] + ax[1]))
-        d4 = json.load(open(PMC_TRAFFIC_C4)) if (PMC_TRAFFIC_C4 and B == 64 and N == 128000) else None
+        d4 = json.load(open(PMC_TRAFFIC_C4)) if (PMC_TRAFFIC_C4 and B == PMC_BATCH and N == 128000) else None
         traffic = gemm_traffic(d4, GEMM_KERNELS_C4) if d4 else None
         res["roofline"].update({
             "traffic": traffic, "traffic_unit": "HBM bytes per GEMM-family launch",
@@ -175,19 +177,22 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=64, help="utterances in flight per GPU (engine slots)")
+    # 164 utterances x 399 frames = 65 436 rows = 512 row tiles of 128: every linear's grid (6 / 18 / 24 column
+    # tiles on base, 8 / 24 / 32 on large) fills whole rounds of the 512 resident 128 x 128 blocks (64: 3.125 rounds of
+    # the N = 1024 grids); measured 37.2 -> 38.2 utt/s (base) and 36.0 -> 38.1 (C4) on one box
+    ap.add_argument("--batch", type=int, default=BATCH, help="utterances in flight per GPU (engine slots)")
     ap.add_argument("--n-samples", type=int, default=128000)
     ap.add_argument("--suta-steps", type=int, default=10)
     ap.add_argument("--model", default="wav2vec2-base")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip the per-kernel HIP-event timing pass")
-    ap.add_argument("--timing-steps", type=int, default=2,
+    ap.add_argument("--timing-steps", type=int, default=1,
                     help="batches of the separate, untimed roofline pass (per-launch HIP events, eager)")
     ap.add_argument("--precision", default="fp32", choices=["fp32", "fp32-split-bf16", "bf16"],
                     help="GEMM arithmetic: exact fp32 MFMA, fp32-accurate 3-way bf16 split, or bf16 (config C4)")
     ap.add_argument("--no-c4", dest="c4", action="store_false",
                     help="skip the config-C4 line (wav2vec2-large, 20 SUTA steps, bf16 GEMMs; 1 GPU only)")
-    ap.add_argument("--c4-batch", type=int, default=64)
+    ap.add_argument("--c4-batch", type=int, default=BATCH)
     ap.add_argument("--only-c4", action="store_true", help="print only the config-C4 line (profiling)")
     ap.add_argument("--no-split", dest="also_split", action="store_false",
                     help="do not also time the fp32-accurate split-bf16 GEMM mode")

@@ -129,8 +129,9 @@ struct GemmParams {
     const void* Ab;
     const void* Bb;
     long ldab, ldbb;
-    void* Cb;   // optional bf16 copy of the stored C (Z == 1): the A plane of the next bf16-plane GEMM
+    void* Cb;   // optional bf16 copy of the stored C: the A plane of the next bf16-plane GEMM
     long ldcb;
+    long sCb1;  // Cb's stride per z1 (bf16 elements; Z-batched conv-stack planes)
     int off32;  // internal: every epilogue operand (rows x ld) within 4 GiB -> 32-bit offset epilogue
     // bf16-plane GEMMs (Cb given, gemm_hb_kernel, no split-K): C2 (EPI_STORE_PRE) and aux (EPI_DGELU) hold bf16
     // elements (ld and batch strides in elements; ldc2 even) -- the FFN pre-activation u of config C4

@@ -392,6 +392,23 @@ struct suta_engine {
         const char* e = std::getenv("SUTA_PRE_BF16");
         return !(e && atoi(e) == 0);
     }
+    // layer-mode conv stack on bf16 planes: the conv outputs z_i (conv0's by conv0_vec, the others by the conv GEMMs'
+    // epilogues) and the activation gradients da_i (the conv input-gradient GEMMs) stored in bf16 only, in place in
+    // their fp32 buffers; the conv LayerNorms read them widened -- torch autocast's bf16 conv outputs and gradients,
+    // about half the conv stack's LayerNorm bytes (SUTA_CONV_Z_BF16=0: fp32 storage, for A/B runs)
+    bool conv_z_bf16() const {
+        if (!conv_planes() || !conv_dx_planes() || !fused_conv_ln() || c.K[0] != 10 || c.S[0] != 5) return false;
+        const char* e = std::getenv("SUTA_CONV_Z_BF16");
+        return !(e && atoi(e) == 0);
+    }
+    // stable-LN layers: the input gradients of QKV and FFN1 (the dy of LN1 / LN2 backward) written by their GEMMs as a
+    // bf16 plane only (plane 2) and read so by the LayerNorm backward -- torch autocast's bf16 matmul gradient; 104 MB
+    // less written and read per LayerNorm backward on C4 (SUTA_DY_PLANES=0: fp32 dy, for A/B runs)
+    bool dy_planes() const {
+        if (!fp32_acts_dead() || !c.stable) return false;
+        const char* e = std::getenv("SUTA_DY_PLANES");
+        return !(e && atoi(e) == 0);
+    }
     // conv input gradients on the bf16 planes too (SUTA_CONV_DX_PLANES=0: fp32-staged x6 kernels, for A/B runs)
     bool conv_dx_planes() const {
         if (!conv_planes()) return false;
@@ -642,19 +659,21 @@ void suta_engine::forward(int B) {
                                 k.K[0], k.S[0], P + o_cg[0], P + o_cbeta[0], pl.gn_mean, pl.gn_rstd, pl.a[0],
                                 pl.dpart, rL0(), st);
         }, 4.0 * B * ((double)pl.N + (double)pl.Lc[0] * k.C[0]));  // waveform read, activation written
-    } else {
+    }
+    const bool zbf = k.layer_mode && conv_z_bf16();  // z_i in bf16, in place in the fp32 buffers
+    if (k.layer_mode) {
         timed(F_FRONT, [&] {
             launch_conv0(pl.x, pl.N, P + o_cw[0], k.conv_bias ? P + o_cb[0] : nullptr, Pn, pl.z[0], B, pl.Lc[0],
-                         k.C[0], k.K[0], k.S[0], st);
-        }, 4.0 * B * ((double)pl.N + (double)pl.Lc[0] * k.C[0]));
+                         k.C[0], k.K[0], k.S[0], st, zbf ? pl.z[0] : nullptr);
+        }, (zbf ? 2.0 : 4.0) * B * ((double)pl.N + (double)pl.Lc[0] * k.C[0]));
     }
     const bool cpl = conv_planes();
     if (k.layer_mode) {
         timed(F_NORM, [&] {
             // with conv planes only the bf16 activation is read (the next conv GEMM and its weight gradient)
-            launch_layernorm_fwd(pl.z[0], P + o_cg[0], P + o_cbeta[0], Pn, pl.Lc[0], cpl ? nullptr : pl.a[0],
-                                 pl.cxhat[0], pl.crstd[0], B * pl.Lc[0], k.C[0], 1e-5f, 1, st,
-                                 cpl ? conv_act_plane(0) : nullptr, pl.cmean[0]);
+            launch_layernorm_fwd(zbf ? nullptr : pl.z[0], P + o_cg[0], P + o_cbeta[0], Pn, pl.Lc[0],
+                                 cpl ? nullptr : pl.a[0], pl.cxhat[0], pl.crstd[0], B * pl.Lc[0], k.C[0], 1e-5f, 1, st,
+                                 cpl ? conv_act_plane(0) : nullptr, pl.cmean[0], zbf ? pl.z[0] : nullptr);
         });
     }
     for (int i = 1; i < k.nconv; ++i) {
@@ -697,14 +716,19 @@ void suta_engine::forward(int B) {
             g.sC21 = g.sC1;
             gemm(g);
         } else {
-            g.C = pl.z[i];
+            g.C = zbf ? nullptr : pl.z[i];
             g.ldc = k.C[i];
+            if (zbf) {  // bf16 z_i only (the LayerNorm forward and backward read it widened)
+                g.Cb = pl.z[i];
+                g.ldcb = k.C[i];
+                g.sCb1 = (long)pl.Lc[i] * k.C[i];
+            }
             gemm(g);
             timed(F_NORM, [&] {
                 const bool pln = cpl && i + 1 < k.nconv;
-                launch_layernorm_fwd(pl.z[i], P + o_cg[i], P + o_cbeta[i], Pn, pl.Lc[i], pln ? nullptr : pl.a[i],
-                                     pl.cxhat[i], pl.crstd[i], B * pl.Lc[i], k.C[i], 1e-5f, 1, st,
-                                     pln ? conv_act_plane(i) : nullptr, pl.cmean[i]);
+                launch_layernorm_fwd(zbf ? nullptr : pl.z[i], P + o_cg[i], P + o_cbeta[i], Pn, pl.Lc[i],
+                                     pln ? nullptr : pl.a[i], pl.cxhat[i], pl.crstd[i], B * pl.Lc[i], k.C[i], 1e-5f, 1, st,
+                                     pln ? conv_act_plane(i) : nullptr, pl.cmean[i], zbf ? pl.z[i] : nullptr);
             });
         }
     }
@@ -1114,10 +1138,12 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
             // du = (dx @ W2) * gelu'(u); dy2 = du @ W1; dhmid = LN2 bwd(dy2) + dx
             nn_gemm(dx, H, w2[l], k.F, du32, k.F, (int)BT, k.F, H, EPI_DGELU, nullptr, 0, lb.u, k.F, P0, P1,
                     dead && pre_bf16());
-            nn_gemm(du32, k.F, w1[l], H, t2, H, (int)BT, H, k.F, 0, nullptr, 0, nullptr, 0, P1);
+            void* dyp = dy_planes() ? plane(2) : nullptr;  // (plane 2's dctx of the layer above is consumed)
+            nn_gemm(du32, k.F, w1[l], H, dyp ? nullptr : t2, H, (int)BT, H, k.F, 0, nullptr, 0, nullptr, 0, P1, dyp);
             timed(F_NORM, [&] {
-                launch_layernorm_bwd(t2, lb.xhat2, lb.rstd2, P + o_l2g[l], P + o_l2b[l], Pn, T, B, H, 0, nullptr, dx,
-                                     t1, G + o_l2g[l], G + o_l2b[l], Pn, pl.lnpart, st, P0, lb.hmid, lb.mean2);
+                launch_layernorm_bwd(dyp ? nullptr : t2, lb.xhat2, lb.rstd2, P + o_l2g[l], P + o_l2b[l], Pn, T, B, H, 0,
+                                     nullptr, dx, t1, G + o_l2g[l], G + o_l2b[l], Pn, pl.lnpart, st, P0, lb.hmid,
+                                     lb.mean2, dyp);
             });
             dhres = t1;  // dhmid
         }
@@ -1251,11 +1277,14 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
             std::swap(dx, t2);
         } else {
             // dy1 = dqkv @ Wqkv ; dx_in = LN1 bwd(dy1) + dhmid
-            nn_gemm(dqkv_dead ? nullptr : pl.dqkv, 3 * H, wqkv[l], H, t2, H, (int)BT, H, 3 * H, 0, nullptr, 0, nullptr, 0,
-                    fused_bwd ? P1 : nullptr);
+            // (plane 2 held dctx, consumed by the flash backward above)
+            void* dyp = (dy_planes() && fused_bwd && P1) ? plane(2) : nullptr;
+            nn_gemm(dqkv_dead ? nullptr : pl.dqkv, 3 * H, wqkv[l], H, dyp ? nullptr : t2, H, (int)BT, H, 3 * H, 0, nullptr,
+                    0, nullptr, 0, fused_bwd ? P1 : nullptr, dyp);
             timed(F_NORM, [&] {
-                launch_layernorm_bwd(t2, lb.xhat1, lb.rstd1, P + o_l1g[l], P + o_l1b[l], Pn, T, B, H, 0, nullptr, dhres,
-                                     dx, G + o_l1g[l], G + o_l1b[l], Pn, pl.lnpart, st, P0, lb.x_in, lb.mean1);
+                launch_layernorm_bwd(dyp ? nullptr : t2, lb.xhat1, lb.rstd1, P + o_l1g[l], P + o_l1b[l], Pn, T, B, H, 0,
+                                     nullptr, dhres, dx, G + o_l1g[l], G + o_l1b[l], Pn, pl.lnpart, st, P0, lb.x_in,
+                                     lb.mean1, dyp);
             });
             // dx now holds grad wrt x_in; t1/t2 free
         }
@@ -1373,6 +1402,8 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
     });
     if (!hp.train_feature) return;
     float* other = pl.dzc;
+    // bf16 conv storage: z_i and (below the last layer) da_i are bf16 planes in place in their fp32 buffers
+    const bool zbf = k.layer_mode && conv_z_bf16();
     for (int i = last; i >= 1; --i) {
         // cur: group mode -> dz_i ; layer mode -> da_i
         bool bias_done = false;
@@ -1380,6 +1411,7 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
         if (k.layer_mode) {
             timed(F_NORM, [&] {
                 // fused: the LayerNorm backward also sums the conv bias gradient (one read of dz_i)
+                const int bfin = zbf ? (2 | (i < last ? 1 : 0)) : 0;
                 if (!pl.cxhat[i] && (fused_conv_ln() || cpl) &&
                     layernorm_bwd_conv_part_floats(B, pl.Lc[i], k.C[i], 0) <= pl.lnpart_floats &&
                     launch_layernorm_bwd_conv(cur, pl.crstd[i], P + o_cg[i], P + o_cbeta[i], Pn, pl.Lc[i], B, k.C[i],
@@ -1387,8 +1419,10 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
                                               cpl && conv_dx_planes() ? nullptr : other, G + o_cg[i], G + o_cbeta[i],
                                               k.conv_bias ? G + o_cb[i] : nullptr,
                                               nullptr, Pn, pl.lnpart, st, pl.z[i], pl.cmean[i], nullptr, 0, 0, 0,
-                                              cpl ? conv_dz_plane() : nullptr)) {
+                                              cpl ? conv_dz_plane() : nullptr, bfin)) {
                     bias_done = true;
+                } else if (zbf) {
+                    throw SutaError(SUTA_ERR_UNSUPPORTED, "conv stack in bf16: the fused LayerNorm backward is required");
                 } else {
                     launch_layernorm_bwd(cur, pl.cxhat[i], pl.crstd[i], P + o_cg[i], P + o_cbeta[i], Pn, pl.Lc[i], B,
                                          k.C[i], 1, nullptr, nullptr, other, G + o_cg[i], G + o_cbeta[i], Pn, pl.lnpart,
@@ -1475,6 +1509,12 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
                     g.ldbb = Cout;
                     g.tb = 0;
                     g.sB1 = (long)Kt * Cin * Cout;
+                    if (zbf) {  // da_{i-1} in bf16 only (the next LayerNorm backward reads it widened)
+                        g.C = nullptr;
+                        g.Cb = reinterpret_cast<__bf16*>(other) + (long)rho * Cin;
+                        g.ldcb = (long)S_ * Cin;
+                        g.sCb1 = (long)Lin * Cin;
+                    }
                 }
                 gemm(g);
             }
@@ -1493,12 +1533,16 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
     bool fused0 = false;
     timed(F_NORM, [&] {
         // fused: the LayerNorm backward also sums the conv0 bias and weight gradients (dz0 read once)
-        if (!pl.cxhat[0] && fused_conv_ln() && k.K[0] == 10 &&
+        if (!pl.cxhat[0] && (fused_conv_ln() || zbf) && k.K[0] == 10 &&
             layernorm_bwd_conv_part_floats(B, pl.Lc[0], k.C[0], 10) <= pl.lnpart_floats &&
-            launch_layernorm_bwd_conv(cur, pl.crstd[0], P + o_cg[0], P + o_cbeta[0], Pn, pl.Lc[0], B, k.C[0], other,
+            // dz0 itself is consumed in registers (conv0's bias and weight gradients): not stored
+            launch_layernorm_bwd_conv(cur, pl.crstd[0], P + o_cg[0], P + o_cbeta[0], Pn, pl.Lc[0], B, k.C[0], nullptr,
                                       G + o_cg[0], G + o_cbeta[0], k.conv_bias ? G + o_cb[0] : nullptr, G + o_cw[0], Pn,
-                                      pl.lnpart, st, pl.z[0], pl.cmean[0], pl.x, pl.N, k.S[0], 10)) {
+                                      pl.lnpart, st, pl.z[0], pl.cmean[0], pl.x, pl.N, k.S[0], 10, nullptr,
+                                      zbf ? (2 | (last > 0 ? 1 : 0)) : 0)) {
             fused0 = true;
+        } else if (zbf) {
+            throw SutaError(SUTA_ERR_UNSUPPORTED, "conv stack in bf16: the fused conv0 LayerNorm backward is required");
         } else {
             launch_layernorm_bwd(cur, pl.cxhat[0], pl.crstd[0], P + o_cg[0], P + o_cbeta[0], Pn, pl.Lc[0], B, k.C[0], 1,
                                  nullptr, nullptr, other, G + o_cg[0], G + o_cbeta[0], Pn, pl.lnpart, st, nullptr,

@@ -209,8 +209,8 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
     if (hbt && (p.M % 8 || p.N % 8 || p.ldab % 8 || p.ldbb % 8 || !aligned16(p.Ab) || !aligned16(p.Bb) || p.Cb ||
                 ((p.sA0 | p.sA1 | p.sB0 | p.sB1) % 8)))
         throw std::invalid_argument("gemm: MN-contiguous bf16 planes need M, N, ld, batch strides % 8 == 0, 16-B alignment");
-    if (p.Cb && (!hb || p.Z != 1 || (reinterpret_cast<uintptr_t>(p.Cb) & 7)))
-        throw std::invalid_argument("gemm: a bf16 output plane needs the bf16-plane kernel, Z == 1, 8-B alignment");
+    if (p.Cb && (!hb || (p.Z != 1 && (p.sCb1 % 4 || p.zdiv != 1)) || (reinterpret_cast<uintptr_t>(p.Cb) & 7)))
+        throw std::invalid_argument("gemm: a bf16 output plane needs the bf16-plane kernel, 8-B alignment (Z > 1: sCb1 % 4 == 0)");
     if (hb && (p.K % 8 || p.ldab % 8 || p.ldbb % 8 || !aligned16(p.Ab) || !aligned16(p.Bb) ||
                (p.Z > 1 && ((p.sA0 | p.sA1 | p.sB0 | p.sB1) % 8))))
         throw std::invalid_argument("gemm: bf16 planes need K, ld and batch strides % 8 == 0 and 16-B alignment");
@@ -245,7 +245,8 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
 
     // split-K when the grid cannot fill 256 CUs and K is long
     int splits = 1;
-    if (ws && p.K >= 1024 && blocks < 256 && tile != 6 && !p.preb) {  // (the split-K reduce has no bf16 pre store)
+    // (the split-K reduce has no bf16 pre store and no batched bf16 C plane)
+    if (ws && p.K >= 1024 && blocks < 256 && tile != 6 && !p.preb && !(p.Cb && p.Z > 1)) {
         splits = (int)std::min<long>(16, (512 + blocks - 1) / blocks);
         while (splits > 1 && (long)splits * p.Z * p.M * (long)p.N > ws_floats) --splits;
         splits = std::min(splits, std::max(1, (p.K + 255) / 256));  // >= 256 K per split

@@ -345,7 +345,7 @@ __device__ __forceinline__ void gemm_epilogue_fast(const GemmParams& p, const f3
                     }
                 }
                 if (CB) {
-                    __bf16* Cb = reinterpret_cast<__bf16*>(p.Cb);
+                    __bf16* Cb = reinterpret_cast<__bf16*>(p.Cb) + z1 * p.sCb1;
                     if (cbpair) {
                         // (column, column + 1) pairs: lanes 2i / 2i + 1 swap one value (DPP quad_perm [1,0,3,2]);
                         // the even lane writes row r, the odd lane row r + 1 (registers r, r + 1: consecutive rows)
@@ -512,7 +512,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, const f32x16 
                         const float o = row < rlim ? v[r] : 0.f;
                         if (!CB || p.C) C[(long)row * p.ldc + col] = o;  // bf16-plane GEMMs: C may be dead
                         if (CB && !(interior && (p.ldcb & 1) == 0))
-                            reinterpret_cast<__bf16*>(p.Cb)[(long)row * p.ldcb + col] = (__bf16)o;
+                            (reinterpret_cast<__bf16*>(p.Cb) + z1 * p.sCb1)[(long)row * p.ldcb + col] = (__bf16)o;
                     }
                 }
                 if (CB && interior && (p.ldcb & 1) == 0) {
@@ -531,8 +531,8 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, const f32x16 
                         cb2 pr;
                         pr[0] = (__bf16)(odd ? q : a);
                         pr[1] = (__bf16)(odd ? b : q);
-                        *reinterpret_cast<cb2*>(reinterpret_cast<__bf16*>(p.Cb) + (long)(row + (odd ? 1 : 0)) * p.ldcb +
-                                                (col & ~1)) = pr;
+                        *reinterpret_cast<cb2*>(reinterpret_cast<__bf16*>(p.Cb) + z1 * p.sCb1 +
+                                                (long)(row + (odd ? 1 : 0)) * p.ldcb + (col & ~1)) = pr;
                     }
                 }
             }

@@ -10,7 +10,7 @@ void launch_wave_normalize(const float* x, float* y, int B, long N, const int* l
 
 // conv0: z[b][t][c] = sum_k x[b][s*t + k] * W[b][k][c] (+ bias[b][c]);  W stored [k][c] per utterance.
 void launch_conv0(const float* x, long N, const float* W, const float* bias, long wstride, float* z, int B, int L0,
-                  int C, int K, int S, hipStream_t st);
+                  int C, int K, int S, hipStream_t st, void* zb = nullptr);  // zb: bf16 output instead of z
 
 // Fused conv0 + GroupNorm + GELU (group mode): conv0 is recomputed from the waveform in each pass.
 // fwd: mean/rstd per (utterance, channel) and a = gelu(GN(conv0(x))).  dpart: >= B*ceil(L0/128)*2*C + B*C doubles.
@@ -30,17 +30,20 @@ void launch_front_gn_bwd(const float* x, long N, const float* W, const float* bi
 // at pstride.  Stores y, xhat, rstd.  gelu_out: y = gelu(LN(x)) (feature-encoder "layer" mode).
 void launch_layernorm_fwd(const float* x, const float* g, const float* beta, long pstride, int rows_per_utt,
                           float* y, float* xhat, float* rstd, int rows, int D, float eps, int gelu_out,
-                          hipStream_t st, void* yb = nullptr, float* mean = nullptr);
+                          hipStream_t st, void* yb = nullptr, float* mean = nullptr, const void* xb = nullptr);
 // yb: optional bf16 copy of y (bf16-plane GEMMs); xhat may be null when `mean` is given: the row means
-// are stored instead and the backward recomputes x-hat from the (stored) input
+// are stored instead and the backward recomputes x-hat from the (stored) input; xb: the input as a bf16 plane
+// (x null; vectorised widths)
 // LayerNorm backward.  gin = dy (times gelu'(xhat*g+beta) when gelu_in); dx = LN-bwd(gin)
 // (times gelu'(post_aux) when post_aux) (+ resid).  dgamma/dbeta (may be null) summed per
 // utterance into the grad buffer (gstride per utterance).  part: >= B*ceil(rows_per_utt/16)*2*D floats.
 void launch_layernorm_bwd(const float* dy, const float* xhat, const float* rstd, const float* g, const float* beta,
                           long pstride, int rows_per_utt, int B, int D, int gelu_in, const float* post_aux,
                           const float* resid, float* dx, float* dgamma, float* dbeta, long gstride, float* part,
-                          hipStream_t st, void* dxb = nullptr, const float* x = nullptr, const float* mean = nullptr);
-// dxb: optional bf16 copy of dx; xhat null: x-hat = (x - mean) * rstd recomputed from the LayerNorm input
+                          hipStream_t st, void* dxb = nullptr, const float* x = nullptr, const float* mean = nullptr,
+                          const void* dyb = nullptr);
+// dxb: optional bf16 copy of dx; xhat null: x-hat = (x - mean) * rstd recomputed from the LayerNorm input;
+// dyb: dy given as a bf16 plane instead (dy must be null; vectorised widths 512 / 768 / 1024 only)
 
 // Layer-mode conv stack (D = 512, GELU after the LayerNorm, x-hat recomputed from the stored conv output x and
 // its row means): the LayerNorm backward that also sums the conv bias gradient (dbias, may be null) and, with
@@ -52,7 +55,8 @@ long layernorm_bwd_conv_part_floats(int B, int rows_per_utt, int D, int ktaps);
 bool launch_layernorm_bwd_conv(const float* dy, const float* rstd, const float* g, const float* beta, long pstride,
                                int rows_per_utt, int B, int D, float* dx, float* dgamma, float* dbeta, float* dbias,
                                float* dw, long gstride, float* part, hipStream_t st, const float* x, const float* mean,
-                               const float* xw, long xws, int xs, int ktaps, void* dxb = nullptr);
+                               const float* xw, long xws, int xs, int ktaps, void* dxb = nullptr, int bf16_in = 0);
+// bf16_in: bit 0 dy, bit 1 x given as bf16 planes (the pointers reinterpreted; conv stack on bf16 planes)
 // Column sums per utterance: out[b][c] = sum_{t < rows} x[b][t][c]   (bias gradients).
 void launch_colsum(const float* x, int B, int rows, int C, float* out, long ostride, float* part, hipStream_t st);
 

@@ -84,6 +84,18 @@ __global__ __launch_bounds__(256) void conv0_kernel(const float* __restrict__ x,
     }
 }
 
+typedef __bf16 lnbf16x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x4 load_bf16x4(const __bf16* src) {  // one 8-B load, exact widening
+    const lnbf16x4 b = *reinterpret_cast<const lnbf16x4*>(src);
+    return f32x4{(float)b[0], (float)b[1], (float)b[2], (float)b[3]};
+}
+__device__ __forceinline__ void store_bf16x4(__bf16* dst, f32x4 v) {  // RNE, one 8-B store
+    lnbf16x4 b;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) b[e] = (__bf16)v[e];
+    *reinterpret_cast<lnbf16x4*>(dst) = b;
+}
+
 // Vectorised form (layer-norm conv stack: conv0 output stored): a thread owns 4 consecutive channels
 // (C / 4 threads per frame, 256 / (C / 4) frames per pass), taps KT / stride ST compile-time, 16-B stores;
 // per-element arithmetic and order as conv0_kernel.  Requires C % 4 == 0 and 256 % (C / 4) == 0.
@@ -91,7 +103,8 @@ constexpr int C0V_ROWS = 64;
 template <int KT, int ST>
 __global__ __launch_bounds__(256) void conv0_vec_kernel(const float* __restrict__ x, long N,
                                                         const float* __restrict__ W, const float* __restrict__ bias,
-                                                        long wstride, float* __restrict__ z, int L0, int C) {
+                                                        long wstride, float* __restrict__ z, int L0, int C,
+                                                        __bf16* __restrict__ zb) {
     __shared__ float xs[C0V_ROWS * ST + KT + 16];
     const int b = blockIdx.y;
     const int t0 = blockIdx.x * C0V_ROWS;
@@ -111,7 +124,7 @@ __global__ __launch_bounds__(256) void conv0_vec_kernel(const float* __restrict_
     f32x4 bv = {0.f, 0.f, 0.f, 0.f};
     if (bias) bv = *reinterpret_cast<const f32x4*>(bias + (long)b * wstride + c);
     const int rows = min(C0V_ROWS, L0 - t0);
-    float* zb = z + ((long)b * L0 + t0) * C + c;
+    const long o0 = ((long)b * L0 + t0) * C + c;
     for (int r = fr; r < rows; r += fpp) {
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -122,7 +135,8 @@ __global__ __launch_bounds__(256) void conv0_vec_kernel(const float* __restrict_
         }
 #pragma unroll
         for (int e = 0; e < 4; ++e) acc[e] = acc[e] + bv[e];
-        *reinterpret_cast<f32x4*>(zb + (long)r * C) = acc;
+        if (zb) store_bf16x4(zb + o0 + (long)r * C, acc);  // bf16 storage (conv stack on bf16 planes)
+        else *reinterpret_cast<f32x4*>(z + o0 + (long)r * C) = acc;
     }
 }
 
@@ -287,13 +301,6 @@ __global__ __launch_bounds__(256) void conv0_dw_reduce(const float* __restrict__
     dW[(long)b * gstride + i] = (float)s;
 }
 
-typedef __bf16 lnbf16x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void store_bf16x4(__bf16* dst, f32x4 v) {  // RNE, one 8-B store
-    lnbf16x4 b;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) b[e] = (__bf16)v[e];
-    *reinterpret_cast<lnbf16x4*>(dst) = b;
-}
 
 // ------------------------------------------------------------------------------------------
 // LayerNorm over D (<= 1024): one wave per row
@@ -429,7 +436,7 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* __restr
 // Vectorised LayerNorm forward for D = 256 * NV: one wave per row, lane l owns the 16-B column
 // groups l + 64 i.  gamma / beta are read as scalars (their offsets in the flat parameter buffer need
 // not be 16-B aligned).
-template <int NV, bool GV>
+template <int NV, bool GV, bool XB = false>  // XB: x is a bf16 plane (widened exactly on load)
 __global__ __launch_bounds__(256) void layernorm_fwd_vec_kernel(const float* __restrict__ x,
                                                                 const float* __restrict__ g,
                                                                 const float* __restrict__ beta, long pstride,
@@ -446,7 +453,8 @@ __global__ __launch_bounds__(256) void layernorm_fwd_vec_kernel(const float* __r
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
-        v[i] = reinterpret_cast<const f32x4*>(x + row * D)[lane + 64 * i];
+        if constexpr (XB) v[i] = load_bf16x4(reinterpret_cast<const __bf16*>(x) + row * D + 4 * (lane + 64 * i));
+        else v[i] = reinterpret_cast<const f32x4*>(x + row * D)[lane + 64 * i];
         s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
     }
     s = wave_sum(s);
@@ -495,8 +503,10 @@ __global__ __launch_bounds__(256) void layernorm_fwd_vec_kernel(const float* __r
 
 // Vectorised LayerNorm backward for D = 256 * NV: lane l owns the 16-B column groups l + 64 i
 // (i < NV) of every row, so every row access is a fully coalesced 1-KiB wave load.  Same arithmetic,
-// order and partial layout as layernorm_bwd_kernel.
-template <int NV, bool GV>
+// order and partial layout as layernorm_bwd_kernel.  DYB: dy is a bf16 plane (the input gradient of the linear
+// the LayerNorm feeds, written by that GEMM in bf16 only -- torch autocast's bf16 matmul gradient), widened
+// exactly on load.
+template <int NV, bool GV, bool DYB = false>
 __global__ __launch_bounds__(256) void layernorm_bwd_vec_kernel(
     const float* __restrict__ dy, const float* __restrict__ xhat, const float* __restrict__ rstd,
     const float* __restrict__ g, const float* __restrict__ beta, long pstride, int rows_per_utt, int gelu_in,
@@ -537,7 +547,8 @@ __global__ __launch_bounds__(256) void layernorm_bwd_vec_kernel(
 #pragma unroll
         for (int i = 0; i < NV; ++i) {
             xh[i] = xr[lane + 64 * i];
-            gi[i] = dr[lane + 64 * i];
+            if constexpr (DYB) gi[i] = load_bf16x4(reinterpret_cast<const __bf16*>(dy) + row * D + 4 * (lane + 64 * i));
+            else gi[i] = dr[lane + 64 * i];
         }
         // every load of the row in flight together (the epilogue operands used to wait behind the reductions)
         if (post_aux) {
@@ -606,7 +617,7 @@ __global__ __launch_bounds__(256) void layernorm_bwd_vec_kernel(
 // at 64 x 8 s on wav2vec2-large).  Rows in chunks of CROWS per block (larger chunks for the long layers
 // keep the partial slabs small); partial layout [B][nchunk][2 + 1 + KT][D]: dgamma, dbeta, dbias, dW0 rows;
 // fixed-order reductions (waves, then chunks in order): deterministic.
-template <int NV, bool GV, int KT>
+template <int NV, bool GV, int KT, bool DYB = false, bool XB = false>  // DYB / XB: dy / x as bf16 planes
 __global__ __launch_bounds__(256) void layernorm_bwd_conv_kernel(
     const float* __restrict__ dy, const float* __restrict__ rstd, const float* __restrict__ g,
     const float* __restrict__ beta, long pstride, int rows_per_utt, float* __restrict__ dx, float* __restrict__ part,
@@ -648,8 +659,10 @@ __global__ __launch_bounds__(256) void layernorm_bwd_conv_kernel(
         const float mu = meanp[row];
 #pragma unroll
         for (int i = 0; i < NV; ++i) {
-            xh[i] = xr[lane + 64 * i];
-            gi[i] = dr[lane + 64 * i];
+            if constexpr (XB) xh[i] = load_bf16x4(reinterpret_cast<const __bf16*>(xin) + row * D + 4 * (lane + 64 * i));
+            else xh[i] = xr[lane + 64 * i];
+            if constexpr (DYB) gi[i] = load_bf16x4(reinterpret_cast<const __bf16*>(dy) + row * D + 4 * (lane + 64 * i));
+            else gi[i] = dr[lane + 64 * i];
         }
         float xt[KT > 0 ? KT : 1];
         if constexpr (KT > 0) {
@@ -1443,12 +1456,14 @@ void launch_wave_normalize(const float* x, float* y, int B, long N, const int* l
 }
 
 void launch_conv0(const float* x, long N, const float* W, const float* bias, long wstride, float* z, int B, int L0,
-                  int C, int K, int S, hipStream_t st) {
+                  int C, int K, int S, hipStream_t st, void* zb) {
     auto a16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
-    if (K == 10 && S == 5 && C % 4 == 0 && C / 4 <= 256 && 256 % (C / 4) == 0 && wstride % 4 == 0 && a16(W) &&
-        a16(z) && (!bias || a16(bias))) {  // every wav2vec2 conv0
+    const bool vec = K == 10 && S == 5 && C % 4 == 0 && C / 4 <= 256 && 256 % (C / 4) == 0 && wstride % 4 == 0 &&
+                     a16(W) && (zb ? (reinterpret_cast<uintptr_t>(zb) & 7) == 0 : a16(z)) && (!bias || a16(bias));
+    if (zb && !vec) throw std::invalid_argument("conv0: bf16 output needs the vectorised kernel (K 10, S 5)");
+    if (vec) {  // every wav2vec2 conv0
         hipLaunchKernelGGL((conv0_vec_kernel<10, 5>), dim3(cdiv(L0, C0V_ROWS), B), dim3(256), 0, st, x, N, W, bias,
-                           wstride, z, L0, C);
+                           wstride, z, L0, C, reinterpret_cast<__bf16*>(zb));
         return;
     }
     hipLaunchKernelGGL(conv0_kernel, dim3(cdiv(L0, C0_ROWS), B), dim3(256), 0, st, x, N, W, bias, wstride, z, L0, C,
@@ -1459,9 +1474,25 @@ static int ew_grid(long n) { return (int)std::min<long>(2048, std::max<long>(1, 
 
 void launch_layernorm_fwd(const float* x, const float* g, const float* beta, long pstride, int rows_per_utt,
                           float* y, float* xhat, float* rstd, int rows, int D, float eps, int gelu_out,
-                          hipStream_t st, void* yb_, float* mean) {
+                          hipStream_t st, void* yb_, float* mean, const void* xb) {
     __bf16* yb = reinterpret_cast<__bf16*>(yb_);
     if (!xhat && !mean) throw std::runtime_error("layernorm_fwd: x-hat or the row means must be stored");
+    if (xb) {  // bf16 input plane (conv stack on bf16 planes): the vectorised widths, 16-B gamma / beta only
+        auto al = [](const void* q, int a) { return q == nullptr || (reinterpret_cast<uintptr_t>(q) & (a - 1)) == 0; };
+        if (x || !(D == 768 || D == 1024 || D == 512) || !al(xb, 8) || !al(y, 16) || !al(xhat, 16) || !al(g, 16) ||
+            !al(beta, 16) || pstride % 4)
+            throw std::invalid_argument("layernorm_fwd: a bf16 input plane needs the vectorised widths");
+        const float* xp = reinterpret_cast<const float*>(xb);
+        const dim3 grid(cdiv(rows, 4));
+#define LNFB(NV_)                                                                                                  \
+        hipLaunchKernelGGL((layernorm_fwd_vec_kernel<NV_, true, true>), grid, dim3(256), 0, st, xp, g, beta, pstride,    \
+                           rows_per_utt, y, xhat, rstd, rows, eps, gelu_out, yb, mean)
+        if (D == 768) LNFB(3);
+        else if (D == 1024) LNFB(4);
+        else LNFB(2);
+#undef LNFB
+        return;
+    }
     if (!y && !(yb && (D == 768 || D == 1024 || D == 512)))
         throw std::runtime_error("layernorm_fwd: the fp32 output may be skipped only beside a bf16 plane");
     dim3 grid(cdiv(rows, 4));
@@ -1490,7 +1521,7 @@ void launch_layernorm_fwd(const float* x, const float* g, const float* beta, lon
 void launch_layernorm_bwd(const float* dy, const float* xhat, const float* rstd, const float* g, const float* beta,
                           long pstride, int rows_per_utt, int B, int D, int gelu_in, const float* post_aux,
                           const float* resid, float* dx, float* dgamma, float* dbeta, long gstride, float* part,
-                          hipStream_t st, void* dxb_, const float* x, const float* mean) {
+                          hipStream_t st, void* dxb_, const float* x, const float* mean, const void* dyb) {
     __bf16* dxb = reinterpret_cast<__bf16*>(dxb_);
     if (!xhat && (!x || !mean)) throw std::runtime_error("layernorm_bwd: x-hat or (x, row means) needed");
     const int nchunk = cdiv(rows_per_utt, LNB_ROWS);
@@ -1499,6 +1530,22 @@ void launch_layernorm_bwd(const float* dy, const float* xhat, const float* rstd,
     auto a16 = [](const void* q) { return q == nullptr || (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
     const bool vec = a16(dy) && a16(xhat) && a16(x) && a16(dx) && a16(post_aux) && a16(resid) && a16(part);
     const bool gv = a16(g) && a16(beta) && pstride % 4 == 0;
+    if (dyb) {  // bf16 dy plane: the vectorised widths only (the engine's dead-buffer predicate guarantees them)
+        if (dy || !vec || !gv || (reinterpret_cast<uintptr_t>(dyb) & 7) || !(D == 768 || D == 1024 || D == 512))
+            throw std::invalid_argument("layernorm_bwd: a bf16 dy plane needs the vectorised widths and 16-B gamma");
+        const float* dyp = reinterpret_cast<const float*>(dyb);
+#define LNBB(NV_)                                                                                                  \
+        hipLaunchKernelGGL((layernorm_bwd_vec_kernel<NV_, true, true>), grid, dim3(256), 0, st, dyp, xhat, rstd, g, beta, \
+                           pstride, rows_per_utt, gelu_in, post_aux, resid, dx, pp, nchunk, dxb, x, mean)
+        if (D == 768) LNBB(3);
+        else if (D == 1024) LNBB(4);
+        else LNBB(2);
+#undef LNBB
+        if (pp)
+            hipLaunchKernelGGL(chunk_reduce, dim3(cdiv(D, 256), B), dim3(256), 0, st, pp, nchunk, 2, D, dgamma, dbeta,
+                               gstride);
+        return;
+    }
 #define LNB(NV_)                                                                                                   \
     hipLaunchKernelGGL((gv ? layernorm_bwd_vec_kernel<NV_, true> : layernorm_bwd_vec_kernel<NV_, false>), grid,      \
                        dim3(256), 0, st, dy, xhat, rstd, g, beta, pstride, rows_per_utt, gelu_in, post_aux, resid, dx, \
@@ -1530,15 +1577,37 @@ long layernorm_bwd_conv_part_floats(int B, int rows_per_utt, int D, int ktaps) {
 bool launch_layernorm_bwd_conv(const float* dy, const float* rstd, const float* g, const float* beta, long pstride,
                                int rows_per_utt, int B, int D, float* dx, float* dgamma, float* dbeta, float* dbias,
                                float* dw, long gstride, float* part, hipStream_t st, const float* x, const float* mean,
-                               const float* xw, long xws, int xs, int ktaps, void* dxb) {
+                               const float* xw, long xws, int xs, int ktaps, void* dxb, int bf16_in) {
     auto a16 = [](const void* q) { return q == nullptr || (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
-    if (D != 512 || !(ktaps == 0 || ktaps == 10) || (ktaps && !xw) || !x || !mean || !dgamma || !dbeta || !(dx || dxb) ||
-        !(a16(dy) && a16(x) && a16(dx) && a16(part)))
+    const bool dyb = bf16_in & 1, xb = bf16_in & 2;  // dy / x given as bf16 planes (8-B aligned suffices)
+    if (D != 512 || !(ktaps == 0 || ktaps == 10) || (ktaps && !xw) || !x || !mean || !dgamma || !dbeta || (!(dx || dxb) && ktaps == 0) ||
+        !((dyb || a16(dy)) && (xb || a16(x)) && a16(dx) && a16(part)))
         return false;
     const int crows = rows_per_utt >= 4096 ? 128 : 16;
     const int nchunk = cdiv(rows_per_utt, crows);
     const bool gv = a16(g) && a16(beta) && pstride % 4 == 0;
     const dim3 grid(nchunk, B);
+    if (bf16_in) {  // conv stack on bf16 planes: 16-B gamma / beta (every SUTA layout)
+        if (!gv) return false;
+#define LBCB(KT_, DB_, XB_)                                                                                      \
+        hipLaunchKernelGGL((layernorm_bwd_conv_kernel<2, true, KT_, DB_, XB_>), grid, dim3(256), 0, st, dy, rstd, g, beta, \
+                           pstride, rows_per_utt, dx, part, nchunk, crows, x, mean, xw, xws, xs,                    \
+                           reinterpret_cast<__bf16*>(dxb))
+        if (ktaps == 10) {
+            if (dyb && xb) LBCB(10, true, true);
+            else if (xb) LBCB(10, false, true);
+            else return false;
+        } else {
+            if (dyb && xb) LBCB(0, true, true);
+            else if (xb) LBCB(0, false, true);
+            else return false;
+        }
+#undef LBCB
+        const int nvec = 3 + ktaps;
+        hipLaunchKernelGGL(chunk_reduce_conv, dim3(cdiv(D, 256), B, nvec), dim3(256), 0, st, part, nchunk, nvec, D,
+                           dgamma, dbeta, dbias, dw, gstride);
+        return true;
+    }
 #define LBC(GV_, KT_)                                                                                         \
     hipLaunchKernelGGL((layernorm_bwd_conv_kernel<2, GV_, KT_>), grid, dim3(256), 0, st, dy, rstd, g, beta, pstride, \
                        rows_per_utt, dx, part, nchunk, crows, x, mean, xw, xws, xs, reinterpret_cast<__bf16*>(dxb))

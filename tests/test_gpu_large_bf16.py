@@ -351,3 +351,32 @@ def test_ffn_preactivation_bf16_equals_fp32(monkeypatch, model):
     for u in range(2):
         np.testing.assert_array_equal(out["1"][0][u], out["0"][0][u])  # step 0: the forward does not read u
         assert_bf16_close(out["1"][3][u], out["0"][3][u], 0.97, f"pre bf16 step 3 utt {u}", rtol=rtol)
+
+
+@pytest.mark.parametrize("switch", ["SUTA_CONV_Z_BF16", "SUTA_DY_PLANES"])
+def test_bf16_storage_of_conv_outputs_and_dy_equals_fp32_storage(monkeypatch, switch):
+    """bf16 mode, wav2vec2-large: (SUTA_CONV_Z_BF16) the conv stack's outputs z_i and activation gradients da_i
+    stored in bf16 by conv0 / the conv GEMM epilogues and read widened by the conv LayerNorms, and (SUTA_DY_PLANES)
+    the stable-LN backward's dy written by the QKV / FFN1 input-gradient GEMMs as bf16 planes -- torch autocast's
+    bf16 conv / matmul outputs and gradients (default) -- against fp32 storage (=0).  Ragged pair: adapted logits
+    agree to the bf16 tolerance, reruns are bitwise identical, step 0 is bitwise equal for the backward-only switch."""
+    cfg = get_config("wav2vec2-large")
+    eng = SutaEngine(cfg, synth_weights(cfg), max_batch=2, max_samples=48000)
+    eng.set_precision("bf16")
+    eng.set_graphs(False)  # eager: a replayed graph would keep the kernels it was captured with
+    waves = [synth.wave(48000, 96), synth.wave(30400, 97)]
+    out = {}
+    for on in ("1", "0"):
+        monkeypatch.setenv(switch, on)
+        a, _, _ = eng.adapt_varlen(waves, 3, SutaHParams(), record=[0, 3])
+        b, _, _ = eng.adapt_varlen(waves, 3, SutaHParams(), record=[0, 3])
+        for u in range(2):
+            assert np.array_equal(a[3][u], b[3][u]), (on, u)
+        out[on] = a
+    eng.close()
+    for u in range(2):
+        if switch == "SUTA_DY_PLANES":
+            np.testing.assert_array_equal(out["1"][0][u], out["0"][0][u])  # the forward is unchanged
+        for r in (0, 3):
+            assert_bf16_close(out["1"][r][u], out["0"][r][u], 0.97, f"{switch} step {r} utt {u}",
+                              rtol=BF16_LOGITS_RTOL_LARGE)
