@@ -19,10 +19,11 @@ __device__ __forceinline__ float dgelu_f(float x) {
     return cdf + x * pdf;
 }
 
-// Branch-free erf for the bf16-plane GEMM epilogues (config C4, whose outputs are rounded to bf16): erfc(z),
-// z = |x|, as t exp(-z^2 + P(t)), t = 1 / (1 + z / 2), with the 9-term Chebyshev fit of Numerical Recipes
-// 2nd ed. section 6.2 (fractional error < 1.2e-7 for every z >= 0).  ~18 VALU operations against ~40 for the
-// two-range erff; the exact-fp32 paths keep erff.
+// Branch-free erf for the bf16-plane GEMM epilogues and the conv front-end (conv0_gn_kernel, every mode): erfc(z),
+// z = |x|, as t exp(-z^2 + P(t)), t = 1 / (1 + z / 2), with the 9-term Chebyshev fit of Numerical Recipes 2nd ed.
+// section 6.2 (fractional error < 1.2e-7 for every z >= 0: fp32-accurate).  ~18 VALU operations against ~40 for the
+// two-range erff; SUTA_FAST_GELU=0 restores erff for A/B runs.  (The fp32 GEMM epilogues keep erff: a second GELU
+// form in every fp32 GEMM instantiation grew libsuta.so by 11 MB.)
 __device__ __forceinline__ float erfc_t(float z, float t, float ez2) {  // ez2 = exp(-z^2)
     float p = 0.17087277f;
     p = fmaf(p, t, -0.82215223f);

@@ -598,6 +598,10 @@ void suta_engine::build_plan(int B, long N) {
         pl.dzc2 = ar.take<float>((size_t)B * maxLC);
         const long lnrows = std::max<long>(pl.Lc[0], T);
         pl.lnpart_floats = (long)B * ((lnrows + 15) / 16) * 2 * std::max<long>(H, maxLC / pl.Lc[0] + 1) + 64;
+        if (k.layer_mode && k.C[0] == 512)  // the fused conv LayerNorm backwards' partial slabs (short inputs too)
+            for (int i = 0; i < k.nconv; ++i)
+                pl.lnpart_floats = std::max(pl.lnpart_floats,
+                                            layernorm_bwd_conv_part_floats(B, pl.Lc[i], k.C[i], i == 0 ? 10 : 0));
         pl.lnpart = ar.take<float>((size_t)pl.lnpart_floats);
         pl.dpart = ar.take<double>((size_t)B * ((pl.Lc[0] + 127) / 128 + 2) * 2 * k.C[0] + (size_t)B * k.C[0] * 2);
         pl.c0part = ar.take<float>((size_t)B * ((pl.Lc[0] + 127) / 128) * k.K[0] * k.C[0] + 64);

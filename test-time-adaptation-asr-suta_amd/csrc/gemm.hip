@@ -216,12 +216,8 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
         throw std::invalid_argument("gemm: bf16 planes need K, ld and batch strides % 8 == 0 and 16-B alignment");
     const bool bf16_gbf = p.mode == 2 && glds_ok && p.ta;  // bf16 weight gradients: LDS-DMA fp32 stages
     {
-        static int fg = -1;
-        if (fg < 0) {
-            const char* ev = std::getenv("SUTA_FAST_GELU");
-            fg = (ev && atoi(ev) == 0) ? 0 : 1;
-        }
-        p.fgelu = fg;
+        const char* ev = std::getenv("SUTA_FAST_GELU");  // read per launch: tests flip it within a process
+        p.fgelu = (ev && atoi(ev) == 0) ? 0 : 1;
     }
     if (p.preb && (!hb || !p.Cb || (p.ldc2 & 1)))  // (gemm_hb8_kernel shares the epilogue)
         throw std::invalid_argument("gemm: bf16 pre-activation operands need the bf16-plane kernel with a Cb plane, ldc2 even");

@@ -197,7 +197,7 @@ __global__ __launch_bounds__(256) void gn_bwd_final(const double* __restrict__ p
 constexpr int F0_ROWS = 128;
 // KT/ST: compile-time taps/stride (every wav2vec2 conv0 is K = 10, S = 5) -- keeps the filter in
 // statically indexed registers and lets the tap loop unroll; KT = 0 is the generic (K <= 16) path.
-template <int MODE, int KT, int ST>
+template <int MODE, int KT, int ST, bool FG = false>  // FG: branch-free GELU / GELU' (common.h gelu_fast)
 __global__ __launch_bounds__(256) void conv0_gn_kernel(const float* __restrict__ x, long N, const float* __restrict__ W,
                                                        const float* __restrict__ bias, long wstride, int L0, int C,
                                                        int K, int S, const float* __restrict__ mean,
@@ -262,13 +262,14 @@ __global__ __launch_bounds__(256) void conv0_gn_kernel(const float* __restrict__
                 const float xh = (z - mu) * rs;
                 const long o = (long)r * C + c;
                 if (MODE == 1) {
-                    iob[o] = gelu_f(xh * gg + bt);
+                    iob[o] = FG ? gelu_fast(xh * gg + bt) : gelu_f(xh * gg + bt);
                 } else if (MODE == 2) {
-                    const float dg = iob[o] * dgelu_f(xh * gg + bt);
+                    const float dg = iob[o] * (FG ? dgelu_fast(xh * gg + bt) : dgelu_f(xh * gg + bt));
                     a0 += dg;
                     a1 += (double)dg * xh;
                 } else {
-                    const float dg = iob[o] * dgelu_f(xh * gg + bt);  // recomputed bitwise, as in MODE 2
+                    // recomputed bitwise, as in MODE 2
+                    const float dg = iob[o] * (FG ? dgelu_fast(xh * gg + bt) : dgelu_f(xh * gg + bt));
                     const float dz = rs * gg * (dg - sS - xh * sQ);
 #pragma unroll
                     for (int k = 0; k < (KT > 0 ? KT : 16); ++k)
@@ -1801,9 +1802,17 @@ void launch_adam(float* P, const float* G, float* M, float* V, long pstride, int
     hipLaunchKernelGGL(adam_kernel, dim3((unsigned)nblk, B), dim3(256), 0, st, P, G, M, V, pstride, aa);
 }
 
+// SUTA_FAST_GELU=0: the erff GELU / GELU' everywhere (A/B runs); default: the branch-free form (common.h gelu_fast,
+// erfc fractional error < 1.2e-7: fp32-accurate) in the conv front-end and every GEMM epilogue
+static bool fast_gelu_on() {  // read per launch: tests flip it within a process
+    const char* ev = std::getenv("SUTA_FAST_GELU");
+    return !(ev && atoi(ev) == 0);
+}
 template <int MODE, typename... Args>
 static void launch_conv0_gn(dim3 grid, hipStream_t st, int K, int S, Args... args) {
-    if (K == 10 && S == 5)
+    if (K == 10 && S == 5 && fast_gelu_on())
+        hipLaunchKernelGGL((conv0_gn_kernel<MODE, 10, 5, true>), grid, dim3(256), 0, st, args...);
+    else if (K == 10 && S == 5)
         hipLaunchKernelGGL((conv0_gn_kernel<MODE, 10, 5>), grid, dim3(256), 0, st, args...);
     else
         hipLaunchKernelGGL((conv0_gn_kernel<MODE, 0, 0>), grid, dim3(256), 0, st, args...);

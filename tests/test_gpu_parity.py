@@ -341,3 +341,27 @@ def test_posconv_kernel_equals_gemm_path(monkeypatch):
     for u in range(2):
         np.testing.assert_allclose(b[2][u], a[2][u], rtol=0, atol=2e-5, err_msg=f"ragged utterance {u}")
     ref_eng.close()
+
+
+def test_branch_free_gelu_equals_erff_gelu(monkeypatch):
+    """Exact fp32 mode, wav2vec2-base shapes: the branch-free GELU / GELU' (common.h gelu_fast, erfc fractional error
+    < 1.2e-7) of the conv0 + GroupNorm front-end (default) against the erff forms (SUTA_FAST_GELU=0, read per launch;
+    the oracle parity tests pin the default end to end).  Ragged pair, 3 steps: logits within
+    logits_tol, adapted tensors within the Adam budget."""
+    cfg = get_config("wav2vec2-base")
+    eng = SutaEngine(cfg, synth_weights(cfg), max_batch=2, max_samples=48000)
+    eng.set_graphs(False)
+    waves = [synth.wave(48000, 98), synth.wave(30400, 99)]
+    names = eng.trainable_names()
+    out, par = {}, {}
+    for fg in ("1", "0"):
+        monkeypatch.setenv("SUTA_FAST_GELU", fg)
+        out[fg], _, _ = eng.adapt_varlen(waves, 3, SutaHParams(), record=[0, 3])
+        par[fg] = [{n: eng.get_param(b, n) for n in names} for b in range(2)]
+    eng.close()
+    for u in range(2):
+        for r in (0, 3):
+            np.testing.assert_allclose(out["1"][r][u], out["0"][r][u], rtol=0, atol=logits_tol(2e-5),
+                                       err_msg=f"step {r} utt {u}")
+        for n in names:
+            assert_params_close(par["1"][u][n], par["0"][u][n], 2e-5, 3, name=f"utt {u} {n}")
