@@ -43,7 +43,8 @@ PMC_TRAFFIC_C4 = next((p for p in (os.path.join(ROOT, "profiles", r, f) for r, f
                                    (("r3", "pmc_traffic_c4.json"), ("r2", "close_pmc_traffic_c4.json")))
                        if os.path.exists(p)), None)
 BATCH = 164      # utterances per engine call (see --batch)
-PMC_BATCH = 64   # the batch the committed PMC passes (profiles/r3/pmc_traffic*.json) were taken at
+PMC_BATCH = 164    # the batch the committed headline PMC passes (profiles/r3/pmc_traffic.json) were taken at
+PMC_BATCH_C4 = 64  # the batch of the committed C4 passes (profiles/r3/pmc_traffic_c4.json)
 GEMM_KERNELS = ("gemm_glds_kernel", "gemm_f32_kernel", "gemm_splitk_reduce", "attn_fwd_kernel", "attn_bwd_kernel",
                 "posconv_kernel", "flash_fwd_kernel", "flash_bwd_kernel", "flash_dq_reduce")
 # config C4's GEMM family (bf16 mode): every kernel its "gemm" + "attention" timing families launch
@@ -152,7 +153,7 @@ def bench_c4(args, dev):
                            "launches": int(gn), "avg_launch_ms": round(gms / max(1, gn), 5)}
         gx, ax = tex["gemm"], tex["attention"]
         talg = round((gx[2] + ax[2]) / max(1, gx[1] + ax[1]))
-        d4 = json.load(open(PMC_TRAFFIC_C4)) if (PMC_TRAFFIC_C4 and B == PMC_BATCH and N == 128000) else None
+        d4 = json.load(open(PMC_TRAFFIC_C4)) if (PMC_TRAFFIC_C4 and B == PMC_BATCH_C4 and N == 128000) else None
         traffic = gemm_traffic(d4, GEMM_KERNELS_C4) if d4 else None
         res["roofline"].update({
             "traffic": traffic, "traffic_unit": "HBM bytes per GEMM-family launch",
