@@ -44,7 +44,7 @@ PMC_TRAFFIC_C4 = next((p for p in (os.path.join(ROOT, "profiles", r, f) for r, f
                        if os.path.exists(p)), None)
 BATCH = 164      # utterances per engine call (see --batch)
 PMC_BATCH = 164    # the batch the committed headline PMC passes (profiles/r3/pmc_traffic.json) were taken at
-PMC_BATCH_C4 = 64  # the batch of the committed C4 passes (profiles/r3/pmc_traffic_c4.json)
+PMC_BATCH_C4 = 164 # the batch of the committed C4 passes (profiles/r3/pmc_traffic_c4.json)
 GEMM_KERNELS = ("gemm_glds_kernel", "gemm_f32_kernel", "gemm_splitk_reduce", "attn_fwd_kernel", "attn_bwd_kernel",
                 "posconv_kernel", "flash_fwd_kernel", "flash_bwd_kernel", "flash_dq_reduce")
 # config C4's GEMM family (bf16 mode): every kernel its "gemm" + "attention" timing families launch
