@@ -8,7 +8,15 @@ w2v2-base architecture (no checkpoints offline).
 
 Multi-GPU: one process per GPU (torchrun); every rank adapts its own utterances (no data-path
 collective, weak scaling); a barrier + device sync brackets the timed region and the max
-elapsed time over ranks is used.  value = utterances of all ranks / that time.
+elapsed time over ranks is used.  value = utterances of all ranks / that time.  The collectives
+(barrier, max, gather of per-rank facts) go through `Comm` on `--dist-backend` (nccl = RCCL over
+xGMI, the default; gloo for plumbing runs of several ranks on one device).  The rank loop is
+`run()`, which takes the engine factory and the device, so tests/test_bench_dist.py drives the same
+code with a stand-in engine on CPU ranks.
+
+Beside the headline (rank 0, N = 1 only): the same workload at 64 utterances per call (`batch64`),
+the fp32-accurate split-bf16 GEMM mode, config C4 (wav2vec2-large, 20 steps, bf16) and config C5
+(a seeded TED-like length mix through the driver's ragged grouping).
 """
 import argparse
 import json
@@ -27,8 +35,7 @@ import torch  # noqa: E402
 
 from suta_amd import synth  # noqa: E402
 from suta_amd.config import get_config, num_frames  # noqa: E402
-from suta_amd.engine import SutaEngine, SutaHParams  # noqa: E402
-from suta_amd.flops import reference_schedule_flops, suta_flops  # noqa: E402
+from suta_amd.flops import kernel_base, reference_schedule_flops, suta_flops  # noqa: E402
 from suta_amd.weights import synth_weights  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
@@ -36,23 +43,42 @@ BF16_PEAK_TFLOPS = 2500.0      # MI355X_MICROARCH.md: bf16 dense MFMA peak
 BF16_SPLIT_PEAK_TFLOPS = BF16_PEAK_TFLOPS / 6
 HBM_PEAK_TBS = 8.0             # MI355X_MICROARCH.md: HBM3E peak
 RECORD = [0, 1, 3, 5, 10]
-# newest committed rocprofv3 PMC reduction of this workload (tools/pmc_traffic.py; profiles/<round>/README.md)
-PMC_TRAFFIC = next((p for p in (os.path.join(ROOT, "profiles", r, "pmc_traffic.json") for r in ("r3", "r2", "r1"))
+# newest committed rocprofv3 PMC reduction of each workload (tools/pmc_traffic.py; profiles/<round>/README.md)
+ROUNDS = ("r4", "r3", "r2", "r1")
+PMC_TRAFFIC = next((p for p in (os.path.join(ROOT, "profiles", r, "pmc_traffic.json") for r in ROUNDS)
                     if os.path.exists(p)), None)
-PMC_TRAFFIC_C4 = next((p for p in (os.path.join(ROOT, "profiles", r, f) for r, f in
-                                   (("r3", "pmc_traffic_c4.json"), ("r2", "close_pmc_traffic_c4.json")))
+PMC_TRAFFIC_C4 = next((p for p in (os.path.join(ROOT, "profiles", r, "pmc_traffic_c4.json") for r in ROUNDS)
                        if os.path.exists(p)), None)
-BATCH = 164      # utterances per engine call (see --batch)
-PMC_BATCH = 164    # the batch the committed headline PMC passes (profiles/r3/pmc_traffic.json) were taken at
-PMC_BATCH_C4 = 164 # the batch of the committed C4 passes (profiles/r3/pmc_traffic_c4.json)
+# 164 utterances x 399 frames = 65 436 rows = 512 row tiles of 128: every linear's grid (6 / 18 / 24 column tiles on
+# base, 8 / 24 / 32 on large) fills whole rounds of the 512 resident 128 x 128 blocks.  The batch is tuned to the
+# bench's fixed 8 s length (tile quantisation); the `batch64` object keeps the round-over-round comparison at 64.
+BATCH = 164        # utterances per engine call (see --batch); tests/test_gpu_bench_scale.py pins this layout
+C4_BATCH = BATCH   # config C4's utterances per call (see --c4-batch)
+PMC_BATCH = 164    # the batch the committed headline PMC passes were taken at
+PMC_BATCH_C4 = 164  # the batch of the committed C4 passes
+C5_UTTERANCES = 96  # config C5's seeded TED-like length mix (see --c5-n)
 GEMM_KERNELS = ("gemm_glds_kernel", "gemm_f32_kernel", "gemm_splitk_reduce", "attn_fwd_kernel", "attn_bwd_kernel",
                 "posconv_kernel", "flash_fwd_kernel", "flash_bwd_kernel", "flash_dq_reduce")
-# config C4's GEMM family (bf16 mode): every kernel its "gemm" + "attention" timing families launch
+# config C4's GEMM family (bf16 mode): every kernel its "gemm" + "attention" timing families launch.  Matched to the
+# PMC table by base name (pmc_kernel_bytes: the trace may hold mangled names).
 GEMM_KERNELS_C4 = ("gemm_hb_kernel", "gemm_hb8_kernel", "gemm_hbt_kernel", "gemm_x6_kernel", "gemm_gbf_kernel",
-                   "gemm_splitk_reduce",
-                   "to_bf16_kernel", "posconv_bf16_kernel", "flash_fwd_bf16_kernel", "flash_bwd_bf16_kernel",
-                   "flash_dq_reduce")
+                   "gemm_splitk_reduce", "to_bf16_kernel", "posconv_bf16_kernel", "flash_fwd_bf16p_kernel",
+                   "flash_bwd_bf16p_kernel", "flash_fwd_bf16_kernel", "flash_bwd_bf16_kernel", "flash_dq_reduce")
+# kernels of each family the C4 bench layout must have launched (a missing entry means a stale PMC table)
+C4_REQUIRED = ("gemm_hb_kernel", "gemm_hbt_kernel", "flash_fwd_bf16p_kernel", "flash_bwd_bf16p_kernel", "flash_dq_reduce")
 FRONT_KERNELS = ("conv0_gn_kernel", "col_stats_final", "gn_bwd_final", "conv0_dw_reduce")
+
+
+def pmc_kernel_bytes(d, kernels):
+    """{base name: (launches, bytes per launch)} of `kernels` in the PMC table d (entries merged by base name)."""
+    out = {}
+    for k, v in d.items():
+        b = kernel_base(k)
+        if b in kernels:
+            n0, by0 = out.get(b, (0, 0.0))
+            n = n0 + v["launches"]
+            out[b] = (n, (n0 * by0 + v["launches"] * v["hbm_bytes_per_launch"]) / n)
+    return out
 
 
 def pmc(args):
@@ -63,20 +89,24 @@ def pmc(args):
     return json.load(open(PMC_TRAFFIC))
 
 
-def gemm_traffic(d, kernels=GEMM_KERNELS):
-    """HBM bytes per GEMM-family launch from the PMC passes."""
-    n = sum(d[k]["launches"] for k in kernels if k in d)
-    b = sum(d[k]["launches"] * d[k]["hbm_bytes_per_launch"] for k in kernels if k in d)
+def gemm_traffic(d, kernels=GEMM_KERNELS, required=()):
+    """HBM bytes per GEMM-family launch from the PMC passes (None when a required kernel has no entry)."""
+    kb = pmc_kernel_bytes(d, kernels)
+    if any(r not in kb for r in required):
+        return None
+    n = sum(v[0] for v in kb.values())
+    b = sum(v[0] * v[1] for v in kb.values())
     return round(b / n) if n else None
 
 
 def frontend_traffic(d):
     """HBM bytes per conv front-end call (a forward call = 2 conv0_gn passes + the statistics finaliser; a
     backward call = 2 passes + the GroupNorm-backward finaliser + the conv0 dW reduction)."""
-    if "conv0_gn_kernel" not in d:
+    kb = pmc_kernel_bytes(d, FRONT_KERNELS)
+    if "conv0_gn_kernel" not in kb:
         return None
-    b = sum(d[k]["launches"] * d[k]["hbm_bytes_per_launch"] for k in FRONT_KERNELS if k in d)
-    return b / (d["conv0_gn_kernel"]["launches"] / 2)
+    b = sum(v[0] * v[1] for v in kb.values())
+    return b / (kb["conv0_gn_kernel"][0] / 2)
 
 
 def attention_flops(cfg, T, B):
@@ -113,10 +143,226 @@ def cpu_baseline(cfg, n_samples, suta_steps, budget_s=25.0):
                       f"this time"}
 
 
+# ------------------------------------------------------------------------------------------------
+# the rank loop: collectives, device, timed region
+# ------------------------------------------------------------------------------------------------
+class Comm:
+    """The bench's collectives: a barrier around the timed region, the max of the elapsed times over ranks and a
+    gather of small per-rank facts.  world 1: no process group.  nccl (RCCL over xGMI) reduces device tensors,
+    gloo host tensors."""
+
+    def __init__(self, rank=0, world=1, backend="nccl", device=None):
+        self.rank, self.world, self.backend, self.device = rank, world, backend, device
+        if world > 1:
+            import torch.distributed as tdist
+            self.tdist = tdist
+
+    def barrier(self):
+        if self.world > 1:
+            self.tdist.barrier()
+
+    def max(self, x):
+        if self.world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64,
+                         device=self.device if self.backend == "nccl" else "cpu")
+        self.tdist.all_reduce(t, op=self.tdist.ReduceOp.MAX)
+        return float(t.item())
+
+    def gather(self, obj):
+        if self.world == 1:
+            return [obj]
+        out = [None] * self.world
+        self.tdist.all_gather_object(out, obj)
+        return out
+
+
+class Device:
+    """Where the waveforms live and what the bench waits for: GPU `index` (torch.cuda) or, index None, the
+    host (the CPU plumbing test with a stand-in engine)."""
+
+    def __init__(self, index=None):
+        self.index = index
+
+    def put(self, a):
+        t = torch.from_numpy(a)
+        return t.to(f"cuda:{self.index}") if self.index is not None else t
+
+    def sync(self):
+        if self.index is not None:
+            torch.cuda.synchronize(self.index)
+
+
+def shard_start(rank, nbatches, batch, i):
+    """First utterance index of rank `rank`'s batch i: ranks adapt disjoint utterance ranges."""
+    return (rank * nbatches + i) * batch
+
+
+def timed_batches(eng, waves, first, count, S, hp, record, comm, dev):
+    """`count` adapt calls on waves[first:first+count], bracketed by barrier + device sync on both sides;
+    returns (this rank's elapsed s, max over ranks)."""
+    def fence():
+        comm.barrier()
+        dev.sync()
+        eng.sync()
+    fence()
+    t0 = time.perf_counter()
+    for i in range(count):
+        eng.adapt(waves[first + i], S, hp, record=record, want_logits=False)
+    eng.sync()
+    fence()
+    el = time.perf_counter() - t0
+    return el, comm.max(el)
+
+
+def run(args, rank, world, comm, dev, make_engine):
+    """One rank of the bench; rank 0 prints the JSON line and returns it (other ranks return None)."""
+    from suta_amd.engine import SutaHParams
+    cfg = get_config(args.model)
+    B, N, S = args.batch, args.n_samples, args.suta_steps
+    eng = make_engine(cfg, B, N)
+    eng.set_precision(args.precision)
+    hp = SutaHParams()  # scripts/LS.sh flags
+    nbatches = args.warmup + args.steps
+    # inputs resident in device memory before timing: distinct utterances per rank and batch
+    starts = [shard_start(rank, nbatches, B, i) for i in range(nbatches)]
+    waves = [dev.put(synth.batch(N, B, start=s)) for s in starts]
+    dev.sync()
+    for i in range(args.warmup):
+        eng.adapt(waves[i], S, hp, record=RECORD, want_logits=False)
+    el_rank, el = timed_batches(eng, waves, args.warmup, args.steps, S, hp, RECORD, comm, dev)
+    rank_el = comm.gather(round(el_rank, 6))
+    shards = comm.gather([starts[args.warmup], starts[-1] + B])   # timed utterances [first, end) per rank
+    # roofline pass (outside the timed region): per-launch HIP events on the engine stream; this runs
+    # the eager path (timing disables graph replay), so its batch time is reported separately
+    timing, timing_el, tsteps = None, None, max(1, min(args.timing_steps, args.steps))
+    if not args.no_timing:
+        eng.set_timing(True)
+        comm.barrier()
+        t1 = time.perf_counter()
+        for i in range(tsteps):
+            eng.adapt(waves[args.warmup + i], S, hp, record=RECORD, want_logits=False)
+        eng.sync()
+        timing_el = time.perf_counter() - t1
+        timing = eng.get_timing()
+        timing_ex = eng.get_timing_ex()
+        eng.set_timing(False)
+
+    utts = B * args.steps * world
+    value = utts / el
+    flops_utt = suta_flops(cfg, N, S)
+    out = {
+        "metric": "adapted utterances/sec (whole node) at 10 SUTA steps, w2v2-base; WER parity",
+        "value": round(value, 4), "unit": "utt/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(1000 * el / args.steps, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32", "data": "synthetic", "precision": args.precision,
+        "config": {"workload": f"{args.model} SUTA {S} steps on {N}-sample (8 s) utterances, {B} utterances "
+                               f"per GPU per step, scripts/LS.sh flags",
+                   "model": args.model, "global_batch": B * world, "seq_len": num_frames(cfg, N),
+                   "n_samples": N, "suta_steps": S, "parallelism": f"utterance-sharded x{world}",
+                   "batch_note": "164 utterances x 399 frames = 512 row tiles of 128 (tuned to the bench's fixed "
+                                 "length); see batch64 for the 64-per-call line"},
+        "algorithmic_tflops": round(flops_utt * utts / el / 1e12, 3),
+        "dist": {"backend": comm.backend if world > 1 else None, "rank_elapsed_s": rank_el,
+                 "utterance_shards": shards},
+    }
+    if timing:
+        gms, gn = timing["gemm"]
+        # dominant kernel family: the fp32 MFMA GEMM (every conv/linear/attention product)
+        gemm_flops = flops_utt * B * tsteps  # per-rank algorithmic GEMM-shaped FLOPs of the timing pass
+        achieved = gemm_flops / (gms / 1000.0) / 1e12 if gms > 0 else None
+        d = pmc(args)
+        traffic = gemm_traffic(d) if d else None
+        gx, ax, fx = timing_ex["gemm"], timing_ex["attention"], timing_ex["frontend"]
+        traffic_alg = round((gx[2] + ax[2]) / max(1, gx[1] + ax[1]))
+        out["roofline"] = {"bound": "mfma", "achieved": round(achieved, 3) if achieved else None,
+                           "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                           "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4) if achieved else None,
+                           "traffic": traffic,
+                           "traffic_unit": "HBM bytes per GEMM launch",
+                           "traffic_source": f"{os.path.relpath(PMC_TRAFFIC, ROOT)} (rocprofv3 --pmc FETCH_SIZE x2 + "
+                                             "WRITE_SIZE passes of this workload)" if traffic else None,
+                           "traffic_alg": traffic_alg,
+                           "traffic_alg_def": "algorithmic bytes per GEMM-family launch, measured in this run: every "
+                                              "operand touched once at its stored element size (A unique rows, B per "
+                                              "distinct slice, C written, epilogue operands), no tile re-reads or "
+                                              "split-K partials",
+                           "traffic_ratio": round(traffic / traffic_alg, 3) if traffic and traffic_alg else None,
+                           "kernel": "fp32 MFMA GEMM family: gemm_glds_kernel + gemm_f32_kernel + posconv_kernel + flash attention (flash_fwd_kernel, flash_bwd_kernel + flash_dq_reduce) (all launches)",
+                           "launches": int(gn), "avg_launch_ms": round(gms / max(1, gn), 5),
+                           "measured": f"HIP events around every GEMM-family launch on the engine stream, separate "
+                                       f"pass of {tsteps} batch(es) after the timed region (eager path: "
+                                       f"{round(1000 * timing_el / tsteps, 1)} ms per batch vs "
+                                       f"{round(1000 * el / args.steps, 1)} ms replayed)"}
+        out["time_breakdown_ms"] = {k: round(v[0], 2) for k, v in timing_ex.items()}
+        # conv feature-encoder front-end (north_star: achieved HBM GB/s on the conv front-end)
+        if fx[1]:
+            fms = fx[0] / fx[1]
+            fb = frontend_traffic(d) if d else None
+            out["frontend"] = {"kernel": "conv0_gn_kernel passes (conv0 + GroupNorm + GELU, fwd and bwd) + finalisers",
+                               "calls": int(fx[1]), "avg_call_ms": round(fms, 4),
+                               "alg_bytes_per_call": round(fx[2] / fx[1]),
+                               "alg_tbs": round(fx[2] / fx[1] / (fms / 1000) / 1e12, 3),
+                               "hbm_bytes_per_call": round(fb) if fb else None,
+                               "peak_tbs": HBM_PEAK_TBS}
+            if fb:
+                out["frontend"]["hbm_tbs"] = round(fb / (fms / 1000) / 1e12, 3)
+                out["roofline"]["frontend_hbm_tbs"] = out["frontend"]["hbm_tbs"]
+        # attention products alone (fused kernels): algorithmic FLOPs / their time
+        if ax[1]:
+            T = num_frames(cfg, N)
+            af, ab = attention_flops(cfg, T, B)
+            layers = cfg["num_hidden_layers"]
+            nf, nb = (S + 1) * layers * tsteps, S * layers * tsteps
+            out["attention"] = {"launches": int(ax[1]), "ms": round(ax[0], 2),
+                                "tflops": round((nf * af + nb * ab) / (ax[0] / 1000) / 1e12, 3)}
+    if args.batch64 and B > 64 and args.steps >= 2:
+        # the same workload at 64 utterances per call (the batch of rounds 1-2): round-over-round comparison
+        w64 = [w[:64] for w in waves]
+        eng.adapt(w64[0], S, hp, record=RECORD, want_logits=False)     # new layout: capture on the next call
+        eng.adapt(w64[1], S, hp, record=RECORD, want_logits=False)
+        el64_rank, el64 = timed_batches(eng, w64, args.warmup, args.steps, S, hp, RECORD, comm, dev)
+        out["batch64"] = {"value": round(64 * args.steps * world / el64, 4),
+                          "ms_per_step": round(1000 * el64 / args.steps, 3), "batch": 64}
+    if args.also_split and args.precision == "fp32":
+        # same workload with the fp32-accurate split-bf16 GEMMs (reported beside the headline)
+        eng.set_precision("fp32-split-bf16")
+        eng.adapt(waves[0], S, hp, record=RECORD, want_logits=False)
+        el2_rank, el2 = timed_batches(eng, waves, args.warmup, args.steps, S, hp, RECORD, comm, dev)
+        split = {"precision": "fp32-split-bf16", "value": round(utts / el2, 4),
+                 "ms_per_step": round(1000 * el2 / args.steps, 3)}
+        if not args.no_timing:
+            eng.set_timing(True)
+            for i in range(tsteps):
+                eng.adapt(waves[args.warmup + i], S, hp, record=RECORD, want_logits=False)
+            t2 = eng.get_timing()
+            eng.set_timing(False)
+            gms2 = t2["gemm"][0]
+            ach2 = flops_utt * B * tsteps / (gms2 / 1000.0) / 1e12
+            split["roofline"] = {"bound": "mfma", "achieved": round(ach2, 3), "peak": BF16_SPLIT_PEAK_TFLOPS,
+                                 "unit": "TFLOP/s (fp32-equivalent)", "frac": round(ach2 / BF16_SPLIT_PEAK_TFLOPS, 4),
+                                 "note": "6 bf16 MFMA products per fp32 MAC: peak = 2500 TF bf16 dense / 6"}
+        out["fp32_split_bf16"] = split
+        eng.set_precision("fp32")
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(cfg, N, S)
+    eng.close()
+    if world == 1 and args.precision == "fp32" and dev.index is not None:
+        if args.c4:
+            out["c4"] = bench_c4(args, dev.index)
+        if args.c5:
+            out["c5"] = bench_c5(args, dev.index)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+        return out
+    return None
+
+
 def bench_c4(args, dev):
     """BASELINE.json config C4: wav2vec2-large-960h-lv60 shapes, 20-step SUTA, bf16 GEMMs (operands
     rounded to bf16, fp32 accumulation; norms, softmax, loss, AdamW and master tensors fp32), 1 GPU,
     8 s utterances.  A secondary line beside the C2 headline."""
+    from suta_amd.engine import SutaEngine, SutaHParams
     cfg = get_config("wav2vec2-large")
     B, N, S = args.c4_batch, args.n_samples, 20
     eng = SutaEngine(cfg, synth_weights(cfg), device=dev, max_batch=B, max_samples=N)
@@ -154,7 +400,7 @@ def bench_c4(args, dev):
         gx, ax = tex["gemm"], tex["attention"]
         talg = round((gx[2] + ax[2]) / max(1, gx[1] + ax[1]))
         d4 = json.load(open(PMC_TRAFFIC_C4)) if (PMC_TRAFFIC_C4 and B == PMC_BATCH_C4 and N == 128000) else None
-        traffic = gemm_traffic(d4, GEMM_KERNELS_C4) if d4 else None
+        traffic = gemm_traffic(d4, GEMM_KERNELS_C4, C4_REQUIRED) if d4 else None
         res["roofline"].update({
             "traffic": traffic, "traffic_unit": "HBM bytes per GEMM-family launch",
             "traffic_source": f"{os.path.relpath(PMC_TRAFFIC_C4, ROOT)} (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE "
@@ -173,18 +419,93 @@ def bench_c4(args, dev):
     return res
 
 
-def main():
+def c5_lengths(n, seed=20260416):
+    """Config C5's seeded TED-like length mix: log-normal around 10 s (sigma 0.6), clipped to [2 s, 37.5 s] (the
+    reference's 600 000-sample cap, data.py:19-22), in samples."""
+    rng = np.random.default_rng(seed)
+    sec = np.clip(rng.lognormal(np.log(10.0), 0.6, n), 2.0, 37.5)
+    return np.minimum((sec * 16000).astype(np.int64), 600000)
+
+
+def bench_c5(args, dev):
+    """BASELINE.json config C5 on one GPU: TED-like variable-length utterances (reference corpus/ted.py sorts by
+    transcript length, ascending; data.py truncates at 600 000 samples) adapted as the driver adapts them: length
+    sorted, grouped by suta_amd/main.py ragged_groups with the driver's default --gpu_batch / --gpu_budget_s /
+    --gpu_min_fill, each group one suta_adapt_varlen call (every utterance at its own length).  w2v2-base, 10 steps,
+    LS.sh flags, fp32.  FLOPs on the true lengths; padding is reported, not credited."""
+    from suta_amd.engine import SutaEngine, SutaHParams
+    from suta_amd.main import LAYOUT_QUANTUM, build_parser, ragged_groups
+    drv = build_parser().parse_args([])
+    cfg = get_config("wav2vec2-base")
+    S = 10
+    ns = c5_lengths(args.c5_n)
+    order = np.argsort(ns, kind="stable")
+    groups = [order[g] for g in ragged_groups([int(ns[i]) for i in order], drv.gpu_batch, drv.gpu_budget_s * 16000,
+                                                  drv.gpu_min_fill)]
+    q = LAYOUT_QUANTUM
+    widths = [-(-int(ns[g].max()) // q) * q for g in groups]
+    eng = SutaEngine(cfg, synth_weights(cfg), device=dev, max_batch=max(len(g) for g in groups),
+                     max_samples=max(widths))
+    hp = SutaHParams()
+    pads = []
+    for g, w in zip(groups, widths):
+        p = np.zeros((len(g), w), np.float32)
+        for j, i in enumerate(g):
+            p[j, :ns[i]] = synth.wave(int(ns[i]), 70000 + int(i))
+        pads.append(torch.from_numpy(p).to(f"cuda:{dev}"))
+    lens = [[int(ns[i]) for i in g] for g in groups]
+    big = int(np.argmax([len(g) * w for g, w in zip(groups, widths)]))
+    eng.adapt_varlen(pads[big], 1, hp, record=[1], lengths=lens[big], want_logits=False)   # workspace at its max
+    torch.cuda.synchronize()
+    eng.sync()
+
+    def one_pass():
+        for p, ln in zip(pads, lens):
+            eng.adapt_varlen(p, S, hp, record=RECORD, lengths=ln, want_logits=False)
+        eng.sync()
+    t0 = time.perf_counter()
+    one_pass()
+    el = time.perf_counter() - t0
+    T_true = sum(num_frames(cfg, int(n)) for n in ns)
+    T_pad = sum(len(g) * num_frames(cfg, w) for g, w in zip(groups, widths))
+    flops = sum(suta_flops(cfg, int(n), S) for n in ns)
+    res = {"workload": f"wav2vec2-base SUTA {S} steps, {len(ns)} TED-like utterances (log-normal around 10 s, "
+                       "2-37.5 s, seeded), length-sorted ragged batches grouped by the driver's ragged_groups "
+                       f"(--gpu_batch {drv.gpu_batch}, --gpu_budget_s {drv.gpu_budget_s:g}, --gpu_min_fill "
+                       f"{drv.gpu_min_fill:g}), scripts/LS.sh flags, fp32",
+           "config": "C5", "precision": "fp32", "value": round(len(ns) / el, 4), "unit": "utt/s",
+           "audio_s_per_s": round(float(ns.sum()) / 16000 / el, 2), "seconds": round(el, 3),
+           "n_utterances": len(ns), "mean_seconds": round(float(ns.mean()) / 16000, 2),
+           "max_seconds": round(float(ns.max()) / 16000, 2), "n_batches": len(groups),
+           "batch_sizes": [len(g) for g in groups], "padded_frame_fraction": round(1.0 - T_true / T_pad, 4),
+           "algorithmic_tflops": round(flops / el / 1e12, 3)}
+    if not args.no_timing:
+        eng.set_timing(True)
+        one_pass()
+        t = eng.get_timing()
+        eng.set_timing(False)
+        gms, gn = t["gemm"]
+        ach = flops / (gms / 1000.0) / 1e12
+        res["roofline"] = {"bound": "mfma", "achieved": round(ach, 3), "peak": FP32_MFMA_PEAK_TFLOPS,
+                           "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
+                           "kernel": "fp32 MFMA GEMM family (as the headline), FLOPs on true lengths",
+                           "launches": int(gn), "avg_launch_ms": round(gms / max(1, gn), 5)}
+    eng.close()
+    return res
+
+
+def build_parser():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--warmup", type=int, default=1)
-    # 164 utterances x 399 frames = 65 436 rows = 512 row tiles of 128: every linear's grid (6 / 18 / 24 column
-    # tiles on base, 8 / 24 / 32 on large) fills whole rounds of the 512 resident 128 x 128 blocks (64: 3.125 rounds of
-    # the N = 1024 grids); measured 37.2 -> 38.2 utt/s (base) and 36.0 -> 38.1 (C4) on one box
     ap.add_argument("--batch", type=int, default=BATCH, help="utterances in flight per GPU (engine slots)")
     ap.add_argument("--n-samples", type=int, default=128000)
     ap.add_argument("--suta-steps", type=int, default=10)
     ap.add_argument("--model", default="wav2vec2-base")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="collectives under torchrun: nccl = RCCL over xGMI (one GPU per rank); gloo = host "
+                         "collectives, ranks may share a device (rank r uses GPU LOCAL_RANK mod device count)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip the per-kernel HIP-event timing pass")
     ap.add_argument("--timing-steps", type=int, default=1,
@@ -193,15 +514,24 @@ def main():
                     help="GEMM arithmetic: exact fp32 MFMA, fp32-accurate 3-way bf16 split, or bf16 (config C4)")
     ap.add_argument("--no-c4", dest="c4", action="store_false",
                     help="skip the config-C4 line (wav2vec2-large, 20 SUTA steps, bf16 GEMMs; 1 GPU only)")
-    ap.add_argument("--c4-batch", type=int, default=BATCH)
+    ap.add_argument("--c4-batch", type=int, default=C4_BATCH)
     ap.add_argument("--only-c4", action="store_true", help="print only the config-C4 line (profiling)")
+    ap.add_argument("--no-c5", dest="c5", action="store_false",
+                    help="skip the config-C5 line (TED-like length mix, driver grouping; 1 GPU only)")
+    ap.add_argument("--c5-n", type=int, default=C5_UTTERANCES)
+    ap.add_argument("--only-c5", action="store_true", help="print only the config-C5 line")
+    ap.add_argument("--no-batch64", dest="batch64", action="store_false",
+                    help="skip the 64-utterances-per-call line")
     ap.add_argument("--no-split", dest="also_split", action="store_false",
                     help="do not also time the fp32-accurate split-bf16 GEMM mode")
-    args = ap.parse_args()
+    return ap
 
-    if args.only_c4:
+
+def main():
+    args = build_parser().parse_args()
+    if args.only_c4 or args.only_c5:
         torch.cuda.set_device(0)
-        print(json.dumps(bench_c4(args, 0)), flush=True)
+        print(json.dumps(bench_c4(args, 0) if args.only_c4 else bench_c5(args, 0)), flush=True)
         return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -211,162 +541,28 @@ def main():
               f"`python -m torch.distributed.run --nproc-per-node {args.gpus} bench.py --gpus {args.gpus}`",
               file=sys.stderr)
         sys.exit(2)
-    dist = world > 1
-    if dist:
+    ndev = torch.cuda.device_count()
+    if ndev < 1:
+        raise SystemExit("bench.py needs a GPU (the engine has no CPU path)")
+    if args.dist_backend == "nccl" and world > ndev:
+        raise SystemExit(f"--dist-backend nccl: {world} ranks but {ndev} visible GPU(s); use one rank per GPU, or "
+                         "--dist-backend gloo to share a device")
+    gpu = local % ndev
+    torch.cuda.set_device(gpu)
+    if world > 1:
         import torch.distributed as tdist
-        torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.cuda.current_device()
+        if args.dist_backend == "nccl":
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            tdist.init_process_group("gloo")
+    comm = Comm(rank, world, args.dist_backend, torch.device("cuda", gpu))
+    from suta_amd.engine import SutaEngine
 
-    cfg = get_config(args.model)
-    B, N, S = args.batch, args.n_samples, args.suta_steps
-    eng = SutaEngine(cfg, synth_weights(cfg), device=dev, max_batch=B, max_samples=N)
-    eng.set_precision(args.precision)
-    hp = SutaHParams()  # scripts/LS.sh flags
-    nbatches = args.warmup + args.steps
-    # inputs resident in HBM before timing: distinct utterances per rank and batch
-    waves = [torch.from_numpy(synth.batch(N, B, start=(rank * nbatches + i) * B)).to(f"cuda:{dev}")
-             for i in range(nbatches)]
-    torch.cuda.synchronize()
-
-    for i in range(args.warmup):
-        eng.adapt(waves[i], S, hp, record=RECORD, want_logits=False)
-
-    def barrier():
-        if dist:
-            tdist.barrier()
-        torch.cuda.synchronize()
-        eng.sync()
-
-    barrier()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        eng.adapt(waves[args.warmup + i], S, hp, record=RECORD, want_logits=False)
-    eng.sync()
-    barrier()
-    el = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([el], device=f"cuda:{dev}")
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        el = float(t.item())
-    # roofline pass (outside the timed region): per-launch HIP events on the engine stream; this runs
-    # the eager path (timing disables graph replay), so its batch time is reported separately
-    timing, timing_el, tsteps = None, None, max(1, min(args.timing_steps, args.steps))
-    if not args.no_timing:
-        eng.set_timing(True)
-        barrier()
-        t1 = time.perf_counter()
-        for i in range(tsteps):
-            eng.adapt(waves[args.warmup + i], S, hp, record=RECORD, want_logits=False)
-        eng.sync()
-        timing_el = time.perf_counter() - t1
-        timing = eng.get_timing()
-        timing_ex = eng.get_timing_ex()
-        eng.set_timing(False)
-
-    utts = B * args.steps * world
-    value = utts / el
-    flops_utt = suta_flops(cfg, N, S)
-    out = {
-        "metric": "adapted utterances/sec (whole node) at 10 SUTA steps, w2v2-base; WER parity",
-        "value": round(value, 4), "unit": "utt/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(1000 * el / args.steps, 3), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "f32", "data": "synthetic", "precision": args.precision,
-        "config": {"workload": f"{args.model} SUTA {S} steps on {N}-sample (8 s) utterances, {B} utterances "
-                               f"per GPU per step, scripts/LS.sh flags",
-                   "model": args.model, "global_batch": B * world, "seq_len": num_frames(cfg, N),
-                   "n_samples": N, "suta_steps": S, "parallelism": f"utterance-sharded x{world}"},
-        "algorithmic_tflops": round(flops_utt * utts / el / 1e12, 3),
-    }
-    if timing:
-        gms, gn = timing["gemm"]
-        # dominant kernel family: the fp32 MFMA GEMM (every conv/linear/attention product)
-        gemm_flops = flops_utt * B * tsteps  # per-rank algorithmic GEMM-shaped FLOPs of the timing pass
-        achieved = gemm_flops / (gms / 1000.0) / 1e12 if gms > 0 else None
-        d = pmc(args)
-        traffic = gemm_traffic(d) if d else None
-        gx, ax, fx = timing_ex["gemm"], timing_ex["attention"], timing_ex["frontend"]
-        traffic_alg = round((gx[2] + ax[2]) / max(1, gx[1] + ax[1]))
-        out["roofline"] = {"bound": "mfma", "achieved": round(achieved, 3) if achieved else None,
-                           "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                           "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4) if achieved else None,
-                           "traffic": traffic,
-                           "traffic_unit": "HBM bytes per GEMM launch",
-                           "traffic_source": f"{os.path.relpath(PMC_TRAFFIC, ROOT)} (rocprofv3 --pmc FETCH_SIZE x2 + "
-                                             "WRITE_SIZE passes of this workload)" if traffic else None,
-                           "traffic_alg": traffic_alg,
-                           "traffic_alg_def": "algorithmic bytes per GEMM-family launch, measured in this run: every "
-                                              "operand touched once (A unique rows, B per distinct slice, C written, "
-                                              "epilogue operands), no tile re-reads or split-K partials",
-                           "traffic_ratio": round(traffic / traffic_alg, 3) if traffic and traffic_alg else None,
-                           "kernel": "fp32 MFMA GEMM family: gemm_glds_kernel + gemm_f32_kernel + posconv_kernel + flash attention (flash_fwd_kernel, flash_bwd_kernel + flash_dq_reduce) (all launches)",
-                           "launches": int(gn), "avg_launch_ms": round(gms / max(1, gn), 5),
-                           "measured": f"HIP events around every GEMM-family launch on the engine stream, separate "
-                                       f"pass of {tsteps} batch(es) after the timed region (eager path: "
-                                       f"{round(1000 * timing_el / tsteps, 1)} ms per batch vs "
-                                       f"{round(1000 * el / args.steps, 1)} ms replayed)"}
-        out["time_breakdown_ms"] = {k: round(v[0], 2) for k, v in timing_ex.items()}
-        # conv feature-encoder front-end (north_star: achieved HBM GB/s on the conv front-end)
-        if fx[1]:
-            fms = fx[0] / fx[1]
-            fb = frontend_traffic(d) if d else None
-            out["frontend"] = {"kernel": "conv0_gn_kernel passes (conv0 + GroupNorm + GELU, fwd and bwd) + finalisers",
-                               "calls": int(fx[1]), "avg_call_ms": round(fms, 4),
-                               "alg_bytes_per_call": round(fx[2] / fx[1]),
-                               "alg_tbs": round(fx[2] / fx[1] / (fms / 1000) / 1e12, 3),
-                               "hbm_bytes_per_call": round(fb) if fb else None,
-                               "peak_tbs": HBM_PEAK_TBS}
-            if fb:
-                out["frontend"]["hbm_tbs"] = round(fb / (fms / 1000) / 1e12, 3)
-                out["roofline"]["frontend_hbm_tbs"] = out["frontend"]["hbm_tbs"]
-        # attention products alone (fused kernels): algorithmic FLOPs / their time
-        if ax[1]:
-            T = num_frames(cfg, N)
-            af, ab = attention_flops(cfg, T, B)
-            layers = cfg["num_hidden_layers"]
-            nf, nb = (S + 1) * layers * tsteps, S * layers * tsteps
-            out["attention"] = {"launches": int(ax[1]), "ms": round(ax[0], 2),
-                                "tflops": round((nf * af + nb * ab) / (ax[0] / 1000) / 1e12, 3)}
-    if args.also_split and args.precision == "fp32":
-        # same workload with the fp32-accurate split-bf16 GEMMs (reported beside the headline)
-        eng.set_precision("fp32-split-bf16")
-        eng.adapt(waves[0], S, hp, record=RECORD, want_logits=False)
-        barrier()
-        t1 = time.perf_counter()
-        for i in range(args.steps):
-            eng.adapt(waves[args.warmup + i], S, hp, record=RECORD, want_logits=False)
-        eng.sync()
-        barrier()
-        el2 = time.perf_counter() - t1
-        if dist:
-            t = torch.tensor([el2], device=f"cuda:{dev}")
-            tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-            el2 = float(t.item())
-        split = {"precision": "fp32-split-bf16", "value": round(utts / el2, 4),
-                 "ms_per_step": round(1000 * el2 / args.steps, 3)}
-        if not args.no_timing:
-            eng.set_timing(True)
-            for i in range(tsteps):
-                eng.adapt(waves[args.warmup + i], S, hp, record=RECORD, want_logits=False)
-            t2 = eng.get_timing()
-            eng.set_timing(False)
-            gms2 = t2["gemm"][0]
-            ach2 = flops_utt * B * tsteps / (gms2 / 1000.0) / 1e12
-            split["roofline"] = {"bound": "mfma", "achieved": round(ach2, 3), "peak": BF16_SPLIT_PEAK_TFLOPS,
-                                 "unit": "TFLOP/s (fp32-equivalent)", "frac": round(ach2 / BF16_SPLIT_PEAK_TFLOPS, 4),
-                                 "note": "6 bf16 MFMA products per fp32 MAC: peak = 2500 TF bf16 dense / 6"}
-        out["fp32_split_bf16"] = split
-        eng.set_precision("fp32")
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(cfg, N, S)
-    eng.close()
-    if world == 1 and args.c4 and args.precision == "fp32":
-        out["c4"] = bench_c4(args, dev)
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-    if dist:
+    def make_engine(cfg, B, N):
+        return SutaEngine(cfg, synth_weights(cfg), device=gpu, max_batch=B, max_samples=N)
+    run(args, rank, world, comm, Device(gpu), make_engine)
+    if world > 1:
+        import torch.distributed as tdist
         tdist.destroy_process_group()
 
 

@@ -186,6 +186,24 @@ constexpr int FK = 64;
 constexpr int FK_LDT = FK + 4;  // transposed V tile row stride
 constexpr int FF_NW_BF = 4;     // waves per block of the bf16 forward
 
+// An utterance with no valid key (tl <= 0) has no softmax: its rows get ctx = 0 and LSE = -inf, and the kernel
+// returns before any LDS image is filled (the peeled last tile would otherwise run tile -1 on stale LDS).  The host
+// rejects zero-frame utterances (engine set_lengths: "utterance too short"), so this is a guard, not a path.
+__device__ __forceinline__ void flash_fwd_no_keys(float* ctx, __bf16* ctxb, float* lse, long row0, long bhT, int T,
+                                                  int H, int hd, int q0, int l32, int h) {
+    const int q = q0 + l32;
+    if (q0 >= T || q >= T) return;
+    float* cr = ctx + (row0 + q) * H + hd * 64 + 32 * h;
+#pragma unroll
+    for (int c = 0; c < 32; ++c) cr[c] = 0.f;
+    if (ctxb) {
+        __bf16* br = ctxb + (row0 + q) * H + hd * 64 + 32 * h;
+#pragma unroll
+        for (int c = 0; c < 32; ++c) br[c] = (__bf16)0.f;
+    }
+    if (h == 0) lse[bhT + q] = -INFINITY;
+}
+
 template <int NW, bool BF16>
 __global__ __launch_bounds__(NW * 64) void flash_fwd_kernel(const float* __restrict__ qkv, float* __restrict__ ctx,
                                                             float* __restrict__ lse, int T, int NH, int H, float scale,
@@ -204,6 +222,10 @@ __global__ __launch_bounds__(NW * 64) void flash_fwd_kernel(const float* __restr
     const float* Kb = Qb + H;
     const float* Vb = Qb + 2 * H;
     const int q0 = (qb * NW + w) * 32;
+    if (tl <= 0) {  // (block-uniform: one utterance per block)
+        flash_fwd_no_keys(ctx, ctxb, lse, (long)u * T, (long)bh * T, T, H, hd, q0, l32, h);
+        return;
+    }
     const bool active = q0 < T;
     const float sl2 = scale * LOG2E;
     RowReg<BF16> qv;
@@ -616,6 +638,10 @@ __global__ __launch_bounds__(FF_NW_BF * 64) void flash_fwd_bf16_kernel(
     const float* Kb = Qb + H;
     const float* Vb = Qb + 2 * H;
     const int q0 = (qb * NW + w) * 32;
+    if (tl <= 0) {  // (block-uniform: one utterance per block)
+        flash_fwd_no_keys(ctx, ctxb, lse, (long)u * T, (long)bh * T, T, H, hd, q0, l32, h);
+        return;
+    }
     const bool active = q0 < T;
     const float sl2 = scale * LOG2E;
     RowReg<true> qv;
@@ -794,6 +820,10 @@ __global__ __launch_bounds__(NW * 64) void flash_fwd_bf16p_kernel(
     const long ld = 3L * H;
     const __bf16* Qb = qkvb + (long)u * T * ld + hd * 64;
     const int q0 = (qb * NW + w) * 32;
+    if (tl <= 0) {  // (block-uniform: one utterance per block)
+        flash_fwd_no_keys(ctx, ctxb, lse, (long)u * T, (long)bh * T, T, H, hd, q0, l32, h);
+        return;
+    }
     const bool active = q0 < T;
     const float sl2 = scale * LOG2E;
     RowReg<true> qv;
@@ -1339,11 +1369,8 @@ static int fb_nw() {
 }
 
 // bf16 mode: LDS images in bf16 (flash_*_bf16_kernel; env SUTA_FLASH_BF16_IMG=0 selects the fp32-image
-// instantiations for A/B runs; read at every launch, so one process can run both)
-static bool fb_img() {
-    const char* e = std::getenv("SUTA_FLASH_BF16_IMG");
-    return !(e && atoi(e) == 0);
-}
+// instantiations for A/B runs; from the call's switch snapshot, common.h SutaSwitches)
+static bool fb_img() { return suta_switches().flash_bf16_img != 0; }
 
 long flash_dq_scratch_floats(int B, int T, int NH) {
     const int ng = (T + 31) / 32, nkb = (ng + fb_nw() - 1) / fb_nw();
@@ -1351,11 +1378,8 @@ long flash_dq_scratch_floats(int B, int T, int NH) {
 }
 
 // bf16 mode, bf16 qkv plane given: flash_fwd_bf16p_kernel (env SUTA_FLASH_FWD_PLANE=0 keeps the fp32-row
-// kernels for A/B runs; read at every launch)
-static bool ff_plane() {
-    const char* e = std::getenv("SUTA_FLASH_FWD_PLANE");
-    return !(e && atoi(e) == 0);
-}
+// kernels for A/B runs; from the call's switch snapshot)
+static bool ff_plane() { return suta_switches().flash_fwd_plane != 0; }
 
 bool flash_fwd_reads_plane(bool bf16, const void* qkvb, int H) { return bf16 && qkvb && H % 8 == 0 && ff_plane(); }
 
@@ -1369,9 +1393,8 @@ bool launch_flash_fwd(const float* qkv, float* ctx, float* lse, int B, int T, in
     if (!qkv && !on_plane) throw std::invalid_argument("flash_fwd: fp32 qkv not written and the plane kernel not taken");
     if (on_plane) {
         if (reinterpret_cast<uintptr_t>(qkvb) & 15) throw std::invalid_argument("flash_fwd: bf16 qkv plane not 16-B aligned");
-        // SUTA_FLASH_FWD_NW=8: 8-wave blocks (256 queries share each K / V tile copy); read at every launch
-        const char* ev = std::getenv("SUTA_FLASH_FWD_NW");
-        if (ev && atoi(ev) == 8) {
+        // SUTA_FLASH_FWD_NW=8: 8-wave blocks (256 queries share each K / V tile copy); switch snapshot
+        if (suta_switches().flash_fwd_nw == 8) {
             const int nqb8 = (ng + 7) / 8;
             hipLaunchKernelGGL(flash_fwd_bf16p_kernel<8>, dim3((unsigned)((long)B * NH * nqb8)), dim3(512), 0, st,
                                reinterpret_cast<const __bf16*>(qkvb), ctx, lse, T, NH, H, scale, tlen, nqb8, ctxb);
@@ -1409,11 +1432,8 @@ static void flash_bwd_go(dim3 grid, hipStream_t st, const float* qkv, const floa
 }
 
 // bf16 mode, bf16 planes of qkv and dctx given: flash_bwd_bf16p_kernel (env SUTA_FLASH_BWD_PLANE=0 keeps the
-// fp32-row kernels for A/B runs; read at every launch)
-static bool fb_plane() {
-    const char* e = std::getenv("SUTA_FLASH_BWD_PLANE");
-    return !(e && atoi(e) == 0);
-}
+// fp32-row kernels for A/B runs; from the call's switch snapshot)
+static bool fb_plane() { return suta_switches().flash_bwd_plane != 0; }
 
 bool flash_bwd_reads_planes(bool bf16, const void* qkvb, const void* dctxb, int H) {
     return bf16 && fb_nw() == FBB_NW && qkvb && dctxb && H % 8 == 0 && fb_plane();

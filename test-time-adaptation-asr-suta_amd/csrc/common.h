@@ -53,6 +53,30 @@ __device__ __forceinline__ float dgelu_fast(float x) {
     return cdf + x * (0.39894228040143268f * e);
 }
 
+// A/B switches read from the environment (SUTA_* = 0 selects the path a round replaced).  They decide which
+// buffers a forward writes in which format (fp32 or a bf16 plane) and which the backward reads, so one snapshot is
+// taken per engine call (suta_latch_switches, at the start of suta_forward / suta_step / suta_adapt*) and every
+// launcher and engine predicate of that call reads the snapshot: a switch flipped between a forward and its
+// backward, or between graph capture and replay, cannot mismatch formats.  The snapshot is part of the engine's
+// graph key.  Launchers used without an engine (tools/) take a snapshot on first use.
+struct SutaSwitches {
+    int latched;
+    int fast_gelu;        // SUTA_FAST_GELU: branch-free GELU / GELU' (front-end and bf16-plane epilogues)
+    int flash_fwd_plane;  // SUTA_FLASH_FWD_PLANE: flash forward on the bf16 qkv plane
+    int flash_bwd_plane;  // SUTA_FLASH_BWD_PLANE: flash backward on the bf16 qkv / dctx planes
+    int flash_bf16_img;   // SUTA_FLASH_BF16_IMG: bf16 LDS images in the fp32-row bf16 flash kernels
+    int conv_planes;      // SUTA_CONV_PLANES
+    int pre_bf16;         // SUTA_PRE_BF16
+    int conv_z_bf16;      // SUTA_CONV_Z_BF16
+    int dy_planes;        // SUTA_DY_PLANES
+    int conv_dx_planes;   // SUTA_CONV_DX_PLANES
+    int fused_conv_ln;    // SUTA_FUSED_CONV_LN
+    int hb8;              // SUTA_HB8 (default 0): 256 x 256 ping-pong bf16-plane GEMM selection mode
+    int flash_fwd_nw;     // SUTA_FLASH_FWD_NW (default 4): waves per block of the bf16-plane flash forward
+};
+void suta_latch_switches();
+const SutaSwitches& suta_switches();  // the snapshot (taken now if none was)
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -99,11 +99,8 @@ struct DevBuf {
 };
 
 // SUTA_FUSED_CONV_LN=0: the layer-mode conv stack's LayerNorm backward without the fused bias / conv0 weight
-// gradient sums (separate column-sum pass and GEMM), for A/B runs; read at every call
-static bool fused_conv_ln() {
-    const char* e = std::getenv("SUTA_FUSED_CONV_LN");
-    return !(e && atoi(e) == 0);
-}
+// gradient sums (separate column-sum pass and GEMM), for A/B runs; from the call's switch snapshot
+static bool fused_conv_ln() { return suta_switches().fused_conv_ln != 0; }
 
 struct Arena {
     char* base = nullptr;
@@ -122,29 +119,42 @@ struct Arena {
 // rows (overlapping strided conv rows and conv-A windows counted once), B once per distinct batch slice
 // (shared weights once), C written (read too when accumulating), and the epilogue's stored
 // pre-activation, residual and auxiliary operands.  Split-K partials and tile re-reads are not counted.
-double gemm_alg_bytes(const GemmParams& p) {
+// Element sizes follow what the launch reads and writes: 2 B for a bf16 operand plane (Ab, Bb), the bf16 C
+// plane (Cb) and the bf16 pre-activation operands (preb: C2 / aux), 4 B for fp32 operands; an fp32 C that is
+// not written (p.C null: the bf16 plane is the only output) costs nothing.  a_fp32: A is read as fp32 even
+// though p.Ab is set (the to_bf16 conversion inside the same timed launch reads the fp32 source once).
+double gemm_alg_bytes(const GemmParams& p, bool a_fp32 = false) {
     auto zeff = [&](long s0, long s1) -> double {
         if (s0 == 0 && s1 == 0) return 1.0;
         if (s0 == 0) return (double)((p.Z + p.zdiv - 1) / std::max(1, p.zdiv));
         return (double)p.Z;
     };
+    const bool bf = p.mode == SUTA_PRECISION_BF16;
+    const double ea = (bf && p.Ab && !a_fp32) ? 2.0 : 4.0;
+    const double eb = (bf && p.Bb) ? 2.0 : 4.0;
+    const double epre = p.preb ? 2.0 : 4.0;
     double a;
     if (p.segK > 0) {
         const long rows = std::min<long>((long)p.M + p.K / p.segK - 1, p.Mvalid > 0 ? p.Mvalid : p.M);
         a = (double)rows * p.segK;
     } else if (!p.ta) {
-        a = p.lda < p.K ? (double)(p.M - 1) * p.lda + p.K : (double)p.M * p.K;
+        const long lda = (bf && p.Ab && !a_fp32) ? p.ldab : p.lda;
+        a = lda < p.K ? (double)(p.M - 1) * lda + p.K : (double)p.M * p.K;
     } else {
-        a = p.lda < p.M ? (double)(p.K - 1) * p.lda + p.M : (double)p.M * p.K;
+        const long lda = (bf && p.Ab && !a_fp32) ? p.ldab : p.lda;
+        a = lda < p.M ? (double)(p.K - 1) * lda + p.M : (double)p.M * p.K;
     }
     const double mn = (double)p.M * p.N;
-    double bytes = a * zeff(p.sA0, p.sA1) + (double)p.K * p.N * zeff(p.sB0, p.sB1);
-    double c = mn * ((p.epi & EPI_ACCUM) ? 2 : 1);
-    if (p.epi & EPI_STORE_PRE) c += mn;
-    if (p.epi & EPI_RESID) c += mn;
-    if (p.epi & (EPI_DGELU | EPI_SMBWD)) c += mn;
+    double bytes = ea * a * zeff(p.sA0, p.sA1) + eb * (double)p.K * p.N * zeff(p.sB0, p.sB1);
+    double c = 0.0;
+    if (p.C) c += 4.0 * mn * ((p.epi & EPI_ACCUM) ? 2 : 1);
+    if (p.Cb && bf) c += 2.0 * mn;
+    if (p.epi & EPI_STORE_PRE) c += epre * mn;
+    if (p.epi & EPI_RESID) c += 4.0 * mn;
+    if (p.epi & EPI_DGELU) c += epre * mn;
+    if (p.epi & EPI_SMBWD) c += 4.0 * mn;
     bytes += c * p.Z;
-    return 4.0 * bytes;
+    return bytes;
 }
 
 struct LayerBufs {
@@ -252,6 +262,7 @@ struct suta_engine {
         int ragged = 0, mode = 0, steps = 0, want_logits = 0, want_ids = 0;
         suta_hparams hp{};
         std::vector<int> rec;
+        SutaSwitches sw{};  // the call's A/B switch snapshot (buffer formats and kernel choices captured)
     };
     hipGraphExec_t loop_graph = nullptr;
     GraphKey gkey;
@@ -343,8 +354,7 @@ struct suta_engine {
     DevBuf convact, convwt;
     bool conv_planes() const {
         if (!use_planes() || !c.layer_mode) return false;
-        const char* e = std::getenv("SUTA_CONV_PLANES");
-        if (e && atoi(e) == 0) return false;
+        if (!suta_switches().conv_planes) return false;
         for (int i = 0; i < c.nconv; ++i)
             if (c.C[i] != 512 || (i > 0 && ((long)c.K[i] * c.C[i - 1] % 8 || (long)c.S[i] * c.C[i - 1] % 8))) return false;
         return true;
@@ -388,9 +398,7 @@ struct suta_engine {
     // bf16 mode with planes: the FFN pre-activation u (stored by FFN1, read by the FFN2 input gradient's gelu')
     // kept in bf16 (SUTA_PRE_BF16=0: fp32, for A/B runs)
     bool pre_bf16() const {
-        if (!use_planes()) return false;
-        const char* e = std::getenv("SUTA_PRE_BF16");
-        return !(e && atoi(e) == 0);
+        return use_planes() && suta_switches().pre_bf16;
     }
     // layer-mode conv stack on bf16 planes: the conv outputs z_i (conv0's by conv0_vec, the others by the conv GEMMs'
     // epilogues) and the activation gradients da_i (the conv input-gradient GEMMs) stored in bf16 only, in place in
@@ -398,22 +406,17 @@ struct suta_engine {
     // about half the conv stack's LayerNorm bytes (SUTA_CONV_Z_BF16=0: fp32 storage, for A/B runs)
     bool conv_z_bf16() const {
         if (!conv_planes() || !conv_dx_planes() || !fused_conv_ln() || c.K[0] != 10 || c.S[0] != 5) return false;
-        const char* e = std::getenv("SUTA_CONV_Z_BF16");
-        return !(e && atoi(e) == 0);
+        return suta_switches().conv_z_bf16 != 0;
     }
     // stable-LN layers: the input gradients of QKV and FFN1 (the dy of LN1 / LN2 backward) written by their GEMMs as a
     // bf16 plane only (plane 2) and read so by the LayerNorm backward -- torch autocast's bf16 matmul gradient; 104 MB
     // less written and read per LayerNorm backward on C4 (SUTA_DY_PLANES=0: fp32 dy, for A/B runs)
     bool dy_planes() const {
-        if (!fp32_acts_dead() || !c.stable) return false;
-        const char* e = std::getenv("SUTA_DY_PLANES");
-        return !(e && atoi(e) == 0);
+        return fp32_acts_dead() && c.stable && suta_switches().dy_planes;
     }
     // conv input gradients on the bf16 planes too (SUTA_CONV_DX_PLANES=0: fp32-staged x6 kernels, for A/B runs)
     bool conv_dx_planes() const {
-        if (!conv_planes()) return false;
-        const char* e = std::getenv("SUTA_CONV_DX_PLANES");
-        return !(e && atoi(e) == 0);
+        return conv_planes() && suta_switches().conv_dx_planes;
     }
     // bf16 plane of layer l's qkv [B*T][3H]: written by the QKV GEMM, read by the flash forward and, in the
     // backward, by the flash backward (kept for every layer, like the fp32 qkv)
@@ -428,7 +431,6 @@ struct suta_engine {
     void gemm(const GemmParams& p0) {
         GemmParams p = p0;
         p.mode = gemm_mode;
-        const double ab = timing ? gemm_alg_bytes(p) : 0.0;
         gemm_shape.clear();
         if (timing && gemm_census_is_on()) {  // per-shape time table (census + timing: tools/gemm_shapes.py)
             char key[200];
@@ -438,7 +440,7 @@ struct suta_engine {
             gemm_shape = key;
         }
         if (gemm_mode == SUTA_PRECISION_BF16 && p.Ab && p.Bb) {  // both planes given by the caller (conv stack)
-            timed(F_GEMM, [&] { gemm_launch(p, st, plan.splitws, plan.splitws_floats); }, ab);
+            timed(F_GEMM, [&] { gemm_launch(p, st, plan.splitws, plan.splitws_floats); }, timing ? gemm_alg_bytes(p) : 0.0);
             return;
         }
         if (gemm_mode == SUTA_PRECISION_BF16 && p.segK == 0 && !p.ta && p.Z == 1 && p.K % 8 == 0 && p.lda % 4 == 0 &&
@@ -449,7 +451,8 @@ struct suta_engine {
                 p.Bb = p.tb ? it->second.first : it->second.second;
                 p.ldbb = p.K;
                 if (p.Ab) {  // the producer of A wrote its bf16 plane
-                    timed(F_GEMM, [&] { gemm_launch(p, st, plan.splitws, plan.splitws_floats); }, ab);
+                    timed(F_GEMM, [&] { gemm_launch(p, st, plan.splitws, plan.splitws_floats); },
+                          timing ? gemm_alg_bytes(p) : 0.0);
                     return;
                 }
                 if (!p.A) throw SutaError(SUTA_ERR_UNSUPPORTED, "gemm: neither an fp32 A nor its bf16 plane");
@@ -459,7 +462,7 @@ struct suta_engine {
                 timed(F_GEMM, [&] {
                     launch_to_bf16(p.A, p.lda, p.M, p.K, abuf.p, st);
                     gemm_launch(p, st, plan.splitws, plan.splitws_floats);
-                }, ab);
+                }, timing ? gemm_alg_bytes(p, true) : 0.0);
                 return;
             }
         }
@@ -468,7 +471,7 @@ struct suta_engine {
         if (p.Cb) throw SutaError(SUTA_ERR_UNSUPPORTED, "gemm: a bf16 C plane (read by the next kernel) requested on a plane-less GEMM");
         p.Ab = nullptr;  // (plane-less GEMM: a plane given for a non-frozen B is ignored)
         p.Cb = nullptr;
-        timed(F_GEMM, [&] { gemm_launch(p, st, plan.splitws, plan.splitws_floats); }, ab);
+        timed(F_GEMM, [&] { gemm_launch(p, st, plan.splitws, plan.splitws_floats); }, timing ? gemm_alg_bytes(p) : 0.0);
     }
 
     int multiplicity(const TP& t, int train_feature, int bias_only) const {
@@ -514,8 +517,10 @@ void suta_engine::build_plan(int B, long N) {
     pl.N = N;
     long L = N;
     for (int i = 0; i < k.nconv; ++i) {
+        // (a conv input shorter than its kernel has no output frame: torch's Conv1d raises; C division would
+        // round (L - K) / S toward zero and report one frame)
+        if (L < k.K[i]) throw SutaError(SUTA_ERR_ARG, "utterance too short for the conv feature encoder");
         L = (L - k.K[i]) / k.S[i] + 1;
-        if (L < 1) throw SutaError(SUTA_ERR_ARG, "utterance too short for the conv feature encoder");
         pl.Lc[i] = (int)L;
     }
     pl.T = pl.Lc[k.nconv - 1];
@@ -633,8 +638,8 @@ void suta_engine::set_lengths(int B, const int64_t* ns) {
         if (ns[b] < 1 || ns[b] > pl.N) throw SutaError(SUTA_ERR_ARG, "n_samples[b] outside [1, layout length]");
         long L = ns[b];
         for (int i = 0; i < c.nconv; ++i) {
+            if (L < c.K[i]) throw SutaError(SUTA_ERR_ARG, "utterance too short for the conv feature encoder");
             L = (L - c.K[i]) / c.S[i] + 1;
-            if (L < 1) throw SutaError(SUTA_ERR_ARG, "utterance too short for the conv feature encoder");
             if (i == 0) l0[b] = (int)L;
         }
         pl.h_n[b] = (int)ns[b];
@@ -873,7 +878,8 @@ void suta_engine::forward(int B) {
                 if (!launch_flash_fwd(qkv_dead ? nullptr : lb.qkv, lb.ctx, lb.lse, B, T, NH, H, d, scale, rT(),
                                       gemm_mode == SUTA_PRECISION_BF16, st, P0, qkvp))
                     throw SutaError(SUTA_ERR_UNSUPPORTED, "flash attention shape");
-            }, 4.0 * BT * (4.0 * H + NH));  // Q, K, V read; ctx and LSE written
+            }, (double)BT * ((qkv_dead || (bf && qkvp && flash_fwd_reads_plane(bf, qkvp, H)) ? 2.0 : 4.0) * 3.0 * H +
+                            4.0 * H + (P0 && bf ? 2.0 * H : 0.0) + 4.0 * NH));  // Q, K, V read; ctx (+ plane), LSE written
         if (!fused) {
             {  // S = Q K^T * scale
                 GemmParams g;
@@ -1170,7 +1176,12 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
                 if (!launch_flash_bwd(qkv_dead ? nullptr : lb.qkv, pl.ctx, lb.lse, pl.delta, dqkv_dead ? nullptr : pl.dqkv, pl.dqp, B, T,
                                       NH, H, d, scale, rT(), gemm_mode == SUTA_PRECISION_BF16, st, P1, qkvp, dctxp))
                     throw SutaError(SUTA_ERR_UNSUPPORTED, "flash attention shape");
-            }, 4.0 * BT * (7.0 * H + 2.0 * NH));  // Q, K, V, dctx, LSE, delta read; dQ, dK, dV written
+            }, [&] {  // Q, K, V, dO, LSE, delta read; dQ, dK, dV written (fp32 and / or the bf16 plane)
+                const bool bf = gemm_mode == SUTA_PRECISION_BF16;
+                const bool planes = bf && qkvp && dctxp && flash_bwd_reads_planes(bf, qkvp, dctxp, H);
+                return (double)BT * ((planes ? 2.0 : 4.0) * 4.0 * H + 4.0 * 2.0 * NH + (dqkv_dead ? 0.0 : 12.0 * H) +
+                                     (P1 && bf ? 6.0 * H : 0.0));
+            }());
         if (!fused_bwd) {
             {  // dS = scale * P * (dctx_h @ V_h^T - delta)
                 GemmParams g;
@@ -1705,7 +1716,8 @@ bool suta_engine::graph_key_repeats(const GraphKey& k) {
     const bool same = gkey_seen && gkey.B == k.B && gkey.N == k.N && gkey.ragged == k.ragged &&
                       gkey.mode == k.mode && gkey.steps == k.steps && gkey.want_logits == k.want_logits &&
                       gkey.want_ids == k.want_ids && gkey.rec == k.rec &&
-                      std::memcmp(&gkey.hp, &k.hp, sizeof(suta_hparams)) == 0;
+                      std::memcmp(&gkey.hp, &k.hp, sizeof(suta_hparams)) == 0 &&
+                      std::memcmp(&gkey.sw, &k.sw, sizeof(SutaSwitches)) == 0;
     if (!same) {
         drop_graph();
         gkey = k;
@@ -1829,7 +1841,8 @@ const char* suta_last_error(void) { return g_err.c_str(); }
 int32_t suta_num_frames(const suta_model_config* cfg, int64_t n, int64_t* out) {
     return guard([&] {
         long L = n;
-        for (int i = 0; i < cfg->num_conv_layers; ++i) L = (L - cfg->conv_kernel[i]) / cfg->conv_stride[i] + 1;
+        for (int i = 0; i < cfg->num_conv_layers; ++i)  // 0 frames once a layer's input is shorter than its kernel
+            L = L < cfg->conv_kernel[i] ? 0 : (L - cfg->conv_kernel[i]) / cfg->conv_stride[i] + 1;
         *out = L;
     });
 }
@@ -2047,6 +2060,7 @@ int32_t suta_forward(suta_engine* e, const float* wav, int32_t on_dev, int32_t n
     return guard([&] {
         check_batch(e, batch, n);
         HIPCHK(hipSetDevice(e->device));
+        suta_latch_switches();
         e->build_plan(batch, n);
         e->set_lengths(batch, nullptr);
         e->stage_input(wav, on_dev, norm, batch, n);
@@ -2064,6 +2078,7 @@ int32_t suta_step(suta_engine* e, const float* wav, int32_t on_dev, int32_t norm
     return guard([&] {
         check_batch(e, batch, n);
         HIPCHK(hipSetDevice(e->device));
+        suta_latch_switches();
         e->build_plan(batch, n);
         e->set_lengths(batch, nullptr);
         e->stage_input(wav, on_dev, norm, batch, n);
@@ -2090,6 +2105,7 @@ static void adapt_impl(suta_engine* e, const float* wav, int32_t on_dev, int32_t
                        int32_t nrec, float* logits_out, int32_t logits_on_dev, int32_t* ids_out, int64_t* frames_out) {
     check_batch(e, batch, n);
     if (steps < 0) throw SutaError(SUTA_ERR_ARG, "steps < 0");
+    suta_latch_switches();
     for (int i = 0; i < nrec; ++i)
         if (rec[i] < 0 || rec[i] > steps) throw SutaError(SUTA_ERR_ARG, "record step outside [0, steps]");
     HIPCHK(hipSetDevice(e->device));
@@ -2119,6 +2135,7 @@ static void adapt_impl(suta_engine* e, const float* wav, int32_t on_dev, int32_t
     key.want_ids = ids_out != nullptr;
     key.hp = *hp;
     key.rec.assign(rec, rec + nrec);
+    key.sw = suta_switches();
     const bool graph_ok = e->graph_key_repeats(key);
     e->run_adapt_loop(batch, *hp, steps, rec, nrec, rec_logits, rec_ids, graph_ok);
     if (logits_out && nrec)

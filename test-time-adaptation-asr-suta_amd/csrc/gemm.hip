@@ -59,13 +59,18 @@ std::string gemm_census_text() {
     return out;
 }
 
+// Each launch also counts one "grid <kernel> <BMxBN> gx=<column tiles> gy=<row tiles> z=<Z> split=<k>" entry, so
+// a test can assert the tile grid a layout reaches (e.g. the 512 row tiles of 164 x 399 frames).
 static void census(const char* kernel, int BM, int BN, const GemmParams& p, int splits) {
     if (!g_census_on) return;
-    char key[160];
+    char key[160], gkey[160];
     snprintf(key, sizeof key, "%s %dx%d z=%ld split=%d %s%s%s", kernel, BM, BN, (long)p.Z, splits, p.ta ? "T" : "N",
              p.tb ? "T" : "N", p.segK > 0 ? (p.segB ? " conv-seg" : " conv") : "");
+    snprintf(gkey, sizeof gkey, "grid %s %dx%d gx=%d gy=%d z=%ld split=%d", kernel, BM, BN, (p.N + BN - 1) / BN,
+             (p.M + BM - 1) / BM, (long)p.Z, splits);
     std::lock_guard<std::mutex> lk(g_census_mu);
     ++g_census[key];
+    ++g_census[gkey];
 }
 
 void gemm_set_mode(int mode) { g_mode = mode; }
@@ -178,10 +183,9 @@ static bool use_tile160(long M, long N, long Z) {
 // C4 measured 1.3 % slower with it on every eligible linear -- at one block per CU the fused epilogues are
 // exposed).  SUTA_HB8=1: every eligible GEMM; =2: forced on every K % 32 == 0 (tests: small grids, edge tiles);
 // =3: only GEMMs whose epilogue reads no second operand and writes no extra output; =4: only without a bf16 C
-// copy.  Read per launch so tests can switch it.
+// copy.  From the call's switch snapshot (common.h SutaSwitches).
 static int use_hb8(const GemmParams& p) {
-    const char* e = std::getenv("SUTA_HB8");
-    const int mode = e ? atoi(e) : 0;
+    const int mode = suta_switches().hb8;
     if (p.K % 32 != 0 || mode == 0 || p.Z != 1 || p.segK > 0) return 0;
     if (mode == 2) return 1;
     if (mode == 3 && ((p.epi & (EPI_GELU | EPI_RESID | EPI_STORE_PRE | EPI_DGELU | EPI_ACCUM | EPI_SMBWD)) || p.Cb))
@@ -215,10 +219,7 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
                (p.Z > 1 && ((p.sA0 | p.sA1 | p.sB0 | p.sB1) % 8))))
         throw std::invalid_argument("gemm: bf16 planes need K, ld and batch strides % 8 == 0 and 16-B alignment");
     const bool bf16_gbf = p.mode == 2 && glds_ok && p.ta;  // bf16 weight gradients: LDS-DMA fp32 stages
-    {
-        const char* ev = std::getenv("SUTA_FAST_GELU");  // read per launch: tests flip it within a process
-        p.fgelu = (ev && atoi(ev) == 0) ? 0 : 1;
-    }
+    p.fgelu = suta_switches().fast_gelu;  // (the engine call's switch snapshot)
     if (p.preb && (!hb || !p.Cb || (p.ldc2 & 1)))  // (gemm_hb8_kernel shares the epilogue)
         throw std::invalid_argument("gemm: bf16 pre-activation operands need the bf16-plane kernel with a Cb plane, ldc2 even");
     if (hb && p.segK > 0 && (p.segK % 8 || p.pad < 0 || (p.segB && (p.sBseg % 8))))

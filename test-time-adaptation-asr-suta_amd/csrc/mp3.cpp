@@ -8,12 +8,16 @@
 // antialias coefficients are typed below.  Everything else (IMDCT, windows, polyphase matrixing, requantisation,
 // stereo ratios) is computed from the formulas of the standard, in double precision.
 //
-// Decoder delay and gapless trimming follow FFmpeg (the MP3 backend of torchaudio): the Xing / Info frame is
-// not decoded; when it carries an encoder tag (LAME / Lavc / Lavf) the first enc_delay + 529 samples are dropped
-// and max(0, enc_padding - 529) samples at the end; without a tag every decoded sample is returned.
+// Decoder delay and gapless trimming follow FFmpeg (the MP3 backend of torchaudio; libavformat mp3dec.c
+// mp3_parse_info_tag and the demuxer's discard window): the Xing / Info frame is not decoded; when it carries an
+// encoder tag (LAME / Lavc / Lavf) the first enc_delay + 529 samples are dropped, and only when the Xing frames
+// field is present (flags & 1, count F != 0) the decoded positions [F * spf - enc_padding + 529, F * spf) are dropped
+// from every frame (packet) that overlaps them -- measured from the Xing count, not from the frames this scan finds,
+// so a truncated stream keeps its tail; without a tag every decoded sample is returned.
 #include "../../include/suta_audio.h"
 #include "mp3_tables.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <string>
@@ -699,7 +703,16 @@ class Decoder {
 struct Stream {
     int channels = 0, rate = 0, lsf = 0;
     std::vector<int64_t> frames;  // offsets of the audio frames (the Xing / Info frame excluded)
-    int64_t skip = 0, end_trim = 0;
+    int64_t skip = 0;             // leading decoded samples dropped (enc_delay + 529 with an encoder tag)
+    // FFmpeg's end discard window [first_discard, last_discard) in decoded sample positions (0 = none)
+    int64_t first_discard = 0, last_discard = 0;
+    int spf() const { return lsf ? 576 : 1152; }
+    // samples of frame k that survive the end discard (the demuxer trims each packet that overlaps the window)
+    int64_t frame_keep(int64_t k) const {
+        const int64_t n = spf(), s0 = k * n, e0 = s0 + n;
+        if (last_discard > 0 && e0 >= first_discard && s0 < last_discard) return n - std::min<int64_t>(e0 - first_discard, n);
+        return n;
+    }
 };
 
 int scan(const uint8_t* buf, int64_t len, Stream* s) {
@@ -711,7 +724,7 @@ int scan(const uint8_t* buf, int64_t len, Stream* s) {
     }
     Header first{};
     bool have_first = false, tagged = false;
-    int64_t enc_delay = 0, enc_pad = 0;
+    int64_t enc_delay = 0, enc_pad = 0, xing_frames = 0;
     while (o + 4 <= len) {
         Header h;
         if (!parse_header(buf + o, &h) || (have_first && (h.sfreq != first.sfreq || h.channels != first.channels))) {
@@ -731,6 +744,8 @@ int scan(const uint8_t* buf, int64_t len, Stream* s) {
             int64_t x = o + 4 + 2 * h.crc + h.side_bytes;
             if (x + 8 <= len && (std::memcmp(buf + x, "Xing", 4) == 0 || std::memcmp(buf + x, "Info", 4) == 0)) {
                 uint32_t flags = ((uint32_t)buf[x + 4] << 24) | (buf[x + 5] << 16) | (buf[x + 6] << 8) | buf[x + 7];
+                if ((flags & 1) && x + 12 <= len)
+                    xing_frames = ((int64_t)buf[x + 8] << 24) | (buf[x + 9] << 16) | (buf[x + 10] << 8) | buf[x + 11];
                 int64_t t = x + 8 + ((flags & 1) ? 4 : 0) + ((flags & 2) ? 4 : 0) + ((flags & 4) ? 100 : 0) +
                             ((flags & 8) ? 4 : 0);
                 if (t + 24 <= o + h.frame_bytes &&
@@ -758,13 +773,17 @@ int scan(const uint8_t* buf, int64_t len, Stream* s) {
     s->lsf = first.lsf;
     if (tagged) {
         s->skip = enc_delay + 529;
-        s->end_trim = enc_pad > 529 ? enc_pad - 529 : 0;
+        if (xing_frames > 0) {
+            s->first_discard = xing_frames * s->spf() - enc_pad + 529;
+            s->last_discard = xing_frames * s->spf();
+        }
     }
     return 0;
 }
 
 int64_t output_samples(const Stream& s) {
-    int64_t n = (int64_t)s.frames.size() * (s.lsf ? 576 : 1152) - s.skip - s.end_trim;
+    int64_t n = -s.skip;
+    for (int64_t k = 0; k < (int64_t)s.frames.size(); ++k) n += s.frame_keep(k);
     return n > 0 ? n : 0;
 }
 
@@ -802,9 +821,14 @@ int32_t suta_mp3_decode(const uint8_t* buf, int64_t len, float* out, int64_t out
         rc = dec.frame(buf + off, h, pcm, &st, strict != 0);
         if (rc) return rc;
     }
+    // kept decoded positions: frame k contributes its first frame_keep(k) samples; then the leading skip is dropped
+    std::vector<int64_t> src;
+    src.reserve((size_t)(total + s.skip));
+    for (int64_t k = 0; k < (int64_t)s.frames.size(); ++k)
+        for (int64_t i = 0, n = s.frame_keep(k); i < n; ++i) src.push_back(k * s.spf() + i);
     for (int ch = 0; ch < s.channels; ++ch)
         for (int64_t i = 0; i < total; ++i) {
-            int64_t j = i + s.skip;
+            const int64_t j = src[(size_t)(i + s.skip)];
             out[ch * out_capacity + i] = j < (int64_t)pcm[ch].size() ? pcm[ch][j] : 0.0f;
         }
     if (stats) {

@@ -1802,12 +1802,40 @@ void launch_adam(float* P, const float* G, float* M, float* V, long pstride, int
     hipLaunchKernelGGL(adam_kernel, dim3((unsigned)nblk, B), dim3(256), 0, st, P, G, M, V, pstride, aa);
 }
 
+static SutaSwitches g_switches{};
+
+void suta_latch_switches() {
+    auto on = [](const char* name) {  // default on; "0" selects the replaced path
+        const char* ev = std::getenv(name);
+        return (ev && atoi(ev) == 0) ? 0 : 1;
+    };
+    SutaSwitches s{};
+    s.fast_gelu = on("SUTA_FAST_GELU");
+    s.flash_fwd_plane = on("SUTA_FLASH_FWD_PLANE");
+    s.flash_bwd_plane = on("SUTA_FLASH_BWD_PLANE");
+    s.flash_bf16_img = on("SUTA_FLASH_BF16_IMG");
+    s.conv_planes = on("SUTA_CONV_PLANES");
+    s.pre_bf16 = on("SUTA_PRE_BF16");
+    s.conv_z_bf16 = on("SUTA_CONV_Z_BF16");
+    s.dy_planes = on("SUTA_DY_PLANES");
+    s.conv_dx_planes = on("SUTA_CONV_DX_PLANES");
+    s.fused_conv_ln = on("SUTA_FUSED_CONV_LN");
+    const char* hb8 = std::getenv("SUTA_HB8");
+    s.hb8 = hb8 ? atoi(hb8) : 0;
+    const char* fnw = std::getenv("SUTA_FLASH_FWD_NW");
+    s.flash_fwd_nw = (fnw && atoi(fnw) == 8) ? 8 : 4;
+    s.latched = 1;
+    g_switches = s;
+}
+
+const SutaSwitches& suta_switches() {
+    if (!g_switches.latched) suta_latch_switches();
+    return g_switches;
+}
+
 // SUTA_FAST_GELU=0: the erff GELU / GELU' everywhere (A/B runs); default: the branch-free form (common.h gelu_fast,
 // erfc fractional error < 1.2e-7: fp32-accurate) in the conv front-end and every GEMM epilogue
-static bool fast_gelu_on() {  // read per launch: tests flip it within a process
-    const char* ev = std::getenv("SUTA_FAST_GELU");
-    return !(ev && atoi(ev) == 0);
-}
+static bool fast_gelu_on() { return suta_switches().fast_gelu != 0; }
 template <int MODE, typename... Args>
 static void launch_conv0_gn(dim3 grid, hipStream_t st, int K, int S, Args... args) {
     if (K == 10 && S == 5 && fast_gelu_on())

@@ -52,3 +52,22 @@ def reference_schedule_flops(cfg: dict, n_samples: int, steps: int) -> float:
     """What the reference loop executes per utterance: a vanilla forward, then per step a grad forward,
     a backward and a no-grad re-inference forward (main.py:172-215, 330-348): (2S+1) F + S B."""
     return (2 * steps + 1) * forward_flops(cfg, n_samples) + steps * backward_flops(cfg, n_samples)
+
+
+def kernel_base(name: str) -> str:
+    """Base name of a kernel as rocprofv3 tables spell it, mangled or demangled, template arguments dropped:
+    '_ZN12_GLOBAL__N_122flash_fwd_bf16p_kernelILi4EEEvPKDF16b...' and
+    'void (anonymous namespace)::flash_fwd_bf16p_kernel<4>(...)' -> 'flash_fwd_bf16p_kernel' (the PMC / trace
+    reductions key kernel families by this name)."""
+    if name.startswith("_Z"):
+        i = 3 if name.startswith("_ZN") else 2
+        idents = []
+        while i < len(name) and name[i].isdigit():
+            j = i
+            while j < len(name) and name[j].isdigit():
+                j += 1
+            n = int(name[i:j])
+            idents.append(name[j:j + n])
+            i = j + n
+        return idents[-1] if idents else name
+    return name.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0].split("<")[0].strip()

@@ -61,9 +61,11 @@ def build_parser(sdpl: bool = False):
     # engine-only options
     p.add_argument("--synthetic_weights", action="store_true", help="seeded random weights (no checkpoint)")
     p.add_argument("--device", type=int, default=None)
-    p.add_argument("--gpu_batch", type=int, default=64,
+    # defaults = the layout the headline bench measures (bench.py BATCH: 164 x 8 s = 1312 s of audio per call, about
+    # 59 GB of workspace at 0.36 GB per 8 s utterance, of the 288 GB of HBM)
+    p.add_argument("--gpu_batch", type=int, default=164,
                    help="max utterances adapted together as one ragged batch (episodic runs; 1 = one per call)")
-    p.add_argument("--gpu_budget_s", type=float, default=512.0,
+    p.add_argument("--gpu_budget_s", type=float, default=1312.0,
                    help="max padded audio seconds per ragged batch (utterances x longest)")
     p.add_argument("--gpu_min_fill", type=float, default=0.35,
                    help="ragged grouping: 0 = greedy; > 0 = padding-minimising partition charging a batch at least "

@@ -33,14 +33,17 @@ def test_library_exports_every_symbol():
         assert hasattr(lib, name), name
 
 
-@pytest.mark.parametrize("n", [400, 16000, 12345, 128000, 600000])
+@pytest.mark.parametrize("n", [399, 400, 16000, 12345, 128000, 600000])
 def test_num_frames_matches_conv_recursion(n):
+    """399 samples: conv6's input is 1 frame, shorter than its kernel (2): no frame (torch's Conv1d raises; the
+    engine rejects the utterance), where C's truncating division would have reported one."""
     lib = E.load_library()
     cfg = get_config("wav2vec2-base")
     c = E.config_to_c(cfg)
     out = ctypes.c_int64()
     assert lib.suta_num_frames(ctypes.byref(c), n, ctypes.byref(out)) == 0
-    assert out.value == num_frames(cfg, n)
+    assert out.value == max(0, num_frames(cfg, n))
+    assert (out.value == 0) == (n == 399)
 
 
 def test_frame_counts_from_survey():

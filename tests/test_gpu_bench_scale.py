@@ -1,20 +1,24 @@
 """GPU tier: parity at the bench's own scale and on the replayed (hipGraph) ragged path.
 
-* The headline layout exactly as bench.py runs it: 64 x 128 000-sample utterances x 10 SUTA steps in
-  one suta_adapt call, scripts/LS.sh flags, record steps 0/1/3/5/10, the second call of a repeated
-  layout (so every step is a graph replay, as in the timed region).  Slots 0, 31 and 63 are compared
-  with the CPU oracle (oracle/w2v2_cpu.run_suta): logits within 5e-5 absolute (the base-size
-  tolerance of tests/test_gpu_parity.py), adapted tensors by tests/parity.assert_params_close.
+* The headline layout exactly as bench.py runs it: bench.BATCH (164) x 128 000-sample utterances x 10 SUTA
+  steps in one suta_adapt call, scripts/LS.sh flags, record steps 0/1/3/5/10, the second call of a repeated
+  layout (so every step is a graph replay, as in the timed region).  The first / middle / last slots are
+  compared with the CPU oracle (oracle/w2v2_cpu.run_suta): logits within 5e-5 absolute (the base-size
+  tolerance of tests/test_gpu_parity.py), adapted tensors by tests/parity.assert_params_close.  The batch is
+  imported from bench.py, so a change of the bench's batch moves this pin with it; the launch census asserts
+  the grids that batch reaches (B x 399 rows -> ceil(B*399/128) row tiles of the linears, Z = B conv GEMMs).
+* Config C4 at bench.C4_BATCH likewise (bf16, 20 steps) against the exact-fp32 engine and the oracle.
 * Ragged batches that share a quantised layout but differ in per-utterance lengths: the second call
   replays the captured step with new lengths (device-side length buffers); it must equal single runs
   and the eager (graphs off) execution bitwise.
 * Ragged batches with T > 512 frames (long utterances: the attention path for long keys plus
-  ragged masks) against single runs.
+  ragged masks) against single runs; the minimal-length utterance (T = 1) beside a long one.
 """
 import numpy as np
 import pytest
 import torch
 
+import bench
 from suta_amd import synth
 from suta_amd.config import get_config
 from suta_amd.engine import SutaEngine, SutaHParams
@@ -23,25 +27,42 @@ from tests.parity import assert_params_close, logits_tol
 
 pytestmark = pytest.mark.gpu
 
-BENCH_RECORD = [0, 1, 3, 5, 10]   # bench.py RECORD
+BENCH_RECORD = bench.RECORD   # [0, 1, 3, 5, 10]
+
+
+def _slots(B):
+    return sorted({0, B // 2, B - 1})
+
+
+def _row_tiles(B, T, tile=128):
+    return -(-(B * T) // tile)
 
 
 def test_bench_layout_matches_oracle():
+    """reference main.py:347-348 (S x forward_and_adapt per utterance) at the bench's batch."""
     from oracle import w2v2_cpu as W
     import os
     torch.set_num_threads(min(16, len(os.sched_getaffinity(0))))
     cfg = get_config("wav2vec2-base")
     sd = synth_weights(cfg)
-    B, N, S = 64, 128000, 10
+    B, N, S = bench.BATCH, 128000, 10
     eng = SutaEngine(cfg, sd, device=0, max_batch=B, max_samples=N)
     hp = SutaHParams()
     warm = torch.from_numpy(synth.batch(N, B, start=0)).cuda()
     x = synth.batch(N, B, start=B)          # bench.py's first timed batch at --warmup 1
+    eng.set_census(True)
     eng.adapt(warm, S, hp, record=BENCH_RECORD, want_logits=False)          # captures the step graph
+    census = eng.get_census()
+    eng.set_census(False)
     logits, ids, T = eng.adapt(torch.from_numpy(x).cuda(), S, hp, record=BENCH_RECORD)   # replayed
     assert T == 399
+    txt = "\n".join(f"{k}: {v}" for k, v in sorted(census.items()))
+    gy = _row_tiles(B, T)
+    for gx in (6, 18, 24):   # N = 768 (out-proj, FFN2, their dX), 2304 (QKV), 3072 (FFN1, dX of FFN2)
+        assert any(k.startswith("grid glds 128x128 ") and f" gx={gx} gy={gy} z=1 " in k for k in census), (gx, gy, txt)
+    assert any(k.startswith(("glds ", "f32 ")) and f" z={B} " in k for k in census), txt   # per-utterance conv GEMMs
     sdt = {k: torch.from_numpy(v) for k, v in sd.items()}
-    for slot in (0, 31, 63):
+    for slot in _slots(B):
         ref, final = W.run_suta(sdt, cfg, torch.from_numpy(x[slot])[None], S, record=[0, 1, 5, 10])
         for r in (0, 1, 5, 10):
             np.testing.assert_allclose(logits[r][slot], ref[r][0].numpy(), rtol=0, atol=5e-5,
@@ -129,21 +150,22 @@ def test_ragged_ted_lengths_equal_singles():
 
 
 def test_c4_bench_layout_bf16():
-    """Config C4 exactly as bench.py --only-c4 runs it: wav2vec2-large, 64 x 128 000 samples, 20 SUTA steps,
-    bf16 GEMMs, the second call of the layout (every step a graph replay).  Slots 0 / 31 / 63 against the
-    exact-fp32 engine adapting each utterance alone (bf16 tolerance of tests/parity.py: 2.5 % of max|ref|,
-    greedy ids on >= 97 % of frames) at steps 0 / 1 / 5 / 20, and slot 0 against the CPU oracle at steps 0
+    """Config C4 exactly as bench.py --only-c4 runs it: wav2vec2-large, bench.C4_BATCH x 128 000 samples, 20 SUTA
+    steps, bf16 GEMMs, the second call of the layout (every step a graph replay).  First / middle / last slots
+    against the exact-fp32 engine adapting each utterance alone (bf16 tolerance of tests/parity.py: 2.5 % of
+    max|ref|, greedy ids on >= 97 % of frames) at steps 0 / 1 / 5 / 20, and slot 0 against the CPU oracle at steps 0
     and 20.  The launch census of the capturing call shows the schedules this layout reaches: the linears on
-    the bf16-plane kernel (hb), the conv stack's per-utterance (Z = 64) GEMMs on bf16 planes -- forward and
-    input gradients (conv-A rows, per-tap weight segments) on hb, weight gradients on the MN-contiguous hbt
-    kernel -- and the per-utterance feature-projection weight gradient."""
+    the bf16-plane kernel (hb) over ceil(B x 399 / 128) row tiles, the conv stack's per-utterance (Z = B) GEMMs on
+    bf16 planes -- forward and input gradients (conv-A rows, per-tap weight segments) on hb, weight gradients on the
+    MN-contiguous hbt kernel -- and the per-utterance feature-projection weight gradient.
+    Reference main.py:181,205 (forward and backward through the encoder)."""
     from oracle import w2v2_cpu as W
     import os
     from tests.parity import BF16_LOGITS_RTOL_LARGE, assert_bf16_close
     torch.set_num_threads(min(16, len(os.sched_getaffinity(0))))
     cfg = get_config("wav2vec2-large")
     sd = synth_weights(cfg)
-    B, N, S = 64, 128000, 20
+    B, N, S = bench.C4_BATCH, 128000, 20
     rec = [0, 1, 5, 20]
     eng = SutaEngine(cfg, sd, device=0, max_batch=B, max_samples=N)
     eng.set_precision("bf16")
@@ -158,13 +180,17 @@ def test_c4_bench_layout_bf16():
     assert T == 399
     txt = "\n".join(f"{k}: {v}" for k, v in sorted(census.items()))
     print(txt)
+    gy = _row_tiles(B, T)
+    z = f" z={B} "
+    for gx in (8, 24, 32):   # N = 1024 (out-proj, FFN2, dX), 3072 (QKV), 4096 (FFN1, dX of FFN2)
+        assert any(k.startswith("grid hb 128x128 ") and f" gx={gx} gy={gy} z=1 " in k for k in census), (gx, gy, txt)
     assert any(k.startswith("hb ") and " z=1 " in k for k in census), txt
-    assert any(k.startswith("hb 128x128 z=64 ") and k.endswith(" conv-seg") for k in census), txt   # conv dX
-    assert any(k.startswith("hb ") and " z=64 " in k and "conv" not in k for k in census), txt     # conv forward
-    assert any(k.startswith("hbt ") and " z=64 " in k for k in census), txt                        # conv dW
-    assert any(" z=64 " in k and k.startswith(("gbf", "x6_1plane")) for k in census), txt
+    assert any(k.startswith("hb 128x128" + z) and k.endswith(" conv-seg") for k in census), txt   # conv dX
+    assert any(k.startswith("hb ") and z in k and "conv" not in k for k in census), txt     # conv forward
+    assert any(k.startswith("hbt ") and z in k for k in census), txt                        # conv dW
+    assert any(z in k and k.startswith(("gbf", "x6_1plane")) for k in census), txt
     eng.set_precision("fp32")
-    for slot in (0, 31, 63):
+    for slot in _slots(B):
         ref, _, _ = eng.adapt(x[slot], S, hp, record=rec)
         for r in rec:
             assert_bf16_close(logits[r][slot], ref[r][0], 0.97, f"C4 slot {slot} step {r}", rtol=BF16_LOGITS_RTOL_LARGE)
@@ -176,4 +202,24 @@ def test_c4_bench_layout_bf16():
                 np.testing.assert_allclose(ref[r][0], o[r][0].numpy(), rtol=0, atol=5e-5, err_msg=f"fp32 vs oracle {r}")
                 assert_bf16_close(logits[r][0], o[r][0].numpy(), 0.97, f"C4 slot 0 step {r} vs oracle",
                                   rtol=BF16_LOGITS_RTOL_LARGE)
+    eng.close()
+
+
+def test_minimal_length_utterance_in_ragged_batch():
+    """T = 1 (400 samples: the shortest input the conv stack accepts) beside a 2 s utterance in one ragged call,
+    against each alone; 399 samples is rejected by the host (no zero-frame utterance reaches the kernels)."""
+    cfg = get_config("wav2vec2-base")
+    eng = SutaEngine(cfg, synth_weights(cfg), device=0, max_batch=2, max_samples=32000)
+    hp = SutaHParams()
+    rec = [0, 2]
+    waves = [synth.wave(32000, 360), synth.wave(400, 361)]
+    lv, iv, tv = eng.adapt_varlen(waves, 2, hp, record=rec)
+    assert list(tv) == [99, 1]
+    for b, (l1, p1, t1) in enumerate(_singles(eng, waves, 2, hp, rec)):
+        assert tv[b] == t1
+        for r in rec:
+            assert np.all(np.isfinite(lv[r][b]))
+            np.testing.assert_allclose(lv[r][b], l1[r], rtol=0, atol=logits_tol(hp.lr), err_msg=f"utt {b} step {r}")
+    with pytest.raises(RuntimeError, match="too short"):
+        eng.adapt_varlen([synth.wave(32000, 362), synth.wave(399, 363)], 1, hp, record=[1])
     eng.close()

@@ -120,3 +120,69 @@ def test_decode_channels_dispatches_mp3(tmp_path):
     assert D.audio_info(str(p)) == (23087, 44100)
     # channels concatenated, resampled to 16 kHz (torchaudio length rule), as the reader hands to the engine
     assert D.decoded_length(str(p)) == 2 * -(-160 * 23087 // 441)
+
+
+def _info_layout(data):
+    """(x, flags, tag offset) of the real file's Info frame: x = the 'Info' marker."""
+    x = data.index(b"Info")
+    flags = int.from_bytes(data[x + 4:x + 8], "big")
+    t = x + 8 + (4 if flags & 1 else 0) + (4 if flags & 2 else 0) + (100 if flags & 4 else 0) + (4 if flags & 8 else 0)
+    assert data[t:t + 4] in (b"LAME", b"Lavc", b"Lavf")
+    return x, flags, t
+
+
+def _with_padding(data, pad):
+    x, flags, t = _info_layout(data)
+    v = int.from_bytes(data[t + 21:t + 24], "big")
+    v = (v & ~4095) | pad
+    return data[:t + 21] + v.to_bytes(3, "big") + data[t + 24:]
+
+
+def _frame_offsets(data):
+    """Audio frame offsets of the real file (44.1 kHz, constant frame length of its bitrate, padding bit aware)."""
+    x, _, _ = _info_layout(data)
+    o = data.rfind(b"\xff", 0, x - 4)   # the Info frame's sync
+    while not (data[o] == 0xFF and data[o + 1] & 0xE0 == 0xE0):
+        o -= 1
+    offs = []
+    rates = [0, 32, 40, 48, 56, 64, 80, 96, 112, 128, 160, 192, 224, 256, 320]
+    while o + 4 <= len(data) and data[o] == 0xFF and data[o + 1] & 0xE0 == 0xE0:
+        br, pad = rates[data[o + 2] >> 4], (data[o + 2] >> 1) & 1
+        offs.append(o)
+        o += 144000 * br // 44100 + pad
+    return offs[1:]   # the Info frame carries no audio
+
+
+def test_gapless_end_trim_follows_the_xing_frame_count(tmp_path):
+    """FFmpeg (torchaudio's MP3 backend) trims the end only from the Xing frames field: the decoded positions
+    [F * 1152 - enc_padding + 529, F * 1152) of the frames that overlap them.  Builder-made variants of the real
+    file: encoder padding 1600 (F = 21: 21 * 1152 - 576 - 1600 samples), the frames field removed (flags & 1 cleared:
+    no end trim, 21 * 1152 - 576 - 529), and a stream cut after 15 frames (its tail is before the window: kept)."""
+    data = open(REAL, "rb").read()
+    x, flags, t = _info_layout(data)
+    assert flags & 1 and int.from_bytes(data[x + 8:x + 12], "big") == 21
+    full, _ = D.mp3_decode(REAL)
+    padded = _with_padding(data, 1600)
+    p = tmp_path / "pad.mp3"
+    p.write_bytes(padded)
+    y, _ = D.mp3_decode(str(p))
+    assert y.shape[1] == 21 * 1152 - 576 - 1600 == D.mp3_info(str(p))[2]
+    np.testing.assert_array_equal(y, full[:, :y.shape[1]])
+    # frames field removed: the Info frame keeps its length (4 zero bytes appended at its end)
+    nofr = bytearray(padded)
+    nofr[x + 4:x + 8] = (flags & ~1).to_bytes(4, "big")
+    offs = _frame_offsets(data)
+    info_end = offs[0]
+    body = bytes(nofr[:x + 8]) + bytes(nofr[x + 12:info_end]) + b"\x00" * 4 + bytes(nofr[info_end:])
+    q = tmp_path / "noframes.mp3"
+    q.write_bytes(body)
+    z, _ = D.mp3_decode(str(q))
+    assert z.shape[1] == 21 * 1152 - 576 - 529 == D.mp3_info(str(q))[2]
+    np.testing.assert_array_equal(z, full)
+    # truncated after 15 audio frames (a partial 16th): no end trim, the leading skip stays
+    cut = padded[:offs[15] + 100]
+    r = tmp_path / "cut.mp3"
+    r.write_bytes(cut)
+    w, _ = D.mp3_decode(str(r))
+    assert w.shape[1] == 15 * 1152 - 576 - 529
+    np.testing.assert_array_equal(w, full[:, :w.shape[1]])

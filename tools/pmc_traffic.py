@@ -7,7 +7,14 @@ usage: python tools/pmc_traffic.py FETCH_counter_collection.csv WRITE_counter_co
 import collections
 import csv
 import json
+import os
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import suta_loader  # noqa: E402
+
+suta_loader.load()
+from suta_amd.flops import kernel_base  # noqa: E402
 
 
 def load(path, counter):
@@ -17,7 +24,7 @@ def load(path, counter):
         if r.get("Counter_Name") != counter:
             continue
         key = (r.get("Dispatch_Id"), r.get("Counter_Name"))
-        name = r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0].split("<")[0]
+        name = kernel_base(r["Kernel_Name"])  # one entry per kernel base name (mangled or demangled)
         v = float(r["Counter_Value"])
         if key not in seen:
             seen.add(key)
