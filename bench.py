@@ -436,6 +436,9 @@ def bench_c5(args, dev):
     from suta_amd.engine import SutaEngine, SutaHParams
     from suta_amd.main import LAYOUT_QUANTUM, build_parser, ragged_groups
     drv = build_parser().parse_args([])
+    for k in ("gpu_batch", "gpu_budget_s", "gpu_min_fill"):   # bench overrides (A/B of the driver's defaults)
+        if getattr(args, "c5_" + k, None) is not None:
+            setattr(drv, k, getattr(args, "c5_" + k))
     cfg = get_config("wav2vec2-base")
     S = 10
     ns = c5_lengths(args.c5_n)
@@ -520,6 +523,9 @@ def build_parser():
                     help="skip the config-C5 line (TED-like length mix, driver grouping; 1 GPU only)")
     ap.add_argument("--c5-n", type=int, default=C5_UTTERANCES)
     ap.add_argument("--only-c5", action="store_true", help="print only the config-C5 line")
+    ap.add_argument("--c5-gpu-batch", type=int, default=None, help="C5 grouping override (default: the driver's)")
+    ap.add_argument("--c5-gpu-budget-s", type=float, default=None, help="C5 grouping override (default: the driver's)")
+    ap.add_argument("--c5-gpu-min-fill", type=float, default=None, help="C5 grouping override (default: the driver's)")
     ap.add_argument("--no-batch64", dest="batch64", action="store_false",
                     help="skip the 64-utterances-per-call line")
     ap.add_argument("--no-split", dest="also_split", action="store_false",

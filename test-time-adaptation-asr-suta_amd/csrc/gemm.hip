@@ -230,20 +230,24 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
                : p.mode == 2   ? choose_tile_bf16(p.M, p.N, p.Z, !bf16_gbf)
                                : choose_tile(p.M, p.N, p.Z, p.K, p.mode);
     const bool glds_path = p.mode == 0 && g_nbuf == 3 && glds_ok;
+    if ((tile == 8 || tile == 9) && !(hb && p.K % 32 == 0 && p.K >= 128 && p.Z == 1 && p.segK == 0)) tile = 0;
     if (tile == 7 && !glds_path) tile = 0;  // the 160-row tile exists only in the default LDS-DMA kernel
     if (tile == 6 && !(hb && p.K % 32 == 0)) tile = 0;  // the 256 x 256 tile is the bf16-plane ping-pong kernel only
     if (g_force_tile < 0 && tile == 0 && glds_path && use_tile160(p.M, p.N, p.Z)) tile = 7;
     // tiles 0 = 128x128, 1 = 128x64, 2 = 64x128, 3 = 64x64, 7 = 160x128; bf16 mode also 4 = 256x128,
     // 5 = 128x256
-    const int BM = tile == 7 ? 160 : (tile == 4 || tile == 6) ? 256 : (tile == 0 || tile == 1 || tile == 5) ? 128 : 64;
-    const int BN = (tile == 5 || tile == 6) ? 256 : (tile == 0 || tile == 2 || tile == 4 || tile == 7) ? 128 : 64;
+    // 8 / 9: the 256 x 256 slice-ring bf16-plane kernel (gemm_hbx.hip) on v_mfma_f32_32x32x16_bf16 / 16x16x32
+    const bool big = tile == 4 || tile == 6 || tile == 8 || tile == 9;
+    const int BM = tile == 7 ? 160 : big ? 256 : (tile == 0 || tile == 1 || tile == 5) ? 128 : 64;
+    const int BN = (tile == 5 || tile == 6 || tile == 8 || tile == 9) ? 256
+                   : (tile == 0 || tile == 2 || tile == 4 || tile == 7) ? 128 : 64;
     const int gx = (p.N + BN - 1) / BN, gy = (p.M + BM - 1) / BM;
     const long blocks = (long)gx * gy * p.Z;
 
     // split-K when the grid cannot fill 256 CUs and K is long
     int splits = 1;
     // (the split-K reduce has no bf16 pre store and no batched bf16 C plane)
-    if (ws && p.K >= 1024 && blocks < 256 && tile != 6 && !p.preb && !(p.Cb && p.Z > 1)) {
+    if (ws && p.K >= 1024 && blocks < 256 && tile != 6 && tile != 8 && tile != 9 && !p.preb && !(p.Cb && p.Z > 1)) {
         splits = (int)std::min<long>(16, (512 + blocks - 1) / blocks);
         while (splits > 1 && (long)splits * p.Z * p.M * (long)p.N > ws_floats) --splits;
         splits = std::min(splits, std::max(1, (p.K + 255) / 256));  // >= 256 K per split
@@ -295,8 +299,13 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
             hbns = ev ? std::max(2, atoi(ev)) : 2;
         }
         const int ns = g_force_tile >= 0 ? g_nbuf : (tile == 0 ? hbns : 2);
-        census(tile == 6 ? "hb8" : "hb", BM, BN, p, splits);
-        gemm_run_hb(tile, ns, p, grid, st);
+        if (tile == 8 || tile == 9) {
+            census(tile == 8 ? "hbx" : "hbx16", BM, BN, p, splits);
+            gemm_run_hbx(tile == 8 ? 1 : 2, p, grid, st);
+        } else {
+            census(tile == 6 ? "hb8" : "hb", BM, BN, p, splits);
+            gemm_run_hb(tile, ns, p, grid, st);
+        }
     } else if (p.mode == 2) {
         // bf16: register-staged one-plane kernel; weight gradients (and benchmark variants 3 / 8) on
         // register-converted LDS-DMA stages (8 = BK64 x 2)

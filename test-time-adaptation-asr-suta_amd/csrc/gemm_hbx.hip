@@ -1,0 +1,229 @@
+// 256 x 256 bf16-plane GEMM with a slice ring and reads one slice ahead ("hbx"; SUTA_PRECISION_BF16 linears).
+//
+// Same operands and epilogue as gemm_hb_kernel (A [M][K], B [N][K] bf16 planes, k-contiguous; fp32 accumulation;
+// the shared fp32 / bf16-C epilogue), different main loop:
+//   * one block of 8 waves per CU (2 along M x 4 along N), wave tile 128 x 64: 2x the MFMA work per LDS byte of
+//     the 128 x 128 tile (the bf16 operand stream through L2 -> LDS is what bounds the 128 x 128 kernel);
+//   * 32-deep K slices in a ring of NR = 4 LDS slots (32 KB each: A 256 x 32 + B 256 x 32 bf16), filled by LDS-DMA
+//     three slices ahead of the one being consumed, retired by a counted vmcnt that leaves the newest slice in
+//     flight across the barrier (never vmcnt(0) in the loop);
+//   * ONE barrier per slice, and the fragments of slice s+1 are read into a second register set while the MFMAs of
+//     slice s run (the reads, the DMA issue and the MFMAs interleaved by sched_group_barrier), so no MFMA waits on
+//     an LDS read issued in its own slice.
+// Hazards (slice s in ring slot s % 4):
+//   RAW -- a wave reads slice s+1 only after barrier B_s, which every wave passes after its own counted wait for
+//          its DMA share of slice s+1;
+//   WAR -- slice s+3 is DMA'd into slot (s+3) % 4 = (s-1) % 4 right after B_s; slice s-1's fragments were read
+//          during iteration s-2 and consumed by the MFMAs of iteration s-1, which every wave finished before B_s.
+// LDS image: rows of 64 B (32 bf16 = four 16-B chunks); chunk c of row r sits in slot c ^ g((r >> 2) & 3),
+// g = {0, 2, 3, 1}, applied to the per-lane DMA SOURCE address (LDS-DMA writes are lane-linear).  Conflict-free
+// for the ds_read_b128 lane groups of both MFMA shapes (32x32x16: lane -> row l & 31, chunk 2 kc + (l >> 5);
+// 16x16x32: row l & 15, chunk l >> 4): the 16 lanes of a group land on 16 distinct 16-B bank slots.
+// MS: MFMA shape, 32 (v_mfma_f32_32x32x16_bf16, the epilogue's fragment form) or 16 (v_mfma_f32_16x16x32_bf16).
+// Requires K % 32 == 0 and K >= 128, no split-K, Z == 1, no conv-A rows (the dispatcher's conditions).
+#include "gemm_kernels.h"
+#include <cstdlib>
+#include <stdexcept>
+#include <type_traits>
+
+namespace {
+
+constexpr int X_BM = 256, X_BN = 256, X_KS = 16;  // slice depth in 4-byte units (32 bf16)
+constexpr int X_NR = 4;                           // ring slots
+constexpr int X_NWV = 8;
+constexpr int X_SLOT = (X_BM + X_BN) * X_KS;      // 4-byte units per slot (32 KB)
+constexpr int X_NPW = (X_BM + X_BN) * X_KS / (256 * X_NWV);  // DMA instructions per wave per slice (4)
+
+__device__ __forceinline__ int hbx_swz(int row) {
+    const int q = (row >> 2) & 3;
+    return (0x1320 >> (4 * q)) & 3;  // g = {0, 2, 3, 1}
+}
+
+// per-lane DMA sources of one operand (ROWS rows of the tile): NI = ROWS * KS / (256 * NWV) pieces per wave
+template <int ROWS>
+struct XStream {
+    static constexpr int NI = ROWS * X_KS / (256 * X_NWV);
+    const float* ptr[NI];
+    int inc[NI];
+    __device__ __forceinline__ void init(const float* __restrict__ src, long ld, int row0, int nrows, int w, int lane) {
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int ci = i * X_NWV + w;  // 1-KiB piece of the operand's slice image = 16 rows
+            const int row = ci * 16 + lane / 4;
+            const int c = (lane & 3) ^ hbx_swz(row);
+            const bool ok = row0 + row < nrows;
+            ptr[i] = ok ? src + (long)(row0 + row) * ld + c * 4 : g_zero16;
+            inc[i] = ok ? X_KS : 0;
+        }
+    }
+};
+
+template <int ROWS>
+__device__ __forceinline__ void xstream_issue(XStream<ROWS>& sm, float* dst, int w) {
+#pragma unroll
+    for (int i = 0; i < XStream<ROWS>::NI; ++i) {
+        const float* g = sm.ptr[i];
+        __builtin_amdgcn_global_load_lds(g, (lds_ptr_t)(dst + (i * X_NWV + w) * 256), 16, 0, 0);
+        sm.ptr[i] = g + sm.inc[i];
+    }
+}
+
+// 16 B of row `row`, chunk c (8 bf16 at k = 8c..8c+7 of the slice)
+__device__ __forceinline__ bf16x8 xfrag(const float* lds, int row, int c) {
+    return *reinterpret_cast<const bf16x8*>(lds + row * X_KS + ((c ^ hbx_swz(row)) * 4));
+}
+
+// one 16-deep k-chunk of a slice (MS 32: A 4 row blocks, B 2; MS 16: one 32-deep slice's half -- A 4 row blocks of
+// 16, B 4 column blocks of 16, the m-half `hm` of the wave tile)
+template <int MS>
+struct XFr;
+template <>
+struct XFr<32> {
+    bf16x8 a[4], b[2];
+};
+template <>
+struct XFr<16> {
+    bf16x8 a[4], b[4];
+};
+
+template <int MS, bool CB, int EM>
+__global__ __launch_bounds__(512, 1) void gemm_hbx_kernel(GemmParams p) {
+    __shared__ __attribute__((aligned(16))) float smem[X_NR * X_SLOT];
+    const TileId tid = xcd_tile(p.order);
+    const float* A = reinterpret_cast<const float*>(p.Ab);
+    const float* B = reinterpret_cast<const float*>(p.Bb);
+    const long lda = p.ldab / 2, ldb = p.ldbb / 2;  // in 4-byte units
+    const int m0 = tid.y * X_BM, n0 = tid.x * X_BN;
+    const int nst = p.K / 32;
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wr = wid >> 2, wc = wid & 3;
+    const int h = lane >> 5, l32 = lane & 31, l16 = lane & 15, q4 = lane >> 4;
+
+    constexpr int AM = MS == 32 ? 4 : 8, AN = MS == 32 ? 2 : 4;  // fragments of the 128 x 64 wave tile
+    typedef typename std::conditional<MS == 32, f32x16, f32x4>::type Acc;
+    Acc acc[AM][AN];
+#pragma unroll
+    for (int i = 0; i < AM; ++i)
+#pragma unroll
+        for (int j = 0; j < AN; ++j)
+#pragma unroll
+            for (int r = 0; r < (MS == 32 ? 16 : 4); ++r) acc[i][j][r] = 0.f;
+
+    XStream<X_BM> sa;
+    XStream<X_BN> sb;
+    sa.init(A, lda, m0, p.M, wid, lane);
+    sb.init(B, ldb, n0, p.N, wid, lane);
+    auto issue = [&](int s) {
+        float* st = smem + (s % X_NR) * X_SLOT;
+        xstream_issue(sa, st, wid);
+        xstream_issue(sb, st + X_BM * X_KS, wid);
+    };
+    // part c of slice s: MS 32 -> k-chunk c (k 16c..16c+15); MS 16 -> the wave tile's m-half c (k 0..31)
+    auto read = [&](int s, int c, XFr<MS>& f) {
+        const float* As = smem + (s % X_NR) * X_SLOT;
+        const float* Bs = As + X_BM * X_KS;
+        if constexpr (MS == 32) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) f.b[j] = xfrag(Bs, wc * 64 + j * 32 + l32, 2 * c + h);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) f.a[i] = xfrag(As, wr * 128 + i * 32 + l32, 2 * c + h);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) f.b[j] = xfrag(Bs, wc * 64 + j * 16 + l16, q4);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) f.a[i] = xfrag(As, wr * 128 + (4 * c + i) * 16 + l16, q4);
+        }
+    };
+    auto mfma = [&](int c, const XFr<MS>& f) {
+        if constexpr (MS == 32) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[i], f.b[j], acc[i][j], 0, 0, 0);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[4 * c + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[i], f.b[j], acc[4 * c + i][j], 0, 0, 0);
+        }
+    };
+    constexpr int NMF = 16;  // MFMAs per half-slice part (MS 32: 8 of 32x32x16 = 16 cycles-equivalents... see below)
+    (void)NMF;
+    // one slice step.  On entry X holds part 0 of slice s.  [counted wait + barrier B_s] -> DMA of slice s+3;
+    // read part 1 of slice s into Y; MFMAs of part 0 (X); read part 0 of slice s+1 into X (after B_s: landed);
+    // MFMAs of part 1 (Y).  Each read batch overlaps the other part's MFMAs.
+    auto step = [&](int s, XFr<MS>& X, XFr<MS>& Y, auto dma_tag, auto rd_tag) {
+        constexpr bool DMA = decltype(dma_tag)::value, RD = decltype(rd_tag)::value;
+        if (s + 2 < nst) wait_vm<X_NPW>();  // slice s+1 landed; s+2 may stay in flight
+        else wait_vm<0>();
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (DMA) issue(s + 3);
+        read(s, 1, Y);
+        mfma(0, X);
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (RD) read(s + 1, 0, X);
+        mfma(1, Y);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    using T1 = std::true_type;
+    using T0 = std::false_type;
+
+    // prologue: slices 0, 1, 2 in flight; slice 0 landed; its part 0 read (nst >= 4: the dispatcher's K >= 128)
+    issue(0);
+    issue(1);
+    issue(2);
+    wait_vm<2 * X_NPW>();
+    __builtin_amdgcn_s_barrier();
+    XFr<MS> fx, fy;
+    read(0, 0, fx);
+    int s = 0;
+    for (; s + 3 < nst; ++s) step(s, fx, fy, T1{}, T1{});
+    if (s + 1 < nst) step(s++, fx, fy, T0{}, T1{});
+    if (s + 1 < nst) step(s++, fx, fy, T0{}, T1{});
+    step(s, fx, fy, T0{}, T0{});
+    wait_vm<0>();
+
+    const bool interior = m0 + X_BM <= p.M && n0 + X_BN <= p.N;
+    if constexpr (MS == 32) {
+        gemm_epilogue<2, 2, CB, EM>(p, reinterpret_cast<const f32x16(&)[2][2]>(acc[0]), 0, 0, m0 + wr * 128,
+                                    n0 + wc * 64, h, l32, interior, tid.z);
+        gemm_epilogue<2, 2, CB, EM>(p, reinterpret_cast<const f32x16(&)[2][2]>(acc[2]), 0, 0, m0 + wr * 128 + 64,
+                                    n0 + wc * 64, h, l32, interior, tid.z);
+    } else {
+        // 16x16 fragments: column l & 15, rows 4 (l >> 4) + r -- plain fp32 C (bench form)
+        float* C = p.C;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = m0 + wr * 128 + i * 16 + 4 * q4 + r, col = n0 + wc * 64 + j * 16 + l16;
+                    if (interior || (row < p.M && col < p.N)) C[(long)row * p.ldc + col] = acc[i][j][r] * p.alpha;
+                }
+    }
+}
+
+template <int MS, int EM>
+void launch_hbx_em(const GemmParams& p, dim3 grid, hipStream_t st) {
+    if (p.Cb) hipLaunchKernelGGL((gemm_hbx_kernel<MS, true, EM>), grid, dim3(512), 0, st, p);
+    else hipLaunchKernelGGL((gemm_hbx_kernel<MS, false, EM>), grid, dim3(512), 0, st, p);
+}
+
+}  // namespace
+
+// variant 1: v_mfma_f32_32x32x16_bf16 with the shared epilogue (every flag); 2: v_mfma_f32_16x16x32_bf16, plain fp32
+// C only (main-loop benchmark: tools/hb_bench)
+void gemm_run_hbx(int variant, const GemmParams& p, dim3 grid, hipStream_t st) {
+    if (variant == 2) {
+        if (p.epi != 0 || p.Cb || !p.C) throw std::invalid_argument("hbx variant 2: plain fp32 C only");
+        hipLaunchKernelGGL((gemm_hbx_kernel<16, false, 0>), grid, dim3(512), 0, st, p);
+        return;
+    }
+    launch_hbx_em<32, -1>(p, grid, st);
+}

@@ -1962,3 +1962,4 @@ __global__ __launch_bounds__(256, 2) void gemm_hbt_kernel(GemmParams p) {
 void gemm_run_gbf(int bk64, int nprod, int tile, const GemmParams& p, dim3 grid, hipStream_t st);  // gemm_gbf.hip
 void gemm_run_hb(int tile, int ns, const GemmParams& p, dim3 grid, hipStream_t st);                         // gemm_hb.hip
 void gemm_run_hbt(const GemmParams& p, dim3 grid, hipStream_t st);                                          // gemm_hb.hip
+void gemm_run_hbx(int variant, const GemmParams& p, dim3 grid, hipStream_t st);                             // gemm_hbx.hip

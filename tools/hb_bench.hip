@@ -1,4 +1,6 @@
-// bf16-plane GEMM (gemm_hb_kernel) microbenchmark + check on the C4 (w2v2-large, 64 x 8 s) linear shapes.
+// bf16-plane GEMM microbenchmark + check on the C4 linear shapes (w2v2-large, M = 164 x 399 rows: bench.py's layout):
+// gemm_hb_kernel (128 x 128), gemm_hb8_kernel (256 x 256 ping-pong), gemm_hbx_kernel (256 x 256 slice ring; 32x32x16
+// and 16x16x32 MFMA forms).  Variants run interleaved, `rounds` times each (median reported).
 // Build: hipcc -O3 --offload-arch=gfx950 -I test-time-adaptation-asr-suta_amd/csrc -c tools/hb_bench.hip -o /tmp/hb.o
 //        && hipcc --offload-arch=gfx950 /tmp/hb.o test-time-adaptation-asr-suta_amd/csrc/gemm*.o -o tools/hb_bench
 #include <hip/hip_runtime.h>
@@ -6,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
+#include <algorithm>
 #include "common.h"
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
@@ -27,11 +30,12 @@ __global__ void ref(const __bf16* A, const __bf16* B, int M, int N, int K, int r
 }
 
 int main(int argc, char** argv) {
-    const int M = 25536;
+    const int M = 164 * 399;
     struct S { const char* name; int N, K; } shapes[] = {
         {"qkv  N3072 K1024", 3072, 1024}, {"out  N1024 K1024", 1024, 1024}, {"ffn1 N4096 K1024", 4096, 1024},
         {"ffn2 N1024 K4096", 1024, 4096}, {"dqkv N1024 K3072", 1024, 3072}, {"edge N1000 K1024", 1000, 1024}};
-    const int reps = argc > 1 ? atoi(argv[1]) : 20;
+    const int reps = argc > 1 ? atoi(argv[1]) : 10;
+    const int rounds = argc > 2 ? atoi(argv[2]) : 3;
     __bf16 *A, *B;
     float *C, *R;
     CK(hipMalloc(&A, (size_t)M * 4096 * 2));
@@ -43,57 +47,68 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    // (tile, ns, pf) -- gemm_run_hb (6: 256x256 ping-pong; pf: SUTA_HB8_PF, fragments read one phase ahead)
-    const int variants[][3] = {{0, 2, 0}, {0, 5, 0}, {0, 6, 0}, {6, 2, 0}, {0, 2, 0}, {0, 5, 0}, {0, 6, 0}, {6, 2, 0}};
+    // (tile, ns, cb-capable): 0 = hb 128 x 128, 6 = hb8, 8 = hbx (32x32x16), 9 = hbx16 (16x16x32, plain C only)
+    const int variants[][3] = {{0, 2, 1}, {6, 2, 1}, {8, 2, 1}, {9, 2, 0}};
+    const char* vname[] = {"hb128", "hb8  ", "hbx32", "hbx16"};
+    constexpr int NV = 4;
     __bf16* Cb;
     CK(hipMalloc(&Cb, (size_t)M * 4096 * 2));
+    setenv("SUTA_HB8_PF", "0", 1);
     for (auto& s : shapes) {
-        for (auto& vt : variants) {
-            const int ti = vt[0], ns = vt[1];
-            setenv("SUTA_HB8_PF", vt[2] ? "1" : "0", 1);
-            {
-                GemmParams p;
-                gemm_init(p);
-                p.mode = 2;
-                p.A = reinterpret_cast<const float*>(A);  // unused by the plane kernel (alignment only)
-                p.B = reinterpret_cast<const float*>(B);
-                p.M = M; p.N = s.N; p.K = s.K;
-                p.lda = s.K; p.ldb = s.K; p.tb = 1;
-                p.C = C; p.ldc = s.N;
-                p.Ab = A; p.Bb = B; p.ldab = s.K; p.ldbb = s.K;
-                gemm_set_variant(ti, ns);
-                for (int w = 0; w < 3; ++w) gemm_launch(p, 0, nullptr, 0);
+        GemmParams p;
+        gemm_init(p);
+        p.mode = 2;
+        p.A = reinterpret_cast<const float*>(A);  // unused by the plane kernels (alignment only)
+        p.B = reinterpret_cast<const float*>(B);
+        p.M = M; p.N = s.N; p.K = s.K;
+        p.lda = s.K; p.ldb = s.K; p.tb = 1;
+        p.C = C; p.ldc = s.N;
+        p.Ab = A; p.Bb = B; p.ldab = s.K; p.ldbb = s.K;
+        std::vector<float> ms[NV];
+        for (int rd = 0; rd < rounds; ++rd)
+            for (int v = 0; v < NV; ++v) {
+                gemm_set_variant(variants[v][0], variants[v][1]);
+                for (int w = 0; w < 2; ++w) gemm_launch(p, 0, nullptr, 0);
                 CK(hipEventRecord(e0, 0));
                 for (int r = 0; r < reps; ++r) gemm_launch(p, 0, nullptr, 0);
                 CK(hipEventRecord(e1, 0));
                 CK(hipEventSynchronize(e1));
-                float ms = 0;
-                CK(hipEventElapsedTime(&ms, e0, e1));
-                ms /= reps;
-                const double tf = 2.0 * M * s.N * (double)s.K / (ms * 1e-3) / 1e12;
-                // check a row sample
-                const int rstep = 97, rows = (M + rstep - 1) / rstep;
-                hipLaunchKernelGGL(ref, dim3(((long)rows * s.N + 255) / 256), dim3(256), 0, 0, A, B, M, s.N, s.K, rstep, R);
-                std::vector<float> hc((size_t)M * s.N), hr((size_t)rows * s.N);
-                CK(hipMemcpy(hc.data(), C, hc.size() * 4, hipMemcpyDeviceToHost));
-                CK(hipMemcpy(hr.data(), R, hr.size() * 4, hipMemcpyDeviceToHost));
-                double err = 0, errb = 0;
-                {   // the bf16 copy of C (epilogue CB path): one extra launch with the plane on
-                    GemmParams q = p;
-                    q.Cb = Cb; q.ldcb = s.N;
-                    gemm_launch(q, 0, nullptr, 0);
-                    CK(hipDeviceSynchronize());
-                    std::vector<__bf16> hb((size_t)M * s.N);
-                    CK(hipMemcpy(hb.data(), Cb, hb.size() * 2, hipMemcpyDeviceToHost));
-                    for (size_t i = 0; i < hb.size(); i += 13) errb = fmax(errb, fabs((float)hb[i] - hc[i]) / (fabs(hc[i]) + 1.0));
-                }
-                for (int r = 0; r < rows; ++r)
-                    for (int n = 0; n < s.N; ++n)
-                        err = fmax(err, fabs(hc[(size_t)r * rstep * s.N + n] - hr[(size_t)r * s.N + n]));
-                printf("%s tile %d ns %d pf %d: %.4f ms %.1f TF maxerr %.2e bf16-copy relerr %.2e\n", s.name, ti, ns, vt[2], ms, tf, err, errb);
-                fflush(stdout);
+                float t = 0;
+                CK(hipEventElapsedTime(&t, e0, e1));
+                ms[v].push_back(t / reps);
             }
-    }
+        for (int v = 0; v < NV; ++v) {
+            gemm_set_variant(variants[v][0], variants[v][1]);
+            CK(hipMemset(C, 0, (size_t)M * s.N * 4));
+            gemm_launch(p, 0, nullptr, 0);
+            const int rstep = 97, rows = (M + rstep - 1) / rstep;
+            hipLaunchKernelGGL(ref, dim3(((long)rows * s.N + 255) / 256), dim3(256), 0, 0, A, B, M, s.N, s.K, rstep, R);
+            std::vector<float> hc((size_t)M * s.N), hr((size_t)rows * s.N);
+            CK(hipMemcpy(hc.data(), C, hc.size() * 4, hipMemcpyDeviceToHost));
+            CK(hipMemcpy(hr.data(), R, hr.size() * 4, hipMemcpyDeviceToHost));
+            double err = 0, errb = -1;
+            for (int r = 0; r < rows; ++r)
+                for (int n = 0; n < s.N; ++n)
+                    err = fmax(err, fabs(hc[(size_t)r * rstep * s.N + n] - hr[(size_t)r * s.N + n]));
+            if (variants[v][2]) {   // the bf16 copy of C (epilogue CB path)
+                GemmParams q = p;
+                q.Cb = Cb; q.ldcb = s.N;
+                gemm_launch(q, 0, nullptr, 0);
+                CK(hipDeviceSynchronize());
+                std::vector<__bf16> hb((size_t)M * s.N);
+                CK(hipMemcpy(hb.data(), Cb, hb.size() * 2, hipMemcpyDeviceToHost));
+                errb = 0;
+                for (size_t i = 0; i < hb.size(); i += 13) errb = fmax(errb, fabs((float)hb[i] - hc[i]) / (fabs(hc[i]) + 1.0));
+            }
+            std::vector<float> m = ms[v];
+            std::sort(m.begin(), m.end());
+            const float med = m[m.size() / 2], mn = m[0];
+            const double tf = 2.0 * M * s.N * (double)s.K / (med * 1e-3) / 1e12;
+            const double tfb = 2.0 * M * s.N * (double)s.K / (mn * 1e-3) / 1e12;
+            printf("%s %s: median %.4f ms %.1f TF (best %.1f) maxerr %.2e bf16-copy relerr %.2e\n", s.name, vname[v], med, tf,
+                   tfb, err, errb);
+            fflush(stdout);
+        }
     }
     return 0;
 }
