@@ -73,6 +73,8 @@ struct SutaSwitches {
     int fused_conv_ln;    // SUTA_FUSED_CONV_LN
     int hb8;              // SUTA_HB8 (default 0): 256 x 256 ping-pong bf16-plane GEMM selection mode
     int flash_fwd_nw;     // SUTA_FLASH_FWD_NW (default 4): waves per block of the bf16-plane flash forward
+    int hbx;              // SUTA_HBX (default 1): the 256 x 256 slice-ring bf16-plane GEMM for plain-epilogue linears
+                          // on full grids; 2: on every eligible bf16-plane linear (tests: small grids, edge tiles)
 };
 void suta_latch_switches();
 const SutaSwitches& suta_switches();  // the snapshot (taken now if none was)

@@ -194,6 +194,20 @@ static int use_hb8(const GemmParams& p) {
     return ((p.M + 255) / 256) * ((p.N + 255) / 256) >= 256;
 }
 
+// 256 x 256 slice-ring bf16-plane kernel (gemm_hbx.hip, v_mfma_f32_32x32x16_bf16; bitwise the 128 x 128 kernel's
+// results: same MFMA, same k order) for the linears whose epilogue is bias / residual / the bf16 C plane, on grids of at
+// least one full round of 256 tiles.  tools/hb_bench (C4 shapes at M = 164 x 399, same box): qkv 741 -> 889 TF,
+// out-proj 604 -> 784, FFN1 749 -> 858, FFN2 865 -> 1055, dQKV 808 -> 1022; with the GELU / GELU' epilogues equal to
+// 128 x 128 (576 vs 588, 577 vs 572: one block per CU exposes the epilogue), so those keep the 128 x 128 kernel.
+// SUTA_HBX=0: off (A/B runs); 2: every eligible linear, any epilogue and grid (tests).
+static bool use_hbx(const GemmParams& p) {
+    const int mode = suta_switches().hbx;
+    if (!mode || p.Z != 1 || p.segK > 0 || p.K % 32 || p.K < 128 || (p.epi & (EPI_ACCUM | EPI_SMBWD))) return false;
+    if (mode == 2) return true;  // SUTA_HBX=2: every eligible linear (tests)
+    if (p.epi & (EPI_GELU | EPI_DGELU | EPI_STORE_PRE)) return false;
+    return (long)((p.M + 255) / 256) * ((p.N + 255) / 256) >= 256;
+}
+
 void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
     if (p.M <= 0 || p.N <= 0 || p.Z <= 0) return;
     const int second = ((p.epi & EPI_RESID) != 0) + ((p.epi & EPI_ACCUM) != 0) + ((p.epi & EPI_SMBWD) != 0);
@@ -226,7 +240,7 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
         throw std::invalid_argument("gemm: conv-A bf16 planes need segK and the tap stride % 8 == 0");
     int tile = hbt || (hb && p.segK > 0) ? 0
                : g_force_tile >= 0 ? g_force_tile
-               : hb            ? (use_hb8(p) ? 6 : choose_tile_hb(p.M, p.N, p.Z))
+               : hb            ? (use_hb8(p) ? 6 : use_hbx(p) ? 8 : choose_tile_hb(p.M, p.N, p.Z))
                : p.mode == 2   ? choose_tile_bf16(p.M, p.N, p.Z, !bf16_gbf)
                                : choose_tile(p.M, p.N, p.Z, p.K, p.mode);
     const bool glds_path = p.mode == 0 && g_nbuf == 3 && glds_ok;

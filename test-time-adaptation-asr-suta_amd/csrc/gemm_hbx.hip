@@ -86,6 +86,133 @@ struct XFr<16> {
     bf16x8 a[4], b[4];
 };
 
+// Epilogue of 16x16 accumulator fragments (v_mfma_f32_16x16x32_bf16: register r of acc[i][j] is row 16 i + 4 (lane >> 4)
+// + r, column 16 j + (lane & 15) of the wave tile).  The flags of the bf16 linears (bias, residual, bias + GELU +
+// pre-activation store, GELU', ragged row mask; fp32 C and / or the bf16 C plane; bf16 pre-activation operands) with
+// the same operations in the same order as gemm_epilogue; interior tiles with 32-bit offsets (scalar row bases +
+// one lane offset per fragment), edge tiles element by element with bounds checks.  No split-K, ACCUM or SMBWD
+// (gemm_run_hbx checks).
+template <int FM, int FN, bool CB, int EM>
+__device__ __forceinline__ void epilogue16(const GemmParams& p, const f32x4 (&acc)[FM][FN], int rbase, int cbase,
+                                           int lane, bool interior) {
+    const int e = p.epi & EM;
+    const int q4 = lane >> 4, l16 = lane & 15;
+    float* C = p.C;
+    const float* bias = p.bias;
+    const float* R = p.R;
+    const int rlim = (e & EPI_ROWMASK) ? p.zrows[0] : 0x7fffffff;
+    const bool preb = CB && p.preb;
+    const float alpha = p.alpha;
+    typedef __bf16 cb2 __attribute__((ext_vector_type(2)));
+    const bool odd = lane & 1;
+    __bf16* Cb = CB ? reinterpret_cast<__bf16*>(p.Cb) : nullptr;
+    const bool fast = interior && p.off32 && (!CB || (p.ldcb & 1) == 0) && (!preb || (p.ldc2 & 1) == 0);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+            const int rb = rbase + 16 * i + 4 * q4;
+            const int col = cbase + 16 * j + l16;
+            float v[4], xa[4], xr[4];
+            if (fast) {
+                const unsigned uc = (unsigned)col;
+                if (e & EPI_DGELU) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        xa[r] = preb ? (float)*byte_at(reinterpret_cast<const __bf16*>(p.aux) + (long)(rb + r) * p.ldaux, 2u * uc)
+                                     : *byte_at(p.aux + (long)(rb + r) * p.ldaux, 4u * uc);
+                }
+                if (e & EPI_RESID) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) xr[r] = *byte_at(R + (long)(rb + r) * p.ldr, 4u * uc);
+                }
+            } else {
+                const int cc = min(col, p.N - 1);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const long row = min(rb + r, p.M - 1);
+                    if (e & EPI_DGELU)
+                        xa[r] = preb ? (float)reinterpret_cast<const __bf16*>(p.aux)[row * p.ldaux + cc] : p.aux[row * p.ldaux + cc];
+                    if (e & EPI_RESID) xr[r] = R[row * p.ldr + cc];
+                }
+            }
+            const float bj = (e & EPI_BIAS) ? bias[min(col, p.N - 1)] : 0.f;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                v[r] = acc[i][j][r] * alpha;
+                if (e & EPI_BIAS) v[r] += bj;
+            }
+            if (e & EPI_STORE_PRE) {
+                if (preb && fast) {  // (column, column + 1) bf16 pairs: lanes 2i / 2i + 1 swap one value
+#pragma unroll
+                    for (int r = 0; r < 4; r += 2) {
+                        const float a = v[r], b = v[r + 1];
+                        const float q = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(odd ? a : b), 0xB1, 0xF, 0xF, false));
+                        cb2 pr;
+                        pr[0] = (__bf16)(odd ? q : a);
+                        pr[1] = (__bf16)(odd ? b : q);
+                        *reinterpret_cast<cb2*>(byte_at(reinterpret_cast<__bf16*>(p.C2) + (long)(rb + r + (odd ? 1 : 0)) * p.ldc2,
+                                                        2u * (unsigned)(col & ~1))) = pr;
+                    }
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (interior || (rb + r < p.M && col < p.N)) {
+                            if (preb) reinterpret_cast<__bf16*>(p.C2)[(long)(rb + r) * p.ldc2 + col] = (__bf16)v[r];
+                            else p.C2[(long)(rb + r) * p.ldc2 + col] = v[r];
+                        }
+                }
+            }
+            if ((e & EPI_GELU) && CB && p.fgelu) {  // (uniform choice hoisted out of the element loop)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = gelu_fast(v[r]);
+            } else if (e & EPI_GELU) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = gelu_f(v[r]);
+            }
+            if ((e & EPI_DGELU) && CB && p.fgelu) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] *= dgelu_fast(xa[r]);
+            } else if (e & EPI_DGELU) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] *= dgelu_f(xa[r]);
+            }
+            if (e & EPI_RESID) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] += xr[r];
+            }
+            if (e & EPI_ROWMASK) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if (rb + r >= rlim) v[r] = 0.f;
+            }
+            if (C) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    if (fast) *byte_at(C + (long)(rb + r) * p.ldc, 4u * (unsigned)col) = v[r];
+                    else if (rb + r < p.M && col < p.N) C[(long)(rb + r) * p.ldc + col] = v[r];
+                }
+            }
+            if (CB) {
+                if (fast) {
+#pragma unroll
+                    for (int r = 0; r < 4; r += 2) {
+                        const float a = v[r], b = v[r + 1];
+                        const float q = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(odd ? a : b), 0xB1, 0xF, 0xF, false));
+                        cb2 pr;
+                        pr[0] = (__bf16)(odd ? q : a);
+                        pr[1] = (__bf16)(odd ? b : q);
+                        *reinterpret_cast<cb2*>(byte_at(Cb + (long)(rb + r + (odd ? 1 : 0)) * p.ldcb, 2u * (unsigned)(col & ~1))) = pr;
+                    }
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (rb + r < p.M && col < p.N) Cb[(long)(rb + r) * p.ldcb + col] = (__bf16)v[r];
+                }
+            }
+        }
+}
+
 template <int MS, bool CB, int EM>
 __global__ __launch_bounds__(512, 1) void gemm_hbx_kernel(GemmParams p) {
     __shared__ __attribute__((aligned(16))) float smem[X_NR * X_SLOT];
@@ -195,17 +322,11 @@ __global__ __launch_bounds__(512, 1) void gemm_hbx_kernel(GemmParams p) {
         gemm_epilogue<2, 2, CB, EM>(p, reinterpret_cast<const f32x16(&)[2][2]>(acc[2]), 0, 0, m0 + wr * 128 + 64,
                                     n0 + wc * 64, h, l32, interior, tid.z);
     } else {
-        // 16x16 fragments: column l & 15, rows 4 (l >> 4) + r -- plain fp32 C (bench form)
-        float* C = p.C;
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int row = m0 + wr * 128 + i * 16 + 4 * q4 + r, col = n0 + wc * 64 + j * 16 + l16;
-                    if (interior || (row < p.M && col < p.N)) C[(long)row * p.ldc + col] = acc[i][j][r] * p.alpha;
-                }
+        // two 64-row halves (bounds the epilogue's live temporaries beside the accumulators)
+        epilogue16<4, 4, CB, EM>(p, reinterpret_cast<const f32x4(&)[4][4]>(acc[0]), m0 + wr * 128, n0 + wc * 64, lane,
+                                 interior);
+        epilogue16<4, 4, CB, EM>(p, reinterpret_cast<const f32x4(&)[4][4]>(acc[4]), m0 + wr * 128 + 64, n0 + wc * 64,
+                                 lane, interior);
     }
 }
 
@@ -215,15 +336,29 @@ void launch_hbx_em(const GemmParams& p, dim3 grid, hipStream_t st) {
     else hipLaunchKernelGGL((gemm_hbx_kernel<MS, false, EM>), grid, dim3(512), 0, st, p);
 }
 
+// epilogue classes of the bf16 linears (as gemm_hb_ep.hip): bias / residual, bias + GELU + pre-activation store,
+// GELU'; ragged row masks in each
+constexpr int XEM_A = EPI_BIAS | EPI_RESID | EPI_ROWMASK;
+constexpr int XEM_G = EPI_BIAS | EPI_GELU | EPI_STORE_PRE | EPI_ROWMASK;
+constexpr int XEM_D = EPI_DGELU | EPI_ROWMASK;
+
 }  // namespace
 
-// variant 1: v_mfma_f32_32x32x16_bf16 with the shared epilogue (every flag); 2: v_mfma_f32_16x16x32_bf16, plain fp32
-// C only (main-loop benchmark: tools/hb_bench)
+// variant 1: v_mfma_f32_32x32x16_bf16 with the shared epilogue (class-specialised kernels for the linears' epilogue
+// classes, the generic one otherwise); 2: v_mfma_f32_16x16x32_bf16 with epilogue16 (the linears' classes only)
 void gemm_run_hbx(int variant, const GemmParams& p, dim3 grid, hipStream_t st) {
+    const int e = p.epi;
+    if (p.splits > 1 || p.Z != 1 || (e & (EPI_ACCUM | EPI_SMBWD)))
+        throw std::invalid_argument("hbx: no split-K, batches, ACCUM or SMBWD");
     if (variant == 2) {
-        if (p.epi != 0 || p.Cb || !p.C) throw std::invalid_argument("hbx variant 2: plain fp32 C only");
-        hipLaunchKernelGGL((gemm_hbx_kernel<16, false, 0>), grid, dim3(512), 0, st, p);
+        if ((e & ~XEM_A) == 0) launch_hbx_em<16, XEM_A>(p, grid, st);
+        else if ((e & ~XEM_G) == 0) launch_hbx_em<16, XEM_G>(p, grid, st);
+        else if ((e & ~XEM_D) == 0) launch_hbx_em<16, XEM_D>(p, grid, st);
+        else throw std::invalid_argument("hbx 16x16: epilogue flags outside the linears' classes");
         return;
     }
-    launch_hbx_em<32, -1>(p, grid, st);
+    if ((e & ~XEM_A) == 0) launch_hbx_em<32, XEM_A>(p, grid, st);
+    else if ((e & ~XEM_G) == 0) launch_hbx_em<32, XEM_G>(p, grid, st);
+    else if ((e & ~XEM_D) == 0) launch_hbx_em<32, XEM_D>(p, grid, st);
+    else launch_hbx_em<32, -1>(p, grid, st);
 }

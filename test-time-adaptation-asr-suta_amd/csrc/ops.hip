@@ -1820,6 +1820,8 @@ void suta_latch_switches() {
     s.dy_planes = on("SUTA_DY_PLANES");
     s.conv_dx_planes = on("SUTA_CONV_DX_PLANES");
     s.fused_conv_ln = on("SUTA_FUSED_CONV_LN");
+    const char* hbx = std::getenv("SUTA_HBX");
+    s.hbx = hbx ? atoi(hbx) : 1;
     const char* hb8 = std::getenv("SUTA_HB8");
     s.hb8 = hb8 ? atoi(hb8) : 0;
     const char* fnw = std::getenv("SUTA_FLASH_FWD_NW");

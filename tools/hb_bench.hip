@@ -48,7 +48,7 @@ int main(int argc, char** argv) {
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     // (tile, ns, cb-capable): 0 = hb 128 x 128, 6 = hb8, 8 = hbx (32x32x16), 9 = hbx16 (16x16x32, plain C only)
-    const int variants[][3] = {{0, 2, 1}, {6, 2, 1}, {8, 2, 1}, {9, 2, 0}};
+    const int variants[][3] = {{0, 2, 1}, {6, 2, 1}, {8, 2, 1}, {9, 2, 1}};
     const char* vname[] = {"hb128", "hb8  ", "hbx32", "hbx16"};
     constexpr int NV = 4;
     __bf16* Cb;
@@ -108,6 +108,75 @@ int main(int argc, char** argv) {
             printf("%s %s: median %.4f ms %.1f TF (best %.1f) maxerr %.2e bf16-copy relerr %.2e\n", s.name, vname[v], med, tf,
                    tfb, err, errb);
             fflush(stdout);
+        }
+    }
+    // epilogue-heavy C4 shapes (bf16 C plane only, bf16 pre-activation operand): FFN1 forward (bias + GELU +
+    // pre-activation store) and the FFN2 input gradient (x GELU'(u)); variants compared on their Cb outputs
+    {
+        float* bias;
+        __bf16 *U, *Cref;
+        CK(hipMalloc(&bias, 4096 * 4));
+        CK(hipMalloc(&U, (size_t)M * 4096 * 2));
+        CK(hipMalloc(&Cref, (size_t)M * 4096 * 2));
+        hipLaunchKernelGGL(fillb, dim3((M * 4096L + 255) / 256), dim3(256), 0, 0, U, (long)M * 4096, 3u);
+        std::vector<float> hbias(4096);
+        for (int i = 0; i < 4096; ++i) hbias[i] = 0.01f * (i % 17) - 0.08f;
+        CK(hipMemcpy(bias, hbias.data(), 4096 * 4, hipMemcpyHostToDevice));
+        for (int form = 0; form < 2; ++form) {
+            GemmParams p;
+            gemm_init(p);
+            p.mode = 2;
+            p.A = reinterpret_cast<const float*>(A);
+            p.B = reinterpret_cast<const float*>(B);
+            p.M = M; p.N = 4096; p.K = 1024;
+            p.lda = 1024; p.ldb = 1024; p.tb = 1;
+            p.C = nullptr; p.ldc = 4096;
+            p.Ab = A; p.Bb = B; p.ldab = 1024; p.ldbb = 1024;
+            p.Cb = Cb; p.ldcb = 4096; p.preb = 1;
+            if (form == 0) {
+                p.epi = EPI_BIAS | EPI_STORE_PRE | EPI_GELU;
+                p.bias = bias;
+                p.C2 = reinterpret_cast<float*>(U); p.ldc2 = 4096;
+            } else {
+                p.epi = EPI_DGELU;
+                p.aux = reinterpret_cast<const float*>(U); p.ldaux = 4096;
+            }
+            const int evs[] = {0, 1, 2, 3};  // hb128, hb8, hbx32, hbx16
+            std::vector<float> ms[4];
+            for (int rd = 0; rd < rounds; ++rd)
+                for (int v : evs) {
+                    gemm_set_variant(variants[v][0], variants[v][1]);
+                    if (form == 0) hipLaunchKernelGGL(fillb, dim3((M * 4096L + 255) / 256), dim3(256), 0, 0, U, (long)M * 4096, 3u);
+                    for (int w = 0; w < 2; ++w) gemm_launch(p, 0, nullptr, 0);
+                    CK(hipEventRecord(e0, 0));
+                    for (int r = 0; r < reps; ++r) gemm_launch(p, 0, nullptr, 0);
+                    CK(hipEventRecord(e1, 0));
+                    CK(hipEventSynchronize(e1));
+                    float tt = 0;
+                    CK(hipEventElapsedTime(&tt, e0, e1));
+                    ms[v].push_back(tt / reps);
+                }
+            for (int v : evs) {
+                gemm_set_variant(variants[v][0], variants[v][1]);
+                hipLaunchKernelGGL(fillb, dim3((M * 4096L + 255) / 256), dim3(256), 0, 0, U, (long)M * 4096, 3u);
+                gemm_launch(p, 0, nullptr, 0);
+                CK(hipDeviceSynchronize());
+                double dmax = 0;
+                if (v == 0) CK(hipMemcpy(Cref, Cb, (size_t)M * 4096 * 2, hipMemcpyDeviceToDevice));
+                else {
+                    std::vector<__bf16> a((size_t)M * 4096), b((size_t)M * 4096);
+                    CK(hipMemcpy(a.data(), Cb, a.size() * 2, hipMemcpyDeviceToHost));
+                    CK(hipMemcpy(b.data(), Cref, b.size() * 2, hipMemcpyDeviceToHost));
+                    for (size_t i = 0; i < a.size(); i += 7) dmax = fmax(dmax, fabs((float)a[i] - (float)b[i]) / (fabs((float)b[i]) + 1.0));
+                }
+                std::vector<float> m = ms[v];
+                std::sort(m.begin(), m.end());
+                const double tf = 2.0 * M * 4096.0 * 1024.0 / (m[m.size() / 2] * 1e-3) / 1e12;
+                printf("%s %s: median %.4f ms %.1f TF (best %.1f) vs hb128 Cb relerr %.2e\n",
+                       form == 0 ? "ffn1 epi=bias+gelu+pre" : "ffn2dx epi=dgelu    ", vname[v], m[m.size() / 2], tf,
+                       2.0 * M * 4096.0 * 1024.0 / (m[0] * 1e-3) / 1e12, dmax);
+                fflush(stdout);
+            }
         }
     }
     return 0;

@@ -1,0 +1,16 @@
+# hbx integration: parity tests (bitwise vs the 128 x 128 kernel, C4 bench layout census) and a same-box C4 A/B
+set -e
+export TMPDIR=/tmp
+O=gpurun_out/r4hbxint
+mkdir -p $O
+( while sleep 50; do echo "tick $(date +%T)"; done ) &
+HB=$!
+trap "kill $HB" EXIT
+timeout -k 10 600 python -u -m pytest -x -v --timeout 500 --timeout-method thread tests/test_gpu_large_bf16.py::test_bf16_hbx_slice_ring_kernel_bitwise_equals_128_tile tests/test_gpu_bench_scale.py::test_c4_bench_layout_bf16 > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
+tail -3 $O/tests.log
+for i in 1 2; do
+  for x in 1 0; do
+    SUTA_HBX=$x timeout -k 10 300 python bench.py --only-c4 --steps 4 > $O/c4_hbx$x.$i.json 2> $O/c4_hbx$x.$i.err
+    python -c "import json; d=json.load(open('$O/c4_hbx$x.$i.json')); print('hbx=$x', d['value'], d['roofline']['frac'], d['time_breakdown_ms']['gemm'])"
+  done
+done
