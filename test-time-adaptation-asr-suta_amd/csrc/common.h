@@ -79,6 +79,40 @@ struct SutaSwitches {
 void suta_latch_switches();
 const SutaSwitches& suta_switches();  // the snapshot (taken now if none was)
 
+// GELU / GELU' of the bf16-plane GEMM epilogues (config C4: the result is rounded to a bf16 plane), two elements per
+// call on packed fp32 arithmetic (v_pk_mul_f32 / v_pk_fma_f32: half the VALU instructions of two scalar calls).
+// erf by Abramowitz & Stegun 7.1.28, erf(z) = 1 - (1 + a1 z + ... + a6 z^6)^-16 for z >= 0, |error| <= 3e-7 (the
+// bf16 output's own rounding step is 4e-3 relative): Phi(x) = 0.5 q for x < 0 and 1 - 0.5 q for x >= 0, q = p^-16
+// evaluated without cancellation.  About 9 VALU operations per element against ~22 for gelu_fast.
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2v phi_as2(f32x2v x, f32x2v& q) {
+    const f32x2v z = __builtin_elementwise_abs(x) * 0.70710678118654752f;
+    f32x2v p = z * 0.0000430638f + 0.0002765672f;
+    p = p * z + 0.0001520143f;
+    p = p * z + 0.0092705272f;
+    p = p * z + 0.0422820123f;
+    p = p * z + 0.0705230784f;
+    p = p * z + 1.0f;
+    p = p * p;
+    p = p * p;
+    p = p * p;
+    p = p * p;
+    q = f32x2v{__builtin_amdgcn_rcpf(p.x), __builtin_amdgcn_rcpf(p.y)};
+    const f32x2v h = 0.5f * q;
+    return f32x2v{x.x >= 0.f ? 1.0f - h.x : h.x, x.y >= 0.f ? 1.0f - h.y : h.y};
+}
+__device__ __forceinline__ f32x2v gelu2_bf16ep(f32x2v x) {
+    f32x2v q;
+    return x * phi_as2(x, q);
+}
+__device__ __forceinline__ f32x2v dgelu2_bf16ep(f32x2v x) {
+    f32x2v q;
+    const f32x2v cdf = phi_as2(x, q);
+    const f32x2v a = x * x * (-0.5f * 1.4426950408889634f);  // log2 of exp(-x^2 / 2)
+    const f32x2v e = f32x2v{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
+    return cdf + (x * 0.39894228040143268f) * e;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -165,14 +165,22 @@ __device__ __forceinline__ void epilogue16(const GemmParams& p, const f32x4 (&ac
             }
             if ((e & EPI_GELU) && CB && p.fgelu) {  // (uniform choice hoisted out of the element loop)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] = gelu_fast(v[r]);
+                for (int r = 0; r < 4; r += 2) {
+                    const f32x2v g = gelu2_bf16ep(f32x2v{v[r], v[r + 1]});
+                    v[r] = g.x;
+                    v[r + 1] = g.y;
+                }
             } else if (e & EPI_GELU) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) v[r] = gelu_f(v[r]);
             }
             if ((e & EPI_DGELU) && CB && p.fgelu) {
 #pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] *= dgelu_fast(xa[r]);
+                for (int r = 0; r < 4; r += 2) {
+                    const f32x2v g = dgelu2_bf16ep(f32x2v{xa[r], xa[r + 1]});
+                    v[r] *= g.x;
+                    v[r + 1] *= g.y;
+                }
             } else if (e & EPI_DGELU) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) v[r] *= dgelu_f(xa[r]);

@@ -249,6 +249,26 @@ def test_bf16_hbx_slice_ring_kernel_bitwise_equals_128_tile(monkeypatch):
         assert np.array_equal(v, params["0"][n]), n
 
 
+def test_bf16_epilogue_gelu_as_equals_erff(monkeypatch):
+    """The bf16-plane GEMM epilogues' GELU / GELU' (common.h gelu2_bf16ep / dgelu2_bf16ep: Abramowitz & Stegun 7.1.28
+    erf, |error| <= 3e-7, packed fp32, default) against erff (SUTA_FAST_GELU=0), wav2vec2-large in bf16 mode: the
+    outputs are bf16 planes, so the two agree to bf16 tolerance (greedy ids >= 97 %)."""
+    cfg = get_config("wav2vec2-large")
+    sd = synth_weights(cfg)
+    waves = [synth.wave(32000, 84), synth.wave(20000, 85)]
+    out = {}
+    for fg in ("1", "0"):
+        monkeypatch.setenv("SUTA_FAST_GELU", fg)
+        eng = SutaEngine(cfg, sd, max_batch=2, max_samples=32000)
+        eng.set_precision("bf16")
+        out[fg], _, _ = eng.adapt_varlen(waves, 3, SutaHParams(), record=[0, 3])
+        eng.close()
+    for r in (0, 3):
+        for u in range(2):
+            assert_bf16_close(out["1"][r][u], out["0"][r][u], 0.97, f"A&S GELU vs erff step {r} utt {u}",
+                              rtol=BF16_LOGITS_RTOL_LARGE)
+
+
 @pytest.mark.parametrize("preset", ["wav2vec2-base", "wav2vec2-large"])
 def test_flash_fwd_plane_kernel_equals_row_kernel(monkeypatch, preset):
     """flash_fwd_bf16p_kernel (Q / K / V read from the QKV GEMM's bf16 plane, V^T by transposed LDS reads;

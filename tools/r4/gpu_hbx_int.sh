@@ -1,4 +1,5 @@
-# hbx integration: parity tests (bitwise vs the 128 x 128 kernel, C4 bench layout census) and a same-box C4 A/B
+# hbx integration: GEMM bench (main loop + epilogue shapes), parity tests (bitwise vs the 128 x 128 kernel, A&S GELU
+# vs erff, C4 bench layout census) and a same-box C4 A/B (SUTA_HBX=1 / 0, interleaved)
 set -e
 export TMPDIR=/tmp
 O=gpurun_out/r4hbxint
@@ -6,7 +7,9 @@ mkdir -p $O
 ( while sleep 50; do echo "tick $(date +%T)"; done ) &
 HB=$!
 trap "kill $HB" EXIT
-timeout -k 10 600 python -u -m pytest -x -v --timeout 500 --timeout-method thread tests/test_gpu_large_bf16.py::test_bf16_hbx_slice_ring_kernel_bitwise_equals_128_tile tests/test_gpu_bench_scale.py::test_c4_bench_layout_bf16 > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
+timeout -k 10 300 ./tools/hb_bench 10 3 > $O/hb_bench.log 2>&1 || { cat $O/hb_bench.log; exit 1; }
+grep -E "hbx32|hb128" $O/hb_bench.log
+timeout -k 10 900 python -u -m pytest -x -v --timeout 500 --timeout-method thread tests/test_gpu_large_bf16.py::test_bf16_hbx_slice_ring_kernel_bitwise_equals_128_tile tests/test_gpu_large_bf16.py::test_bf16_epilogue_gelu_as_equals_erff tests/test_gpu_bench_scale.py::test_c4_bench_layout_bf16 > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
 tail -3 $O/tests.log
 for i in 1 2; do
   for x in 1 0; do
