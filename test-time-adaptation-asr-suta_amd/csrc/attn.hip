@@ -412,32 +412,35 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void flash_bwd_kernel(
 #pragma unroll
         for (int e = 0; e < 4; ++e) Kt[(c4 + e) * KBP + row] = x[e];
     }
-    // query tiles: Q and dO rows, LSE and delta
-    f32x4 qr[QPT], orr[QPT];
-    float lr = 0.f;
-    auto fetch = [&](int qt) {
+    // query tiles: Q and dO rows, LSE and delta, in two register stages (loads of tile qt+2 issued at the start of
+    // tile qt, written to LDS at the end of tile qt+1: two tiles of compute cover a load's latency)
+    struct Stg {
+        f32x4 qr[QPT], orr[QPT];
+        float lr;
+    };
+    auto fetch = [&](int qt, Stg& sg) {
 #pragma unroll
         for (int n = 0; n < QPT; ++n) {
             const int it = threadIdx.x + n * NT, row = it >> 4, c4 = (it & 15) * 4, q = qt * 32 + row;
-            qr[n] = orr[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+            sg.qr[n] = sg.orr[n] = f32x4{0.f, 0.f, 0.f, 0.f};
             if (q < T) {
-                qr[n] = *reinterpret_cast<const f32x4*>(Qb + (long)q * ld + c4);
-                orr[n] = *reinterpret_cast<const f32x4*>(Ob + (long)q * H + c4);
+                sg.qr[n] = *reinterpret_cast<const f32x4*>(Qb + (long)q * ld + c4);
+                sg.orr[n] = *reinterpret_cast<const f32x4*>(Ob + (long)q * H + c4);
             }
         }
-        lr = 0.f;
+        sg.lr = 0.f;
         const int qq = qt * 32 + (threadIdx.x & 31);
-        if (threadIdx.x < 64 && qq < T) lr = threadIdx.x < 32 ? lb[qq] : db[qq];
+        if (threadIdx.x < 64 && qq < T) sg.lr = threadIdx.x < 32 ? lb[qq] : db[qq];
     };
-    auto put = [&](int buf) {
+    auto put = [&](int buf, const Stg& sg) {
 #pragma unroll
         for (int n = 0; n < QPT; ++n) {
             const int it = threadIdx.x + n * NT, row = it >> 4, c4 = (it & 15) * 4;
-            *reinterpret_cast<f32x4*>(Qs + (buf * 32 + row) * FA_LD + c4) = qr[n];
-            *reinterpret_cast<f32x4*>(Ds + (buf * 32 + row) * FA_LD + c4) = orr[n];
+            *reinterpret_cast<f32x4*>(Qs + (buf * 32 + row) * FA_LD + c4) = sg.qr[n];
+            *reinterpret_cast<f32x4*>(Ds + (buf * 32 + row) * FA_LD + c4) = sg.orr[n];
         }
-        if (threadIdx.x < 32) Ls[buf * 32 + threadIdx.x] = lr;
-        else if (threadIdx.x < 64) Dl[buf * 32 + threadIdx.x - 32] = lr;
+        if (threadIdx.x < 32) Ls[buf * 32 + threadIdx.x] = sg.lr;
+        else if (threadIdx.x < 64) Dl[buf * 32 + threadIdx.x - 32] = sg.lr;
     };
 
     f32x16 dv[2], dk[2];
@@ -454,12 +457,18 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void flash_bwd_kernel(
     if (!active && w < ngb)         // keys past the length: their dS columns stay 0 for the dQ product
         for (int r = 0; r < 32; ++r)
             if (h == 0) Ss[r * KBP + 32 * w + l32] = 0.f;
-    fetch(0);
-    put(0);
+    // AHEAD = 2 (the exact fp32 instantiation of the headline): two register stages; 1 (the A/B-only instantiations,
+    // which the second stage would push into scratch): fetch tile qt+1 at the start of tile qt, as before
+    constexpr int AHEAD = (!BF16 && NW == 8) ? 2 : 1;
+    Stg sa, sb;
+    fetch(0, sa);
+    put(0, sa);
     __syncthreads();
-    for (int qt = 0; qt < nqt; ++qt) {
+    if (AHEAD == 2 && nqt > 1) fetch(1, sb);
+    // tile qt: fetch tile qt+AHEAD into fx (its previous content is in LDS), put tile qt+1 from py
+    auto tile = [&](int qt, Stg& fx, const Stg& py) {
         const int q0 = qt * 32, buf = qt & 1;
-        if (qt + 1 < nqt) fetch(qt + 1);
+        if (qt + AHEAD < nqt) fetch(qt + AHEAD, fx);
         const float* Qt = Qs + buf * 32 * FA_LD;
         const float* Dt = Ds + buf * 32 * FA_LD;
         const float* Lt = Ls + buf * 32;
@@ -470,20 +479,20 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void flash_bwd_kernel(
             for (int v = 0; v < 16; ++v) s[v] = dp[v] = 0.f;
             prod_rows<BF16>(s, Qt, kv, l32, h);   // S[q][key]: query r8(v,h), key on the lane
             prod_rows<BF16>(dp, Dt, vv, l32, h);  // dP[q][key]
-            f32x4 lq[4], dq[4];  // LSE / delta of the lane's rows r8(v, h): 4 runs of 4 consecutive rows
+            const bool kok = key < tl;
+            // LSE / delta of the lane's rows r8(v, h): 4 runs of 4 consecutive rows, one run live at a time
 #pragma unroll
             for (int a = 0; a < 4; ++a) {
-                lq[a] = *reinterpret_cast<const f32x4*>(Lt + 8 * a + 4 * h);
-                dq[a] = *reinterpret_cast<const f32x4*>(Dlt + 8 * a + 4 * h);
-            }
-            const bool kok = key < tl;
+                const f32x4 lq = *reinterpret_cast<const f32x4*>(Lt + 8 * a + 4 * h);
+                const f32x4 dq = *reinterpret_cast<const f32x4*>(Dlt + 8 * a + 4 * h);
 #pragma unroll
-            for (int v = 0; v < 16; ++v) {
-                const int r = r8(v, h);
-                const bool ok = kok && q0 + r < T;
-                const float p = ok ? __builtin_amdgcn_exp2f(sl2 * s[v] - LOG2E * lq[v >> 2][v & 3]) : 0.f;
-                s[v] = p;
-                dp[v] = scale * (p * (dp[v] - dq[v >> 2][v & 3]));
+                for (int b = 0; b < 4; ++b) {
+                    const int v = 4 * a + b, r = r8(v, h);
+                    const bool ok = kok && q0 + r < T;
+                    const float p = ok ? __builtin_amdgcn_exp2f(sl2 * s[v] - LOG2E * lq[b]) : 0.f;
+                    s[v] = p;
+                    dp[v] = scale * (p * (dp[v] - dq[b]));
+                }
             }
             apply_rows<BF16>(dv, Dt, s, l32, h);   // dV^T[n][key] += sum_q dO[q][n] P[q][key]
             apply_rows<BF16>(dk, Qt, dp, l32, h);  // dK^T[d][key] += sum_q Q[q][d] dS[q][key]
@@ -533,8 +542,18 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void flash_bwd_kernel(
             for (int r = 0; r < 4; ++r)
                 if (q0 + 16 * qi + 4 * g + r < T) dr[r * 64] = c0[r] + c1[r];
         }
-        if (qt + 1 < nqt) put(buf ^ 1);
+        if (qt + 1 < nqt) put(buf ^ 1, py);
         __syncthreads();  // next tile visible; dS tile free
+    };
+    if constexpr (AHEAD == 2) {
+        int qt = 0;
+        for (; qt + 1 < nqt; qt += 2) {
+            tile(qt, sa, sb);
+            tile(qt + 1, sb, sa);
+        }
+        if (qt < nqt) tile(qt, sa, sb);
+    } else {
+        for (int qt = 0; qt < nqt; ++qt) tile(qt, sa, sa);
     }
     // dK, dV rows of this wave's keys (0 past the length): lane = key, registers = 4 consecutive columns
     if (w >= ngb || key >= T) return;
@@ -1193,23 +1212,27 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
 #pragma unroll
         for (int e = 0; e < 8; ++e) Kt[(c8 + e) * FBB_KB + row] = x[e];
     }
-    // query-tile copy: threads 0..255 one 16-B chunk of the Q rows, 256..511 one of the dO rows
+    // query-tile copy: threads 0..255 one 16-B chunk of the Q rows, 256..511 one of the dO rows.  Two register
+    // stages: the loads of tile qt+2 are issued at the start of tile qt and written to LDS at the end of tile qt+1,
+    // so a global load has two tiles of compute to land (one tile was shorter than its latency: parked waves)
     const bool isq = threadIdx.x < 256;
     const int crow = (threadIdx.x & 255) >> 3, ccol = (threadIdx.x & 7) * 8;
-    fbf16x8 xr;
-    float lr = 0.f;
-    auto fetch = [&](int qt) {
-        const int q = qt * 32 + crow;
-        xr = fbf16x8{};
-        if (q < T) xr = *reinterpret_cast<const fbf16x8*>(isq ? Qb + (long)q * ld + ccol : Ob + (long)q * H + ccol);
-        lr = 0.f;
-        const int qq = qt * 32 + (threadIdx.x & 31);
-        if (threadIdx.x < 64 && qq < T) lr = threadIdx.x < 32 ? lb[qq] : db[qq];
+    struct Stg {
+        fbf16x8 xr;
+        float lr;
     };
-    auto put = [&](int buf) {
-        *reinterpret_cast<fbf16x8*>((isq ? Qr : Dr) + (buf * 32 + crow) * FB_RS + ccol) = xr;
-        if (threadIdx.x < 32) Ls[buf * 32 + threadIdx.x] = lr;
-        else if (threadIdx.x < 64) Dl[buf * 32 + threadIdx.x - 32] = lr;
+    auto fetch = [&](int qt, Stg& sg) {
+        const int q = qt * 32 + crow;
+        sg.xr = fbf16x8{};
+        if (q < T) sg.xr = *reinterpret_cast<const fbf16x8*>(isq ? Qb + (long)q * ld + ccol : Ob + (long)q * H + ccol);
+        sg.lr = 0.f;
+        const int qq = qt * 32 + (threadIdx.x & 31);
+        if (threadIdx.x < 64 && qq < T) sg.lr = threadIdx.x < 32 ? lb[qq] : db[qq];
+    };
+    auto put = [&](int buf, const Stg& sg) {
+        *reinterpret_cast<fbf16x8*>((isq ? Qr : Dr) + (buf * 32 + crow) * FB_RS + ccol) = sg.xr;
+        if (threadIdx.x < 32) Ls[buf * 32 + threadIdx.x] = sg.lr;
+        else if (threadIdx.x < 64) Dl[buf * 32 + threadIdx.x - 32] = sg.lr;
     };
     f32x16 dv[2], dk[2];
 #pragma unroll
@@ -1225,17 +1248,19 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
     if (!active && w < ngb)
         for (int r = 0; r < 32; ++r)
             if (h == 0) Ss[r * FBB_KB + 32 * w + l32] = (__bf16)0.f;
-    fetch(0);
-    put(0);
+    Stg sa, sb;
+    fetch(0, sa);
+    put(0, sa);
     __syncthreads();
-    fbf16x8 kfr[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-        if (32 * j < kq) kfr[j] = *reinterpret_cast<const fbf16x8*>(Kt + (16 * di + l16) * FBB_KB + 32 * j + 8 * g);
+    if (nqt > 1) fetch(1, sb);
+    // (the dQ product's K^T fragments are read from the K^T image per tile: holding them in registers, 32 VGPRs,
+    // made the two-stage prefetch spill)
+    const __bf16* kfrow = Kt + (16 * di + l16) * FBB_KB + 8 * g;
     const bool odd = lane & 1;
-    for (int qt = 0; qt < nqt; ++qt) {
+    // tile qt: fetch tile qt+2 into fx (its previous content, tile qt, is in LDS), put tile qt+1 from py
+    auto tile = [&](int qt, Stg& fx, const Stg& py) {
         const int q0 = qt * 32, buf = qt & 1;
-        if (qt + 1 < nqt) fetch(qt + 1);
+        if (qt + 2 < nqt) fetch(qt + 2, fx);
         const float* Lt = Ls + buf * 32;
         const float* Dlt = Dl + buf * 32;
         if (active) {
@@ -1292,16 +1317,23 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
             for (int j = 0; j < 8; ++j)
                 if (32 * j < kq)
                     c[j & 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                        *reinterpret_cast<const fbf16x8*>(ar + 32 * j), kfr[j], c[j & 1], 0, 0, 0);
+                        *reinterpret_cast<const fbf16x8*>(ar + 32 * j),
+                        *reinterpret_cast<const fbf16x8*>(kfrow + 32 * j), c[j & 1], 0, 0, 0);
             const f32x4 c0 = c[0], c1 = c[1];
             float* dr = dqb + (long)(q0 + 16 * qi + 4 * g) * 64 + 16 * di + l16;
 #pragma unroll
             for (int r = 0; r < 4; ++r)
                 if (q0 + 16 * qi + 4 * g + r < T) dr[r * 64] = c0[r] + c1[r];
         }
-        if (qt + 1 < nqt) put(buf ^ 1);
+        if (qt + 1 < nqt) put(buf ^ 1, py);
         __syncthreads();
+    };
+    int qt = 0;
+    for (; qt + 1 < nqt; qt += 2) {
+        tile(qt, sa, sb);
+        tile(qt + 1, sb, sa);
     }
+    if (qt < nqt) tile(qt, sa, sb);
     if (w >= ngb || key >= T) return;
     float* dkr = dqkv + ((long)u * T + key) * ld + H + hd * 64 + 4 * h;
     float* dvr = dkr + H;

@@ -75,6 +75,8 @@ struct SutaSwitches {
     int flash_fwd_nw;     // SUTA_FLASH_FWD_NW (default 4): waves per block of the bf16-plane flash forward
     int hbx;              // SUTA_HBX (default 1): the 256 x 256 slice-ring bf16-plane GEMM for plain-epilogue linears
                           // on full grids; 2: on every eligible bf16-plane linear (tests: small grids, edge tiles)
+    int splitk;           // SUTA_SPLITK (default 1): split-K for small grids; 0 = never (tests comparing kernels
+                          // bitwise: a split changes the k summation order)
 };
 void suta_latch_switches();
 const SutaSwitches& suta_switches();  // the snapshot (taken now if none was)

@@ -261,7 +261,8 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
     // split-K when the grid cannot fill 256 CUs and K is long
     int splits = 1;
     // (the split-K reduce has no bf16 pre store and no batched bf16 C plane)
-    if (ws && p.K >= 1024 && blocks < 256 && tile != 6 && tile != 8 && tile != 9 && !p.preb && !(p.Cb && p.Z > 1)) {
+    if (ws && suta_switches().splitk && p.K >= 1024 && blocks < 256 && tile != 6 && tile != 8 && tile != 9 && !p.preb &&
+        !(p.Cb && p.Z > 1)) {
         splits = (int)std::min<long>(16, (512 + blocks - 1) / blocks);
         while (splits > 1 && (long)splits * p.Z * p.M * (long)p.N > ws_floats) --splits;
         splits = std::min(splits, std::max(1, (p.K + 255) / 256));  // >= 256 K per split

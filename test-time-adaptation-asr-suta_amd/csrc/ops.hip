@@ -1822,6 +1822,7 @@ void suta_latch_switches() {
     s.fused_conv_ln = on("SUTA_FUSED_CONV_LN");
     const char* hbx = std::getenv("SUTA_HBX");
     s.hbx = hbx ? atoi(hbx) : 1;
+    s.splitk = on("SUTA_SPLITK");
     const char* hb8 = std::getenv("SUTA_HB8");
     s.hb8 = hb8 ? atoi(hb8) : 0;
     const char* fnw = std::getenv("SUTA_FLASH_FWD_NW");

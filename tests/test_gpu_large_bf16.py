@@ -218,9 +218,11 @@ def test_bf16_hb8_pingpong_kernel(monkeypatch):
 def test_bf16_hbx_slice_ring_kernel_bitwise_equals_128_tile(monkeypatch):
     """gemm_hbx_kernel (256 x 256 tile, 32-deep slice ring, v_mfma_f32_32x32x16_bf16) forced on every bf16-plane linear
     (SUTA_HBX=2: every epilogue class -- bias / residual, bias + GELU + bf16 pre-activation, GELU' -- small grids and
-    edge tiles of a ragged pair: 198 and 124 rows of a 256-row tile) against the 128 x 128 kernel (SUTA_HBX=0):
-    the same MFMA in the same k order, so logits and adapted tensors are bitwise equal; and the large model's
-    20-step SUTA against the reference goldens g7 (bf16 tolerance).  Reference main.py:181,205."""
+    edge tiles of a ragged pair: 198 and 124 rows of a 256-row tile) against the 128 x 128 kernel (SUTA_HBX=0), both
+    without split-K (SUTA_SPLITK=0: a split sums k in another order): the same MFMA in the same k order, so logits and
+    adapted tensors are bitwise equal; and the large model's 20-step SUTA against the reference goldens g7 (bf16
+    tolerance).  Reference main.py:181,205."""
+    monkeypatch.setenv("SUTA_SPLITK", "0")
     z = _load("g7_large_16000.npz")
     cfg = get_config("wav2vec2-large")
     sd = synth_weights(cfg)
