@@ -77,6 +77,8 @@ struct SutaSwitches {
                           // on full grids; 2: on every eligible bf16-plane linear (tests: small grids, edge tiles)
     int splitk;           // SUTA_SPLITK (default 1): split-K for small grids; 0 = never (tests comparing kernels
                           // bitwise: a split changes the k summation order)
+    int hbx_t;            // SUTA_HBX_T (default 1): gemm_hbx accumulates C^T fragments (row-per-lane epilogue, 16-B
+                          // stores); 0 = the column-per-lane form shared with the 128 x 128 kernel
 };
 void suta_latch_switches();
 const SutaSwitches& suta_switches();  // the snapshot (taken now if none was)

@@ -195,16 +195,17 @@ static int use_hb8(const GemmParams& p) {
 }
 
 // 256 x 256 slice-ring bf16-plane kernel (gemm_hbx.hip, v_mfma_f32_32x32x16_bf16; bitwise the 128 x 128 kernel's
-// results: same MFMA, same k order) for the linears whose epilogue is bias / residual / the bf16 C plane, on grids of at
-// least one full round of 256 tiles.  tools/hb_bench (C4 shapes at M = 164 x 399, same box): qkv 741 -> 889 TF,
-// out-proj 604 -> 784, FFN1 749 -> 858, FFN2 865 -> 1055, dQKV 808 -> 1022; with the GELU / GELU' epilogues equal to
-// 128 x 128 (576 vs 588, 577 vs 572: one block per CU exposes the epilogue), so those keep the 128 x 128 kernel.
+// results: same MFMA, same k order) for the linears on grids of at least one full round of 256 tiles.  tools/hb_bench
+// (C4 shapes at M = 164 x 399, same box): qkv 741 -> 889 TF, out-proj 604 -> 784, FFN1 749 -> 858, FFN2 865 -> 1055,
+// dQKV 808 -> 1022.  With the column-per-lane epilogue the GELU / GELU' classes measured equal to 128 x 128 (576 vs
+// 588, 577 vs 572: 128 two-lane-pair dword stores per bf16 plane per wave, store-issue bound at one block per CU), so
+// they take hbx only with its row-per-lane epilogue (SUTA_HBX_T, 16-B stores).
 // SUTA_HBX=0: off (A/B runs); 2: every eligible linear, any epilogue and grid (tests).
 static bool use_hbx(const GemmParams& p) {
     const int mode = suta_switches().hbx;
     if (!mode || p.Z != 1 || p.segK > 0 || p.K % 32 || p.K < 128 || (p.epi & (EPI_ACCUM | EPI_SMBWD))) return false;
     if (mode == 2) return true;  // SUTA_HBX=2: every eligible linear (tests)
-    if (p.epi & (EPI_GELU | EPI_DGELU | EPI_STORE_PRE)) return false;
+    if ((p.epi & (EPI_GELU | EPI_DGELU | EPI_STORE_PRE)) && !(suta_switches().hbx_t && hbx_t_ok(p, false))) return false;
     return (long)((p.M + 255) / 256) * ((p.N + 255) / 256) >= 256;
 }
 

@@ -22,6 +22,7 @@
 // MS: MFMA shape, 32 (v_mfma_f32_32x32x16_bf16, the epilogue's fragment form) or 16 (v_mfma_f32_16x16x32_bf16).
 // Requires K % 32 == 0 and K >= 128, no split-K, Z == 1, no conv-A rows (the dispatcher's conditions).
 #include "gemm_kernels.h"
+#include <cstdint>
 #include <cstdlib>
 #include <stdexcept>
 #include <type_traits>
@@ -221,7 +222,191 @@ __device__ __forceinline__ void epilogue16(const GemmParams& p, const f32x4 (&ac
         }
 }
 
-template <int MS, bool CB, int EM>
+// Row-per-lane epilogue of the transposed accumulators (TR: the MFMAs take B as their first operand, so acc[i][j]
+// holds C^T: lane l carries row 32 i + (l & 31) of the wave tile, register r = 4 g + k its column 32 j + 8 g +
+// 4 (l >> 5) + k).  Each lane holds runs of 4 consecutive columns; v_permlane32_swap pairs the half-waves' runs of
+// column groups (g, g + 1) into 16 contiguous bytes per lane (cdna_hip_programming.md T21), so every bf16 plane
+// (C plane, pre-activation store, GELU' operand) moves in 16-B accesses and fp32 operands in float4s: 16 store
+// instructions per bf16 plane per wave instead of 128 two-lane-pair dword stores.  Same operations in the same order
+// as gemm_epilogue (elementwise; packed GELU pairs are lane-independent).  Rows past M are predicated per lane;
+// column tiles past N take the element-wise path.  gemm_run_hbx checks alignment (16-B bases, ld % 8 for the bf16
+// planes, % 4 for the fp32 ones) and off32 before choosing this form.
+typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ unsigned pack_bf16x2(float a, float b) {
+    bf16x2v t;
+    t[0] = (__bf16)a;
+    t[1] = (__bf16)b;
+    return __builtin_bit_cast(unsigned, t);
+}
+__device__ __forceinline__ float bf16_lo(unsigned u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float bf16_hi(unsigned u) { return __uint_as_float(u & 0xffff0000u); }
+
+// runs (g0, g0 + 1) of 4 bf16 each (x0 = cols 0-1, y0 = cols 2-3 of run g0; x1, y1 of run g0 + 1) <-> one 16-B chunk
+// per lane (lower half-wave: cols 8 g0 .. 8 g0 + 7, upper: 8 g0 + 8 .. 8 g0 + 15); the exchange is its own inverse
+__device__ __forceinline__ void swap_runs(unsigned& x0, unsigned& y0, unsigned& x1, unsigned& y1) {
+    auto rx = __builtin_amdgcn_permlane32_swap(x0, x1, false, false);
+    auto ry = __builtin_amdgcn_permlane32_swap(y0, y1, false, false);
+    x0 = rx[0];
+    x1 = rx[1];
+    y0 = ry[0];
+    y1 = ry[1];
+}
+
+// column tiles past N: element by element (same arithmetic, bounds-checked stores)
+template <bool CB, int EM>
+__device__ __forceinline__ void epilogue_t_edge(const GemmParams& p, const f32x16 (&acc)[4][2], int rbase, int cbase,
+                                                int lane) {
+    const int e = p.epi & EM;
+    const int h = lane >> 5, l32 = lane & 31;
+    const int rlim = (e & EPI_ROWMASK) ? p.zrows[0] : 0x7fffffff;
+    const bool preb = CB && p.preb;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int row = rbase + 32 * i + l32;
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int col = cbase + 32 * j + 8 * (r >> 2) + 4 * h + (r & 3);
+                if (row >= p.M || col >= p.N) continue;
+                float v = acc[i][j][r] * p.alpha;
+                if (e & EPI_BIAS) v += p.bias[col];
+                if (e & EPI_STORE_PRE) {
+                    if (preb) reinterpret_cast<__bf16*>(p.C2)[(long)row * p.ldc2 + col] = (__bf16)v;
+                    else p.C2[(long)row * p.ldc2 + col] = v;
+                }
+                if (e & EPI_GELU) v = (CB && p.fgelu) ? gelu2_bf16ep(f32x2v{v, v}).x : gelu_f(v);
+                if (e & EPI_DGELU) {
+                    const float xa = preb ? (float)reinterpret_cast<const __bf16*>(p.aux)[(long)row * p.ldaux + col]
+                                          : p.aux[(long)row * p.ldaux + col];
+                    v *= (CB && p.fgelu) ? dgelu2_bf16ep(f32x2v{xa, xa}).x : dgelu_f(xa);
+                }
+                if (e & EPI_RESID) v += p.R[(long)row * p.ldr + col];
+                if (row >= rlim) v = 0.f;
+                if (!CB || p.C) p.C[(long)row * p.ldc + col] = v;
+                if (CB) reinterpret_cast<__bf16*>(p.Cb)[(long)row * p.ldcb + col] = (__bf16)v;
+            }
+    }
+}
+
+template <bool CB, int EM>
+__device__ __forceinline__ void epilogue_t(const GemmParams& p, const f32x16 (&acc)[4][2], int rbase, int cbase,
+                                           int lane) {
+    if (cbase + 64 > p.N) {
+        epilogue_t_edge<CB, EM>(p, acc, rbase, cbase, lane);
+        return;
+    }
+    const int e = p.epi & EM;
+    const int h = lane >> 5, l32 = lane & 31;
+    const float alpha = p.alpha;
+    const int rlim = (e & EPI_ROWMASK) ? p.zrows[0] : 0x7fffffff;
+    const bool preb = CB && p.preb;
+    // one bf16 plane's 8 values of runs (2q, 2q + 1) as one 16-B chunk per lane
+    auto store_bf16 = [&](__bf16* d, const float* v, bool rok) {
+        unsigned x0 = pack_bf16x2(v[0], v[1]), y0 = pack_bf16x2(v[2], v[3]);
+        unsigned x1 = pack_bf16x2(v[4], v[5]), y1 = pack_bf16x2(v[6], v[7]);
+        swap_runs(x0, y0, x1, y1);
+        if (rok) *reinterpret_cast<u32x4v*>(d) = u32x4v{x0, y0, x1, y1};
+    };
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int row = rbase + 32 * i + l32;
+        const long rowc = min(row, p.M - 1);
+        const bool rok = row < p.M;
+        const bool zero = (e & EPI_ROWMASK) && row >= rlim;
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {  // runs 2q, 2q + 1: columns nb .. nb + 15 of the block
+                const int nb = cbase + 32 * j + 16 * q;
+                float v[8], xa[8], xr[8];
+                if (e & EPI_DGELU) {
+                    if (preb) {
+                        const u32x4v w = *reinterpret_cast<const u32x4v*>(reinterpret_cast<const __bf16*>(p.aux) +
+                                                                           rowc * p.ldaux + nb + 8 * h);
+                        unsigned x0 = w[0], y0 = w[1], x1 = w[2], y1 = w[3];
+                        swap_runs(x0, y0, x1, y1);
+                        xa[0] = bf16_lo(x0); xa[1] = bf16_hi(x0); xa[2] = bf16_lo(y0); xa[3] = bf16_hi(y0);
+                        xa[4] = bf16_lo(x1); xa[5] = bf16_hi(x1); xa[6] = bf16_lo(y1); xa[7] = bf16_hi(y1);
+                    } else {
+#pragma unroll
+                        for (int t = 0; t < 2; ++t) {
+                            const f32x4 w = *reinterpret_cast<const f32x4*>(p.aux + rowc * p.ldaux + nb + 8 * t + 4 * h);
+#pragma unroll
+                            for (int k = 0; k < 4; ++k) xa[4 * t + k] = w[k];
+                        }
+                    }
+                }
+                if (e & EPI_RESID) {
+#pragma unroll
+                    for (int t = 0; t < 2; ++t) {
+                        const f32x4 w = *reinterpret_cast<const f32x4*>(p.R + rowc * p.ldr + nb + 8 * t + 4 * h);
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) xr[4 * t + k] = w[k];
+                    }
+                }
+#pragma unroll
+                for (int t = 0; t < 2; ++t) {
+                    f32x4 bj = {0.f, 0.f, 0.f, 0.f};
+                    if (e & EPI_BIAS) bj = *reinterpret_cast<const f32x4*>(p.bias + nb + 8 * t + 4 * h);
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        v[4 * t + k] = acc[i][j][8 * q + 4 * t + k] * alpha;
+                        if (e & EPI_BIAS) v[4 * t + k] += bj[k];
+                    }
+                }
+                if (e & EPI_STORE_PRE) {
+                    if (preb) store_bf16(reinterpret_cast<__bf16*>(p.C2) + (long)row * p.ldc2 + nb + 8 * h, v, rok);
+                    else if (rok)
+#pragma unroll
+                        for (int t = 0; t < 2; ++t)
+                            *reinterpret_cast<f32x4*>(p.C2 + (long)row * p.ldc2 + nb + 8 * t + 4 * h) =
+                                f32x4{v[4 * t], v[4 * t + 1], v[4 * t + 2], v[4 * t + 3]};
+                }
+                if ((e & EPI_GELU) && CB && p.fgelu) {
+#pragma unroll
+                    for (int r = 0; r < 8; r += 2) {
+                        const f32x2v g2 = gelu2_bf16ep(f32x2v{v[r], v[r + 1]});
+                        v[r] = g2.x;
+                        v[r + 1] = g2.y;
+                    }
+                } else if (e & EPI_GELU) {
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) v[r] = gelu_f(v[r]);
+                }
+                if ((e & EPI_DGELU) && CB && p.fgelu) {
+#pragma unroll
+                    for (int r = 0; r < 8; r += 2) {
+                        const f32x2v g2 = dgelu2_bf16ep(f32x2v{xa[r], xa[r + 1]});
+                        v[r] *= g2.x;
+                        v[r + 1] *= g2.y;
+                    }
+                } else if (e & EPI_DGELU) {
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) v[r] *= dgelu_f(xa[r]);
+                }
+                if (e & EPI_RESID) {
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) v[r] += xr[r];
+                }
+                if (zero) {
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) v[r] = 0.f;
+                }
+                if ((!CB || p.C) && rok) {
+#pragma unroll
+                    for (int t = 0; t < 2; ++t)
+                        *reinterpret_cast<f32x4*>(p.C + (long)row * p.ldc + nb + 8 * t + 4 * h) =
+                            f32x4{v[4 * t], v[4 * t + 1], v[4 * t + 2], v[4 * t + 3]};
+                }
+                if (CB) store_bf16(reinterpret_cast<__bf16*>(p.Cb) + (long)row * p.ldcb + nb + 8 * h, v, rok);
+            }
+    }
+}
+
+template <int MS, bool CB, int EM, bool TR>
 __global__ __launch_bounds__(512, 1) void gemm_hbx_kernel(GemmParams p) {
     __shared__ __attribute__((aligned(16))) float smem[X_NR * X_SLOT];
     const TileId tid = xcd_tile(p.order);
@@ -276,7 +461,8 @@ __global__ __launch_bounds__(512, 1) void gemm_hbx_kernel(GemmParams p) {
             for (int i = 0; i < 4; ++i)
 #pragma unroll
                 for (int j = 0; j < 2; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[i], f.b[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = TR ? __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.b[j], f.a[i], acc[i][j], 0, 0, 0)
+                                   : __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[i], f.b[j], acc[i][j], 0, 0, 0);
         } else {
 #pragma unroll
             for (int i = 0; i < 4; ++i)
@@ -324,7 +510,9 @@ __global__ __launch_bounds__(512, 1) void gemm_hbx_kernel(GemmParams p) {
     wait_vm<0>();
 
     const bool interior = m0 + X_BM <= p.M && n0 + X_BN <= p.N;
-    if constexpr (MS == 32) {
+    if constexpr (TR) {
+        epilogue_t<CB, EM>(p, reinterpret_cast<const f32x16(&)[4][2]>(acc[0]), m0 + wr * 128, n0 + wc * 64, lane);
+    } else if constexpr (MS == 32) {
         gemm_epilogue<2, 2, CB, EM>(p, reinterpret_cast<const f32x16(&)[2][2]>(acc[0]), 0, 0, m0 + wr * 128,
                                     n0 + wc * 64, h, l32, interior, tid.z);
         gemm_epilogue<2, 2, CB, EM>(p, reinterpret_cast<const f32x16(&)[2][2]>(acc[2]), 0, 0, m0 + wr * 128 + 64,
@@ -338,11 +526,30 @@ __global__ __launch_bounds__(512, 1) void gemm_hbx_kernel(GemmParams p) {
     }
 }
 
-template <int MS, int EM>
+template <int MS, int EM, bool TR = false>
 void launch_hbx_em(const GemmParams& p, dim3 grid, hipStream_t st) {
-    if (p.Cb) hipLaunchKernelGGL((gemm_hbx_kernel<MS, true, EM>), grid, dim3(512), 0, st, p);
-    else hipLaunchKernelGGL((gemm_hbx_kernel<MS, false, EM>), grid, dim3(512), 0, st, p);
+    if (p.Cb) hipLaunchKernelGGL((gemm_hbx_kernel<MS, true, EM, TR>), grid, dim3(512), 0, st, p);
+    else hipLaunchKernelGGL((gemm_hbx_kernel<MS, false, EM, TR>), grid, dim3(512), 0, st, p);
 }
+
+// operands of the row-per-lane epilogue: 16-B bases, leading dimensions in whole 16-B chunks
+}  // namespace
+
+bool hbx_t_ok(const GemmParams& p, bool check_off32) {
+    auto a16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+    const int e = p.epi;
+    if (check_off32 && !p.off32) return false;
+    if ((!p.Cb || p.C) && !(a16(p.C) && p.ldc % 4 == 0)) return false;
+    if (p.Cb && !(a16(p.Cb) && p.ldcb % 8 == 0)) return false;
+    if ((e & EPI_BIAS) && !a16(p.bias)) return false;
+    if ((e & EPI_RESID) && !(a16(p.R) && p.ldr % 4 == 0)) return false;
+    const bool preb = p.Cb && p.preb;
+    if ((e & EPI_DGELU) && !(a16(p.aux) && p.ldaux % (preb ? 8 : 4) == 0)) return false;
+    if ((e & EPI_STORE_PRE) && !(a16(p.C2) && p.ldc2 % (preb ? 8 : 4) == 0)) return false;
+    return true;
+}
+
+namespace {
 
 // epilogue classes of the bf16 linears (as gemm_hb_ep.hip): bias / residual, bias + GELU + pre-activation store,
 // GELU'; ragged row masks in each
@@ -364,6 +571,11 @@ void gemm_run_hbx(int variant, const GemmParams& p, dim3 grid, hipStream_t st) {
         else if ((e & ~XEM_D) == 0) launch_hbx_em<16, XEM_D>(p, grid, st);
         else throw std::invalid_argument("hbx 16x16: epilogue flags outside the linears' classes");
         return;
+    }
+    if (suta_switches().hbx_t && hbx_t_ok(p, true)) {  // C^T accumulators, row-per-lane 16-B epilogue
+        if ((e & ~XEM_A) == 0) return launch_hbx_em<32, XEM_A, true>(p, grid, st);
+        if ((e & ~XEM_G) == 0) return launch_hbx_em<32, XEM_G, true>(p, grid, st);
+        if ((e & ~XEM_D) == 0) return launch_hbx_em<32, XEM_D, true>(p, grid, st);
     }
     if ((e & ~XEM_A) == 0) launch_hbx_em<32, XEM_A>(p, grid, st);
     else if ((e & ~XEM_G) == 0) launch_hbx_em<32, XEM_G>(p, grid, st);

@@ -1823,6 +1823,7 @@ void suta_latch_switches() {
     const char* hbx = std::getenv("SUTA_HBX");
     s.hbx = hbx ? atoi(hbx) : 1;
     s.splitk = on("SUTA_SPLITK");
+    s.hbx_t = on("SUTA_HBX_T");
     const char* hb8 = std::getenv("SUTA_HB8");
     s.hb8 = hb8 ? atoi(hb8) : 0;
     const char* fnw = std::getenv("SUTA_FLASH_FWD_NW");

@@ -218,10 +218,11 @@ def test_bf16_hb8_pingpong_kernel(monkeypatch):
 def test_bf16_hbx_slice_ring_kernel_bitwise_equals_128_tile(monkeypatch):
     """gemm_hbx_kernel (256 x 256 tile, 32-deep slice ring, v_mfma_f32_32x32x16_bf16) forced on every bf16-plane linear
     (SUTA_HBX=2: every epilogue class -- bias / residual, bias + GELU + bf16 pre-activation, GELU' -- small grids and
-    edge tiles of a ragged pair: 198 and 124 rows of a 256-row tile) against the 128 x 128 kernel (SUTA_HBX=0), both
-    without split-K (SUTA_SPLITK=0: a split sums k in another order): the same MFMA in the same k order, so logits and
-    adapted tensors are bitwise equal; and the large model's 20-step SUTA against the reference goldens g7 (bf16
-    tolerance).  Reference main.py:181,205."""
+    edge tiles of a ragged pair: 198 and 124 rows of a 256-row tile), in both epilogue forms (SUTA_HBX_T=1: C^T
+    accumulators, row-per-lane 16-B stores; 0: the column-per-lane form), against the 128 x 128 kernel (SUTA_HBX=0),
+    all without split-K (SUTA_SPLITK=0: a split sums k in another order): the same MFMA products in the same k order, so
+    logits and adapted tensors are bitwise equal; and the large model's 20-step SUTA against the reference goldens g7
+    (bf16 tolerance).  Reference main.py:181,205."""
     monkeypatch.setenv("SUTA_SPLITK", "0")
     z = _load("g7_large_16000.npz")
     cfg = get_config("wav2vec2-large")
@@ -229,11 +230,12 @@ def test_bf16_hbx_slice_ring_kernel_bitwise_equals_128_tile(monkeypatch):
     steps = [int(s) for s in z["steps"]]
     waves = [synth.wave(32000, 82), synth.wave(20000, 83)]
     out, params = {}, {}
-    for mode in ("2", "0"):
+    for mode, tr in (("0", "1"), ("2", "1"), ("2", "0")):
         monkeypatch.setenv("SUTA_HBX", mode)
+        monkeypatch.setenv("SUTA_HBX_T", tr)
         eng = SutaEngine(cfg, sd, max_batch=2, max_samples=32000)
         eng.set_precision("bf16")
-        if mode == "2":
+        if mode == "2" and tr == "1":
             eng.set_census(True)
             logits, _, _ = eng.adapt(_g7_wave(), 20, SutaHParams(), record=steps)
             census = eng.get_census()
@@ -241,14 +243,16 @@ def test_bf16_hbx_slice_ring_kernel_bitwise_equals_128_tile(monkeypatch):
             assert any(k.startswith("hbx 256x256 ") for k in census), census
             for j, s in enumerate(steps):
                 assert_bf16_close(logits[s][0], z["logits"][j], 0.97, f"hbx large step {s}", rtol=BF16_LOGITS_RTOL_LARGE)
-        out[mode], _, _ = eng.adapt_varlen(waves, 3, SutaHParams(), record=[0, 3])
-        params[mode] = {n: eng.get_param(1, n) for n in eng.trainable_names()}
+        key = mode + tr
+        out[key], _, _ = eng.adapt_varlen(waves, 3, SutaHParams(), record=[0, 3])
+        params[key] = {n: eng.get_param(1, n) for n in eng.trainable_names()}
         eng.close()
-    for r in (0, 3):
-        for u in range(2):
-            assert np.array_equal(out["2"][r][u], out["0"][r][u]), (r, u)
-    for n, v in params["2"].items():
-        assert np.array_equal(v, params["0"][n]), n
+    for key in ("21", "20"):
+        for r in (0, 3):
+            for u in range(2):
+                assert np.array_equal(out[key][r][u], out["01"][r][u]), (key, r, u)
+        for n, v in params[key].items():
+            assert np.array_equal(v, params["01"][n]), (key, n)
 
 
 def test_bf16_epilogue_gelu_as_equals_erff(monkeypatch):

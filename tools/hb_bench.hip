@@ -1,8 +1,9 @@
 // bf16-plane GEMM microbenchmark + check on the C4 linear shapes (w2v2-large, M = 164 x 399 rows: bench.py's layout):
-// gemm_hb_kernel (128 x 128), gemm_hb8_kernel (256 x 256 ping-pong), gemm_hbx_kernel (256 x 256 slice ring; 32x32x16
-// and 16x16x32 MFMA forms).  Variants run interleaved, `rounds` times each (median reported).
+// gemm_hb_kernel (128 x 128), gemm_hbx_kernel (256 x 256 slice ring) with its two epilogue forms (column-per-lane
+// accumulators, and C^T accumulators with 16-B row-per-lane stores).  Variants run interleaved, `rounds` times each (median reported).
 // Build: hipcc -O3 --offload-arch=gfx950 -I test-time-adaptation-asr-suta_amd/csrc -c tools/hb_bench.hip -o /tmp/hb.o
-//        && hipcc --offload-arch=gfx950 /tmp/hb.o test-time-adaptation-asr-suta_amd/csrc/gemm*.o -o tools/hb_bench
+//        && hipcc --offload-arch=gfx950 /tmp/hb.o test-time-adaptation-asr-suta_amd/csrc/gemm*.o \
+//           test-time-adaptation-asr-suta_amd/csrc/ops.o -o tools/hb_bench
 #include <hip/hip_runtime.h>
 #include <cmath>
 #include <cstdio>
@@ -47,10 +48,16 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    // (tile, ns, cb-capable): 0 = hb 128 x 128, 6 = hb8, 8 = hbx (32x32x16), 9 = hbx16 (16x16x32, plain C only)
-    const int variants[][3] = {{0, 2, 1}, {6, 2, 1}, {8, 2, 1}, {9, 2, 1}};
-    const char* vname[] = {"hb128", "hb8  ", "hbx32", "hbx16"};
-    constexpr int NV = 4;
+    // (tile, ns, cb-capable, SUTA_HBX_T): 0 = hb 128 x 128, 8 = hbx (32x32x16) with the column-per-lane epilogue
+    // and with C^T accumulators + the row-per-lane epilogue (hbxT)
+    const int variants[][4] = {{0, 2, 1, 0}, {8, 2, 1, 0}, {8, 2, 1, 1}};
+    const char* vname[] = {"hb128", "hbx32", "hbxT "};
+    constexpr int NV = 3;
+    auto set_variant = [&](int v) {
+        setenv("SUTA_HBX_T", variants[v][3] ? "1" : "0", 1);
+        suta_latch_switches();
+        gemm_set_variant(variants[v][0], variants[v][1]);
+    };
     __bf16* Cb;
     CK(hipMalloc(&Cb, (size_t)M * 4096 * 2));
     setenv("SUTA_HB8_PF", "0", 1);
@@ -67,7 +74,7 @@ int main(int argc, char** argv) {
         std::vector<float> ms[NV];
         for (int rd = 0; rd < rounds; ++rd)
             for (int v = 0; v < NV; ++v) {
-                gemm_set_variant(variants[v][0], variants[v][1]);
+                set_variant(v);
                 for (int w = 0; w < 2; ++w) gemm_launch(p, 0, nullptr, 0);
                 CK(hipEventRecord(e0, 0));
                 for (int r = 0; r < reps; ++r) gemm_launch(p, 0, nullptr, 0);
@@ -78,7 +85,7 @@ int main(int argc, char** argv) {
                 ms[v].push_back(t / reps);
             }
         for (int v = 0; v < NV; ++v) {
-            gemm_set_variant(variants[v][0], variants[v][1]);
+            set_variant(v);
             CK(hipMemset(C, 0, (size_t)M * s.N * 4));
             gemm_launch(p, 0, nullptr, 0);
             const int rstep = 97, rows = (M + rstep - 1) / rstep;
@@ -141,11 +148,11 @@ int main(int argc, char** argv) {
                 p.epi = EPI_DGELU;
                 p.aux = reinterpret_cast<const float*>(U); p.ldaux = 4096;
             }
-            const int evs[] = {0, 1, 2, 3};  // hb128, hb8, hbx32, hbx16
-            std::vector<float> ms[4];
+            const int evs[] = {0, 1, 2};
+            std::vector<float> ms[NV];
             for (int rd = 0; rd < rounds; ++rd)
                 for (int v : evs) {
-                    gemm_set_variant(variants[v][0], variants[v][1]);
+                    set_variant(v);
                     if (form == 0) hipLaunchKernelGGL(fillb, dim3((M * 4096L + 255) / 256), dim3(256), 0, 0, U, (long)M * 4096, 3u);
                     for (int w = 0; w < 2; ++w) gemm_launch(p, 0, nullptr, 0);
                     CK(hipEventRecord(e0, 0));
@@ -157,7 +164,7 @@ int main(int argc, char** argv) {
                     ms[v].push_back(tt / reps);
                 }
             for (int v : evs) {
-                gemm_set_variant(variants[v][0], variants[v][1]);
+                set_variant(v);
                 hipLaunchKernelGGL(fillb, dim3((M * 4096L + 255) / 256), dim3(256), 0, 0, U, (long)M * 4096, 3u);
                 gemm_launch(p, 0, nullptr, 0);
                 CK(hipDeviceSynchronize());

@@ -1,5 +1,6 @@
-# hbx integration: GEMM bench (main loop + epilogue shapes), parity tests (bitwise vs the 128 x 128 kernel, A&S GELU
-# vs erff, C4 bench layout census) and a same-box C4 A/B (SUTA_HBX=1 / 0, interleaved)
+# hbx integration: GEMM bench (main loop + epilogue shapes; hb128 / hbx column-per-lane / hbxT row-per-lane), parity
+# tests (bitwise vs the 128 x 128 kernel in both epilogue forms, A&S GELU vs erff, C4 bench layout census, flash
+# backward parity) and a same-box C4 A/B (SUTA_HBX_T=1 / 0, interleaved)
 set -e
 export TMPDIR=/tmp
 O=gpurun_out/r4hbxint
@@ -8,12 +9,12 @@ mkdir -p $O
 HB=$!
 trap "kill $HB" EXIT
 if [ -z "$NOBENCH" ]; then timeout -k 10 300 ./tools/hb_bench 10 3 > $O/hb_bench.log 2>&1 || { cat $O/hb_bench.log; exit 1; }; fi
-[ -n "$NOBENCH" ] || grep -E "hbx32|hb128" $O/hb_bench.log
-timeout -k 10 900 python -u -m pytest -x -v --timeout 500 --timeout-method thread tests/test_gpu_large_bf16.py::test_bf16_hbx_slice_ring_kernel_bitwise_equals_128_tile tests/test_gpu_large_bf16.py::test_bf16_epilogue_gelu_as_equals_erff tests/test_gpu_bench_scale.py::test_c4_bench_layout_bf16 > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
+[ -n "$NOBENCH" ] || grep -E "hbx|hb128" $O/hb_bench.log
+timeout -k 10 900 python -u -m pytest -x -v --timeout 500 --timeout-method thread tests/test_gpu_large_bf16.py tests/test_gpu_bench_scale.py::test_c4_bench_layout_bf16 ${EXTRA_TESTS} > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
 tail -3 $O/tests.log
 for i in 1 2; do
   for x in 1 0; do
-    SUTA_HBX=$x timeout -k 10 300 python bench.py --only-c4 --steps 4 > $O/c4_hbx$x.$i.json 2> $O/c4_hbx$x.$i.err
-    python -c "import json; d=json.load(open('$O/c4_hbx$x.$i.json')); print('hbx=$x', d['value'], d['roofline']['frac'], d['time_breakdown_ms']['gemm'])"
+    SUTA_HBX_T=$x timeout -k 10 300 python bench.py --only-c4 --steps 4 > $O/c4_t$x.$i.json 2> $O/c4_t$x.$i.err
+    python -c "import json; d=json.load(open('$O/c4_t$x.$i.json')); print('hbx_t=$x', d['value'], d['roofline']['frac'], d['time_breakdown_ms'])"
   done
 done
