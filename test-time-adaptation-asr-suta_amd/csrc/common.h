@@ -77,6 +77,7 @@ struct SutaSwitches {
                           // on full grids; 2: on every eligible bf16-plane linear (tests: small grids, edge tiles)
     int splitk;           // SUTA_SPLITK (default 1): split-K for small grids; 0 = never (tests comparing kernels
                           // bitwise: a split changes the k summation order)
+    int fused_delta;      // SUTA_FUSED_DELTA (default 1): the flash backward's delta in the dctx GEMM's epilogue
     int hbx_t;            // SUTA_HBX_T (default 1): gemm_hbx accumulates C^T fragments (row-per-lane epilogue, 16-B
                           // stores); 0 = the column-per-lane form shared with the 128 x 128 kernel
 };
@@ -153,6 +154,7 @@ enum {
     EPI_ACCUM = 32,
     EPI_SMBWD = 64,  // softmax backward: v = alpha * aux(m,n) * (acc - rowv[m])  (dS from dP, P, delta)
     EPI_ROWMASK = 128,  // ragged batch: rows >= zrows[z / zdiv] are stored as 0
+    EPI_DELTA = 256,    // flash-backward row term from the dctx GEMM (gemm_hbx C^T epilogue only): see GemmParams.dlt_o
 };
 
 struct GemmParams {
@@ -204,9 +206,19 @@ struct GemmParams {
     // internal: bf16-plane epilogues (Cb given) evaluate GELU / GELU' with gelu_fast / dgelu_fast (SUTA_FAST_GELU=0:
     // erff, for A/B runs)
     int fgelu;
+    // EPI_DELTA: delta[(b * dNH + head) * dT + t] = sum_d C(row, 64 head + d) * O(row, 64 head + d), row = b * dT + t,
+    // O = dlt_o (fp32 [M][ldo], the attention forward's ctx), C = the epilogue's final value (dctx): the softmax
+    // backward's row term, summed in the order of ops.hip attn_delta_kernel (bitwise the same delta)
+    const float* dlt_o;
+    long ldo;
+    float* delta;
+    int dT, dNH;
 };
 
 void gemm_init(GemmParams& p);
+// whether gemm_launch(p) takes the 256 x 256 bf16-plane kernel with its C^T epilogue (the one that carries EPI_DELTA);
+// p as it will be launched (planes routed)
+bool gemm_hbx_t_selected(const GemmParams& p);
 // Launch; ws/ws_floats: scratch for split-K (may be null -> no split).
 void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats);
 // Benchmark/test override: tile (-1 auto, 0 128x128, 1 128x64, 2 64x128, 3 64x64), LDS buffers (1|2).

@@ -153,6 +153,7 @@ double gemm_alg_bytes(const GemmParams& p, bool a_fp32 = false) {
     if (p.epi & EPI_RESID) c += 4.0 * mn;
     if (p.epi & EPI_DGELU) c += epre * mn;
     if (p.epi & EPI_SMBWD) c += 4.0 * mn;
+    if (p.epi & EPI_DELTA) c += 4.0 * mn + 4.0 * (double)p.M * p.dNH;  // O read, delta written
     bytes += c * p.Z;
     return bytes;
 }
@@ -428,6 +429,18 @@ struct suta_engine {
         return reinterpret_cast<char*>(qkvplanes.p) + l * per;
     }
     void build_weight_planes();
+    // whether gemm(p0) takes the 256 x 256 bf16-plane kernel's C^T epilogue (the producer's A plane given, B a frozen
+    // weight with planes): the condition for fusing EPI_DELTA into it
+    bool routes_to_hbx_t(const GemmParams& p0) {
+        if (gemm_mode != SUTA_PRECISION_BF16 || !p0.Ab || p0.segK != 0 || p0.ta || p0.Z != 1 || p0.K % 8) return false;
+        auto it = wplanes.find(p0.B);
+        if (it == wplanes.end() || !(p0.tb ? p0.ldb == p0.K : p0.ldb == p0.N)) return false;
+        GemmParams p = p0;
+        p.mode = gemm_mode;
+        p.Bb = p.tb ? it->second.first : it->second.second;
+        p.ldbb = p.K;
+        return gemm_hbx_t_selected(p);
+    }
     void gemm(const GemmParams& p0) {
         GemmParams p = p0;
         p.mode = gemm_mode;
@@ -1161,9 +1174,42 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
         void* dctxp = (pl.flash && P0) ? plane(2) : nullptr;   // dO plane of the flash backward
         void* qkvp = (pl.flash && P0) ? qkv_plane(l) : nullptr;
         if (!qkvp) dctxp = nullptr;
-        nn_gemm(dhres, H, wo[l], H, pl.ctx, H, (int)BT, H, H, 0, nullptr, 0, nullptr, 0, P0, dctxp);
-        // softmax-backward row term delta = rowsum(dctx * ctx) per head, fused into the dP epilogue
-        timed(F_SOFTMAX, [&] { launch_attn_delta(pl.ctx, lb.ctx, pl.delta, B, T, NH, d, st); });
+        // softmax-backward row term delta = rowsum(dctx * ctx) per head: in the dctx GEMM's epilogue when it takes the
+        // C^T-epilogue kernel and the flash backward reads the dctx plane (the fp32 dctx is then not written), else a
+        // separate pass over the fp32 dctx
+        bool delta_fused = false;
+        if (pl.flash && dctxp && d == 64 && suta_switches().fused_delta &&
+            flash_bwd_reads_planes(gemm_mode == SUTA_PRECISION_BF16, qkvp, dctxp, H)) {
+            GemmParams g;
+            gemm_init(g);
+            g.A = dhres;
+            g.lda = H;
+            g.Ab = P0;
+            g.ldab = H;
+            g.Cb = dctxp;
+            g.ldcb = H;
+            g.B = wo[l];
+            g.ldb = H;
+            g.C = nullptr;
+            g.ldc = H;
+            g.M = (int)BT;
+            g.N = H;
+            g.K = H;
+            g.epi = EPI_DELTA;
+            g.dlt_o = lb.ctx;
+            g.ldo = H;
+            g.delta = pl.delta;
+            g.dT = T;
+            g.dNH = NH;
+            if (routes_to_hbx_t(g)) {
+                gemm(g);
+                delta_fused = true;
+            }
+        }
+        if (!delta_fused) {
+            nn_gemm(dhres, H, wo[l], H, pl.ctx, H, (int)BT, H, H, 0, nullptr, 0, nullptr, 0, P0, dctxp);
+            timed(F_SOFTMAX, [&] { launch_attn_delta(pl.ctx, lb.ctx, pl.delta, B, T, NH, d, st); });
+        }
         // flash backward: P recomputed from the LSE, dQ, dK, dV into dqkv (else the GEMM path below)
         const bool fused_bwd = pl.flash;
         // with bf16 planes the QKV input-gradient GEMM reads only dqkv's bf16 plane: the fp32 copy is not written

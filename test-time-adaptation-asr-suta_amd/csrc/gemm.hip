@@ -209,6 +209,29 @@ static bool use_hbx(const GemmParams& p) {
     return (long)((p.M + 255) / 256) * ((p.N + 255) / 256) >= 256;
 }
 
+// 32-bit epilogue offsets: M x ld elements of every operand the epilogue touches within 4 GiB
+// (SUTA_EPI_FAST=0: the general epilogue everywhere, for A/B runs)
+static int epilogue_off32(const GemmParams& p) {
+    static int fast = -1;
+    if (fast < 0) {
+        const char* ev = std::getenv("SUTA_EPI_FAST");
+        fast = (ev && atoi(ev) == 0) ? 0 : 1;
+    }
+    const double lim = 4294967295.0 - 1024.0;
+    auto fits = [&](long ld, double esz) { return (double)p.M * (double)std::max(ld, (long)p.N) * esz < lim; };
+    return fits(p.ldc, 4) && (!(p.epi & EPI_RESID) || fits(p.ldr, 4)) &&
+           (!(p.epi & (EPI_DGELU | EPI_SMBWD)) || fits(p.ldaux, 4)) && (!(p.epi & EPI_STORE_PRE) || fits(p.ldc2, 4)) &&
+           (!(p.epi & EPI_DELTA) || fits(p.ldo, 4)) && (!p.Cb || fits(p.ldcb, 2)) && p.ldc >= 0 && p.ldr >= 0 &&
+           p.ldaux >= 0 && p.ldc2 >= 0 && p.ldcb >= 0 && p.ldo >= 0 && fast;
+}
+
+bool gemm_hbx_t_selected(const GemmParams& p0) {
+    GemmParams p = p0;
+    p.off32 = epilogue_off32(p);
+    const bool hb = p.mode == 2 && p.Ab && p.Bb && !p.ta && p.segK == 0;
+    return hb && g_force_tile < 0 && !use_hb8(p) && use_hbx(p) && suta_switches().hbx_t && hbx_t_ok(p, true);
+}
+
 void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
     if (p.M <= 0 || p.N <= 0 || p.Z <= 0) return;
     const int second = ((p.epi & EPI_RESID) != 0) + ((p.epi & EPI_ACCUM) != 0) + ((p.epi & EPI_SMBWD) != 0);
@@ -272,20 +295,9 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
     if (splits > 1) splits = (p.K + p.kchunk - 1) / p.kchunk;
     p.splits = splits;
     p.ws = ws;
-    {  // 32-bit epilogue offsets: M x ld elements of every operand the epilogue touches within 4 GiB
-       // (SUTA_EPI_FAST=0: the general epilogue everywhere, for A/B runs)
-        static int fast = -1;
-        if (fast < 0) {
-            const char* ev = std::getenv("SUTA_EPI_FAST");
-            fast = (ev && atoi(ev) == 0) ? 0 : 1;
-        }
-        const double lim = 4294967295.0 - 1024.0;
-        auto fits = [&](long ld, double esz) { return (double)p.M * (double)std::max(ld, (long)p.N) * esz < lim; };
-        p.off32 = fits(p.ldc, 4) && (!(p.epi & EPI_RESID) || fits(p.ldr, 4)) &&
-                  (!(p.epi & (EPI_DGELU | EPI_SMBWD)) || fits(p.ldaux, 4)) && (!(p.epi & EPI_STORE_PRE) || fits(p.ldc2, 4)) &&
-                  (!p.Cb || fits(p.ldcb, 2)) && p.ldc >= 0 && p.ldr >= 0 && p.ldaux >= 0 && p.ldc2 >= 0 && p.ldcb >= 0 &&
-                  fast;
-    }
+    p.off32 = epilogue_off32(p);
+    if ((p.epi & EPI_DELTA) && !(tile == 8 && suta_switches().hbx_t && hbx_t_ok(p, true)))
+        throw std::invalid_argument("gemm: EPI_DELTA needs the 256 x 256 bf16-plane kernel's C^T epilogue (gemm_hbx_t_selected)");
     {
         static int ord = -1;  // SUTA_GEMM_ORDER=1: m-fastest; =G >= 2: bands of G tile rows (A/B runs)
         if (ord < 0) {

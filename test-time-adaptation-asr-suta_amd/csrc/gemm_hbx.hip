@@ -316,6 +316,7 @@ __device__ __forceinline__ void epilogue_t(const GemmParams& p, const f32x16 (&a
         const long rowc = min(row, p.M - 1);
         const bool rok = row < p.M;
         const bool zero = (e & EPI_ROWMASK) && row >= rlim;
+        float sg[4];  // EPI_DELTA: the lane's 4-column dot products, summed over j (attn_delta_kernel's first level)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -395,6 +396,14 @@ __device__ __forceinline__ void epilogue_t(const GemmParams& p, const f32x16 (&a
 #pragma unroll
                     for (int r = 0; r < 8; ++r) v[r] = 0.f;
                 }
+                if (e & EPI_DELTA) {
+#pragma unroll
+                    for (int t = 0; t < 2; ++t) {
+                        const f32x4 o = *reinterpret_cast<const f32x4*>(p.dlt_o + rowc * p.ldo + nb + 8 * t + 4 * h);
+                        const float d4 = fmaf(v[4 * t + 3], o[3], fmaf(v[4 * t + 2], o[2], fmaf(v[4 * t + 1], o[1], v[4 * t] * o[0])));
+                        sg[2 * q + t] = j == 0 ? d4 : sg[2 * q + t] + d4;
+                    }
+                }
                 if ((!CB || p.C) && rok) {
 #pragma unroll
                     for (int t = 0; t < 2; ++t)
@@ -403,6 +412,16 @@ __device__ __forceinline__ void epilogue_t(const GemmParams& p, const f32x16 (&a
                 }
                 if (CB) store_bf16(reinterpret_cast<__bf16*>(p.Cb) + (long)row * p.ldcb + nb + 8 * h, v, rok);
             }
+        if (e & EPI_DELTA) {
+            // the head is the wave's 64 columns; attn_delta_kernel's xor tree over its 16 four-column groups
+            // (d / 4 = 8 j + 2 g + h: levels j, g >> 1, g & 1, then the half-wave h)
+            const float l2 = (sg[0] + sg[2]) + (sg[1] + sg[3]);
+            const float other = __shfl_xor(l2, 32, 64);
+            if (h == 0 && rok) {
+                const int b = row / p.dT, t = row - b * p.dT;
+                p.delta[((long)b * p.dNH + cbase / 64) * p.dT + t] = l2 + other;
+            }
+        }
     }
 }
 
@@ -546,6 +565,9 @@ bool hbx_t_ok(const GemmParams& p, bool check_off32) {
     const bool preb = p.Cb && p.preb;
     if ((e & EPI_DGELU) && !(a16(p.aux) && p.ldaux % (preb ? 8 : 4) == 0)) return false;
     if ((e & EPI_STORE_PRE) && !(a16(p.C2) && p.ldc2 % (preb ? 8 : 4) == 0)) return false;
+    if ((e & EPI_DELTA) && !(e == EPI_DELTA && a16(p.dlt_o) && p.ldo % 4 == 0 && p.delta && p.dT > 0 &&
+                             (long)p.dNH * 64 == p.N && p.M % p.dT == 0))
+        return false;
     return true;
 }
 
@@ -556,6 +578,7 @@ namespace {
 constexpr int XEM_A = EPI_BIAS | EPI_RESID | EPI_ROWMASK;
 constexpr int XEM_G = EPI_BIAS | EPI_GELU | EPI_STORE_PRE | EPI_ROWMASK;
 constexpr int XEM_D = EPI_DGELU | EPI_ROWMASK;
+constexpr int XEM_L = EPI_DELTA;  // the attention out-projection's input gradient with the flash backward's delta
 
 }  // namespace
 
@@ -565,6 +588,8 @@ void gemm_run_hbx(int variant, const GemmParams& p, dim3 grid, hipStream_t st) {
     const int e = p.epi;
     if (p.splits > 1 || p.Z != 1 || (e & (EPI_ACCUM | EPI_SMBWD)))
         throw std::invalid_argument("hbx: no split-K, batches, ACCUM or SMBWD");
+    if ((e & EPI_DELTA) && !(variant == 1 && suta_switches().hbx_t && hbx_t_ok(p, true)))
+        throw std::invalid_argument("hbx: EPI_DELTA needs the C^T epilogue and its operand conditions");
     if (variant == 2) {
         if ((e & ~XEM_A) == 0) launch_hbx_em<16, XEM_A>(p, grid, st);
         else if ((e & ~XEM_G) == 0) launch_hbx_em<16, XEM_G>(p, grid, st);
@@ -573,6 +598,7 @@ void gemm_run_hbx(int variant, const GemmParams& p, dim3 grid, hipStream_t st) {
         return;
     }
     if (suta_switches().hbx_t && hbx_t_ok(p, true)) {  // C^T accumulators, row-per-lane 16-B epilogue
+        if (e == XEM_L) return launch_hbx_em<32, XEM_L, true>(p, grid, st);
         if ((e & ~XEM_A) == 0) return launch_hbx_em<32, XEM_A, true>(p, grid, st);
         if ((e & ~XEM_G) == 0) return launch_hbx_em<32, XEM_G, true>(p, grid, st);
         if ((e & ~XEM_D) == 0) return launch_hbx_em<32, XEM_D, true>(p, grid, st);

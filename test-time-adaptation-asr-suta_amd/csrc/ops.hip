@@ -1085,7 +1085,7 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const f32x4* __restrict
     float s = 0.f;
     if (item < items) {
         const f32x4 a = dO[g], c = O[g];
-        s = a[0] * c[0] + a[1] * c[1] + a[2] * c[2] + a[3] * c[3];
+        s = fmaf(a[3], c[3], fmaf(a[2], c[2], fmaf(a[1], c[1], a[0] * c[0])));  // (gemm_hbx's EPI_DELTA: same order)
     }
 #pragma unroll
     for (int o = G / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
@@ -1824,6 +1824,7 @@ void suta_latch_switches() {
     s.hbx = hbx ? atoi(hbx) : 1;
     s.splitk = on("SUTA_SPLITK");
     s.hbx_t = on("SUTA_HBX_T");
+    s.fused_delta = on("SUTA_FUSED_DELTA");
     const char* hb8 = std::getenv("SUTA_HB8");
     s.hb8 = hb8 ? atoi(hb8) : 0;
     const char* fnw = std::getenv("SUTA_FLASH_FWD_NW");

@@ -255,6 +255,31 @@ def test_bf16_hbx_slice_ring_kernel_bitwise_equals_128_tile(monkeypatch):
             assert np.array_equal(v, params["01"][n]), (key, n)
 
 
+def test_bf16_fused_delta_bitwise_equals_separate_pass(monkeypatch):
+    """The flash backward's row term delta = rowsum(dctx * ctx) computed in the dctx GEMM's C^T epilogue (EPI_DELTA,
+    gemm_hbx; the fp32 dctx is then not written) against the separate attn_delta_kernel pass (SUTA_FUSED_DELTA=0):
+    the epilogue sums in the kernel's order (4-column fma dots, then its xor tree), so logits and adapted tensors are
+    bitwise equal.  wav2vec2-large in bf16 mode on a ragged pair, hbx forced on the small grid (SUTA_HBX=2)."""
+    monkeypatch.setenv("SUTA_SPLITK", "0")
+    monkeypatch.setenv("SUTA_HBX", "2")
+    cfg = get_config("wav2vec2-large")
+    sd = synth_weights(cfg)
+    waves = [synth.wave(32000, 86), synth.wave(20000, 87)]
+    out, params = {}, {}
+    for fd in ("1", "0"):
+        monkeypatch.setenv("SUTA_FUSED_DELTA", fd)
+        eng = SutaEngine(cfg, sd, max_batch=2, max_samples=32000)
+        eng.set_precision("bf16")
+        out[fd], _, _ = eng.adapt_varlen(waves, 3, SutaHParams(), record=[0, 3])
+        params[fd] = {n: eng.get_param(1, n) for n in eng.trainable_names()}
+        eng.close()
+    for r in (0, 3):
+        for u in range(2):
+            assert np.array_equal(out["1"][r][u], out["0"][r][u]), (r, u)
+    for n, v in params["1"].items():
+        assert np.array_equal(v, params["0"][n]), n
+
+
 def test_bf16_epilogue_gelu_as_equals_erff(monkeypatch):
     """The bf16-plane GEMM epilogues' GELU / GELU' (common.h gelu2_bf16ep / dgelu2_bf16ep: Abramowitz & Stegun 7.1.28
     erf, |error| <= 3e-7, packed fp32, default) against erff (SUTA_FAST_GELU=0), wav2vec2-large in bf16 mode: the
