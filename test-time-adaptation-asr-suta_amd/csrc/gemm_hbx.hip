@@ -291,24 +291,59 @@ __device__ __forceinline__ void epilogue_t_edge(const GemmParams& p, const f32x1
     }
 }
 
-template <bool CB, int EM>
+// ST (staged): the 32-row band i of each output plane goes through a wave-private LDS image (the slice ring, free
+// after the main loop) and leaves in full 128-B lines: 16-B chunks written per lane as the fragments hold them
+// (chunk c of row r in slot c ^ (r & 7): conflict-free ds_write_b128 / ds_read_b128), read back row-contiguous
+// (8 lanes = one 128-B bf16 row of the wave tile, 16 lanes = one 256-B fp32 row) and stored with every lane of an
+// instruction in 8 whole lines.  Without ST a store instruction touches 32 rows.
+template <bool CB, int EM, bool ST>
 __device__ __forceinline__ void epilogue_t(const GemmParams& p, const f32x16 (&acc)[4][2], int rbase, int cbase,
-                                           int lane) {
+                                           int lane, char* stage) {
     if (cbase + 64 > p.N) {
         epilogue_t_edge<CB, EM>(p, acc, rbase, cbase, lane);
         return;
     }
+    // staging images per wave (bytes): bf16 pre-activation 4 KB, fp32 C 8 KB, bf16 C plane 4 KB
+    char* const s_pre = stage;
+    char* const s_c32 = stage + 4096;
+    char* const s_cb = stage + 12288;
+    const bool st_pre = ST && (p.epi & EM & EPI_STORE_PRE) && CB && p.preb;
+    const bool st_c32 = ST && (!CB || p.C);
     const int e = p.epi & EM;
     const int h = lane >> 5, l32 = lane & 31;
     const float alpha = p.alpha;
     const int rlim = (e & EPI_ROWMASK) ? p.zrows[0] : 0x7fffffff;
     const bool preb = CB && p.preb;
-    // one bf16 plane's 8 values of runs (2q, 2q + 1) as one 16-B chunk per lane
-    auto store_bf16 = [&](__bf16* d, const float* v, bool rok) {
+    // one bf16 plane's 8 values of runs (2q, 2q + 1) as one 16-B chunk per lane: to global (d) or to the staging
+    // image (img, chunk c of row l32)
+    auto store_bf16 = [&](__bf16* d, const float* v, bool rok, char* img, int c) {
         unsigned x0 = pack_bf16x2(v[0], v[1]), y0 = pack_bf16x2(v[2], v[3]);
         unsigned x1 = pack_bf16x2(v[4], v[5]), y1 = pack_bf16x2(v[6], v[7]);
         swap_runs(x0, y0, x1, y1);
-        if (rok) *reinterpret_cast<u32x4v*>(d) = u32x4v{x0, y0, x1, y1};
+        if (img) *reinterpret_cast<u32x4v*>(img + l32 * 128 + ((c ^ (l32 & 7)) << 4)) = u32x4v{x0, y0, x1, y1};
+        else if (rok) *reinterpret_cast<u32x4v*>(d) = u32x4v{x0, y0, x1, y1};
+    };
+    // staged band i -> global: bf16 images 4 rows... 8 rows x 128 B per instruction, fp32 4 rows x 256 B
+    auto flush_bf16 = [&](const char* img, __bf16* base, long ld, int row0) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int r = 8 * k + (lane >> 3), c = lane & 7;
+            const u32x4v w = *reinterpret_cast<const u32x4v*>(img + r * 128 + ((c ^ (r & 7)) << 4));
+            if (row0 + r < p.M) *reinterpret_cast<u32x4v*>(base + (long)(row0 + r) * ld + cbase + 8 * c) = w;
+        }
+    };
+    auto flush_f32 = [&](const char* img, float* base, long ld, int row0) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int r = 4 * k + (lane >> 4), c = lane & 15;
+            const f32x4 w = *reinterpret_cast<const f32x4*>(img + r * 256 + ((c ^ (r & 7)) << 4));
+            if (row0 + r < p.M) *reinterpret_cast<f32x4*>(base + (long)(row0 + r) * ld + cbase + 4 * c) = w;
+        }
+    };
+    auto wave_sync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -359,7 +394,9 @@ __device__ __forceinline__ void epilogue_t(const GemmParams& p, const f32x16 (&a
                     }
                 }
                 if (e & EPI_STORE_PRE) {
-                    if (preb) store_bf16(reinterpret_cast<__bf16*>(p.C2) + (long)row * p.ldc2 + nb + 8 * h, v, rok);
+                    if (preb)
+                        store_bf16(reinterpret_cast<__bf16*>(p.C2) + (long)row * p.ldc2 + nb + 8 * h, v, rok,
+                                   st_pre ? s_pre : nullptr, 4 * j + 2 * q + h);
                     else if (rok)
 #pragma unroll
                         for (int t = 0; t < 2; ++t)
@@ -404,14 +441,31 @@ __device__ __forceinline__ void epilogue_t(const GemmParams& p, const f32x16 (&a
                         sg[2 * q + t] = j == 0 ? d4 : sg[2 * q + t] + d4;
                     }
                 }
-                if ((!CB || p.C) && rok) {
+                if (st_c32) {
+#pragma unroll
+                    for (int t = 0; t < 2; ++t) {
+                        const int c = 8 * j + 4 * q + 2 * t + h;  // 16-B chunk of the 256-B fp32 row
+                        *reinterpret_cast<f32x4*>(s_c32 + l32 * 256 + ((c ^ (l32 & 7)) << 4)) =
+                            f32x4{v[4 * t], v[4 * t + 1], v[4 * t + 2], v[4 * t + 3]};
+                    }
+                } else if ((!CB || p.C) && rok) {
 #pragma unroll
                     for (int t = 0; t < 2; ++t)
                         *reinterpret_cast<f32x4*>(p.C + (long)row * p.ldc + nb + 8 * t + 4 * h) =
                             f32x4{v[4 * t], v[4 * t + 1], v[4 * t + 2], v[4 * t + 3]};
                 }
-                if (CB) store_bf16(reinterpret_cast<__bf16*>(p.Cb) + (long)row * p.ldcb + nb + 8 * h, v, rok);
+                if (CB)
+                    store_bf16(reinterpret_cast<__bf16*>(p.Cb) + (long)row * p.ldcb + nb + 8 * h, v, rok,
+                               ST ? s_cb : nullptr, 4 * j + 2 * q + h);
             }
+        if constexpr (ST) {
+            wave_sync();
+            const int row0 = rbase + 32 * i;
+            if (st_pre) flush_bf16(s_pre, reinterpret_cast<__bf16*>(p.C2), p.ldc2, row0);
+            if (st_c32) flush_f32(s_c32, p.C, p.ldc, row0);
+            if (CB) flush_bf16(s_cb, reinterpret_cast<__bf16*>(p.Cb), p.ldcb, row0);
+            wave_sync();
+        }
         if (e & EPI_DELTA) {
             // the head is the wave's 64 columns; attn_delta_kernel's xor tree over its 16 four-column groups
             // (d / 4 = 8 j + 2 g + h: levels j, g >> 1, g & 1, then the half-wave h)
@@ -425,7 +479,7 @@ __device__ __forceinline__ void epilogue_t(const GemmParams& p, const f32x16 (&a
     }
 }
 
-template <int MS, bool CB, int EM, bool TR>
+template <int MS, bool CB, int EM, int TR>
 __global__ __launch_bounds__(512, 1) void gemm_hbx_kernel(GemmParams p) {
     __shared__ __attribute__((aligned(16))) float smem[X_NR * X_SLOT];
     const TileId tid = xcd_tile(p.order);
@@ -529,8 +583,13 @@ __global__ __launch_bounds__(512, 1) void gemm_hbx_kernel(GemmParams p) {
     wait_vm<0>();
 
     const bool interior = m0 + X_BM <= p.M && n0 + X_BN <= p.N;
-    if constexpr (TR) {
-        epilogue_t<CB, EM>(p, reinterpret_cast<const f32x16(&)[4][2]>(acc[0]), m0 + wr * 128, n0 + wc * 64, lane);
+    if constexpr (TR == 2) {
+        __syncthreads();  // every wave is done with the ring: wave-private 16-KB staging images
+        epilogue_t<CB, EM, true>(p, reinterpret_cast<const f32x16(&)[4][2]>(acc[0]), m0 + wr * 128, n0 + wc * 64, lane,
+                                 reinterpret_cast<char*>(smem) + wid * 16384);
+    } else if constexpr (TR == 1) {
+        epilogue_t<CB, EM, false>(p, reinterpret_cast<const f32x16(&)[4][2]>(acc[0]), m0 + wr * 128, n0 + wc * 64, lane,
+                                  nullptr);
     } else if constexpr (MS == 32) {
         gemm_epilogue<2, 2, CB, EM>(p, reinterpret_cast<const f32x16(&)[2][2]>(acc[0]), 0, 0, m0 + wr * 128,
                                     n0 + wc * 64, h, l32, interior, tid.z);
@@ -545,7 +604,7 @@ __global__ __launch_bounds__(512, 1) void gemm_hbx_kernel(GemmParams p) {
     }
 }
 
-template <int MS, int EM, bool TR = false>
+template <int MS, int EM, int TR = 0>
 void launch_hbx_em(const GemmParams& p, dim3 grid, hipStream_t st) {
     if (p.Cb) hipLaunchKernelGGL((gemm_hbx_kernel<MS, true, EM, TR>), grid, dim3(512), 0, st, p);
     else hipLaunchKernelGGL((gemm_hbx_kernel<MS, false, EM, TR>), grid, dim3(512), 0, st, p);
@@ -597,11 +656,18 @@ void gemm_run_hbx(int variant, const GemmParams& p, dim3 grid, hipStream_t st) {
         else throw std::invalid_argument("hbx 16x16: epilogue flags outside the linears' classes");
         return;
     }
-    if (suta_switches().hbx_t && hbx_t_ok(p, true)) {  // C^T accumulators, row-per-lane 16-B epilogue
-        if (e == XEM_L) return launch_hbx_em<32, XEM_L, true>(p, grid, st);
-        if ((e & ~XEM_A) == 0) return launch_hbx_em<32, XEM_A, true>(p, grid, st);
-        if ((e & ~XEM_G) == 0) return launch_hbx_em<32, XEM_G, true>(p, grid, st);
-        if ((e & ~XEM_D) == 0) return launch_hbx_em<32, XEM_D, true>(p, grid, st);
+    const int tr = suta_switches().hbx_t;
+    if (tr && hbx_t_ok(p, true)) {  // C^T accumulators, row-per-lane epilogue (2: LDS-staged whole-line stores)
+        if (tr == 2) {
+            if (e == XEM_L) return launch_hbx_em<32, XEM_L, 2>(p, grid, st);
+            if ((e & ~XEM_A) == 0) return launch_hbx_em<32, XEM_A, 2>(p, grid, st);
+            if ((e & ~XEM_G) == 0) return launch_hbx_em<32, XEM_G, 2>(p, grid, st);
+            if ((e & ~XEM_D) == 0) return launch_hbx_em<32, XEM_D, 2>(p, grid, st);
+        }
+        if (e == XEM_L) return launch_hbx_em<32, XEM_L, 1>(p, grid, st);
+        if ((e & ~XEM_A) == 0) return launch_hbx_em<32, XEM_A, 1>(p, grid, st);
+        if ((e & ~XEM_G) == 0) return launch_hbx_em<32, XEM_G, 1>(p, grid, st);
+        if ((e & ~XEM_D) == 0) return launch_hbx_em<32, XEM_D, 1>(p, grid, st);
     }
     if ((e & ~XEM_A) == 0) launch_hbx_em<32, XEM_A>(p, grid, st);
     else if ((e & ~XEM_G) == 0) launch_hbx_em<32, XEM_G>(p, grid, st);

@@ -1823,7 +1823,8 @@ void suta_latch_switches() {
     const char* hbx = std::getenv("SUTA_HBX");
     s.hbx = hbx ? atoi(hbx) : 1;
     s.splitk = on("SUTA_SPLITK");
-    s.hbx_t = on("SUTA_HBX_T");
+    const char* hbxt = std::getenv("SUTA_HBX_T");
+    s.hbx_t = hbxt ? std::min(2, std::max(0, atoi(hbxt))) : 1;
     s.fused_delta = on("SUTA_FUSED_DELTA");
     const char* hb8 = std::getenv("SUTA_HB8");
     s.hb8 = hb8 ? atoi(hb8) : 0;

@@ -155,10 +155,11 @@ def test_c4_bench_layout_bf16():
     against the exact-fp32 engine adapting each utterance alone (bf16 tolerance of tests/parity.py: 2.5 % of
     max|ref|, greedy ids on >= 97 % of frames) at steps 0 / 1 / 5 / 20, and slot 0 against the CPU oracle at steps 0
     and 20.  The launch census of the capturing call shows the schedules this layout reaches: the linears on
-    the bf16-plane kernel (hb) over ceil(B x 399 / 128) row tiles, the conv stack's per-utterance (Z = B) GEMMs on
+    the bf16-plane kernels, the conv stack's per-utterance (Z = B) GEMMs on
     bf16 planes -- forward and input gradients (conv-A rows, per-tap weight segments) on hb, weight gradients on the
-    MN-contiguous hbt kernel -- and the per-utterance feature-projection weight gradient.  The plain-epilogue linears
-    run on the 256 x 256 slice-ring kernel (hbx) over ceil(B x 399 / 256) row tiles.
+    MN-contiguous hbt kernel -- and the per-utterance feature-projection weight gradient.  The linears run on the
+    256 x 256 slice-ring kernel (hbx) over ceil(B x 399 / 256) row tiles, the K = 32 lm_head input gradient on the
+    128 x 128 one over ceil(B x 399 / 128).
     Reference main.py:181,205 (forward and backward through the encoder)."""
     from oracle import w2v2_cpu as W
     import os
@@ -183,13 +184,13 @@ def test_c4_bench_layout_bf16():
     print(txt)
     gy = _row_tiles(B, T)
     z = f" z={B} "
-    # plain-epilogue linears on the 256 x 256 slice-ring kernel: N = 1024 (out-proj, FFN2, input gradients), 3072 (QKV)
-    for gx in (4, 12):
+    # the linears on the 256 x 256 slice-ring kernel: N = 1024 (out-proj, FFN2, input gradients), 3072 (QKV), 4096
+    # (the GELU / GELU' linears FFN1 and the FFN2 input gradient, through the C^T epilogue)
+    for gx in (4, 12, 16):
         assert any(k.startswith("grid hbx 256x256 ") and f" gx={gx} gy={_row_tiles(B, T, 256)} z=1 " in k
                    for k in census), (gx, txt)
-    # the GELU / GELU' linears (FFN1 forward, FFN2 input gradient: N = 4096) on the 128 x 128 kernel
-    assert any(k.startswith("grid hb 128x128 ") and f" gx=32 gy={gy} z=1 " in k for k in census), (gy, txt)
-    assert any(k.startswith("hb ") and " z=1 " in k for k in census), txt
+    # the K = 32 lm_head input gradient (below hbx's K >= 128) on the 128 x 128 kernel
+    assert any(k.startswith("grid hb 128x128 ") and f" gx=8 gy={gy} z=1 " in k for k in census), (gy, txt)
     assert any(k.startswith("hb 128x128" + z) and k.endswith(" conv-seg") for k in census), txt   # conv dX
     assert any(k.startswith("hb ") and z in k and "conv" not in k for k in census), txt     # conv forward
     assert any(k.startswith("hbt ") and z in k for k in census), txt                        # conv dW

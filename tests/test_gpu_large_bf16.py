@@ -218,8 +218,9 @@ def test_bf16_hb8_pingpong_kernel(monkeypatch):
 def test_bf16_hbx_slice_ring_kernel_bitwise_equals_128_tile(monkeypatch):
     """gemm_hbx_kernel (256 x 256 tile, 32-deep slice ring, v_mfma_f32_32x32x16_bf16) forced on every bf16-plane linear
     (SUTA_HBX=2: every epilogue class -- bias / residual, bias + GELU + bf16 pre-activation, GELU' -- small grids and
-    edge tiles of a ragged pair: 198 and 124 rows of a 256-row tile), in both epilogue forms (SUTA_HBX_T=1: C^T
-    accumulators, row-per-lane 16-B stores; 0: the column-per-lane form), against the 128 x 128 kernel (SUTA_HBX=0),
+    edge tiles of a ragged pair: 198 and 124 rows of a 256-row tile), in every epilogue form (SUTA_HBX_T=1: C^T
+    accumulators, row-per-lane 16-B stores; 2: the same staged through LDS into whole-line stores; 0: the
+    column-per-lane form), against the 128 x 128 kernel (SUTA_HBX=0),
     all without split-K (SUTA_SPLITK=0: a split sums k in another order): the same MFMA products in the same k order, so
     logits and adapted tensors are bitwise equal; and the large model's 20-step SUTA against the reference goldens g7
     (bf16 tolerance).  Reference main.py:181,205."""
@@ -230,7 +231,7 @@ def test_bf16_hbx_slice_ring_kernel_bitwise_equals_128_tile(monkeypatch):
     steps = [int(s) for s in z["steps"]]
     waves = [synth.wave(32000, 82), synth.wave(20000, 83)]
     out, params = {}, {}
-    for mode, tr in (("0", "1"), ("2", "1"), ("2", "0")):
+    for mode, tr in (("0", "1"), ("2", "1"), ("2", "2"), ("2", "0")):
         monkeypatch.setenv("SUTA_HBX", mode)
         monkeypatch.setenv("SUTA_HBX_T", tr)
         eng = SutaEngine(cfg, sd, max_batch=2, max_samples=32000)
@@ -247,7 +248,7 @@ def test_bf16_hbx_slice_ring_kernel_bitwise_equals_128_tile(monkeypatch):
         out[key], _, _ = eng.adapt_varlen(waves, 3, SutaHParams(), record=[0, 3])
         params[key] = {n: eng.get_param(1, n) for n in eng.trainable_names()}
         eng.close()
-    for key in ("21", "20"):
+    for key in ("21", "22", "20"):
         for r in (0, 3):
             for u in range(2):
                 assert np.array_equal(out[key][r][u], out["01"][r][u]), (key, r, u)

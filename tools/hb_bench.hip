@@ -50,11 +50,12 @@ int main(int argc, char** argv) {
     CK(hipEventCreate(&e1));
     // (tile, ns, cb-capable, SUTA_HBX_T): 0 = hb 128 x 128, 8 = hbx (32x32x16) with the column-per-lane epilogue
     // and with C^T accumulators + the row-per-lane epilogue (hbxT)
-    const int variants[][4] = {{0, 2, 1, 0}, {8, 2, 1, 0}, {8, 2, 1, 1}};
-    const char* vname[] = {"hb128", "hbx32", "hbxT "};
-    constexpr int NV = 3;
+    const int variants[][4] = {{0, 2, 1, 0}, {8, 2, 1, 0}, {8, 2, 1, 1}, {8, 2, 1, 2}};
+    const char* vname[] = {"hb128", "hbx32", "hbxT ", "hbxTS"};
+    constexpr int NV = 4;
     auto set_variant = [&](int v) {
-        setenv("SUTA_HBX_T", variants[v][3] ? "1" : "0", 1);
+        const char* tv[] = {"0", "1", "2"};
+        setenv("SUTA_HBX_T", tv[variants[v][3]], 1);
         suta_latch_switches();
         gemm_set_variant(variants[v][0], variants[v][1]);
     };
@@ -129,7 +130,11 @@ int main(int argc, char** argv) {
         std::vector<float> hbias(4096);
         for (int i = 0; i < 4096; ++i) hbias[i] = 0.01f * (i % 17) - 0.08f;
         CK(hipMemcpy(bias, hbias.data(), 4096 * 4, hipMemcpyHostToDevice));
-        for (int form = 0; form < 2; ++form) {
+        // forms: 0 FFN1 (bias + GELU + bf16 pre), 1 FFN2 input gradient (x GELU'(u)), 2 FFN1 without the GELU
+        // (bias + bf16 pre: the GELU's own cost), 3 no epilogue, bf16 C plane only (C dead: the QKV / FFN1 form)
+        const char* fname[] = {"ffn1 epi=bias+gelu+pre", "ffn2dx epi=dgelu    ", "ffn1 epi=bias+pre    ",
+                               "ffn1 epi=none Cb only "};
+        for (int form = 0; form < 4; ++form) {
             GemmParams p;
             gemm_init(p);
             p.mode = 2;
@@ -140,20 +145,23 @@ int main(int argc, char** argv) {
             p.C = nullptr; p.ldc = 4096;
             p.Ab = A; p.Bb = B; p.ldab = 1024; p.ldbb = 1024;
             p.Cb = Cb; p.ldcb = 4096; p.preb = 1;
-            if (form == 0) {
-                p.epi = EPI_BIAS | EPI_STORE_PRE | EPI_GELU;
+            if (form == 0 || form == 2) {
+                p.epi = EPI_BIAS | EPI_STORE_PRE | (form == 0 ? EPI_GELU : 0);
                 p.bias = bias;
                 p.C2 = reinterpret_cast<float*>(U); p.ldc2 = 4096;
-            } else {
+            } else if (form == 1) {
                 p.epi = EPI_DGELU;
                 p.aux = reinterpret_cast<const float*>(U); p.ldaux = 4096;
+            } else {
+                p.epi = 0;
+                p.preb = 0;
             }
-            const int evs[] = {0, 1, 2};
+            const int evs[] = {0, 1, 2, 3};
             std::vector<float> ms[NV];
             for (int rd = 0; rd < rounds; ++rd)
                 for (int v : evs) {
                     set_variant(v);
-                    if (form == 0) hipLaunchKernelGGL(fillb, dim3((M * 4096L + 255) / 256), dim3(256), 0, 0, U, (long)M * 4096, 3u);
+                    if (form == 0 || form == 2) hipLaunchKernelGGL(fillb, dim3((M * 4096L + 255) / 256), dim3(256), 0, 0, U, (long)M * 4096, 3u);
                     for (int w = 0; w < 2; ++w) gemm_launch(p, 0, nullptr, 0);
                     CK(hipEventRecord(e0, 0));
                     for (int r = 0; r < reps; ++r) gemm_launch(p, 0, nullptr, 0);
@@ -180,7 +188,7 @@ int main(int argc, char** argv) {
                 std::sort(m.begin(), m.end());
                 const double tf = 2.0 * M * 4096.0 * 1024.0 / (m[m.size() / 2] * 1e-3) / 1e12;
                 printf("%s %s: median %.4f ms %.1f TF (best %.1f) vs hb128 Cb relerr %.2e\n",
-                       form == 0 ? "ffn1 epi=bias+gelu+pre" : "ffn2dx epi=dgelu    ", vname[v], m[m.size() / 2], tf,
+                       fname[form], vname[v], m[m.size() / 2], tf,
                        2.0 * M * 4096.0 * 1024.0 / (m[0] * 1e-3) / 1e12, dmax);
                 fflush(stdout);
             }
