@@ -78,8 +78,9 @@ struct SutaSwitches {
     int splitk;           // SUTA_SPLITK (default 1): split-K for small grids; 0 = never (tests comparing kernels
                           // bitwise: a split changes the k summation order)
     int fused_delta;      // SUTA_FUSED_DELTA (default 1): the flash backward's delta in the dctx GEMM's epilogue
-    int hbx_t;            // SUTA_HBX_T (default 1): gemm_hbx accumulates C^T fragments (row-per-lane epilogue, 16-B
-                          // stores); 0 = the column-per-lane form shared with the 128 x 128 kernel
+    int hbx_t;            // SUTA_HBX_T (default 2): gemm_hbx accumulates C^T fragments with a row-per-lane epilogue whose
+                          // outputs are staged through LDS into whole-line stores; 1 = direct 16-B row-per-lane stores,
+                          // 0 = the column-per-lane form shared with the 128 x 128 kernel
 };
 void suta_latch_switches();
 const SutaSwitches& suta_switches();  // the snapshot (taken now if none was)

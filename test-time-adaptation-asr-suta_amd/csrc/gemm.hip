@@ -195,17 +195,20 @@ static int use_hb8(const GemmParams& p) {
 }
 
 // 256 x 256 slice-ring bf16-plane kernel (gemm_hbx.hip, v_mfma_f32_32x32x16_bf16; bitwise the 128 x 128 kernel's
-// results: same MFMA, same k order) for the linears on grids of at least one full round of 256 tiles.  tools/hb_bench
-// (C4 shapes at M = 164 x 399, same box): qkv 741 -> 889 TF, out-proj 604 -> 784, FFN1 749 -> 858, FFN2 865 -> 1055,
-// dQKV 808 -> 1022.  With the column-per-lane epilogue the GELU / GELU' classes measured equal to 128 x 128 (576 vs
-// 588, 577 vs 572: 128 two-lane-pair dword stores per bf16 plane per wave, store-issue bound at one block per CU), so
-// they take hbx only with its row-per-lane epilogue (SUTA_HBX_T, 16-B stores).
+// results: same MFMA products, same k order) for the linears on grids of at least one full round of 256 tiles.
+// tools/hb_bench (C4 shapes at M = 164 x 399, same box; profiles/r4/hbx_epilogue_hb_bench.log): qkv 729 -> 875 TF,
+// out-proj 597 -> 770, FFN1 759 -> 854, FFN2 866 -> 1065, dQKV 819 -> 1003.  The GELU / GELU' linears need its C^T
+// epilogue with LDS-staged whole-line stores (SUTA_HBX_T=2): FFN1 (bias + GELU + bf16 pre) 603 -> 737 TF, FFN2 input
+// gradient 611 -> 719; the column-per-lane epilogue (two-lane-pair dword stores, 2 rows per instruction) measured
+// 595 / 627 and direct row-per-lane 16-B stores (32 rows per instruction) 515 / 625, so without the staged form
+// they keep the 128 x 128 kernel.
 // SUTA_HBX=0: off (A/B runs); 2: every eligible linear, any epilogue and grid (tests).
 static bool use_hbx(const GemmParams& p) {
     const int mode = suta_switches().hbx;
     if (!mode || p.Z != 1 || p.segK > 0 || p.K % 32 || p.K < 128 || (p.epi & (EPI_ACCUM | EPI_SMBWD))) return false;
     if (mode == 2) return true;  // SUTA_HBX=2: every eligible linear (tests)
-    if ((p.epi & (EPI_GELU | EPI_DGELU | EPI_STORE_PRE)) && !(suta_switches().hbx_t && hbx_t_ok(p, false))) return false;
+    if ((p.epi & (EPI_GELU | EPI_DGELU | EPI_STORE_PRE)) && !(suta_switches().hbx_t == 2 && hbx_t_ok(p, false)))
+        return false;
     return (long)((p.M + 255) / 256) * ((p.N + 255) / 256) >= 256;
 }
 

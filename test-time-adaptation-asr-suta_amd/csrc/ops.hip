@@ -1824,7 +1824,7 @@ void suta_latch_switches() {
     s.hbx = hbx ? atoi(hbx) : 1;
     s.splitk = on("SUTA_SPLITK");
     const char* hbxt = std::getenv("SUTA_HBX_T");
-    s.hbx_t = hbxt ? std::min(2, std::max(0, atoi(hbxt))) : 1;
+    s.hbx_t = hbxt ? std::min(2, std::max(0, atoi(hbxt))) : 2;
     s.fused_delta = on("SUTA_FUSED_DELTA");
     const char* hb8 = std::getenv("SUTA_HB8");
     s.hb8 = hb8 ? atoi(hb8) : 0;
