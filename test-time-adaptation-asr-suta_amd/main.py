@@ -67,9 +67,10 @@ def build_parser(sdpl: bool = False):
                    help="max utterances adapted together as one ragged batch (episodic runs; 1 = one per call)")
     p.add_argument("--gpu_budget_s", type=float, default=1312.0,
                    help="max padded audio seconds per ragged batch (utterances x longest)")
-    p.add_argument("--gpu_min_fill", type=float, default=0.35,
+    p.add_argument("--gpu_min_fill", type=float, default=0.2,
                    help="ragged grouping: 0 = greedy; > 0 = padding-minimising partition charging a batch at least "
-                        "this fraction of --gpu_budget_s (tools/bench_varlen.py: 0.35 -> 27.2 vs greedy 26.3 utt/s)")
+                        "this fraction of --gpu_budget_s (bench.py c5, TED-like mix at --gpu_batch 164 / --gpu_budget_s "
+                        "1312: 0.35 / 0.2 / 0.1 / 0.05 -> 15.5 / 16.8 / 16.5 / 15.5 utt/s, profiles/r4/c5_mf*.json)")
     p.add_argument("--dist_backend", default="auto", choices=["auto", "nccl", "gloo"],
                    help="torch.distributed backend under torchrun (auto: nccl = RCCL when a GPU is visible)")
     p.add_argument("--num_workers", type=int, default=4,
