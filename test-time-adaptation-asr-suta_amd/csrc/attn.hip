@@ -40,9 +40,11 @@ typedef __bf16 fbf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 fbf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-// [row][64] tiles padded to 72 floats: 16-B row reads of 8 consecutive rows hit 8 distinct 4-bank groups,
-// and the column reads of rows r and r + 4 (lane halves of apply_rows) land 32 banks apart
-constexpr int FA_LD = 72;
+// [row][64] tiles padded to 68 floats (17 16-B slots): the row reads of prod_rows (ds_read_b128, lane l32 -> row
+// l32) put row r in slot r mod 16, so each of gfx950's four 16-lane groups ({0-3,12-15,20-27}, {4-11,16-19,28-31}
+// and the upper half's) reads 16 distinct 4-bank slots (72 = 18 slots put rows r and r + 8 on one slot: 2-way
+// conflicts); the column reads of apply_rows stay conflict-free (32 consecutive floats per 32-lane group)
+constexpr int FA_LD = 68;
 constexpr int FA_LDT = 36;  // [64][32] transposed tiles
 
 __device__ __forceinline__ fbf16x8 cvt8(f32x4 lo, f32x4 hi) {
