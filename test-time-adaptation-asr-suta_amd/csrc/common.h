@@ -77,6 +77,7 @@ struct SutaSwitches {
                           // on full grids; 2: on every eligible bf16-plane linear (tests: small grids, edge tiles)
     int splitk;           // SUTA_SPLITK (default 1): split-K for small grids; 0 = never (tests comparing kernels
                           // bitwise: a split changes the k summation order)
+    int hbx_dbg;          // SUTA_HBX_DBG (tools/hb_bench diagnostics; wrong results): gemm_hbx with parts of its loop removed
     int fused_delta;      // SUTA_FUSED_DELTA (default 1): the flash backward's delta in the dctx GEMM's epilogue
     int hbx_t;            // SUTA_HBX_T (default 2): gemm_hbx accumulates C^T fragments with a row-per-lane epilogue whose
                           // outputs are staged through LDS into whole-line stores; 1 = direct 16-B row-per-lane stores,

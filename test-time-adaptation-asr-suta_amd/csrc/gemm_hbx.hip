@@ -479,7 +479,9 @@ __device__ __forceinline__ void epilogue_t(const GemmParams& p, const f32x16 (&a
     }
 }
 
-template <int MS, bool CB, int EM, int TR>
+// DBG (tools/hb_bench diagnostics only; the results are garbage): 1 no B-operand DMA, 2 no B-fragment reads after
+// the first, 3 no DMA at all, 4 no fragment reads after the first slice
+template <int MS, bool CB, int EM, int TR, int DBG = 0>
 __global__ __launch_bounds__(512, 1) void gemm_hbx_kernel(GemmParams p) {
     __shared__ __attribute__((aligned(16))) float smem[X_NR * X_SLOT];
     const TileId tid = xcd_tile(p.order);
@@ -509,16 +511,19 @@ __global__ __launch_bounds__(512, 1) void gemm_hbx_kernel(GemmParams p) {
     sb.init(B, ldb, n0, p.N, wid, lane);
     auto issue = [&](int s) {
         float* st = smem + (s % X_NR) * X_SLOT;
-        xstream_issue(sa, st, wid);
-        xstream_issue(sb, st + X_BM * X_KS, wid);
+        if constexpr (DBG != 3) xstream_issue(sa, st, wid);
+        if constexpr (DBG != 1 && DBG != 3) xstream_issue(sb, st + X_BM * X_KS, wid);
     };
     // part c of slice s: MS 32 -> k-chunk c (k 16c..16c+15); MS 16 -> the wave tile's m-half c (k 0..31)
     auto read = [&](int s, int c, XFr<MS>& f) {
         const float* As = smem + (s % X_NR) * X_SLOT;
         const float* Bs = As + X_BM * X_KS;
         if constexpr (MS == 32) {
+            if (DBG == 4 && s > 0) return;
+            if (DBG != 2 || s == 0) {
 #pragma unroll
-            for (int j = 0; j < 2; ++j) f.b[j] = xfrag(Bs, wc * 64 + j * 32 + l32, 2 * c + h);
+                for (int j = 0; j < 2; ++j) f.b[j] = xfrag(Bs, wc * 64 + j * 32 + l32, 2 * c + h);
+            }
 #pragma unroll
             for (int i = 0; i < 4; ++i) f.a[i] = xfrag(As, wr * 128 + i * 32 + l32, 2 * c + h);
         } else {
@@ -573,8 +578,9 @@ __global__ __launch_bounds__(512, 1) void gemm_hbx_kernel(GemmParams p) {
     issue(2);
     wait_vm<2 * X_NPW>();
     __builtin_amdgcn_s_barrier();
-    XFr<MS> fx, fy;
+    XFr<MS> fx{}, fy{};
     read(0, 0, fx);
+    if constexpr (DBG == 2 || DBG == 4) read(0, 1, fy);
     int s = 0;
     for (; s + 3 < nst; ++s) step(s, fx, fy, T1{}, T1{});
     if (s + 1 < nst) step(s++, fx, fy, T0{}, T1{});
@@ -657,6 +663,21 @@ void gemm_run_hbx(int variant, const GemmParams& p, dim3 grid, hipStream_t st) {
         return;
     }
     const int tr = suta_switches().hbx_t;
+    const int dbg = suta_switches().hbx_dbg;
+    if (dbg && tr == 2 && hbx_t_ok(p, true) && (e & ~XEM_A) == 0) {  // tools/hb_bench diagnostics
+        const bool cb = p.Cb != nullptr;
+#define HBX_DBG(D)                                                                                                 \
+        do {                                                                                                       \
+            if (cb) hipLaunchKernelGGL((gemm_hbx_kernel<32, true, XEM_A, 2, D>), grid, dim3(512), 0, st, p);       \
+            else hipLaunchKernelGGL((gemm_hbx_kernel<32, false, XEM_A, 2, D>), grid, dim3(512), 0, st, p);         \
+        } while (0)
+        if (dbg == 1) HBX_DBG(1);
+        else if (dbg == 2) HBX_DBG(2);
+        else if (dbg == 3) HBX_DBG(3);
+        else HBX_DBG(4);
+#undef HBX_DBG
+        return;
+    }
     if (tr && hbx_t_ok(p, true)) {  // C^T accumulators, row-per-lane epilogue (2: LDS-staged whole-line stores)
         if (tr == 2) {
             if (e == XEM_L) return launch_hbx_em<32, XEM_L, 2>(p, grid, st);
