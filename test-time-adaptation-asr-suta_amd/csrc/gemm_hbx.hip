@@ -480,7 +480,8 @@ __device__ __forceinline__ void epilogue_t(const GemmParams& p, const f32x16 (&a
 }
 
 // DBG (tools/hb_bench diagnostics only; the results are garbage): 1 no B-operand DMA, 2 no B-fragment reads after
-// the first, 3 no DMA at all, 4 no fragment reads after the first slice
+// the first, 3 no DMA at all, 4 no fragment reads after the first slice; 5 (correct results) s_setprio(1) around
+// the MFMA halves
 template <int MS, bool CB, int EM, int TR, int DBG = 0>
 __global__ __launch_bounds__(512, 1) void gemm_hbx_kernel(GemmParams p) {
     __shared__ __attribute__((aligned(16))) float smem[X_NR * X_SLOT];
@@ -561,6 +562,22 @@ __global__ __launch_bounds__(512, 1) void gemm_hbx_kernel(GemmParams p) {
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
+        if constexpr (DBG == 5) {  // s_setprio(1) over the MFMA halves (cdna_hip_programming.md T5)
+            if constexpr (DMA) issue(s + 3);
+            read(s, 1, Y);
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_setprio(1);
+            mfma(0, X);
+            __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (RD) read(s + 1, 0, X);
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_setprio(1);
+            mfma(1, Y);
+            __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_sched_barrier(0);
+            return;
+        }
         if constexpr (DMA) issue(s + 3);
         read(s, 1, Y);
         mfma(0, X);
@@ -674,7 +691,8 @@ void gemm_run_hbx(int variant, const GemmParams& p, dim3 grid, hipStream_t st) {
         if (dbg == 1) HBX_DBG(1);
         else if (dbg == 2) HBX_DBG(2);
         else if (dbg == 3) HBX_DBG(3);
-        else HBX_DBG(4);
+        else if (dbg == 4) HBX_DBG(4);
+        else HBX_DBG(5);
 #undef HBX_DBG
         return;
     }

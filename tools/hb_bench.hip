@@ -52,11 +52,11 @@ int main(int argc, char** argv) {
     // and with C^T accumulators + the row-per-lane epilogue (hbxT)
     // (tile, ns, cb-capable, SUTA_HBX_T, SUTA_HBX_DBG): the DBG forms are diagnostics (wrong results): 1 no B DMA,
     // 2 no B fragment reads, 3 no DMA, 4 no fragment reads
-    const int variants[][5] = {{8, 2, 1, 2, 0}, {8, 2, 1, 2, 1}, {8, 2, 1, 2, 2}, {8, 2, 1, 2, 3}, {8, 2, 1, 2, 4}};
-    const char* vname[] = {"hbxTS", "noBdma", "noBrd", "noDMA", "noRd"};
-    constexpr int NV = 5;
+    const int variants[][5] = {{8, 2, 1, 2, 0}, {8, 2, 1, 2, 5}};
+    const char* vname[] = {"hbxTS", "prio "};
+    constexpr int NV = 2;
     auto set_variant = [&](int v) {
-        const char* tv[] = {"0", "1", "2", "3", "4"};
+        const char* tv[] = {"0", "1", "2", "3", "4", "5"};
         setenv("SUTA_HBX_T", tv[variants[v][3]], 1);
         setenv("SUTA_HBX_DBG", tv[variants[v][4]], 1);
         suta_latch_switches();
@@ -159,7 +159,7 @@ int main(int argc, char** argv) {
                 p.epi = 0;
                 p.preb = 0;
             }
-            const int evs[] = {0};
+            const int evs[] = {0, 1};
             std::vector<float> ms[NV];
             for (int rd = 0; rd < rounds; ++rd)
                 for (int v : evs) {
