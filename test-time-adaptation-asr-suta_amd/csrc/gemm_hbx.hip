@@ -627,6 +627,163 @@ __global__ __launch_bounds__(512, 1) void gemm_hbx_kernel(GemmParams p) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// "hbp": the same 256 x 256 tile, C^T accumulators and staged epilogue, with the four-phase K-tile schedule of
+// cdna_hip_programming.md's 256^2 8-phase template (BK = 64, two LDS buffers of four 16-KB half-tiles, one half-tile
+// of DMA issued per phase, counted vmcnt every phase, two barriers per phase, optionally two wave groups one
+// barrier apart with s_setprio(1) over each MFMA cluster).
+// Half-tiles of a K-tile: A0 / A1 = A rows {128 wr + 64 qm + r : wr in 0..1, r < 64} for qm = 0 / 1, B0 / B1 = B rows
+// {64 wc + 32 qn + r : wc in 0..3, r < 32} for qn = 0 / 1 -- so wave (wr, wc)'s quadrant (qm, qn) reads 64 rows of
+// A half qm and 32 of B half qn and the four quadrants cover its contiguous 128 x 64 output (epilogue_t unchanged).
+// LDS rows of 128 B (64 bf16 of K), chunk c of row r in slot c ^ ((r >> 1) & 7): conflict-free ds_read_b128 for
+// 32 consecutive rows at one chunk (both 16-lane group patterns), swizzle on the DMA source address.
+// Phases of K-tile t (buffer t & 1): 1 quadrant (0,0) reads A(qm 0) + B(qn 0); 2 (0,1) reads B(qn 1); 3 (1,1) reads
+// A(qm 1); 4 (1,0) no reads (B(qn 0) kept in registers).  Phase p also issues half-tile p - 1 (A0, B0, B1, A1) of
+// K-tile t + 1 into the other buffer, whose last reads (phase 3 of K-tile t - 1) are two phases back (WAR).  The
+// wait at phase p retires every half issued before phase p - 1 (vmcnt(4)); a half issued at phase q is read at
+// phase q + 3 or later, after that wait and a barrier every wave has passed (RAW; with the wave-group stagger the
+// lagging group's wait still precedes the leading group's read by one barrier).
+constexpr int P_HALF = 16384;  // bytes per half-tile image (128 rows x 128 B)
+
+__device__ __forceinline__ int hbp_swz(int r) { return (r >> 1) & 7; }
+
+template <bool CB, int EM, bool STAG>
+__global__ __launch_bounds__(512, 1) void gemm_hbp_kernel(GemmParams p) {
+    __shared__ __attribute__((aligned(16))) float smem[8 * P_HALF / 4];
+    char* const lds = reinterpret_cast<char*>(smem);
+    const TileId tid = xcd_tile(p.order);
+    const __bf16* A = reinterpret_cast<const __bf16*>(p.Ab);
+    const __bf16* B = reinterpret_cast<const __bf16*>(p.Bb);
+    const int m0 = tid.y * 256, n0 = tid.x * 256;
+    const int nk = p.K / 64;
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wr = wid >> 2, wc = wid & 3;
+
+    // DMA sources: half h (0 A0, 1 B0, 2 B1, 3 A1 -- the issue order), pieces wid and wid + 8 (8 LDS rows each)
+    const __bf16* src[4][2];
+    int inc[4][2];
+#pragma unroll
+    for (int h = 0; h < 4; ++h)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int pc = wid + 8 * i, lr = 8 * pc + (lane >> 3);
+            const int c = (lane & 7) ^ hbp_swz(lr);
+            const bool isa = h == 0 || h == 3;
+            const int q = h == 3 ? 1 : h == 2 ? 1 : 0;  // qm for A halves, qn for B halves
+            const int grow = isa ? m0 + (lr >> 6) * 128 + q * 64 + (lr & 63) : n0 + (lr >> 5) * 64 + q * 32 + (lr & 31);
+            const bool ok = grow < (isa ? p.M : p.N);
+            const long ld = isa ? p.ldab : p.ldbb;
+            src[h][i] = ok ? (isa ? A : B) + (long)grow * ld + 8 * c : reinterpret_cast<const __bf16*>(g_zero16);
+            inc[h][i] = ok ? 64 : 0;
+        }
+    // LDS image of half h in buffer b (images in the order A0, A1, B0, B1)
+    auto himg = [&](int b, int h) -> char* {
+        const int slot = h == 0 ? 0 : h == 3 ? 1 : h == 1 ? 2 : 3;
+        return lds + (b * 4 + slot) * P_HALF;
+    };
+    auto issue = [&](int t, int h) {  // half h of K-tile t into buffer t & 1
+        char* dst = himg(t & 1, h);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const float*>(src[h][i]),
+                                             (lds_ptr_t)(dst + (wid + 8 * i) * 1024), 16, 0, 0);
+            src[h][i] += inc[h][i];
+        }
+    };
+    auto frag = [&](const char* img, int lr, int kk) {
+        const int c = 2 * kk + (lane >> 5);
+        return *reinterpret_cast<const bf16x8*>(img + lr * 128 + ((c ^ hbp_swz(lr)) << 4));
+    };
+    f32x16 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    bf16x8 fa[2][4], fb0[4], fb1[4];
+    auto read_a = [&](int b, int qm) {
+        const char* img = lds + (b * 4 + qm) * P_HALF;
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) fa[bi][kk] = frag(img, wr * 64 + 32 * bi + (lane & 31), kk);
+    };
+    auto read_b = [&](int b, int qn, bf16x8 (&fb)[4]) {
+        const char* img = lds + (b * 4 + 2 + qn) * P_HALF;
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) fb[kk] = frag(img, wc * 32 + (lane & 31), kk);
+    };
+    auto mfma_q = [&](int qm, int qn, const bf16x8 (&fb)[4]) {
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk)
+                acc[2 * qm + bi][qn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[kk], fa[bi][kk], acc[2 * qm + bi][qn], 0, 0, 0);
+    };
+    // counted wait of phase p: the halves issued at phases p - 1 and p (if any) may stay in flight
+    auto wait_phase = [&](int n_out) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (n_out >= 2) wait_vm<4>();
+        else if (n_out == 1) wait_vm<2>();
+        else wait_vm<0>();
+    };
+    auto barrier = [] {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto mfma_phase = [&](int qm, int qn, const bf16x8 (&fb)[4]) {
+        barrier();
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) (vmcnt 63, expcnt 7): this phase's fragment reads
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (STAG) __builtin_amdgcn_s_setprio(1);
+        mfma_q(qm, qn, fb);
+        if constexpr (STAG) __builtin_amdgcn_s_setprio(0);
+        barrier();
+    };
+
+    // prologue: K-tile 0's four halves; A0 and B0 (phase 1's) retired
+#pragma unroll
+    for (int h = 0; h < 4; ++h) issue(0, h);
+    wait_vm<4>();
+    if constexpr (STAG) {
+        if (wr == 1) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier behind group 0
+    }
+    __builtin_amdgcn_s_barrier();
+    for (int t = 0; t < nk; ++t) {
+        const int b = t & 1;
+        const bool nxt = t + 1 < nk;  // halves of K-tile t + 1 issued in this K-tile's phases
+        // phase 1: quadrant (0,0)
+        read_a(b, 0);
+        read_b(b, 0, fb0);
+        if (nxt) issue(t + 1, 0);
+        wait_phase(1 + (nxt ? 1 : 0));  // (phase 4 of the previous K-tile, or the prologue's last half, issued one)
+        mfma_phase(0, 0, fb0);
+        // phase 2: quadrant (0,1)
+        read_b(b, 1, fb1);
+        if (nxt) issue(t + 1, 1);
+        wait_phase(nxt ? 2 : 0);
+        mfma_phase(0, 1, fb1);
+        // phase 3: quadrant (1,1)
+        read_a(b, 1);
+        if (nxt) issue(t + 1, 2);
+        wait_phase(nxt ? 2 : 0);
+        mfma_phase(1, 1, fb1);
+        // phase 4: quadrant (1,0)
+        if (nxt) issue(t + 1, 3);
+        wait_phase(nxt ? 2 : 0);
+        mfma_phase(1, 0, fb0);
+    }
+    wait_vm<0>();
+    if constexpr (STAG) {
+        if (wr == 0) __builtin_amdgcn_s_barrier();  // the leading group's matching barrier
+    }
+    __syncthreads();  // every wave is done with the buffers: wave-private 16-KB staging images
+    epilogue_t<CB, EM, true>(p, acc, m0 + wr * 128, n0 + wc * 64, lane, lds + wid * 16384);
+}
+
 template <int MS, int EM, int TR = 0>
 void launch_hbx_em(const GemmParams& p, dim3 grid, hipStream_t st) {
     if (p.Cb) hipLaunchKernelGGL((gemm_hbx_kernel<MS, true, EM, TR>), grid, dim3(512), 0, st, p);
@@ -681,6 +838,26 @@ void gemm_run_hbx(int variant, const GemmParams& p, dim3 grid, hipStream_t st) {
     }
     const int tr = suta_switches().hbx_t;
     const int dbg = suta_switches().hbx_dbg;
+    const int form = suta_switches().hbx_form;
+    if (form && tr == 2 && p.K % 64 == 0 && hbx_t_ok(p, true) && !dbg) {  // the four-phase K-tile schedule
+        const bool cb = p.Cb != nullptr;
+#define HBP(EM_)                                                                                                   \
+        do {                                                                                                       \
+            if (form == 2) {                                                                                       \
+                if (cb) hipLaunchKernelGGL((gemm_hbp_kernel<true, EM_, true>), grid, dim3(512), 0, st, p);         \
+                else hipLaunchKernelGGL((gemm_hbp_kernel<false, EM_, true>), grid, dim3(512), 0, st, p);           \
+            } else {                                                                                               \
+                if (cb) hipLaunchKernelGGL((gemm_hbp_kernel<true, EM_, false>), grid, dim3(512), 0, st, p);        \
+                else hipLaunchKernelGGL((gemm_hbp_kernel<false, EM_, false>), grid, dim3(512), 0, st, p);          \
+            }                                                                                                      \
+            return;                                                                                                \
+        } while (0)
+        if (e == XEM_L) HBP(XEM_L);
+        if ((e & ~XEM_A) == 0) HBP(XEM_A);
+        if ((e & ~XEM_G) == 0) HBP(XEM_G);
+        if ((e & ~XEM_D) == 0) HBP(XEM_D);
+#undef HBP
+    }
     if (dbg && tr == 2 && hbx_t_ok(p, true) && (e & ~XEM_A) == 0) {  // tools/hb_bench diagnostics
         const bool cb = p.Cb != nullptr;
 #define HBX_DBG(D)                                                                                                 \

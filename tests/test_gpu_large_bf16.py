@@ -220,7 +220,8 @@ def test_bf16_hbx_slice_ring_kernel_bitwise_equals_128_tile(monkeypatch):
     (SUTA_HBX=2: every epilogue class -- bias / residual, bias + GELU + bf16 pre-activation, GELU' -- small grids and
     edge tiles of a ragged pair: 198 and 124 rows of a 256-row tile), in every epilogue form (SUTA_HBX_T=1: C^T
     accumulators, row-per-lane 16-B stores; 2: the same staged through LDS into whole-line stores; 0: the
-    column-per-lane form), against the 128 x 128 kernel (SUTA_HBX=0),
+    column-per-lane form) and main loop (SUTA_HBX_FORM=2: four-phase 64-deep K-tiles, staggered wave groups; 1 the same
+    in lockstep; 0 the 32-deep slice ring), against the 128 x 128 kernel (SUTA_HBX=0),
     all without split-K (SUTA_SPLITK=0: a split sums k in another order): the same MFMA products in the same k order, so
     logits and adapted tensors are bitwise equal; and the large model's 20-step SUTA against the reference goldens g7
     (bf16 tolerance).  Reference main.py:181,205."""
@@ -231,12 +232,14 @@ def test_bf16_hbx_slice_ring_kernel_bitwise_equals_128_tile(monkeypatch):
     steps = [int(s) for s in z["steps"]]
     waves = [synth.wave(32000, 82), synth.wave(20000, 83)]
     out, params = {}, {}
-    for mode, tr in (("0", "1"), ("2", "1"), ("2", "2"), ("2", "0")):
+    for mode, tr, form in (("0", "1", "2"), ("2", "1", "2"), ("2", "2", "2"), ("2", "2", "1"), ("2", "2", "0"),
+                           ("2", "0", "2")):
         monkeypatch.setenv("SUTA_HBX", mode)
         monkeypatch.setenv("SUTA_HBX_T", tr)
+        monkeypatch.setenv("SUTA_HBX_FORM", form)
         eng = SutaEngine(cfg, sd, max_batch=2, max_samples=32000)
         eng.set_precision("bf16")
-        if mode == "2" and tr == "1":
+        if mode == "2" and tr == "2" and form == "2":
             eng.set_census(True)
             logits, _, _ = eng.adapt(_g7_wave(), 20, SutaHParams(), record=steps)
             census = eng.get_census()
@@ -244,16 +247,16 @@ def test_bf16_hbx_slice_ring_kernel_bitwise_equals_128_tile(monkeypatch):
             assert any(k.startswith("hbx 256x256 ") for k in census), census
             for j, s in enumerate(steps):
                 assert_bf16_close(logits[s][0], z["logits"][j], 0.97, f"hbx large step {s}", rtol=BF16_LOGITS_RTOL_LARGE)
-        key = mode + tr
+        key = mode + tr + form
         out[key], _, _ = eng.adapt_varlen(waves, 3, SutaHParams(), record=[0, 3])
         params[key] = {n: eng.get_param(1, n) for n in eng.trainable_names()}
         eng.close()
-    for key in ("21", "22", "20"):
+    for key in ("212", "222", "221", "220", "202"):
         for r in (0, 3):
             for u in range(2):
-                assert np.array_equal(out[key][r][u], out["01"][r][u]), (key, r, u)
+                assert np.array_equal(out[key][r][u], out["012"][r][u]), (key, r, u)
         for n, v in params[key].items():
-            assert np.array_equal(v, params["01"][n]), (key, n)
+            assert np.array_equal(v, params["012"][n]), (key, n)
 
 
 def test_bf16_fused_delta_bitwise_equals_separate_pass(monkeypatch):

@@ -52,13 +52,15 @@ int main(int argc, char** argv) {
     // and with C^T accumulators + the row-per-lane epilogue (hbxT)
     // (tile, ns, cb-capable, SUTA_HBX_T, SUTA_HBX_DBG): the DBG forms are diagnostics (wrong results): 1 no B DMA,
     // 2 no B fragment reads, 3 no DMA, 4 no fragment reads
-    const int variants[][5] = {{8, 2, 1, 2, 0}, {8, 2, 1, 2, 5}};
-    const char* vname[] = {"hbxTS", "prio "};
-    constexpr int NV = 2;
+    // + SUTA_HBX_FORM (6th): 1 the four-phase K-tile schedule (gemm_hbp_kernel), 2 the same with staggered wave groups
+    const int variants[][6] = {{8, 2, 1, 2, 0, 0}, {8, 2, 1, 2, 0, 1}, {8, 2, 1, 2, 0, 2}};
+    const char* vname[] = {"hbxTS", "hbp  ", "hbpS "};
+    constexpr int NV = 3;
     auto set_variant = [&](int v) {
         const char* tv[] = {"0", "1", "2", "3", "4", "5"};
         setenv("SUTA_HBX_T", tv[variants[v][3]], 1);
         setenv("SUTA_HBX_DBG", tv[variants[v][4]], 1);
+        setenv("SUTA_HBX_FORM", tv[variants[v][5]], 1);
         suta_latch_switches();
         gemm_set_variant(variants[v][0], variants[v][1]);
     };
@@ -159,7 +161,7 @@ int main(int argc, char** argv) {
                 p.epi = 0;
                 p.preb = 0;
             }
-            const int evs[] = {0, 1};
+            const int evs[] = {0, 1, 2};
             std::vector<float> ms[NV];
             for (int rd = 0; rd < rounds; ++rd)
                 for (int v : evs) {
