@@ -9,7 +9,7 @@ w=$1
 O=gpurun_out/r4prof
 R=/tmp/r4prof_raw_$w
 mkdir -p $O $R
-if [ $w = c2 ]; then X="python3 bench.py --steps 1 --warmup 0 --no-split --no-cpu-baseline --no-timing --no-c4"
+if [ $w = c2 ]; then X="python3 bench.py --steps 1 --warmup 0 --no-split --no-cpu-baseline --no-timing --no-c4 --no-c5 --no-batch64"
 else X="python3 bench.py --only-c4 --steps 1 --warmup 0 --no-timing"; fi
 SQA="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT"
 SQB="SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_INSTS_VALU_CVT"
