@@ -356,6 +356,48 @@ __global__ __launch_bounds__(NW * 64) void flash_fwd_kernel(const float* __restr
     if (h == 0) lse[(long)bh * T + q] = (m_run + log2f(l_tot)) * (1.0f / LOG2E);  // natural-log LSE
 }
 
+
+// In-launch combination of a head's dQ partials (replaces the flash_dq_reduce pass when cnt is given): every key
+// block of the head publishes its partial (cdna_hip_programming.md's split-K seam protocol: stores drained, block
+// barrier, an agent-scope release, then a ticket on the head's counter); the block drawing nkb - 1 acquires and sums
+// the nkb partials in key-block order -- flash_dq_reduce's order, so dQ is bitwise the same -- into dqkv's Q columns
+// and / or their bf16 plane (rows past the utterance's length get 0, as their dS is 0).  The counters are zeroed
+// by a memset node ahead of every launch.  Every thread of the block must reach this call.
+__device__ __forceinline__ void dq_combine(const float* __restrict__ dqp, float* __restrict__ dqkv,
+                                           __bf16* __restrict__ dqkvb, int* __restrict__ cnt, int* flag, int bh,
+                                           int u, int hd, int T, int NH, int H, int nkb, int tl, int B) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int prev = __hip_atomic_fetch_add(cnt + bh, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = prev == nkb - 1;
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        *flag = last;
+    }
+    __syncthreads();
+    if (!*flag) return;
+    const long stride4 = (long)B * NH * T * 16;  // one key block's partials, in float4
+    const f32x4* pp = reinterpret_cast<const f32x4*>(dqp + (long)bh * T * 64);
+    for (int i = threadIdx.x; i < T * 16; i += blockDim.x) {
+        const int q = i >> 4, c4 = (i & 15) * 4;
+        f32x4 sum = {0.f, 0.f, 0.f, 0.f};
+        if (q < tl)
+            for (int k = 0; k < nkb; ++k) sum += pp[k * stride4 + i];
+        if (dqkv) *reinterpret_cast<f32x4*>(dqkv + ((long)u * T + q) * 3 * H + hd * 64 + c4) = sum;
+        if (dqkvb) {
+            fbf16x4 b4;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) b4[e] = (__bf16)sum[e];
+            *reinterpret_cast<fbf16x4*>(dqkvb + ((long)u * T + q) * 3 * H + hd * 64 + c4) = b4;
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 // backward
 // ------------------------------------------------------------------------------------------------
@@ -373,7 +415,8 @@ template <int NW, bool BF16>
 __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void flash_bwd_kernel(
     const float* __restrict__ qkv, const float* __restrict__ dctx, const float* __restrict__ lse,
     const float* __restrict__ delta, float* __restrict__ dqkv, float* __restrict__ dqp, int T, int NH, int H,
-    float scale, const int* __restrict__ tlen, int nkb, int gpb, int B, __bf16* __restrict__ dqkvb) {
+    float scale, const int* __restrict__ tlen, int nkb, int gpb, int B, __bf16* __restrict__ dqkvb,
+    int* __restrict__ dq_cnt) {
     constexpr int NT = NW * 64;
     constexpr int KBP = fb_kbp<NW>();
     constexpr int QPT = 512 / NT;       // float4 of a 32 x 64 tile per thread
@@ -558,35 +601,37 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void flash_bwd_kernel(
         for (int qt = 0; qt < nqt; ++qt) tile(qt, sa, sa);
     }
     // dK, dV rows of this wave's keys (0 past the length): lane = key, registers = 4 consecutive columns
-    if (w >= ngb || key >= T) return;
-    float* dkr = dqkv + ((long)u * T + key) * ld + H + hd * 64 + 4 * h;
-    float* dvr = dkr + H;
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int a = 0; a < 4; ++a) {
-            f32x4 x, y;
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                x[b] = dk[t][4 * a + b];
-                y[b] = dv[t][4 * a + b];
-            }
-            if (dqkv) {
-                *reinterpret_cast<f32x4*>(dkr + 32 * t + 8 * a) = x;
-                *reinterpret_cast<f32x4*>(dvr + 32 * t + 8 * a) = y;
-            }
-            if (dqkvb) {
-                fbf16x4 bx, by;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    bx[e] = (__bf16)x[e];
-                    by[e] = (__bf16)y[e];
+    if (w < ngb && key < T) {  // dK, dV rows of this wave's keys
+        float* dkr = dqkv + ((long)u * T + key) * ld + H + hd * 64 + 4 * h;
+        float* dvr = dkr + H;
+    #pragma unroll
+        for (int t = 0; t < 2; ++t)
+    #pragma unroll
+            for (int a = 0; a < 4; ++a) {
+                f32x4 x, y;
+    #pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    x[b] = dk[t][4 * a + b];
+                    y[b] = dv[t][4 * a + b];
                 }
-                __bf16* kb = dqkvb + ((long)u * T + key) * ld + H + hd * 64 + 4 * h + 32 * t + 8 * a;
-                *reinterpret_cast<fbf16x4*>(kb) = bx;
-                *reinterpret_cast<fbf16x4*>(kb + H) = by;
+                if (dqkv) {
+                    *reinterpret_cast<f32x4*>(dkr + 32 * t + 8 * a) = x;
+                    *reinterpret_cast<f32x4*>(dvr + 32 * t + 8 * a) = y;
+                }
+                if (dqkvb) {
+                    fbf16x4 bx, by;
+    #pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        bx[e] = (__bf16)x[e];
+                        by[e] = (__bf16)y[e];
+                    }
+                    __bf16* kb = dqkvb + ((long)u * T + key) * ld + H + hd * 64 + 4 * h + 32 * t + 8 * a;
+                    *reinterpret_cast<fbf16x4*>(kb) = bx;
+                    *reinterpret_cast<fbf16x4*>(kb + H) = by;
+                }
             }
-        }
+    }
+    if (dq_cnt) dq_combine(dqp, dqkv, dqkvb, dq_cnt, reinterpret_cast<int*>(Ls), bh, u, hd, T, NH, H, nkb, tl, B);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -980,7 +1025,8 @@ constexpr size_t fbb_lds_bytes() {
 __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16_kernel(
     const float* __restrict__ qkv, const float* __restrict__ dctx, const float* __restrict__ lse,
     const float* __restrict__ delta, float* __restrict__ dqkv, float* __restrict__ dqp, int T, int NH, int H,
-    float scale, const int* __restrict__ tlen, int nkb, int gpb, int B, __bf16* __restrict__ dqkvb) {
+    float scale, const int* __restrict__ tlen, int nkb, int gpb, int B, __bf16* __restrict__ dqkvb,
+    int* __restrict__ dq_cnt) {
     constexpr int NW = FBB_NW, NT = NW * 64;
     constexpr int QPT = 512 / NT;
     extern __shared__ __attribute__((aligned(16))) __bf16 sm16[];
@@ -1135,29 +1181,31 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16_kernel(
         if (qt + 1 < nqt) put(buf ^ 1);
         __syncthreads();
     }
-    if (w >= ngb || key >= T) return;
-    float* dkr = dqkv + ((long)u * T + key) * ld + H + hd * 64 + 4 * h;
-    float* dvr = dkr + H;
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int a = 0; a < 4; ++a) {
-            f32x4 x, y;
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                x[b] = dk[t][4 * a + b];
-                y[b] = dv[t][4 * a + b];
+    if (w < ngb && key < T) {  // dK, dV rows of this wave's keys
+        float* dkr = dqkv + ((long)u * T + key) * ld + H + hd * 64 + 4 * h;
+        float* dvr = dkr + H;
+    #pragma unroll
+        for (int t = 0; t < 2; ++t)
+    #pragma unroll
+            for (int a = 0; a < 4; ++a) {
+                f32x4 x, y;
+    #pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    x[b] = dk[t][4 * a + b];
+                    y[b] = dv[t][4 * a + b];
+                }
+                if (dqkv) {  // null in bf16 mode when only the bf16 plane is read (the QKV input-gradient GEMM)
+                    *reinterpret_cast<f32x4*>(dkr + 32 * t + 8 * a) = x;
+                    *reinterpret_cast<f32x4*>(dvr + 32 * t + 8 * a) = y;
+                }
+                if (dqkvb) {
+                    __bf16* kb2 = dqkvb + ((long)u * T + key) * ld + H + hd * 64 + 4 * h + 32 * t + 8 * a;
+                    *reinterpret_cast<fbf16x4*>(kb2) = cvt4(x);
+                    *reinterpret_cast<fbf16x4*>(kb2 + H) = cvt4(y);
+                }
             }
-            if (dqkv) {  // null in bf16 mode when only the bf16 plane is read (the QKV input-gradient GEMM)
-                *reinterpret_cast<f32x4*>(dkr + 32 * t + 8 * a) = x;
-                *reinterpret_cast<f32x4*>(dvr + 32 * t + 8 * a) = y;
-            }
-            if (dqkvb) {
-                __bf16* kb2 = dqkvb + ((long)u * T + key) * ld + H + hd * 64 + 4 * h + 32 * t + 8 * a;
-                *reinterpret_cast<fbf16x4*>(kb2) = cvt4(x);
-                *reinterpret_cast<fbf16x4*>(kb2 + H) = cvt4(y);
-            }
-        }
+    }
+    if (dq_cnt) dq_combine(dqp, dqkv, dqkvb, dq_cnt, reinterpret_cast<int*>(Ls), bh, u, hd, T, NH, H, nkb, tl, B);
 }
 
 // backward on bf16 operand planes (config C4 with bf16 planes): K and V rows of the wave's keys, the
@@ -1171,7 +1219,8 @@ constexpr size_t fbbp_lds_bytes() { return 2 * ((size_t)(64 + 32) * FBB_KB + 2 *
 __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
     const __bf16* __restrict__ qkvb, const __bf16* __restrict__ dob, const float* __restrict__ lse,
     const float* __restrict__ delta, float* __restrict__ dqkv, float* __restrict__ dqp, int T, int NH, int H,
-    float scale, const int* __restrict__ tlen, int nkb, int gpb, int B, __bf16* __restrict__ dqkvb) {
+    float scale, const int* __restrict__ tlen, int nkb, int gpb, int B, __bf16* __restrict__ dqkvb,
+    int* __restrict__ dq_cnt) {
     constexpr int NW = FBB_NW, NT = NW * 64;
     extern __shared__ __attribute__((aligned(16))) __bf16 sm16[];
     __bf16* Kt = sm16;                            // [64][FBB_KB]   K^T of the block's keys
@@ -1336,29 +1385,31 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
         tile(qt + 1, sb, sa);
     }
     if (qt < nqt) tile(qt, sa, sb);
-    if (w >= ngb || key >= T) return;
-    float* dkr = dqkv + ((long)u * T + key) * ld + H + hd * 64 + 4 * h;
-    float* dvr = dkr + H;
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int a = 0; a < 4; ++a) {
-            f32x4 x, y;
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                x[b] = dk[t][4 * a + b];
-                y[b] = dv[t][4 * a + b];
+    if (w < ngb && key < T) {  // dK, dV rows of this wave's keys
+        float* dkr = dqkv + ((long)u * T + key) * ld + H + hd * 64 + 4 * h;
+        float* dvr = dkr + H;
+    #pragma unroll
+        for (int t = 0; t < 2; ++t)
+    #pragma unroll
+            for (int a = 0; a < 4; ++a) {
+                f32x4 x, y;
+    #pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    x[b] = dk[t][4 * a + b];
+                    y[b] = dv[t][4 * a + b];
+                }
+                if (dqkv) {  // null in bf16 mode when only the bf16 plane is read (the QKV input-gradient GEMM)
+                    *reinterpret_cast<f32x4*>(dkr + 32 * t + 8 * a) = x;
+                    *reinterpret_cast<f32x4*>(dvr + 32 * t + 8 * a) = y;
+                }
+                if (dqkvb) {
+                    __bf16* kb2 = dqkvb + ((long)u * T + key) * ld + H + hd * 64 + 4 * h + 32 * t + 8 * a;
+                    *reinterpret_cast<fbf16x4*>(kb2) = cvt4(x);
+                    *reinterpret_cast<fbf16x4*>(kb2 + H) = cvt4(y);
+                }
             }
-            if (dqkv) {  // null in bf16 mode when only the bf16 plane is read (the QKV input-gradient GEMM)
-                *reinterpret_cast<f32x4*>(dkr + 32 * t + 8 * a) = x;
-                *reinterpret_cast<f32x4*>(dvr + 32 * t + 8 * a) = y;
-            }
-            if (dqkvb) {
-                __bf16* kb2 = dqkvb + ((long)u * T + key) * ld + H + hd * 64 + 4 * h + 32 * t + 8 * a;
-                *reinterpret_cast<fbf16x4*>(kb2) = cvt4(x);
-                *reinterpret_cast<fbf16x4*>(kb2 + H) = cvt4(y);
-            }
-        }
+    }
+    if (dq_cnt) dq_combine(dqp, dqkv, dqkvb, dq_cnt, reinterpret_cast<int*>(Ls), bh, u, hd, T, NH, H, nkb, tl, B);
 }
 
 // dQ = sum over key blocks in order (query rows < tl; rows past it get 0, as their dS is 0)
@@ -1408,7 +1459,7 @@ static bool fb_img() { return suta_switches().flash_bf16_img != 0; }
 
 long flash_dq_scratch_floats(int B, int T, int NH) {
     const int ng = (T + 31) / 32, nkb = (ng + fb_nw() - 1) / fb_nw();
-    return (long)nkb * B * NH * T * 64;
+    return (long)nkb * B * NH * T * 64 + (long)B * NH + 64;  // partials, then the per-head tickets (dq_combine)
 }
 
 // bf16 mode, bf16 qkv plane given: flash_fwd_bf16p_kernel (env SUTA_FLASH_FWD_PLANE=0 keeps the fp32-row
@@ -1452,7 +1503,7 @@ bool launch_flash_fwd(const float* qkv, float* ctx, float* lse, int B, int T, in
 template <int NW, bool BF16>
 static void flash_bwd_go(dim3 grid, hipStream_t st, const float* qkv, const float* dctx, const float* lse,
                          const float* delta, float* dqkv, float* dqp, int T, int NH, int H, float scale,
-                         const int* tlen, int nkb, int gpb, int B, __bf16* dqkvb) {
+                         const int* tlen, int nkb, int gpb, int B, __bf16* dqkvb, int* cnt) {
     constexpr size_t lds = fb_lds_bytes<NW>();
     static bool attr = false;
     if (!attr) {
@@ -1462,7 +1513,7 @@ static void flash_bwd_go(dim3 grid, hipStream_t st, const float* qkv, const floa
         attr = true;
     }
     hipLaunchKernelGGL((flash_bwd_kernel<NW, BF16>), grid, dim3(NW * 64), lds, st, qkv, dctx, lse, delta, dqkv, dqp,
-                       T, NH, H, scale, tlen, nkb, gpb, B, dqkvb);
+                       T, NH, H, scale, tlen, nkb, gpb, B, dqkvb, cnt);
 }
 
 // bf16 mode, bf16 planes of qkv and dctx given: flash_bwd_bf16p_kernel (env SUTA_FLASH_BWD_PLANE=0 keeps the
@@ -1484,6 +1535,14 @@ bool launch_flash_bwd(const float* qkv, const float* dctx, const float* lse, con
     const int gpb = (ng + nkb - 1) / nkb;  // key groups per block (balanced)
     const dim3 grid((unsigned)((long)B * NH * nkb));
     const bool on_planes = flash_bwd_reads_planes(bf16, qkvb, dctxb, H);
+    // SUTA_DQ_INLAUNCH (default): the dQ partials combined by the last key block of each head (dq_combine), the
+    // per-head tickets zeroed ahead of the launch; 0: the separate flash_dq_reduce pass
+    int* cnt = nullptr;
+    if (suta_switches().dq_inlaunch) {
+        cnt = reinterpret_cast<int*>(dqp + (long)nkb * B * NH * T * 64);
+        if (hipMemsetAsync(cnt, 0, sizeof(int) * (size_t)B * NH, st) != hipSuccess)
+            throw std::runtime_error("flash_bwd: ticket memset failed");
+    }
     if (!qkv && !on_planes) throw std::invalid_argument("flash_bwd: fp32 qkv not written and the plane kernel not taken");
     if (on_planes) {
         if ((reinterpret_cast<uintptr_t>(qkvb) | reinterpret_cast<uintptr_t>(dctxb)) & 15)
@@ -1498,7 +1557,7 @@ bool launch_flash_bwd(const float* qkv, const float* dctx, const float* lse, con
         }
         hipLaunchKernelGGL(flash_bwd_bf16p_kernel, grid, dim3(FBB_NW * 64), lds, st,
                            reinterpret_cast<const __bf16*>(qkvb), reinterpret_cast<const __bf16*>(dctxb), lse, delta,
-                           dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb);
+                           dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb, cnt);
     } else if (bf16 && nw == FBB_NW && fb_img()) {
         constexpr size_t lds = fbb_lds_bytes();
         static bool attr = false;
@@ -1509,16 +1568,18 @@ bool launch_flash_bwd(const float* qkv, const float* dctx, const float* lse, con
             attr = true;
         }
         hipLaunchKernelGGL(flash_bwd_bf16_kernel, grid, dim3(FBB_NW * 64), lds, st, qkv, dctx, lse, delta, dqkv, dqp,
-                           T, NH, H, scale, tlen, nkb, gpb, B, dqkvb);
+                           T, NH, H, scale, tlen, nkb, gpb, B, dqkvb, cnt);
     } else if (nw == 4) {
-        if (bf16) flash_bwd_go<4, true>(grid, st, qkv, dctx, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb);
-        else flash_bwd_go<4, false>(grid, st, qkv, dctx, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb);
+        if (bf16) flash_bwd_go<4, true>(grid, st, qkv, dctx, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb, cnt);
+        else flash_bwd_go<4, false>(grid, st, qkv, dctx, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb, cnt);
     } else {
-        if (bf16) flash_bwd_go<8, true>(grid, st, qkv, dctx, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb);
-        else flash_bwd_go<8, false>(grid, st, qkv, dctx, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb);
+        if (bf16) flash_bwd_go<8, true>(grid, st, qkv, dctx, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb, cnt);
+        else flash_bwd_go<8, false>(grid, st, qkv, dctx, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb, cnt);
     }
-    const long n4 = (long)B * NH * T * 16;
-    hipLaunchKernelGGL(flash_dq_reduce, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, dqp, dqkv, B, T, NH, H,
-                       nkb, tlen, dqkvb);
+    if (!cnt) {
+        const long n4 = (long)B * NH * T * 16;
+        hipLaunchKernelGGL(flash_dq_reduce, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, dqp, dqkv, B, T, NH, H,
+                           nkb, tlen, dqkvb);
+    }
     return true;
 }

@@ -284,6 +284,31 @@ def test_bf16_fused_delta_bitwise_equals_separate_pass(monkeypatch):
         assert np.array_equal(v, params["0"][n]), n
 
 
+@pytest.mark.parametrize("model,precision", [("wav2vec2-base", "fp32"), ("wav2vec2-large", "bf16")])
+def test_dq_inlaunch_bitwise_equals_reduce_pass(monkeypatch, model, precision):
+    """The flash backward's dQ partials combined in-launch by each head's last-arriving key block (dq_combine: release
+    fence, ticket, acquire; SUTA_DQ_INLAUNCH=1, default) against the separate flash_dq_reduce pass (=0): both sum the
+    key blocks' partials in block order, so logits and adapted tensors are bitwise equal.  A ragged pair whose longer
+    utterance (T = 474: 15 key groups -> two key blocks per head) exercises the multi-block combination; exact fp32
+    (flash_bwd_kernel) and bf16 planes (flash_bwd_bf16p_kernel)."""
+    cfg = get_config(model)
+    sd = synth_weights(cfg)
+    waves = [synth.wave(152000, 88), synth.wave(64000, 89)]
+    out, params = {}, {}
+    for v in ("1", "0"):
+        monkeypatch.setenv("SUTA_DQ_INLAUNCH", v)
+        eng = SutaEngine(cfg, sd, max_batch=2, max_samples=152000)
+        eng.set_precision(precision)
+        out[v], _, _ = eng.adapt_varlen(waves, 2, SutaHParams(), record=[0, 2])
+        params[v] = {n: eng.get_param(1, n) for n in eng.trainable_names()}
+        eng.close()
+    for r in (0, 2):
+        for u in range(2):
+            assert np.array_equal(out["1"][r][u], out["0"][r][u]), (r, u)
+    for n, v in params["1"].items():
+        assert np.array_equal(v, params["0"][n]), n
+
+
 def test_bf16_epilogue_gelu_as_equals_erff(monkeypatch):
     """The bf16-plane GEMM epilogues' GELU / GELU' (common.h gelu2_bf16ep / dgelu2_bf16ep: Abramowitz & Stegun 7.1.28
     erf, |error| <= 3e-7, packed fp32, default) against erff (SUTA_FAST_GELU=0), wav2vec2-large in bf16 mode: the
