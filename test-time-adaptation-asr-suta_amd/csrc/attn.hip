@@ -1535,8 +1535,10 @@ bool launch_flash_bwd(const float* qkv, const float* dctx, const float* lse, con
     const int gpb = (ng + nkb - 1) / nkb;  // key groups per block (balanced)
     const dim3 grid((unsigned)((long)B * NH * nkb));
     const bool on_planes = flash_bwd_reads_planes(bf16, qkvb, dctxb, H);
-    // SUTA_DQ_INLAUNCH (default): the dQ partials combined by the last key block of each head (dq_combine), the
-    // per-head tickets zeroed ahead of the launch; 0: the separate flash_dq_reduce pass
+    // SUTA_DQ_INLAUNCH=1: the dQ partials combined by the last key block of each head (dq_combine), the per-head
+    // tickets zeroed ahead of the launch; default 0: the separate flash_dq_reduce pass (same-box C4: attention 544 vs
+    // 675 ms per call with the combine -- the reducing block reads both 102-KB partials of its head serially, the
+    // guide's "worth it when the slabs are a few tens of KB" bound)
     int* cnt = nullptr;
     if (suta_switches().dq_inlaunch) {
         cnt = reinterpret_cast<int*>(dqp + (long)nkb * B * NH * T * 64);

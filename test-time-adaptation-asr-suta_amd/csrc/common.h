@@ -80,8 +80,9 @@ struct SutaSwitches {
     int hbx_form;         // SUTA_HBX_FORM (default 2): the 256 x 256 kernel's main loop with the C^T staged epilogue
                           // (SUTA_HBX_T=2) and K % 64 == 0: 2 four-phase 64-deep K-tiles with two wave groups one
                           // barrier apart + s_setprio (gemm_hbp_kernel), 1 the same in lockstep, 0 the 32-deep slice ring
-    int dq_inlaunch;      // SUTA_DQ_INLAUNCH (default 1): flash-backward dQ partials combined in-launch by each head's last
-                          // key block; 0 = the separate flash_dq_reduce pass
+    int dq_inlaunch;      // SUTA_DQ_INLAUNCH (default 0): 1 = flash-backward dQ partials combined in-launch by each head's
+                          // last key block (measured slower: C4 attention 544 -> 675 ms per call, the last block reads
+                          // 2 x 102 KB of partials serially); 0 = the separate flash_dq_reduce pass
     int hbx_dbg;          // SUTA_HBX_DBG (tools/hb_bench diagnostics; wrong results): gemm_hbx with parts of its loop removed
     int fused_delta;      // SUTA_FUSED_DELTA (default 1): the flash backward's delta in the dctx GEMM's epilogue
     int hbx_t;            // SUTA_HBX_T (default 2): gemm_hbx accumulates C^T fragments with a row-per-lane epilogue whose

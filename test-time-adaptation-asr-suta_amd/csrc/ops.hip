@@ -1826,7 +1826,8 @@ void suta_latch_switches() {
     const char* hbxt = std::getenv("SUTA_HBX_T");
     s.hbx_t = hbxt ? std::min(2, std::max(0, atoi(hbxt))) : 2;
     s.fused_delta = on("SUTA_FUSED_DELTA");
-    s.dq_inlaunch = on("SUTA_DQ_INLAUNCH");
+    const char* dqi = std::getenv("SUTA_DQ_INLAUNCH");
+    s.dq_inlaunch = dqi ? atoi(dqi) : 0;
     const char* hform = std::getenv("SUTA_HBX_FORM");
     s.hbx_form = hform ? atoi(hform) : 2;
     const char* hdbg = std::getenv("SUTA_HBX_DBG");

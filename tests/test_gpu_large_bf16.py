@@ -287,7 +287,7 @@ def test_bf16_fused_delta_bitwise_equals_separate_pass(monkeypatch):
 @pytest.mark.parametrize("model,precision", [("wav2vec2-base", "fp32"), ("wav2vec2-large", "bf16")])
 def test_dq_inlaunch_bitwise_equals_reduce_pass(monkeypatch, model, precision):
     """The flash backward's dQ partials combined in-launch by each head's last-arriving key block (dq_combine: release
-    fence, ticket, acquire; SUTA_DQ_INLAUNCH=1, default) against the separate flash_dq_reduce pass (=0): both sum the
+    fence, ticket, acquire; SUTA_DQ_INLAUNCH=1, opt-in) against the separate flash_dq_reduce pass (=0, default): both sum the
     key blocks' partials in block order, so logits and adapted tensors are bitwise equal.  A ragged pair whose longer
     utterance (T = 474: 15 key groups -> two key blocks per head) exercises the multi-block combination; exact fp32
     (flash_bwd_kernel) and bf16 planes (flash_bwd_bf16p_kernel)."""
