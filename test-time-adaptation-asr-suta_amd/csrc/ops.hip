@@ -437,7 +437,9 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* __restr
 // Vectorised LayerNorm forward for D = 256 * NV: one wave per row, lane l owns the 16-B column
 // groups l + 64 i.  gamma / beta are read as scalars (their offsets in the flat parameter buffer need
 // not be 16-B aligned).
-template <int NV, bool GV, bool XB = false>  // XB: x is a bf16 plane (widened exactly on load)
+// RPW rows per wave (the bf16-input conv-stack instantiation): every row's loads are issued before the first row's
+// reductions, RPW x the bytes in flight per wave (a 1-KB bf16 row per wave kept the conv LayerNorms latency-bound)
+template <int NV, bool GV, bool XB = false, int RPW = 1>  // XB: x is a bf16 plane (widened exactly on load)
 __global__ __launch_bounds__(256) void layernorm_fwd_vec_kernel(const float* __restrict__ x,
                                                                 const float* __restrict__ g,
                                                                 const float* __restrict__ beta, long pstride,
@@ -447,15 +449,27 @@ __global__ __launch_bounds__(256) void layernorm_fwd_vec_kernel(const float* __r
                                                                 __bf16* __restrict__ yb, float* __restrict__ meanp) {
     constexpr int D = 256 * NV;
     const int lane = threadIdx.x & 63;
-    const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const long row0 = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
+    f32x4 vv[RPW][NV];
+#pragma unroll
+    for (int j = 0; j < RPW; ++j) {
+        const long rj = min(row0 + j, (long)rows - 1);
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            if constexpr (XB) vv[j][i] = load_bf16x4(reinterpret_cast<const __bf16*>(x) + rj * D + 4 * (lane + 64 * i));
+            else vv[j][i] = reinterpret_cast<const f32x4*>(x + rj * D)[lane + 64 * i];
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < RPW; ++j) {
+    const long row = row0 + j;
     if (row >= rows) return;
     const int u = (int)(row / rows_per_utt);
     f32x4 v[NV];
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
-        if constexpr (XB) v[i] = load_bf16x4(reinterpret_cast<const __bf16*>(x) + row * D + 4 * (lane + 64 * i));
-        else v[i] = reinterpret_cast<const f32x4*>(x + row * D)[lane + 64 * i];
+        v[i] = vv[j][i];
         s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
     }
     s = wave_sum(s);
@@ -499,6 +513,7 @@ __global__ __launch_bounds__(256) void layernorm_fwd_vec_kernel(const float* __r
     if (lane == 0) {
         rstd[row] = rs;
         if (meanp) meanp[row] = mean;
+    }
     }
 }
 
@@ -1484,10 +1499,18 @@ void launch_layernorm_fwd(const float* x, const float* g, const float* beta, lon
             !al(beta, 16) || pstride % 4)
             throw std::invalid_argument("layernorm_fwd: a bf16 input plane needs the vectorised widths");
         const float* xp = reinterpret_cast<const float*>(xb);
-        const dim3 grid(cdiv(rows, 4));
+        // SUTA_LN_RPW (switch snapshot): rows per wave of the bf16-input (conv stack) forward, 1 or 2
+        const int rpw = suta_switches().ln_rpw == 2 ? 2 : 1;
+        const dim3 grid(cdiv(rows, 4 * rpw));
 #define LNFB(NV_)                                                                                                  \
-        hipLaunchKernelGGL((layernorm_fwd_vec_kernel<NV_, true, true>), grid, dim3(256), 0, st, xp, g, beta, pstride,    \
-                           rows_per_utt, y, xhat, rstd, rows, eps, gelu_out, yb, mean)
+        do {                                                                                                       \
+            if (rpw == 2)                                                                                          \
+                hipLaunchKernelGGL((layernorm_fwd_vec_kernel<NV_, true, true, 2>), grid, dim3(256), 0, st, xp, g, beta, \
+                                   pstride, rows_per_utt, y, xhat, rstd, rows, eps, gelu_out, yb, mean);           \
+            else                                                                                                   \
+                hipLaunchKernelGGL((layernorm_fwd_vec_kernel<NV_, true, true>), grid, dim3(256), 0, st, xp, g, beta,   \
+                                   pstride, rows_per_utt, y, xhat, rstd, rows, eps, gelu_out, yb, mean);           \
+        } while (0)
         if (D == 768) LNFB(3);
         else if (D == 1024) LNFB(4);
         else LNFB(2);
@@ -1828,6 +1851,8 @@ void suta_latch_switches() {
     s.fused_delta = on("SUTA_FUSED_DELTA");
     const char* dqi = std::getenv("SUTA_DQ_INLAUNCH");
     s.dq_inlaunch = dqi ? atoi(dqi) : 0;
+    const char* lrpw = std::getenv("SUTA_LN_RPW");
+    s.ln_rpw = lrpw ? atoi(lrpw) : 2;
     const char* hform = std::getenv("SUTA_HBX_FORM");
     s.hbx_form = hform ? atoi(hform) : 2;
     const char* hdbg = std::getenv("SUTA_HBX_DBG");
