@@ -80,7 +80,6 @@ struct SutaSwitches {
     int hbx_form;         // SUTA_HBX_FORM (default 2): the 256 x 256 kernel's main loop with the C^T staged epilogue
                           // (SUTA_HBX_T=2) and K % 64 == 0: 2 four-phase 64-deep K-tiles with two wave groups one
                           // barrier apart + s_setprio (gemm_hbp_kernel), 1 the same in lockstep, 0 the 32-deep slice ring
-    int lnb_pf;           // SUTA_LNB_PF (default 1): conv-stack LayerNorm backward loads the next row ahead; 0 = in order
     int ln_rpw;           // SUTA_LN_RPW (default 2): rows per wave of the bf16-input (conv stack) LayerNorm forward; 1 = one
     int dq_inlaunch;      // SUTA_DQ_INLAUNCH (default 0): 1 = flash-backward dQ partials combined in-launch by each head's
                           // last key block (measured slower: C4 attention 544 -> 675 ms per call, the last block reads

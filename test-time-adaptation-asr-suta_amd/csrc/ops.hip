@@ -633,8 +633,7 @@ __global__ __launch_bounds__(256) void layernorm_bwd_vec_kernel(
 // at 64 x 8 s on wav2vec2-large).  Rows in chunks of CROWS per block (larger chunks for the long layers
 // keep the partial slabs small); partial layout [B][nchunk][2 + 1 + KT][D]: dgamma, dbeta, dbias, dW0 rows;
 // fixed-order reductions (waves, then chunks in order): deterministic.
-// PF: the next row's loads issued before the current row is processed (SUTA_LNB_PF, default on)
-template <int NV, bool GV, int KT, bool DYB = false, bool XB = false, bool PF = true>  // DYB / XB: dy / x as bf16 planes
+template <int NV, bool GV, int KT, bool DYB = false, bool XB = false>  // DYB / XB: dy / x as bf16 planes
 __global__ __launch_bounds__(256) void layernorm_bwd_conv_kernel(
     const float* __restrict__ dy, const float* __restrict__ rstd, const float* __restrict__ g,
     const float* __restrict__ beta, long pstride, int rows_per_utt, float* __restrict__ dx, float* __restrict__ part,
@@ -666,53 +665,25 @@ __global__ __launch_bounds__(256) void layernorm_bwd_conv_kernel(
     }
     const float* xu = xw ? xw + (long)u * xws : nullptr;
     const int r0 = ch * crows, r1 = min(rows_per_utt, r0 + crows);
-    // one row's operands; the next row of the wave is loaded while the current one is processed (two rows of loads
-    // in flight per wave: at 2-3 waves per SIMD a single row in flight kept the pass latency-bound near 3.2 TB/s)
-    struct RowIn {
-        f32x4 xh[NV], gi[NV];
-        float rs, mu;
-        float xt[KT > 0 ? KT : 1];
-    };
-    auto load_row = [&](int r, RowIn& in) {
+    for (int r = r0 + w; r < r1; r += 4) {
         const long row = (long)u * rows_per_utt + r;
         const f32x4* xr = reinterpret_cast<const f32x4*>(xin + row * D);
         const f32x4* dr = reinterpret_cast<const f32x4*>(dy + row * D);
-        in.rs = rstd[row];
-        in.mu = meanp[row];
-#pragma unroll
-        for (int i = 0; i < NV; ++i) {
-            if constexpr (XB) in.xh[i] = load_bf16x4(reinterpret_cast<const __bf16*>(xin) + row * D + 4 * (lane + 64 * i));
-            else in.xh[i] = xr[lane + 64 * i];
-            if constexpr (DYB) in.gi[i] = load_bf16x4(reinterpret_cast<const __bf16*>(dy) + row * D + 4 * (lane + 64 * i));
-            else in.gi[i] = dr[lane + 64 * i];
-        }
-        if constexpr (KT > 0) {
-#pragma unroll
-            for (int k = 0; k < KT; ++k) in.xt[k] = xu[(long)xs * r + k];
-        }
-    };
-    RowIn cur, nxt;
-    if (PF && r0 + w < r1) load_row(r0 + w, cur);
-    for (int r = r0 + w; r < r1; r += 4) {
-        if constexpr (PF) {
-            if (r + 4 < r1) load_row(r + 4, nxt);
-        } else {
-            load_row(r, cur);
-        }
-        const long row = (long)u * rows_per_utt + r;
         f32x4 gi[NV], xh[NV];
         float s1 = 0.f, s2 = 0.f;
-        const float rs = cur.rs;
-        const float mu = cur.mu;
+        const float rs = rstd[row];
+        const float mu = meanp[row];
 #pragma unroll
         for (int i = 0; i < NV; ++i) {
-            xh[i] = cur.xh[i];
-            gi[i] = cur.gi[i];
+            if constexpr (XB) xh[i] = load_bf16x4(reinterpret_cast<const __bf16*>(xin) + row * D + 4 * (lane + 64 * i));
+            else xh[i] = xr[lane + 64 * i];
+            if constexpr (DYB) gi[i] = load_bf16x4(reinterpret_cast<const __bf16*>(dy) + row * D + 4 * (lane + 64 * i));
+            else gi[i] = dr[lane + 64 * i];
         }
         float xt[KT > 0 ? KT : 1];
         if constexpr (KT > 0) {
 #pragma unroll
-            for (int k = 0; k < KT; ++k) xt[k] = cur.xt[k];
+            for (int k = 0; k < KT; ++k) xt[k] = xu[(long)xs * r + k];
         }
 #pragma unroll
         for (int i = 0; i < NV; ++i)
@@ -744,7 +715,6 @@ __global__ __launch_bounds__(256) void layernorm_bwd_conv_kernel(
 #pragma unroll
             for (int k = 0; k < KT; ++k) acc[3 + k][i] += xt[k] * o;
         }
-        if constexpr (PF) cur = nxt;
     }
     f32x4* pp = reinterpret_cast<f32x4*>(part + ((long)u * nchunk + ch) * NVEC * D);
 #pragma unroll
@@ -1643,18 +1613,10 @@ bool launch_layernorm_bwd_conv(const float* dy, const float* rstd, const float* 
     const dim3 grid(nchunk, B);
     if (bf16_in) {  // conv stack on bf16 planes: 16-B gamma / beta (every SUTA layout)
         if (!gv) return false;
-        const bool pf = suta_switches().lnb_pf != 0;  // SUTA_LNB_PF (switch snapshot)
 #define LBCB(KT_, DB_, XB_)                                                                                      \
-        do {                                                                                                     \
-            if (pf)                                                                                              \
-                hipLaunchKernelGGL((layernorm_bwd_conv_kernel<2, true, KT_, DB_, XB_, true>), grid, dim3(256), 0, st, dy, \
-                                   rstd, g, beta, pstride, rows_per_utt, dx, part, nchunk, crows, x, mean, xw, xws, \
-                                   xs, reinterpret_cast<__bf16*>(dxb));                                          \
-            else                                                                                                 \
-                hipLaunchKernelGGL((layernorm_bwd_conv_kernel<2, true, KT_, DB_, XB_, false>), grid, dim3(256), 0, st, dy, \
-                                   rstd, g, beta, pstride, rows_per_utt, dx, part, nchunk, crows, x, mean, xw, xws, \
-                                   xs, reinterpret_cast<__bf16*>(dxb));                                          \
-        } while (0)
+        hipLaunchKernelGGL((layernorm_bwd_conv_kernel<2, true, KT_, DB_, XB_>), grid, dim3(256), 0, st, dy, rstd, g, beta, \
+                           pstride, rows_per_utt, dx, part, nchunk, crows, x, mean, xw, xws, xs,                    \
+                           reinterpret_cast<__bf16*>(dxb))
         if (ktaps == 10) {
             if (dyb && xb) LBCB(10, true, true);
             else if (xb) LBCB(10, false, true);
@@ -1889,7 +1851,6 @@ void suta_latch_switches() {
     s.fused_delta = on("SUTA_FUSED_DELTA");
     const char* dqi = std::getenv("SUTA_DQ_INLAUNCH");
     s.dq_inlaunch = dqi ? atoi(dqi) : 0;
-    s.lnb_pf = on("SUTA_LNB_PF");
     const char* lrpw = std::getenv("SUTA_LN_RPW");
     s.ln_rpw = lrpw ? atoi(lrpw) : 2;
     const char* hform = std::getenv("SUTA_HBX_FORM");
