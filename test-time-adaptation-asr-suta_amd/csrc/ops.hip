@@ -439,7 +439,9 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* __restr
 // not be 16-B aligned).
 // RPW rows per wave (the bf16-input conv-stack instantiation): every row's loads are issued before the first row's
 // reductions, RPW x the bytes in flight per wave (a 1-KB bf16 row per wave kept the conv LayerNorms latency-bound)
-template <int NV, bool GV, bool XB = false, int RPW = 1>  // XB: x is a bf16 plane (widened exactly on load)
+// FG (bf16-input conv-stack instantiations, SUTA_FAST_GELU): the output GELU by the packed A&S form of the bf16-plane
+// GEMM epilogues (common.h gelu2_bf16ep) instead of erff
+template <int NV, bool GV, bool XB = false, int RPW = 1, bool FG = false>  // XB: x is a bf16 plane (widened exactly)
 __global__ __launch_bounds__(256) void layernorm_fwd_vec_kernel(const float* __restrict__ x,
                                                                 const float* __restrict__ g,
                                                                 const float* __restrict__ beta, long pstride,
@@ -504,7 +506,15 @@ __global__ __launch_bounds__(256) void layernorm_fwd_vec_kernel(const float* __r
         for (int e = 0; e < 4; ++e) {
             xh[e] = (v[i][e] - mean) * rs;
             const float t = xh[e] * gg[e] + bb[e];
-            o[e] = gelu_out ? gelu_f(t) : t;
+            o[e] = (gelu_out && !FG) ? gelu_f(t) : t;
+        }
+        if (FG && gelu_out) {
+#pragma unroll
+            for (int e = 0; e < 4; e += 2) {
+                const f32x2v g2 = gelu2_bf16ep(f32x2v{o[e], o[e + 1]});
+                o[e] = g2.x;
+                o[e + 1] = g2.y;
+            }
         }
         if (xhat) reinterpret_cast<f32x4*>(xhat + row * D)[lane + 64 * i] = xh;
         if (y) reinterpret_cast<f32x4*>(y + row * D)[lane + 64 * i] = o;  // null: only the bf16 plane is read
@@ -633,7 +643,8 @@ __global__ __launch_bounds__(256) void layernorm_bwd_vec_kernel(
 // at 64 x 8 s on wav2vec2-large).  Rows in chunks of CROWS per block (larger chunks for the long layers
 // keep the partial slabs small); partial layout [B][nchunk][2 + 1 + KT][D]: dgamma, dbeta, dbias, dW0 rows;
 // fixed-order reductions (waves, then chunks in order): deterministic.
-template <int NV, bool GV, int KT, bool DYB = false, bool XB = false>  // DYB / XB: dy / x as bf16 planes
+// FG (SUTA_FAST_GELU, the bf16-plane instantiations): GELU' by the packed A&S form (common.h dgelu2_bf16ep)
+template <int NV, bool GV, int KT, bool DYB = false, bool XB = false, bool FG = false>  // DYB / XB: dy / x as bf16
 __global__ __launch_bounds__(256) void layernorm_bwd_conv_kernel(
     const float* __restrict__ dy, const float* __restrict__ rstd, const float* __restrict__ g,
     const float* __restrict__ beta, long pstride, int rows_per_utt, float* __restrict__ dx, float* __restrict__ part,
@@ -689,11 +700,22 @@ __global__ __launch_bounds__(256) void layernorm_bwd_conv_kernel(
         for (int i = 0; i < NV; ++i)
 #pragma unroll
             for (int e = 0; e < 4; ++e) xh[i][e] = (xh[i][e] - mu) * rs;  // x-hat recomputed bitwise
+        if constexpr (FG) {
+#pragma unroll
+            for (int i = 0; i < NV; ++i)
+#pragma unroll
+                for (int e = 0; e < 4; e += 2) {
+                    const f32x2v g2 = dgelu2_bf16ep(f32x2v{xh[i][e] * gam[i][e] + bet[i][e],
+                                                           xh[i][e + 1] * gam[i][e + 1] + bet[i][e + 1]});
+                    gi[i][e] *= g2.x;
+                    gi[i][e + 1] *= g2.y;
+                }
+        }
 #pragma unroll
         for (int i = 0; i < NV; ++i)
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                const float d = gi[i][e] * dgelu_f(xh[i][e] * gam[i][e] + bet[i][e]);
+                const float d = FG ? gi[i][e] : gi[i][e] * dgelu_f(xh[i][e] * gam[i][e] + bet[i][e]);
                 gi[i][e] = d;
                 acc[0][i][e] += d * xh[i][e];
                 acc[1][i][e] += d;
@@ -1499,22 +1521,26 @@ void launch_layernorm_fwd(const float* x, const float* g, const float* beta, lon
             !al(beta, 16) || pstride % 4)
             throw std::invalid_argument("layernorm_fwd: a bf16 input plane needs the vectorised widths");
         const float* xp = reinterpret_cast<const float*>(xb);
-        // SUTA_LN_RPW (switch snapshot): rows per wave of the bf16-input (conv stack) forward, 1 or 2
+        // SUTA_LN_RPW (switch snapshot): rows per wave of the bf16-input (conv stack) forward, 1 or 2; SUTA_FAST_GELU:
+        // the packed A&S GELU (FG)
         const int rpw = suta_switches().ln_rpw == 2 ? 2 : 1;
+        const bool fg = suta_switches().fast_gelu != 0;
         const dim3 grid(cdiv(rows, 4 * rpw));
+#define LNFB1(NV_, R_, F_)                                                                                          \
+        hipLaunchKernelGGL((layernorm_fwd_vec_kernel<NV_, true, true, R_, F_>), grid, dim3(256), 0, st, xp, g, beta,    \
+                           pstride, rows_per_utt, y, xhat, rstd, rows, eps, gelu_out, yb, mean)
 #define LNFB(NV_)                                                                                                  \
         do {                                                                                                       \
-            if (rpw == 2)                                                                                          \
-                hipLaunchKernelGGL((layernorm_fwd_vec_kernel<NV_, true, true, 2>), grid, dim3(256), 0, st, xp, g, beta, \
-                                   pstride, rows_per_utt, y, xhat, rstd, rows, eps, gelu_out, yb, mean);           \
-            else                                                                                                   \
-                hipLaunchKernelGGL((layernorm_fwd_vec_kernel<NV_, true, true>), grid, dim3(256), 0, st, xp, g, beta,   \
-                                   pstride, rows_per_utt, y, xhat, rstd, rows, eps, gelu_out, yb, mean);           \
+            if (rpw == 2 && fg) LNFB1(NV_, 2, true);                                                               \
+            else if (rpw == 2) LNFB1(NV_, 2, false);                                                               \
+            else if (fg) LNFB1(NV_, 1, true);                                                                      \
+            else LNFB1(NV_, 1, false);                                                                             \
         } while (0)
         if (D == 768) LNFB(3);
         else if (D == 1024) LNFB(4);
         else LNFB(2);
 #undef LNFB
+#undef LNFB1
         return;
     }
     if (!y && !(yb && (D == 768 || D == 1024 || D == 512)))
@@ -1613,10 +1639,18 @@ bool launch_layernorm_bwd_conv(const float* dy, const float* rstd, const float* 
     const dim3 grid(nchunk, B);
     if (bf16_in) {  // conv stack on bf16 planes: 16-B gamma / beta (every SUTA layout)
         if (!gv) return false;
+        const bool fg = suta_switches().fast_gelu != 0;  // SUTA_FAST_GELU: the packed A&S GELU'
 #define LBCB(KT_, DB_, XB_)                                                                                      \
-        hipLaunchKernelGGL((layernorm_bwd_conv_kernel<2, true, KT_, DB_, XB_>), grid, dim3(256), 0, st, dy, rstd, g, beta, \
-                           pstride, rows_per_utt, dx, part, nchunk, crows, x, mean, xw, xws, xs,                    \
-                           reinterpret_cast<__bf16*>(dxb))
+        do {                                                                                                     \
+            if (fg)                                                                                              \
+                hipLaunchKernelGGL((layernorm_bwd_conv_kernel<2, true, KT_, DB_, XB_, true>), grid, dim3(256), 0, st, dy, \
+                                   rstd, g, beta, pstride, rows_per_utt, dx, part, nchunk, crows, x, mean, xw, xws, \
+                                   xs, reinterpret_cast<__bf16*>(dxb));                                          \
+            else                                                                                                 \
+                hipLaunchKernelGGL((layernorm_bwd_conv_kernel<2, true, KT_, DB_, XB_>), grid, dim3(256), 0, st, dy,   \
+                                   rstd, g, beta, pstride, rows_per_utt, dx, part, nchunk, crows, x, mean, xw, xws, \
+                                   xs, reinterpret_cast<__bf16*>(dxb));                                          \
+        } while (0)
         if (ktaps == 10) {
             if (dyb && xb) LBCB(10, true, true);
             else if (xb) LBCB(10, false, true);
