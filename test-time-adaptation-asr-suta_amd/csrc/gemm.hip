@@ -203,13 +203,20 @@ static int use_hb8(const GemmParams& p) {
 // 595 / 627 and direct row-per-lane 16-B stores (32 rows per instruction) 515 / 625, so without the staged form
 // they keep the 128 x 128 kernel.
 // SUTA_HBX=0: off (A/B runs); 2: every eligible linear, any epilogue and grid (tests).
+// batched (Z > 1) GEMMs -- the conv stack's per-utterance forward -- only on the four-phase form with the staged C^T
+// epilogue (gemm_hbp_kernel rebases its operands per batch)
+static bool hbx_batch_ok(const GemmParams& p) {
+    const SutaSwitches& sw = suta_switches();
+    return p.Z == 1 || (sw.hbx_form && sw.hbx_t == 2 && !sw.hbx_dbg && p.K % 64 == 0 && hbx_t_ok(p, false));
+}
+
 static bool use_hbx(const GemmParams& p) {
     const int mode = suta_switches().hbx;
-    if (!mode || p.Z != 1 || p.segK > 0 || p.K % 32 || p.K < 128 || (p.epi & (EPI_ACCUM | EPI_SMBWD))) return false;
+    if (!mode || p.segK > 0 || p.K % 32 || p.K < 128 || (p.epi & (EPI_ACCUM | EPI_SMBWD)) || !hbx_batch_ok(p)) return false;
     if (mode == 2) return true;  // SUTA_HBX=2: every eligible linear (tests)
     if ((p.epi & (EPI_GELU | EPI_DGELU | EPI_STORE_PRE)) && !(suta_switches().hbx_t == 2 && hbx_t_ok(p, false)))
         return false;
-    return (long)((p.M + 255) / 256) * ((p.N + 255) / 256) >= 256;
+    return (long)((p.M + 255) / 256) * ((p.N + 255) / 256) * p.Z >= 256;
 }
 
 // 32-bit epilogue offsets: M x ld elements of every operand the epilogue touches within 4 GiB
@@ -271,7 +278,8 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
                : p.mode == 2   ? choose_tile_bf16(p.M, p.N, p.Z, !bf16_gbf)
                                : choose_tile(p.M, p.N, p.Z, p.K, p.mode);
     const bool glds_path = p.mode == 0 && g_nbuf == 3 && glds_ok;
-    if ((tile == 8 || tile == 9) && !(hb && p.K % 32 == 0 && p.K >= 128 && p.Z == 1 && p.segK == 0)) tile = 0;
+    if ((tile == 8 || tile == 9) && !(hb && p.K % 32 == 0 && p.K >= 128 && p.segK == 0 && (p.Z == 1 || (tile == 8 && hbx_batch_ok(p)))))
+        tile = 0;
     if (tile == 7 && !glds_path) tile = 0;  // the 160-row tile exists only in the default LDS-DMA kernel
     if (tile == 6 && !(hb && p.K % 32 == 0)) tile = 0;  // the 256 x 256 tile is the bf16-plane ping-pong kernel only
     if (g_force_tile < 0 && tile == 0 && glds_path && use_tile160(p.M, p.N, p.Z)) tile = 7;

@@ -652,8 +652,11 @@ __global__ __launch_bounds__(512, 1) void gemm_hbp_kernel(GemmParams p) {
     __shared__ __attribute__((aligned(16))) float smem[8 * P_HALF / 4];
     char* const lds = reinterpret_cast<char*>(smem);
     const TileId tid = xcd_tile(p.order);
-    const __bf16* A = reinterpret_cast<const __bf16*>(p.Ab);
-    const __bf16* B = reinterpret_cast<const __bf16*>(p.Bb);
+    // batch z (Z-batched GEMMs, the conv stack's per-utterance forward): operand planes offset in bf16 elements, the
+    // epilogue's operands through a rebased copy of the parameters (batch z of a Z = 1 view)
+    const int z1 = tid.z / p.zdiv, z0 = tid.z % p.zdiv;
+    const __bf16* A = reinterpret_cast<const __bf16*>(p.Ab) + z1 * p.sA1 + z0 * p.sA0;
+    const __bf16* B = reinterpret_cast<const __bf16*>(p.Bb) + z1 * p.sB1 + z0 * p.sB0;
     const int m0 = tid.y * 256, n0 = tid.x * 256;
     const int nk = p.K / 64;
     const int lane = threadIdx.x & 63;
@@ -781,7 +784,22 @@ __global__ __launch_bounds__(512, 1) void gemm_hbp_kernel(GemmParams p) {
         if (wr == 0) __builtin_amdgcn_s_barrier();  // the leading group's matching barrier
     }
     __syncthreads();  // every wave is done with the buffers: wave-private 16-KB staging images
-    epilogue_t<CB, EM, true>(p, acc, m0 + wr * 128, n0 + wc * 64, lane, lds + wid * 16384);
+    {  // (one epilogue instantiation: for Z = 1 the rebase adds zero)
+        GemmParams q = p;
+        const bool preb = CB && p.preb;
+        if (p.C) q.C = p.C + z1 * p.sC1 + z0 * p.sC0;
+        if (p.Cb) q.Cb = reinterpret_cast<__bf16*>(p.Cb) + z1 * p.sCb1;
+        if (p.bias) q.bias = p.bias + z1 * p.sBias1 + z0 * p.sBias0;
+        if (p.R) q.R = p.R + z1 * p.sR1 + z0 * p.sR0;
+        if (p.aux)
+            q.aux = preb ? reinterpret_cast<const float*>(reinterpret_cast<const __bf16*>(p.aux) + z1 * p.sAux1 + z0 * p.sAux0)
+                         : p.aux + z1 * p.sAux1 + z0 * p.sAux0;
+        if (p.C2)
+            q.C2 = preb ? reinterpret_cast<float*>(reinterpret_cast<__bf16*>(p.C2) + z1 * p.sC21 + z0 * p.sC20)
+                        : p.C2 + z1 * p.sC21 + z0 * p.sC20;
+        if (p.zrows) q.zrows = p.zrows + z1;
+        epilogue_t<CB, EM, true>(q, acc, m0 + wr * 128, n0 + wc * 64, lane, lds + wid * 16384);
+    }
 }
 
 template <int MS, int EM, int TR = 0>
@@ -804,6 +822,15 @@ bool hbx_t_ok(const GemmParams& p, bool check_off32) {
     const bool preb = p.Cb && p.preb;
     if ((e & EPI_DGELU) && !(a16(p.aux) && p.ldaux % (preb ? 8 : 4) == 0)) return false;
     if ((e & EPI_STORE_PRE) && !(a16(p.C2) && p.ldc2 % (preb ? 8 : 4) == 0)) return false;
+    if (p.Z > 1) {  // batch strides keep every row base 16-B aligned (planes in bf16 elements, fp32 operands in floats)
+        if (((p.sA0 | p.sA1 | p.sB0 | p.sB1) % 8) || (p.Cb && (p.sCb1 % 8 || p.zdiv != 1)) ||
+            ((!p.Cb || p.C) && ((p.sC0 | p.sC1) % 4)) || ((e & EPI_BIAS) && ((p.sBias0 | p.sBias1) % 4)) ||
+            ((e & EPI_RESID) && ((p.sR0 | p.sR1) % 4)) || (e & EPI_DELTA))
+            return false;
+        const long sa = preb ? 8 : 4;
+        if (((e & EPI_DGELU) && ((p.sAux0 | p.sAux1) % sa)) || ((e & EPI_STORE_PRE) && ((p.sC20 | p.sC21) % sa)))
+            return false;
+    }
     if ((e & EPI_DELTA) && !(e == EPI_DELTA && a16(p.dlt_o) && p.ldo % 4 == 0 && p.delta && p.dT > 0 &&
                              (long)p.dNH * 64 == p.N && p.M % p.dT == 0))
         return false;
@@ -825,8 +852,11 @@ constexpr int XEM_L = EPI_DELTA;  // the attention out-projection's input gradie
 // classes, the generic one otherwise); 2: v_mfma_f32_16x16x32_bf16 with epilogue16 (the linears' classes only)
 void gemm_run_hbx(int variant, const GemmParams& p, dim3 grid, hipStream_t st) {
     const int e = p.epi;
-    if (p.splits > 1 || p.Z != 1 || (e & (EPI_ACCUM | EPI_SMBWD)))
-        throw std::invalid_argument("hbx: no split-K, batches, ACCUM or SMBWD");
+    if (p.splits > 1 || (e & (EPI_ACCUM | EPI_SMBWD)))
+        throw std::invalid_argument("hbx: no split-K, ACCUM or SMBWD");
+    if (p.Z != 1 && !(variant == 1 && suta_switches().hbx_form && suta_switches().hbx_t == 2 && p.K % 64 == 0 &&
+                      hbx_t_ok(p, true) && !suta_switches().hbx_dbg))
+        throw std::invalid_argument("hbx: batched GEMMs only on the four-phase form with the staged C^T epilogue");
     if ((e & EPI_DELTA) && !(variant == 1 && suta_switches().hbx_t && hbx_t_ok(p, true)))
         throw std::invalid_argument("hbx: EPI_DELTA needs the C^T epilogue and its operand conditions");
     if (variant == 2) {
