@@ -20,7 +20,8 @@
 // for the ds_read_b128 lane groups of both MFMA shapes (32x32x16: lane -> row l & 31, chunk 2 kc + (l >> 5);
 // 16x16x32: row l & 15, chunk l >> 4): the 16 lanes of a group land on 16 distinct 16-B bank slots.
 // MS: MFMA shape, 32 (v_mfma_f32_32x32x16_bf16, the epilogue's fragment form) or 16 (v_mfma_f32_16x16x32_bf16).
-// Requires K % 32 == 0 and K >= 128, no split-K, Z == 1, no conv-A rows (the dispatcher's conditions).
+// Requires K % 32 == 0 and K >= 128, no split-K, no conv-A rows, and Z == 1 except on the four-phase form
+// (gemm_hbp_kernel below, K % 64 == 0), which rebases its operands per batch (the dispatcher's conditions).
 #include "gemm_kernels.h"
 #include <cstdint>
 #include <cstdlib>
