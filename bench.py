@@ -43,6 +43,7 @@ BF16_PEAK_TFLOPS = 2500.0      # MI355X_MICROARCH.md: bf16 dense MFMA peak
 BF16_SPLIT_PEAK_TFLOPS = BF16_PEAK_TFLOPS / 6
 HBM_PEAK_TBS = 8.0             # MI355X_MICROARCH.md: HBM3E peak
 RECORD = [0, 1, 3, 5, 10]
+C4_RECORD = [0, 1, 5, 10, 20]   # config C4 (20 steps): greedy ids recorded at these steps
 # newest committed rocprofv3 PMC reduction of each workload (tools/pmc_traffic.py; profiles/<round>/README.md)
 ROUNDS = ("r4", "r3", "r2", "r1")
 PMC_TRAFFIC = next((p for p in (os.path.join(ROOT, "profiles", r, "pmc_traffic.json") for r in ROUNDS)
@@ -370,7 +371,7 @@ def bench_c4(args, dev):
     eng = SutaEngine(cfg, synth_weights(cfg), device=dev, max_batch=B, max_samples=N)
     eng.set_precision("bf16")
     hp = SutaHParams()
-    rec = [0, 1, 5, 10, 20]
+    rec = C4_RECORD
     steps = max(1, args.steps // 2)
     waves = [torch.from_numpy(synth.batch(N, B, start=50000 + i * B)).to(f"cuda:{dev}") for i in range(steps + 1)]
     eng.adapt(waves[0], S, hp, record=rec, want_logits=False)

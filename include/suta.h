@@ -85,7 +85,19 @@ typedef struct suta_hparams {
     int32_t episodic;     /* --episodic: reset every slot before adapting */
     float pl_coef;        /* SDPL (main_SDPL.py:143-209): loss = (1 - pl_coef) * SUTA + pl_coef *
                              pseudo-label CTC; 0 = SUTA only (main.py); main_SDPL's driver passes 1 */
+    int32_t optimizer;    /* --opt (main.py:9-18): SUTA_OPT_ADAMW (AdamW, or Adam: identical at weight decay 0)
+                             or SUTA_OPT_SGD (torch.optim.SGD(lr, weight_decay=0): p -= lr * g once per
+                             collect_params entry, the single-tensor order) */
+    int32_t lr_step_size; /* --scheduler torch.optim.lr_scheduler.StepLR (main.py:20-21: step_size 1, gamma
+                             0.7), stepped after every optimizer step (main.py:207-208) and restored with the
+                             episodic reset (main.py:147-152): optimizer step i (counted from the last reset)
+                             uses lr * gamma^floor(i / lr_step_size), the products taken in double as torch
+                             does; 0 = no scheduler */
+    float lr_gamma;
 } suta_hparams;
+
+#define SUTA_OPT_ADAMW 0
+#define SUTA_OPT_SGD 1
 
 /* Weights: `n` tensors named by their HF state_dict key (e.g.
  * "wav2vec2.encoder.layers.0.attention.q_proj.weight"), float32, host memory, HF layout.
@@ -208,6 +220,15 @@ int32_t suta_set_precision(suta_engine* e, int32_t mode);
  * logits and greedy ids into device staging -- is captured once as one graph and replayed per call;
  * a call with a new key runs eagerly.  Per-kernel timing (suta_set_timing) disables it. */
 int32_t suta_set_graphs(suta_engine* e, int32_t enable);
+
+/* How the last suta_adapt / suta_adapt_varlen call ran its loop, and totals over the engine's life
+ * (instrumentation, no reference counterpart; tests pin that the bench's timed mode -- graph replay --
+ * is the one checked against the oracle): last_mode_out = 0 eager, 1 captured then launched, 2 replayed
+ * an earlier capture; captures_out / launches_out = graphs captured / graph launches so far. */
+#define SUTA_LOOP_EAGER 0
+#define SUTA_LOOP_CAPTURED 1
+#define SUTA_LOOP_REPLAYED 2
+int32_t suta_get_graph_stats(suta_engine* e, int32_t* last_mode_out, int64_t* captures_out, int64_t* launches_out);
 
 const char* suta_last_error(void);
 

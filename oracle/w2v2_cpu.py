@@ -308,23 +308,63 @@ def adam_step(params: Dict[str, torch.Tensor], grads: Dict[str, torch.Tensor], s
             p.addcdiv_(state.m[n], denom, value=-step_size)
 
 
+def sgd_step(params: Dict[str, torch.Tensor], grads: Dict[str, torch.Tensor], entries: Sequence[str],
+             lr: float) -> None:
+    """One torch.optim.SGD(params, lr, weight_decay=0).step() (main.py:18; sgd.py _single_tensor_sgd at momentum 0):
+    param.add_(grad, alpha=-lr) once per entry, in list order (a tensor listed k times moves k times)."""
+    with torch.no_grad():
+        for n in entries:
+            params[n].add_(grads[n], alpha=-lr)
+
+
+def step_lr(lr: float, gamma: float, step_size: int, i: int) -> float:
+    """The lr StepLR (main.py:20-21: eval(scheduler)(optimizer, step_size=1, gamma=0.7)) leaves in the param group
+    after i scheduler steps (main.py:207-208): the group lr times gamma, in double, at every step count that is a
+    multiple of step_size (lr_scheduler.py StepLR.get_lr, chained form).  step_size 0: no scheduler."""
+    if step_size <= 0:
+        return lr
+    for e in range(1, i + 1):
+        if e % step_size == 0:
+            lr = lr * gamma
+    return lr
+
+
+class OptCarry:
+    """Optimizer / scheduler state carried from one utterance to the next in non-episodic runs (the reference
+    never restores it then, main.py:327-328): the adapted tensors, Adam moments and the optimizer step count."""
+
+    def __init__(self):
+        self.params = None
+        self.state = None
+        self.nstep = 0
+
+
 # ----------------------------------------------------------------------------------------------
 # Episodic SUTA on one utterance (reference main.py:327-398 + forward_and_adapt main.py:172-215)
 # ----------------------------------------------------------------------------------------------
 def run_suta(params0: Dict[str, torch.Tensor], cfg: dict, x: torch.Tensor, steps: int, *, lr=2e-5, temp=2.5,
              em_coef=0.3, reweight=True, non_blank=True, div_coef=0.0, train_feature=True, bias_only=False,
-             record: Sequence[int] = None, pl_coef: float = 0.0) -> Tuple[Dict[int, torch.Tensor], Dict[str, torch.Tensor]]:
+             record: Sequence[int] = None, pl_coef: float = 0.0, opt: str = "AdamW", lr_step_size: int = 0,
+             lr_gamma: float = 0.7, carry: OptCarry = None) -> Tuple[Dict[int, torch.Tensor], Dict[str, torch.Tensor]]:
     """Returns ({r: logits after r updates} for r in record (0 = vanilla), final trainable tensors).
 
     Uses the minimal schedule (S+1 forwards, S backwards): the re-inference forward of
     step i (main.py:212-214) equals the grad forward of step i+1 (same params, same x).
+    opt: 'AdamW' / 'Adam' (identical at weight decay 0) or 'SGD' (main.py:9-18); lr_step_size > 0: StepLR
+    (main.py:20-21).  carry: non-episodic state from the previous utterance (None = episodic reset).
     """
     if record is None:
         record = list(range(steps + 1))
-    params = {k: v.detach().clone() for k, v in params0.items()}
+    if opt not in ("AdamW", "Adam", "SGD"):
+        raise ValueError(opt)
     entries = trainable_entries(cfg, bias_only=bias_only, train_feature=train_feature)
     uniq = list(dict.fromkeys(entries))
-    state = AdamState(uniq, params)
+    if carry is not None and carry.params is not None:
+        params, state = carry.params, carry.state
+    else:
+        params = {k: v.detach().clone() for k, v in params0.items()}
+        state = AdamState(uniq, params)
+    nstep = carry.nstep if carry is not None else 0
     out: Dict[int, torch.Tensor] = {}
     for i in range(steps + 1):
         for n in uniq:
@@ -339,7 +379,16 @@ def run_suta(params0: Dict[str, torch.Tensor], cfg: dict, x: torch.Tensor, steps
         else:
             loss = suta_loss(logits, em_coef, reweight, temp, non_blank, div_coef)
         grads = torch.autograd.grad(loss, [params[n] for n in uniq])
-        adam_step(params, dict(zip(uniq, grads)), state, entries, lr)
+        lr_i = step_lr(lr, lr_gamma, lr_step_size, nstep)
+        if opt == "SGD":
+            sgd_step(params, dict(zip(uniq, grads)), entries, lr_i)
+        else:
+            adam_step(params, dict(zip(uniq, grads)), state, entries, lr_i)
+        nstep += 1
+    if carry is not None:
+        for n in uniq:
+            params[n].requires_grad_(False)
+        carry.params, carry.state, carry.nstep = params, state, nstep
     return out, {n: params[n].detach().clone() for n in uniq}
 
 

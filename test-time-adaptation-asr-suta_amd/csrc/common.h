@@ -58,7 +58,9 @@ __device__ __forceinline__ float dgelu_fast(float x) {
 // taken per engine call (suta_latch_switches, at the start of suta_forward / suta_step / suta_adapt*) and every
 // launcher and engine predicate of that call reads the snapshot: a switch flipped between a forward and its
 // backward, or between graph capture and replay, cannot mismatch formats.  The snapshot is part of the engine's
-// graph key.  Launchers used without an engine (tools/) take a snapshot on first use.
+// graph key.  Launchers used without an engine (tools/) take a snapshot on first use.  The snapshot is per host
+// thread: an engine call latches and launches on its calling thread, so engines driven from different threads (one
+// per device in one process) never see each other's snapshot.
 struct SutaSwitches {
     int latched;
     int fast_gelu;        // SUTA_FAST_GELU: branch-free GELU / GELU' (front-end and bf16-plane epilogues)
@@ -89,6 +91,8 @@ struct SutaSwitches {
     int hbx_t;            // SUTA_HBX_T (default 2): gemm_hbx accumulates C^T fragments with a row-per-lane epilogue whose
                           // outputs are staged through LDS into whole-line stores; 1 = direct 16-B row-per-lane stores,
                           // 0 = the column-per-lane form shared with the 128 x 128 kernel
+    int epi_fast;         // SUTA_EPI_FAST (default 1): 32-bit-offset GEMM epilogue where every operand fits 4 GiB (p.off32);
+                          // 0 = the general epilogue everywhere
 };
 void suta_latch_switches();
 const SutaSwitches& suta_switches();  // the snapshot (taken now if none was)

@@ -266,6 +266,8 @@ struct suta_engine {
         SutaSwitches sw{};  // the call's A/B switch snapshot (buffer formats and kernel choices captured)
     };
     hipGraphExec_t loop_graph = nullptr;
+    int last_loop_mode = SUTA_LOOP_EAGER;  // suta_get_graph_stats
+    long graph_captures = 0, graph_launches = 0;
     GraphKey gkey;
     bool gkey_seen = false;  // key of the previous suta_adapt call (its lazy allocations are done)
     DevBuf recbuf;           // recorded logits [nrec][B*T*V] then ids [nrec][B*T]
@@ -1634,17 +1636,38 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
     }
 }
 
+// lr of optimizer step i counted from the last reset: torch.optim.lr_scheduler.StepLR (main.py:20-21, step_size 1 and
+// gamma 0.7 there) multiplies the group's lr by gamma, in double, each time its step count (advanced after every
+// optimizer step, main.py:207-208) reaches a multiple of step_size (StepLR.get_lr, the chained form); the episodic
+// reset restores it (main.py:147-152)
+static double scheduled_lr(const suta_hparams& hp, long i) {
+    double lr = py_double(hp.lr);
+    if (hp.lr_step_size <= 0) return lr;
+    const double g = py_double(hp.lr_gamma);
+    for (long e = 1; e <= i; ++e)
+        if (e % hp.lr_step_size == 0) lr = lr * g;
+    return lr;
+}
+
+static void check_optimizer(const suta_hparams& hp) {
+    if (hp.optimizer != SUTA_OPT_ADAMW && hp.optimizer != SUTA_OPT_SGD)
+        throw SutaError(SUTA_ERR_UNSUPPORTED, "optimizer: SUTA_OPT_ADAMW or SUTA_OPT_SGD");
+    if (hp.lr_step_size < 0) throw SutaError(SUTA_ERR_ARG, "lr_step_size < 0");
+}
+
 void suta_engine::adam(int B, const suta_hparams& hp) {
     AdamArgs a{};
+    check_optimizer(hp);
     // Python floats are doubles: recover the decimal the caller meant (0.9f -> 0.9) so the
     // scalars match torch's double-precision host arithmetic (adam.py:495-510)
-    const double lr = py_double(hp.lr), b1 = py_double(hp.beta1), b2 = py_double(hp.beta2);
+    const double lr = scheduled_lr(hp, opt_steps), b1 = py_double(hp.beta1), b2 = py_double(hp.beta2);
     a.beta1 = (float)b1;
     a.beta2 = (float)b2;
     a.omb1 = (float)(1.0 - b1);
     a.omb2 = (float)(1.0 - b2);
     a.eps = (float)py_double(hp.adam_eps);
-    a.lr_wd = (float)(lr * py_double(hp.weight_decay));
+    a.lr_wd = (float)(py_double(hp.lr) * py_double(hp.weight_decay));  // (a flag: the per-step factor is in the table)
+    a.sgd = hp.optimizer == SUTA_OPT_SGD;
     // runs of equal multiplicity over the flat layout
     a.nruns = 0;
     int kmax = 0;
@@ -1665,7 +1688,7 @@ void suta_engine::adam(int B, const suta_hparams& hp) {
             const double t = (double)(opt_steps * kk + j);
             const double bc1 = 1.0 - std::pow(b1, t);
             const double bc2 = 1.0 - std::pow(b2, t);
-            a.step_size[kk - 1][j - 1] = (float)(lr / bc1);
+            a.step_size[kk - 1][j - 1] = (float)(a.sgd ? lr : lr / bc1);
             a.bc2_sqrt[kk - 1][j - 1] = (float)std::sqrt(bc2);
         }
     a.tab = d_adam_tab;
@@ -1677,25 +1700,31 @@ void suta_engine::adam(int B, const suta_hparams& hp) {
     opt_steps += 1;
 }
 
-// Device Adam tables for optimizer steps [0, opt_steps + steps) and the device step counter = opt_steps.
+// Device optimizer tables for steps [0, opt_steps + steps) and the device step counter = opt_steps.
 void suta_engine::prepare_adam(const suta_hparams& hp, int steps) {
+    check_optimizer(hp);
     const long need = opt_steps + std::max(steps, 1);
     if (need > adam_tab_cap) {
         const long cap = std::max<long>(need, 2 * adam_tab_cap);
         if (d_adam_tab) HIPCHK(hipFree(d_adam_tab));
-        HIPCHK(hipMalloc(&d_adam_tab, cap * 50 * sizeof(float)));
+        HIPCHK(hipMalloc(&d_adam_tab, cap * ADAM_TAB * sizeof(float)));
         adam_tab_cap = cap;
         drop_graph();  // captured steps point at the old table
     }
-    const double lr = py_double(hp.lr), b1 = py_double(hp.beta1), b2 = py_double(hp.beta2);
-    h_tab.assign(need * 50, 0.f);
-    for (long s0 = 0; s0 < need; ++s0)
+    const double b1 = py_double(hp.beta1), b2 = py_double(hp.beta2), wd = py_double(hp.weight_decay);
+    h_tab.assign(need * ADAM_TAB, 0.f);
+    for (long s0 = 0; s0 < need; ++s0) {
+        const double lr = scheduled_lr(hp, s0);
+        float* row = h_tab.data() + s0 * ADAM_TAB;
         for (int kk = 1; kk <= 5; ++kk)
             for (int j = 1; j <= kk; ++j) {
                 const double t = (double)(s0 * kk + j);
-                h_tab[s0 * 50 + (kk - 1) * 5 + (j - 1)] = (float)(lr / (1.0 - std::pow(b1, t)));
-                h_tab[s0 * 50 + 25 + (kk - 1) * 5 + (j - 1)] = (float)std::sqrt(1.0 - std::pow(b2, t));
+                row[(kk - 1) * 5 + (j - 1)] = (float)(lr / (1.0 - std::pow(b1, t)));
+                row[25 + (kk - 1) * 5 + (j - 1)] = (float)std::sqrt(1.0 - std::pow(b2, t));
             }
+        row[50] = (float)(1.0 - lr * wd);
+        row[51] = (float)(-lr);
+    }
     h_step = (int)opt_steps;
     HIPCHK(hipMemcpyAsync(d_adam_tab, h_tab.data(), h_tab.size() * sizeof(float), hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(d_step, &h_step, sizeof(int), hipMemcpyHostToDevice, st));
@@ -1733,8 +1762,10 @@ void suta_engine::run_adapt_loop(int B, const suta_hparams& hp, int steps, const
                                  float* rec_logits, int* rec_ids, bool graph_ok) {
     if (!use_graphs || timing || !graph_ok) {
         adapt_loop(B, hp, steps, rec, nrec, rec_logits, rec_ids);
+        last_loop_mode = SUTA_LOOP_EAGER;
         return;
     }
+    last_loop_mode = loop_graph ? SUTA_LOOP_REPLAYED : SUTA_LOOP_CAPTURED;
     if (!loop_graph) {
         const long steps0 = opt_steps;
         hipGraph_t g = nullptr;
@@ -1751,8 +1782,10 @@ void suta_engine::run_adapt_loop(int B, const suta_hparams& hp, int steps, const
         opt_steps = steps0;  // the capture recorded the Adam steps without running them
         HIPCHK(hipGraphInstantiate(&loop_graph, g, nullptr, nullptr, 0));
         HIPCHK(hipGraphDestroy(g));
+        ++graph_captures;
     }
     HIPCHK(hipGraphLaunch(loop_graph, st));
+    ++graph_launches;
     opt_steps += steps;
     if (hp.pl_coef > 0.f && steps > 0) sdpl_used = true;  // the replayed SDPL kernels may raise the error flag
 }
@@ -2345,6 +2378,14 @@ int32_t suta_set_precision(suta_engine* e, int32_t mode) {
 
 int32_t suta_set_graphs(suta_engine* e, int32_t enable) {
     return guard([&] { e->use_graphs = enable != 0; });
+}
+
+int32_t suta_get_graph_stats(suta_engine* e, int32_t* last_mode, int64_t* captures, int64_t* launches) {
+    return guard([&] {
+        if (last_mode) *last_mode = e->last_loop_mode;
+        if (captures) *captures = e->graph_captures;
+        if (launches) *launches = e->graph_launches;
+    });
 }
 
 int32_t suta_set_census(int32_t enable) {

@@ -61,16 +61,19 @@ std::string gemm_census_text() {
 
 // Each launch also counts one "grid <kernel> <BMxBN> gx=<column tiles> gy=<row tiles> z=<Z> split=<k>" entry, so
 // a test can assert the tile grid a layout reaches (e.g. the 512 row tiles of 164 x 399 frames).
+// and one "epi <kernel> <BMxBN> <epilogue flags>" entry (e.g. EPI_DELTA = 256 on hbx: the fused flash-backward delta ran).
 static void census(const char* kernel, int BM, int BN, const GemmParams& p, int splits) {
     if (!g_census_on) return;
-    char key[160], gkey[160];
+    char key[160], gkey[160], ekey[96];
     snprintf(key, sizeof key, "%s %dx%d z=%ld split=%d %s%s%s", kernel, BM, BN, (long)p.Z, splits, p.ta ? "T" : "N",
              p.tb ? "T" : "N", p.segK > 0 ? (p.segB ? " conv-seg" : " conv") : "");
     snprintf(gkey, sizeof gkey, "grid %s %dx%d gx=%d gy=%d z=%ld split=%d", kernel, BM, BN, (p.N + BN - 1) / BN,
              (p.M + BM - 1) / BM, (long)p.Z, splits);
+    snprintf(ekey, sizeof ekey, "epi %s %dx%d %d", kernel, BM, BN, p.epi);
     std::lock_guard<std::mutex> lk(g_census_mu);
     ++g_census[key];
     ++g_census[gkey];
+    ++g_census[ekey];
 }
 
 void gemm_set_mode(int mode) { g_mode = mode; }
@@ -205,9 +208,11 @@ static int use_hb8(const GemmParams& p) {
 // SUTA_HBX=0: off (A/B runs); 2: every eligible linear, any epilogue and grid (tests).
 // batched (Z > 1) GEMMs -- the conv stack's per-utterance forward -- only on the four-phase form with the staged C^T
 // epilogue (gemm_hbp_kernel rebases its operands per batch)
+// (p.off32 already set: gemm_run_hbx refuses a batched GEMM without the 32-bit-offset epilogue, so one without it -- an
+// operand over 4 GiB, or SUTA_EPI_FAST=0 -- must stay on the 128 x 128 kernel)
 static bool hbx_batch_ok(const GemmParams& p) {
     const SutaSwitches& sw = suta_switches();
-    return p.Z == 1 || (sw.hbx_form && sw.hbx_t == 2 && !sw.hbx_dbg && p.K % 64 == 0 && hbx_t_ok(p, false));
+    return p.Z == 1 || (sw.hbx_form && sw.hbx_t == 2 && !sw.hbx_dbg && p.K % 64 == 0 && hbx_t_ok(p, true));
 }
 
 static bool use_hbx(const GemmParams& p) {
@@ -220,13 +225,9 @@ static bool use_hbx(const GemmParams& p) {
 }
 
 // 32-bit epilogue offsets: M x ld elements of every operand the epilogue touches within 4 GiB
-// (SUTA_EPI_FAST=0: the general epilogue everywhere, for A/B runs)
+// (SUTA_EPI_FAST=0 in the call's switch snapshot: the general epilogue everywhere, for A/B runs)
 static int epilogue_off32(const GemmParams& p) {
-    static int fast = -1;
-    if (fast < 0) {
-        const char* ev = std::getenv("SUTA_EPI_FAST");
-        fast = (ev && atoi(ev) == 0) ? 0 : 1;
-    }
+    const int fast = suta_switches().epi_fast;
     const double lim = 4294967295.0 - 1024.0;
     auto fits = [&](long ld, double esz) { return (double)p.M * (double)std::max(ld, (long)p.N) * esz < lim; };
     return fits(p.ldc, 4) && (!(p.epi & EPI_RESID) || fits(p.ldr, 4)) &&
@@ -267,6 +268,7 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
                (p.Z > 1 && ((p.sA0 | p.sA1 | p.sB0 | p.sB1) % 8))))
         throw std::invalid_argument("gemm: bf16 planes need K, ld and batch strides % 8 == 0 and 16-B alignment");
     const bool bf16_gbf = p.mode == 2 && glds_ok && p.ta;  // bf16 weight gradients: LDS-DMA fp32 stages
+    p.off32 = epilogue_off32(p);  // before the tile choice: the 256 x 256 kernel's batched form needs it
     p.fgelu = suta_switches().fast_gelu;  // (the engine call's switch snapshot)
     if (p.preb && (!hb || !p.Cb || (p.ldc2 & 1)))  // (gemm_hb8_kernel shares the epilogue)
         throw std::invalid_argument("gemm: bf16 pre-activation operands need the bf16-plane kernel with a Cb plane, ldc2 even");
@@ -306,7 +308,6 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
     if (splits > 1) splits = (p.K + p.kchunk - 1) / p.kchunk;
     p.splits = splits;
     p.ws = ws;
-    p.off32 = epilogue_off32(p);
     if ((p.epi & EPI_DELTA) && !(tile == 8 && suta_switches().hbx_t && hbx_t_ok(p, true)))
         throw std::invalid_argument("gemm: EPI_DELTA needs the 256 x 256 bf16-plane kernel's C^T epilogue (gemm_hbx_t_selected)");
     {

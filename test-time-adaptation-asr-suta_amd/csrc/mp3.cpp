@@ -821,16 +821,20 @@ int32_t suta_mp3_decode(const uint8_t* buf, int64_t len, float* out, int64_t out
         rc = dec.frame(buf + off, h, pcm, &st, strict != 0);
         if (rc) return rc;
     }
-    // kept decoded positions: frame k contributes its first frame_keep(k) samples; then the leading skip is dropped
-    std::vector<int64_t> src;
-    src.reserve((size_t)(total + s.skip));
-    for (int64_t k = 0; k < (int64_t)s.frames.size(); ++k)
-        for (int64_t i = 0, n = s.frame_keep(k); i < n; ++i) src.push_back(k * s.spf() + i);
-    for (int ch = 0; ch < s.channels; ++ch)
-        for (int64_t i = 0; i < total; ++i) {
-            const int64_t j = src[(size_t)(i + s.skip)];
-            out[ch * out_capacity + i] = j < (int64_t)pcm[ch].size() ? pcm[ch][j] : 0.0f;
+    // kept decoded positions: frame k contributes its first frame_keep(k) samples (from k * spf); the first s.skip
+    // kept positions are dropped.  Copied frame by frame with the skip as a running offset (no per-sample index).
+    for (int ch = 0; ch < s.channels; ++ch) {
+        const int64_t have = (int64_t)pcm[ch].size();
+        int64_t pos = -s.skip;  // output index of the frame's first kept sample
+        for (int64_t k = 0; k < (int64_t)s.frames.size() && pos < total; ++k) {
+            const int64_t n = s.frame_keep(k), base = k * s.spf();
+            for (int64_t i = std::max<int64_t>(0, -pos); i < n && pos + i < total; ++i) {
+                const int64_t j = base + i;
+                out[ch * out_capacity + pos + i] = j < have ? pcm[ch][j] : 0.0f;
+            }
+            pos += n;
         }
+    }
     if (stats) {
         stats[0] = st.frames; stats[1] = st.granules; stats[2] = st.exact; stats[3] = st.overrun; stats[4] = st.lost;
     }

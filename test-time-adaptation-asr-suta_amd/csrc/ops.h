@@ -121,17 +121,21 @@ struct AdamRun {
     int k;
 };
 #define SUTA_MAX_RUNS 24
+#define ADAM_TAB 52  // floats per optimizer step in the device step table
 struct AdamArgs {
     int nruns;
     AdamRun runs[SUTA_MAX_RUNS];
     int blk0[SUTA_MAX_RUNS];  // first block of each run (filled by launch_adam)
     float beta1, beta2, omb1, omb2, eps, lr_wd;  // omb = (1 - beta) rounded from double; lr_wd = lr * wd
+    int sgd;  // SUTA_OPT_SGD: p = fma(g, -lr, p) per sub-step (no moments); the step table's [51] holds -lr
     // per sub-step j (1-based t = step0*k + j): step_size and sqrt(bias_correction2), indexed [k-1][j-1]
     float step_size[5][5];
     float bc2_sqrt[5][5];
-    // device-resident alternative (graph-replayable): tab[step0][0|1][k-1][j-1] = step_size | bc2_sqrt,
-    // step0 read from *step (advanced by launch_step_advance); used when tab != null.  At *step == 0 the
-    // moments are taken as zero (not read): every reset of the slots sets the step counter to 0
+    // device-resident alternative (graph-replayable): tab[step0 * ADAM_TAB + {0|25} + (k-1) * 5 + j-1] =
+    // step_size | bc2_sqrt, tab[.. + 50] = the weight-decay factor 1 - lr_i wd, tab[.. + 51] = -lr_i (SGD), lr_i
+    // the scheduled lr of step step0; step0 read from *step (advanced by launch_step_advance); used when tab !=
+    // null.  At *step == 0 the moments are taken as zero (not read): every reset of the slots sets the step
+    // counter to 0
     const float* tab;
     const int* step;
 };

@@ -1408,6 +1408,9 @@ __device__ __forceinline__ void adam_body(float* __restrict__ P, const float* __
         ss[j] = tab ? tab[(K - 1) * 5 + j] : a.step_size[K - 1][j];
         bs[j] = tab ? tab[25 + (K - 1) * 5 + j] : a.bc2_sqrt[K - 1][j];
     }
+    // AdamW's decoupled decay p *= 1 - lr_i wd (adam.py: param.mul_(1 - lr * weight_decay)), the factor rounded from
+    // double with the step's scheduled lr; off (the reference's wd 0) when lr_wd == 0
+    const float wdf = tab ? tab[50] : 1.0f - a.lr_wd;
     f32x4 g4[ADAM_GPT], p4[ADAM_GPT], m4[ADAM_GPT], v4[ADAM_GPT];
     const f32x4 z = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -1436,7 +1439,7 @@ __device__ __forceinline__ void adam_body(float* __restrict__ P, const float* __
             float p = p4[u][e], m = m4[u][e], v = v4[u][e];
 #pragma unroll
             for (int j = 0; j < K; ++j) {
-                if (a.lr_wd != 0.f) p *= 1.0f - a.lr_wd;
+                if (a.lr_wd != 0.f) p *= wdf;
                 m = m + a.omb1 * (g - m);                 // lerp_(g, 1-beta1), weight < 0.5 form
                 v = v * a.beta2 + a.omb2 * (g * g);        // mul_(beta2).addcmul_(g, g, 1-beta2)
                 const float denom = sqrtf(v) / bs[j] + a.eps;
@@ -1450,6 +1453,38 @@ __device__ __forceinline__ void adam_body(float* __restrict__ P, const float* __
         *reinterpret_cast<f32x4*>(P + idx) = p4[u];
         *reinterpret_cast<f32x4*>(M + idx) = m4[u];
         *reinterpret_cast<f32x4*>(Vv + idx) = v4[u];
+    }
+}
+
+// torch.optim.SGD, single-tensor path at momentum 0 and weight decay 0 (sgd.py _single_tensor_sgd: param.add_(grad,
+// alpha=-lr), once per collect_params entry): K fused multiply-adds p = g (-lr_i) + p (ATen's CPU add kernel is
+// vec::fmadd(b, alpha, a)); no moments are read or written
+template <int K>
+__device__ __forceinline__ void sgd_body(float* __restrict__ P, const float* __restrict__ G, long base, long g0,
+                                         long ngroups, long len, float nlr) {
+    f32x4 g4[ADAM_GPT], p4[ADAM_GPT];
+#pragma unroll
+    for (int u = 0; u < ADAM_GPT; ++u) {
+        const long gi = g0 + u * 256;
+        if (gi < ngroups) {
+            g4[u] = *reinterpret_cast<const f32x4*>(G + base + 4 * gi);
+            p4[u] = *reinterpret_cast<const f32x4*>(P + base + 4 * gi);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < ADAM_GPT; ++u) {
+        const long gi = g0 + u * 256;
+        if (gi >= ngroups) continue;
+        const int nv = (int)min(4L, len - 4 * gi);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            if (e >= nv) break;
+            float p = p4[u][e];
+#pragma unroll
+            for (int j = 0; j < K; ++j) p = fmaf(g4[u][e], nlr, p);
+            p4[u][e] = p;
+        }
+        *reinterpret_cast<f32x4*>(P + base + 4 * gi) = p4[u];
     }
 }
 
@@ -1473,8 +1508,19 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ P, const 
     const long g0 = (long)(bx - blk) * (256 * ADAM_GPT) + threadIdx.x;
     const long base = (long)blockIdx.y * pstride + start;
     const int step = a.step ? *a.step : 1;
-    const float* tab = a.tab ? a.tab + (long)step * 50 : nullptr;
+    const float* tab = a.tab ? a.tab + (long)step * ADAM_TAB : nullptr;
     const bool first = a.step && step == 0;
+    if (a.sgd) {
+        const float nlr = tab ? tab[51] : -a.step_size[0][0];
+        switch (k) {
+            case 1: sgd_body<1>(P, G, base, g0, ngroups, len, nlr); break;
+            case 2: sgd_body<2>(P, G, base, g0, ngroups, len, nlr); break;
+            case 3: sgd_body<3>(P, G, base, g0, ngroups, len, nlr); break;
+            case 4: sgd_body<4>(P, G, base, g0, ngroups, len, nlr); break;
+            default: sgd_body<5>(P, G, base, g0, ngroups, len, nlr); break;
+        }
+        return;
+    }
     switch (k) {
         case 1: adam_body<1>(P, G, M, Vv, base, g0, ngroups, len, a, tab, first); break;
         case 2: adam_body<2>(P, G, M, Vv, base, g0, ngroups, len, a, tab, first); break;
@@ -1859,7 +1905,7 @@ void launch_adam(float* P, const float* G, float* M, float* V, long pstride, int
     hipLaunchKernelGGL(adam_kernel, dim3((unsigned)nblk, B), dim3(256), 0, st, P, G, M, V, pstride, aa);
 }
 
-static SutaSwitches g_switches{};
+static thread_local SutaSwitches g_switches{};  // per host thread (common.h)
 
 void suta_latch_switches() {
     auto on = [](const char* name) {  // default on; "0" selects the replaced path
@@ -1895,6 +1941,7 @@ void suta_latch_switches() {
     s.hb8 = hb8 ? atoi(hb8) : 0;
     const char* fnw = std::getenv("SUTA_FLASH_FWD_NW");
     s.flash_fwd_nw = (fnw && atoi(fnw) == 8) ? 8 : 4;
+    s.epi_fast = on("SUTA_EPI_FAST");
     s.latched = 1;
     g_switches = s;
 }

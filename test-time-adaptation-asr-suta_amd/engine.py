@@ -21,7 +21,7 @@ MAX_CONV = 8
 EXPORTS = ("suta_create", "suta_destroy", "suta_reset", "suta_num_frames", "suta_forward", "suta_step",
            "suta_adapt", "suta_adapt_varlen", "suta_loss_grad", "suta_get_param", "suta_param_info", "suta_sync", "suta_stream", "suta_set_timing",
            "suta_get_timing", "suta_get_timing_ex", "suta_set_precision", "suta_set_graphs", "suta_set_census",
-           "suta_get_census", "suta_last_error")
+           "suta_get_census", "suta_get_graph_stats", "suta_last_error")
 
 
 class ModelConfigC(C.Structure):
@@ -38,7 +38,10 @@ class HParamsC(C.Structure):
     _fields_ = [("lr", C.c_float), ("temp", C.c_float), ("em_coef", C.c_float), ("div_coef", C.c_float),
                 ("beta1", C.c_float), ("beta2", C.c_float), ("adam_eps", C.c_float), ("weight_decay", C.c_float),
                 ("reweight", C.c_int32), ("non_blank", C.c_int32), ("train_feature", C.c_int32),
-                ("bias_only", C.c_int32), ("episodic", C.c_int32), ("pl_coef", C.c_float)]
+                ("bias_only", C.c_int32), ("episodic", C.c_int32), ("pl_coef", C.c_float),
+                ("optimizer", C.c_int32), ("lr_step_size", C.c_int32), ("lr_gamma", C.c_float)]
+
+OPTIMIZERS = {"AdamW": 0, "Adam": 0, "SGD": 1}  # SUTA_OPT_*: Adam == AdamW at the reference's weight decay 0
 
 
 @dataclass
@@ -57,11 +60,19 @@ class SutaHParams:
     eps: float = 1e-8
     weight_decay: float = 0.0
     pl_coef: float = 0.0  # SDPL mix (main_SDPL.py:143-209); 0 = SUTA
+    optimizer: str = "AdamW"  # --opt (main.py:9-18): AdamW / Adam / SGD
+    lr_step_size: int = 0     # StepLR (main.py:20-21: step_size 1, gamma 0.7); 0 = no scheduler
+    lr_gamma: float = 0.7
 
     def to_c(self) -> HParamsC:
+        if self.optimizer not in OPTIMIZERS:
+            raise ValueError(f"optimizer {self.optimizer!r}: the engine implements {sorted(OPTIMIZERS)}")
+        if self.optimizer == "Adam" and self.weight_decay != 0:
+            raise ValueError("Adam with weight decay (L2 in the gradient) is not AdamW; the reference passes 0")
         return HParamsC(self.lr, self.temp, self.em_coef, self.div_coef, self.betas[0], self.betas[1], self.eps,
                         self.weight_decay, int(self.reweight), int(self.non_blank), int(self.train_feature),
-                        int(self.bias_only), int(self.episodic), float(self.pl_coef))
+                        int(self.bias_only), int(self.episodic), float(self.pl_coef), OPTIMIZERS[self.optimizer],
+                        int(self.lr_step_size), float(self.lr_gamma))
 
 
 _lib = None
@@ -107,6 +118,8 @@ def load_library(path: str = LIB_PATH):
         lib.suta_set_census.argtypes = [C.c_int32]
         lib.suta_get_census.argtypes = [C.c_char_p, C.c_int64, i64p]
     lib.suta_set_precision.argtypes = [C.c_void_p, C.c_int32]
+    if hasattr(lib, "suta_get_graph_stats"):
+        lib.suta_get_graph_stats.argtypes = [C.c_void_p, i32p, i64p, i64p]
     lib.suta_last_error.restype = C.c_char_p
     for name in EXPORTS:
         if name != "suta_stream" and name != "suta_last_error" and hasattr(lib, name):
@@ -332,6 +345,15 @@ class SutaEngine:
 
     def set_graphs(self, enable: bool):
         _check(self.lib.suta_set_graphs(self.handle, int(enable)))
+
+    LOOP_MODES = ("eager", "captured", "replayed")
+
+    def graph_stats(self) -> dict:
+        """How the last adapt call ran its loop ('eager' | 'captured' | 'replayed') and the engine's graph
+        captures / launches so far (suta_get_graph_stats)."""
+        m, c, n = C.c_int32(), C.c_int64(), C.c_int64()
+        _check(self.lib.suta_get_graph_stats(self.handle, C.byref(m), C.byref(c), C.byref(n)))
+        return {"last": self.LOOP_MODES[m.value], "captures": c.value, "launches": n.value}
 
     def set_census(self, enable: bool):
         """Start (clear) or stop the process-wide GEMM launch census (suta_set_census)."""

@@ -115,6 +115,41 @@ def ragged_groups(sorted_lengths, max_batch: int, budget_samples: float, min_fil
     return groups[::-1]
 
 
+def resolve_scheduler(name):
+    """--scheduler: the reference eval()s the string in main.py's namespace and calls the result with
+    (optimizer, step_size=1, gamma=0.7) (main.py:20-21); of torch's schedulers only StepLR takes those keywords, so
+    the engine implements StepLR (lr * 0.7^i on optimizer step i, restored per utterance when episodic).  The name
+    is resolved as a dotted path from `torch` (no eval); None = no scheduler.  Returns (lr_step_size, gamma)."""
+    if name is None:
+        return 0, 0.7
+    import torch
+    obj = None
+    parts = str(name).split(".")
+    if parts[0] == "torch":
+        obj = torch
+        for q in parts[1:]:
+            obj = getattr(obj, q, None)
+    if obj is not torch.optim.lr_scheduler.StepLR:
+        raise SystemExit(f"--scheduler {name}: the engine implements torch.optim.lr_scheduler.StepLR (the one torch "
+                         "scheduler the reference's eval(scheduler)(optimizer, step_size=1, gamma=0.7) constructs)")
+    return 1, 0.7
+
+
+def workspace_bytes_per_audio_s(cfg) -> float:
+    """Upper estimate of the engine's device workspace per second of padded audio in a batch (DESIGN.md section 2:
+    measured 0.36 GB per 8 s base utterance = 45 MB/s): 50 frames/s x 4 B x layers x 14 H saved per frame in the
+    encoder, plus ~3 fp32 buffers of the conv stack's 512 channels over its ~6350 frames per second."""
+    return 50 * 4 * cfg["num_hidden_layers"] * 14 * cfg["hidden_size"] + 6350 * 512 * 4 * 3
+
+
+def clamp_budget(budget_s: float, cfg, free_bytes, frac: float = 0.7) -> float:
+    """The ragged-batch audio budget limited to `frac` of the device's free memory (the defaults are sized for the
+    288 GB of an MI355X; a smaller GPU would otherwise fail its first allocation)."""
+    if not free_bytes:
+        return budget_s
+    return max(1.0, min(budget_s, frac * free_bytes / workspace_bytes_per_audio_s(cfg)))
+
+
 def exp_name_of(a, sdpl: bool = False) -> str:
     """main.py:267 (main_SDPL.py:266 when sdpl)."""
     base = (a.dataset_name + "_" + str(a.em_coef) + "_" + str(a.steps) + "_" + str(a.temp) + "_" +
@@ -150,10 +185,10 @@ def main(argv=None, sdpl: bool = False):
     a = build_parser(sdpl).parse_args(argv)
     if sdpl:
         a.train_all = False
-    if a.opt not in ("AdamW", "Adam"):
-        raise SystemExit(f"--opt {a.opt}: only AdamW/Adam are implemented by the engine")
-    if a.scheduler is not None:
-        raise SystemExit("--scheduler: learning-rate schedulers are not implemented by the engine")
+    if a.opt not in ("AdamW", "Adam", "SGD"):
+        raise SystemExit(f"--opt {a.opt}: the engine implements AdamW, Adam (== AdamW at the reference's weight "
+                         "decay 0) and SGD")
+    lr_step_size, lr_gamma = resolve_scheduler(a.scheduler)
     if a.train_all:
         raise SystemExit("--train_all: full-model adaptation is outside the engine's scope")
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -211,11 +246,17 @@ def main(argv=None, sdpl: bool = False):
     say(f"[INFO]    scheduler: {a.scheduler}")
     say(param_names)
     gb = max(1, a.gpu_batch) if a.episodic else 1  # non-episodic adaptation is sequential
+    if torch.cuda.is_available():
+        budget = clamp_budget(a.gpu_budget_s, cfg, torch.cuda.mem_get_info(device)[0])
+        if budget < a.gpu_budget_s:
+            say(f"[suta_amd] --gpu_budget_s {a.gpu_budget_s} exceeds 70 % of the free device memory; using {budget:.0f} s")
+            a.gpu_budget_s = budget
     engine = SutaEngine(cfg, weights, device=device, max_batch=gb)
     engine.set_precision(a.precision)
     hp = SutaHParams(lr=a.lr, temp=a.temp, em_coef=a.em_coef, div_coef=0.0 if sdpl else a.div_coef,
                      reweight=a.reweight, non_blank=a.non_blank, train_feature=a.train_feature,
-                     bias_only=a.bias_only, episodic=a.episodic, pl_coef=1.0 if sdpl else 0.0)
+                     bias_only=a.bias_only, episodic=a.episodic, pl_coef=1.0 if sdpl else 0.0, optimizer=a.opt,
+                     lr_step_size=lr_step_size, lr_gamma=lr_gamma)
     record = [0] + ([c for c in CHECKPOINTS if c <= a.steps] if a.episodic else [])
     if not a.episodic:
         record = sorted(set([0, a.steps]))
@@ -318,6 +359,8 @@ def main(argv=None, sdpl: bool = False):
         print("------------------------------------")
         print(f"[suta_amd] adapted {len(allres)} utterances in {elapsed:.1f} s on rank 0's shard, {world} rank(s)")
         os.makedirs(a.log_dir, exist_ok=True)
+        # the log is written after setup_optimizer rebound `scheduler` to the scheduler object (main.py:308, 445)
+        sched_obj = "None" if a.scheduler is None else "<torch.optim.lr_scheduler.StepLR object>"
         tail = ((f"pl_coef = {a.pl_coef}",) if sdpl else (f"train_all = {str(a.train_all)}", f"train_LN = {str(True)}"))
         with open(os.path.join(a.log_dir, exp_name), "w") as f:
             for ln in lines:
@@ -325,7 +368,7 @@ def main(argv=None, sdpl: bool = False):
             for ln in (f"eposidic? {a.episodic}", f"lr = {a.lr}", f"optim = {a.opt}", f"step = {a.steps}",
                        f"em_coef = {a.em_coef}", f"reweight = {a.reweight}", f"batch size = {a.batch_size}",
                        f"temperature = {a.temp}", f"non_blank = {str(a.non_blank)}", f"extra_noise = {a.extra_noise}",
-                       f"scheduler = {str(a.scheduler)}", f"div_coef = {str(a.div_coef)}",
+                       f"scheduler = {sched_obj}", f"div_coef = {str(a.div_coef)}",
                        f"bias_only = {str(a.bias_only)}", f"train_feature = {str(a.train_feature)}") + tail:
                 f.write(ln + "\n")
         if not sdpl:

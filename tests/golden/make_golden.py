@@ -25,6 +25,11 @@ Fixtures written next to this file:
   g8_collect_params.json  the module names reference collect_params prints (main.py:79-80) and
                      the param_names list it returns (main.py:312-314) for the tiny / base / large
                      geometries under every (bias_only, train_feature) flag pair
+  g9_sched_<variant>.npz  tiny-config runs of the reference driver loop (main.py:308-348) with
+                     --scheduler torch.optim.lr_scheduler.StepLR (setup_optimizer's eval, step_size 1,
+                     gamma 0.7, main.py:20-21, stepped per SUTA step main.py:207-208) and/or --opt SGD
+                     (main.py:9, 18), two utterances, episodic (load_model_and_optimizer restores the
+                     scheduler, main.py:147-155, 327-328) or not: logits after every step + final tensors
   g7_large_16000.npz large-960h-lv60 shapes (layer-norm feature encoder, conv bias, stable
                      pre-LN encoder), 20 SUTA steps (config C4's step count), scripts/LS.sh flags:
                      logits at steps 0,1,5,10,20 + digests of the adapted tensors
@@ -257,6 +262,58 @@ def g7(ref):
         out[f"final/{k}/val"] = flat[idx]
     np.savez_compressed(os.path.join(HERE, f"g7_large_{n}.npz"), **out)
     print("g7", n, "done")
+
+
+def g9(ref):
+    """Reference driver loop with a learning-rate scheduler and/or SGD (main.py:308-348).
+
+    main.py's load_model_and_optimizer reads the module-global `scheduler` (the __main__ block's
+    variable, main.py:151); it is set on the imported module exactly as the script would have it."""
+    from transformers import Wav2Vec2Config, Wav2Vec2ForCTC
+    variants = [("steplr_group", "tiny-group", "AdamW", 5e-4, "torch.optim.lr_scheduler.StepLR", True),
+                ("steplr_layer", "tiny-layer", "AdamW", 5e-4, "torch.optim.lr_scheduler.StepLR", True),
+                ("sgd_group", "tiny-group", "SGD", 2e-2, None, True),
+                ("sgd_steplr_layer", "tiny-layer", "SGD", 2e-2, "torch.optim.lr_scheduler.StepLR", True),
+                ("steplr_group_nonepisodic", "tiny-group", "AdamW", 5e-4, "torch.optim.lr_scheduler.StepLR", False)]
+    steps = 6
+    for vname, preset, opt_name, lr, sched, episodic in variants:
+        cfg = get_config(preset)
+        sd = synth_weights(cfg)
+        torch.manual_seed(0)
+        model = Wav2Vec2ForCTC(Wav2Vec2Config(**cfg)).eval()
+        model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+        model = ref.configure_model(model)
+        with contextlib.redirect_stdout(io.StringIO()):
+            params, names = ref.collect_params(model, False, True, False, True)    # main.py:307
+            opt, sch = ref.setup_optimizer(params, opt_name, lr, scheduler=sched)  # main.py:308
+        ref.scheduler = sch
+        if episodic:
+            model_state, optimizer_state, scheduler_state = ref.copy_model_and_optimizer(model, opt, sch)
+        out = {"weights_sha256": np.array(weights_digest(sd)), "opt": np.array(opt_name), "lr": np.array(lr),
+               "scheduler": np.array(str(sched)), "episodic": np.array(episodic), "steps": np.array(steps),
+               "entries": np.array(names)}
+        for j, n in enumerate((8000, 12345)):
+            x = wave(n, 90 + j)
+            xt = torch.from_numpy(x)[None]
+            if episodic:                                                            # main.py:327-328
+                model, opt, sch = ref.load_model_and_optimizer(model, opt, model_state, optimizer_state,
+                                                               scheduler_state)
+            logits = []
+            with torch.no_grad():
+                logits.append(model(xt).logits[0].numpy().copy())                  # main.py:331-332
+            lrs = []
+            for i in range(steps):                                                  # main.py:347-348
+                lrs.append(opt.param_groups[0]["lr"])
+                o = ref.forward_and_adapt(xt, model, opt, 0.3, True, 2.5, True, sch, 0.0)
+                logits.append(o[0].detach().numpy().copy())
+            out[f"N{n}/x"] = x
+            out[f"N{n}/logits"] = np.stack(logits)
+            out[f"N{n}/lrs"] = np.array(lrs, dtype=np.float64)
+            sdf = model.state_dict()
+            for k in dict.fromkeys(names):
+                out[f"N{n}/final/{k}"] = sdf[k].numpy().copy()
+        np.savez_compressed(os.path.join(HERE, f"g9_sched_{vname}.npz"), **out)
+        print("g9", vname, "done", out[f"N12345/lrs"])
 
 
 def g5(ref):

@@ -50,6 +50,18 @@ def assert_params_close(actual, desired, lr, steps, tight=2e-6, max_frac=0.005, 
     assert diff.max() <= budget, f"{name}: max |diff| {diff.max():.3g} exceeds Adam step budget {budget:.3g}"
 
 
+def assert_sgd_params_close(actual, desired, start, name="", rel=1e-3, tight=2e-6):
+    """SGD (main.py:18, --opt SGD) has no gradient normalisation: a tensor moves by lr * k * sum of its
+    gradients, so two fp32 implementations differ by the gradients' rounding times that move.  Bound every
+    element by tight + rel * the largest displacement from the start value (the oracle matches the
+    reference to 1.2e-7 on the g9 fixtures, whose tensors move by up to ~1e-2)."""
+    a = np.asarray(actual, np.float64).reshape(-1)
+    d = np.asarray(desired, np.float64).reshape(-1)
+    moved = float(np.abs(d - np.asarray(start, np.float64).reshape(-1)).max()) if d.size else 0.0
+    diff = float(np.abs(a - d).max()) if d.size else 0.0
+    assert diff <= tight + rel * moved, f"{name}: max |diff| {diff:.3g} (moved {moved:.3g})"
+
+
 def logits_tol(lr):
     """Absolute logits tolerance after up to 10 SUTA steps at learning rate lr.
 

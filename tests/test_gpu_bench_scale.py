@@ -1,13 +1,17 @@
 """GPU tier: parity at the bench's own scale and on the replayed (hipGraph) ragged path.
 
 * The headline layout exactly as bench.py runs it: bench.BATCH (164) x 128 000-sample utterances x 10 SUTA
-  steps in one suta_adapt call, scripts/LS.sh flags, record steps 0/1/3/5/10, the second call of a repeated
-  layout (so every step is a graph replay, as in the timed region).  The first / middle / last slots are
+  steps in one suta_adapt call, scripts/LS.sh flags, record steps 0/1/3/5/10, greedy ids only (bench.py's timed
+  key: want_logits False).  As in the bench, the first call of the key runs eagerly (the census is taken on it),
+  the second captures the loop and launches it, the third REPLAYS it (suta_get_graph_stats asserts each mode).
+  The replayed call's greedy ids and adapted tensors must equal, bitwise, those of an eager call on the same
+  batch that also copies out logits (replay == eager); that eager call's first / middle / last slots are
   compared with the CPU oracle (oracle/w2v2_cpu.run_suta): logits within 5e-5 absolute (the base-size
   tolerance of tests/test_gpu_parity.py), adapted tensors by tests/parity.assert_params_close.  The batch is
   imported from bench.py, so a change of the bench's batch moves this pin with it; the launch census asserts
   the grids that batch reaches (B x 399 rows -> ceil(B*399/128) row tiles of the linears, Z = B conv GEMMs).
-* Config C4 at bench.C4_BATCH likewise (bf16, 20 steps) against the exact-fp32 engine and the oracle.
+* Config C4 at bench.C4_BATCH likewise (bf16, 20 steps): replay == eager bitwise, eager against the exact-fp32
+  engine and the oracle.
 * Ragged batches that share a quantised layout but differ in per-utterance lengths: the second call
   replays the captured step with new lengths (device-side length buffers); it must equal single runs
   and the eager (graphs off) execution bitwise.
@@ -38,8 +42,36 @@ def _row_tiles(B, T, tile=128):
     return -(-(B * T) // tile)
 
 
+def _timed_mode_equals_eager(eng, warm, x, S, hp, rec, slots):
+    """bench.py's call sequence on one key (ids only): eager warm-up, capture + launch, replay -- then an eager call
+    with logits on the same batch.  Asserts the loop modes, and that the replayed call's ids and adapted tensors
+    equal the eager call's bitwise.  Returns (eager logits, eager ids, T, census of the first (eager) call)."""
+    names = eng.trainable_names()
+    eng.set_census(True)
+    eng.adapt(warm, S, hp, record=rec, want_logits=False)                        # bench warm-up: a new key, eager
+    census = eng.get_census()
+    eng.set_census(False)
+    assert eng.graph_stats()["last"] == "eager"
+    eng.adapt(x, S, hp, record=rec, want_logits=False)                           # 1st timed call: capture + launch
+    g1 = eng.graph_stats()
+    assert g1["last"] == "captured", g1
+    _, ids_r, T = eng.adapt(x, S, hp, record=rec, want_logits=False)             # later timed calls: replay
+    g2 = eng.graph_stats()
+    assert g2["last"] == "replayed" and g2["captures"] == g1["captures"] and g2["launches"] == g1["launches"] + 1, g2
+    par_r = {b: {n: eng.get_param(b, n) for n in names} for b in slots}
+    logits, ids, T2 = eng.adapt(x, S, hp, record=rec)                            # logits wanted: a new key, eager
+    assert eng.graph_stats()["last"] == "eager" and T2 == T
+    for r in rec:
+        assert np.array_equal(ids_r[r], ids[r]), f"replayed ids != eager ids at step {r}"
+    for b in slots:
+        for n in names:
+            assert np.array_equal(par_r[b][n], eng.get_param(b, n)), f"replayed != eager: slot {b} {n}"
+    return logits, ids, T, census
+
+
 def test_bench_layout_matches_oracle():
-    """reference main.py:347-348 (S x forward_and_adapt per utterance) at the bench's batch."""
+    """reference main.py:347-348 (S x forward_and_adapt per utterance) at the bench's batch, in the bench's timed
+    execution mode (graph replay), pinned bitwise to an eager call that is checked against the oracle."""
     from oracle import w2v2_cpu as W
     import os
     torch.set_num_threads(min(16, len(os.sched_getaffinity(0))))
@@ -50,11 +82,8 @@ def test_bench_layout_matches_oracle():
     hp = SutaHParams()
     warm = torch.from_numpy(synth.batch(N, B, start=0)).cuda()
     x = synth.batch(N, B, start=B)          # bench.py's first timed batch at --warmup 1
-    eng.set_census(True)
-    eng.adapt(warm, S, hp, record=BENCH_RECORD, want_logits=False)          # captures the step graph
-    census = eng.get_census()
-    eng.set_census(False)
-    logits, ids, T = eng.adapt(torch.from_numpy(x).cuda(), S, hp, record=BENCH_RECORD)   # replayed
+    logits, ids, T, census = _timed_mode_equals_eager(eng, warm, torch.from_numpy(x).cuda(), S, hp, BENCH_RECORD,
+                                                      _slots(B))
     assert T == 399
     txt = "\n".join(f"{k}: {v}" for k, v in sorted(census.items()))
     gy = _row_tiles(B, T)
@@ -151,15 +180,15 @@ def test_ragged_ted_lengths_equal_singles():
 
 def test_c4_bench_layout_bf16():
     """Config C4 exactly as bench.py --only-c4 runs it: wav2vec2-large, bench.C4_BATCH x 128 000 samples, 20 SUTA
-    steps, bf16 GEMMs, the second call of the layout (every step a graph replay).  First / middle / last slots
+    steps, bf16 GEMMs, greedy ids only, in the bench's timed mode (the key's third call, a graph replay), pinned
+    bitwise to an eager call on the same batch (_timed_mode_equals_eager).  That call's first / middle / last slots
     against the exact-fp32 engine adapting each utterance alone (bf16 tolerance of tests/parity.py: 2.5 % of
     max|ref|, greedy ids on >= 97 % of frames) at steps 0 / 1 / 5 / 20, and slot 0 against the CPU oracle at steps 0
-    and 20.  The launch census of the capturing call shows the schedules this layout reaches: the linears on
-    the bf16-plane kernels, the conv stack's per-utterance (Z = B) GEMMs on
-    bf16 planes -- forward and input gradients (conv-A rows, per-tap weight segments) on hb, weight gradients on the
-    MN-contiguous hbt kernel -- and the per-utterance feature-projection weight gradient.  The linears run on the
-    256 x 256 slice-ring kernel (hbx) over ceil(B x 399 / 256) row tiles, the K = 32 lm_head input gradient on the
-    128 x 128 one over ceil(B x 399 / 128).
+    and 20.  The launch census of the first (eager) call shows the schedules this layout reaches: the linears on
+    the 256 x 256 bf16-plane kernel (hbx) over ceil(B x 399 / 256) row tiles, the K = 32 lm_head input gradient on
+    the 128 x 128 one over ceil(B x 399 / 128), the conv stack's per-utterance (Z = B) GEMMs on bf16 planes --
+    forward on the 256 x 256 kernel, input gradients (conv-A rows, per-tap weight segments), weight gradients on
+    the MN-contiguous hbt kernel -- and the per-utterance feature-projection weight gradient.
     Reference main.py:181,205 (forward and backward through the encoder)."""
     from oracle import w2v2_cpu as W
     import os
@@ -168,30 +197,26 @@ def test_c4_bench_layout_bf16():
     cfg = get_config("wav2vec2-large")
     sd = synth_weights(cfg)
     B, N, S = bench.C4_BATCH, 128000, 20
-    rec = [0, 1, 5, 20]
+    rec = bench.C4_RECORD
     eng = SutaEngine(cfg, sd, device=0, max_batch=B, max_samples=N)
     eng.set_precision("bf16")
     hp = SutaHParams()
     warm = torch.from_numpy(synth.batch(N, B, start=0)).cuda()
     x = synth.batch(N, B, start=B)
-    eng.set_census(True)
-    eng.adapt(warm, S, hp, record=rec, want_logits=False)                 # captures the loop
-    census = eng.get_census()
-    eng.set_census(False)
-    logits, ids, T = eng.adapt(torch.from_numpy(x).cuda(), S, hp, record=rec)   # replayed
+    logits, ids, T, census = _timed_mode_equals_eager(eng, warm, torch.from_numpy(x).cuda(), S, hp, rec, _slots(B))
     assert T == 399
     txt = "\n".join(f"{k}: {v}" for k, v in sorted(census.items()))
     print(txt)
     gy = _row_tiles(B, T)
     z = f" z={B} "
-    # the linears on the 256 x 256 slice-ring kernel: N = 1024 (out-proj, FFN2, input gradients), 3072 (QKV), 4096
-    # (the GELU / GELU' linears FFN1 and the FFN2 input gradient, through the C^T epilogue)
+    # the linears on the 256 x 256 kernel: N = 1024 (out-proj, FFN2, input gradients), 3072 (QKV), 4096 (the GELU /
+    # GELU' linears FFN1 and the FFN2 input gradient, through the C^T epilogue)
     for gx in (4, 12, 16):
         assert any(k.startswith("grid hbx 256x256 ") and f" gx={gx} gy={_row_tiles(B, T, 256)} z=1 " in k
                    for k in census), (gx, txt)
     # the K = 32 lm_head input gradient (below hbx's K >= 128) on the 128 x 128 kernel
     assert any(k.startswith("grid hb 128x128 ") and f" gx=8 gy={gy} z=1 " in k for k in census), (gy, txt)
-    assert any(k.startswith("hb 128x128" + z) and k.endswith(" conv-seg") for k in census), txt   # conv dX
+    assert any(k.startswith(("hb ", "hbx ")) and z in k and k.endswith(" conv-seg") for k in census), txt   # conv dX
     assert any(k.startswith(("hb ", "hbx ")) and z in k and "conv" not in k for k in census), txt  # conv forward
     assert any(k.startswith("hbt ") and z in k for k in census), txt                        # conv dW
     assert any(z in k and k.startswith(("gbf", "x6_1plane")) for k in census), txt

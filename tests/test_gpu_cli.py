@@ -105,7 +105,7 @@ def test_sdpl_cli_end_to_end(tmp_path, capsys):
         assert counts[str(k)][1] == counts["0"][1]
 
 
-def _oracle_counts(ds_files, ds_texts, cfg_name, steps, lr, extra_noise=0.0):
+def _oracle_counts(ds_files, ds_texts, cfg_name, steps, lr, extra_noise=0.0, **opt):
     from oracle import w2v2_cpu as W
     cfg = get_config(cfg_name)
     sd = {k: torch.from_numpy(v) for k, v in synth_weights(cfg).items()}
@@ -114,7 +114,7 @@ def _oracle_counts(ds_files, ds_texts, cfg_name, steps, lr, extra_noise=0.0):
     hyps = {k: [] for k in rec}
     for i, f in enumerate(ds_files):   # i = dataset index = the utterance's noise key
         x = torch.from_numpy(normalize(reader(str(f), i)))[None]
-        lg, _ = W.run_suta(sd, cfg, x, steps, lr=lr, record=rec)
+        lg, _ = W.run_suta(sd, cfg, x, steps, lr=lr, record=rec, **opt)
         for k in rec:
             hyps[k].append(batch_decode(lg[k].argmax(-1).numpy())[0])
     return {k: wer_counts(list(ds_texts), hyps[k]) for k in rec}
@@ -228,3 +228,29 @@ def test_cli_ted_long_utterances_ragged(tmp_path, capsys):
     ref = _oracle_counts(ds.file_list, ds.text, "wav2vec2-base", 3, 2e-5)
     for k, v in ref.items():
         assert tuple(counts[str(k)]) == v, k
+
+
+@pytest.mark.parametrize("opt,lr", [("AdamW", "5e-4"), ("SGD", "2e-2")])
+def test_cli_scheduler_steplr(tmp_path, capsys, opt, lr):
+    """--scheduler torch.optim.lr_scheduler.StepLR (main.py:20-21, 207-208; lr * 0.7^i, restored per utterance) with
+    --opt AdamW / SGD through the drop-in driver, one ragged batch: corpus WER counts equal the CPU oracle's under the
+    same optimizer and schedule (oracle pinned to the reference's own runs by g9); the stdout / log lines name it."""
+    from tests import corpus_fixtures as CF
+    from suta_amd.data import CHiMEDataset
+    CF.chime(tmp_path, n=4)
+    args = (f"--asr tiny-group --synthetic_weights --steps 10 --dataset_name chime --dataset_dir {tmp_path} "
+            f"--temp 2.5 --episodic --em_coef 0.3 --reweight --log_dir {tmp_path}/exps --lr {lr} --non_blank "
+            f"--train_feature --extra_noise 0 --gpu_batch 16 --opt {opt} "
+            f"--scheduler torch.optim.lr_scheduler.StepLR").split()
+    counts = M.main(args)
+    out = capsys.readouterr().out
+    assert "[INFO]    scheduler: torch.optim.lr_scheduler.StepLR" in out and f"optim = {opt}" in out
+    a = M.build_parser().parse_args(args)
+    log = open(os.path.join(a.log_dir, M.exp_name_of(a))).read().splitlines()
+    assert "scheduler = <torch.optim.lr_scheduler.StepLR object>" in log
+    ds = CHiMEDataset(None, 1, str(tmp_path))
+    ref = _oracle_counts(ds.file_list, ds.text, "tiny-group", 10, float(lr), opt=opt, lr_step_size=1)
+    for k, v in ref.items():
+        assert tuple(counts[str(k)]) == v, k
+    with pytest.raises(SystemExit):
+        M.main(args[:-1] + ["torch.optim.lr_scheduler.ExponentialLR"])

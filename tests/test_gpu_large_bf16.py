@@ -269,14 +269,21 @@ def test_bf16_fused_delta_bitwise_equals_separate_pass(monkeypatch):
     cfg = get_config("wav2vec2-large")
     sd = synth_weights(cfg)
     waves = [synth.wave(32000, 86), synth.wave(20000, 87)]
-    out, params = {}, {}
+    out, params, delta_launches = {}, {}, {}
     for fd in ("1", "0"):
         monkeypatch.setenv("SUTA_FUSED_DELTA", fd)
         eng = SutaEngine(cfg, sd, max_batch=2, max_samples=32000)
         eng.set_precision("bf16")
+        eng.set_census(True)
         out[fd], _, _ = eng.adapt_varlen(waves, 3, SutaHParams(), record=[0, 3])
+        census = eng.get_census()
+        eng.set_census(False)
+        # the census's "epi <kernel> <tile> <flags>" entries: EPI_DELTA (256) alone on the 256 x 256 kernel
+        delta_launches[fd] = sum(v for k, v in census.items() if k.startswith("epi hbx 256x256 ") and k.endswith(" 256"))
         params[fd] = {n: eng.get_param(1, n) for n in eng.trainable_names()}
         eng.close()
+    assert delta_launches["1"] == 3 * cfg["num_hidden_layers"], delta_launches   # one dctx GEMM per layer-backward
+    assert delta_launches["0"] == 0, delta_launches
     for r in (0, 3):
         for u in range(2):
             assert np.array_equal(out["1"][r][u], out["0"][r][u]), (r, u)
@@ -494,3 +501,35 @@ def test_bf16_storage_of_conv_outputs_and_dy_equals_fp32_storage(monkeypatch, sw
         for r in (0, 3):
             assert_bf16_close(out["1"][r][u], out["0"][r][u], 0.97, f"{switch} step {r} utt {u}",
                               rtol=BF16_LOGITS_RTOL_LARGE)
+
+
+def test_batched_gemm_without_off32_epilogue_falls_back(monkeypatch):
+    """A batched (Z > 1) GEMM -- the conv stack's per-utterance forward -- that the 256 x 256 kernel cannot take for
+    want of the 32-bit-offset epilogue (SUTA_EPI_FAST=0 here; an operand over 4 GiB in general) runs on the 128 x 128
+    kernel instead of failing (the dispatcher decides with p.off32 known).  wav2vec2-large in bf16 mode, the 256 x 256
+    kernel forced onto every eligible GEMM (SUTA_HBX=2), no split-K, ragged pair: the default run puts the batched conv
+    forward on hbx, the SUTA_EPI_FAST=0 run on hb, and logits and adapted tensors are bitwise equal (the 256 x 256
+    forms are bitwise the 128 x 128 kernel; the general epilogue applies the fast one's operations in its order)."""
+    monkeypatch.setenv("SUTA_SPLITK", "0")
+    monkeypatch.setenv("SUTA_HBX", "2")
+    cfg = get_config("wav2vec2-large")
+    sd = synth_weights(cfg)
+    waves = [synth.wave(32000, 76), synth.wave(20000, 77)]
+    out, params, batched_hbx = {}, {}, {}
+    for fast in ("1", "0"):
+        monkeypatch.setenv("SUTA_EPI_FAST", fast)
+        eng = SutaEngine(cfg, sd, max_batch=2, max_samples=32000)
+        eng.set_precision("bf16")
+        eng.set_census(True)
+        out[fast], _, _ = eng.adapt_varlen(waves, 2, SutaHParams(), record=[0, 2])
+        census = eng.get_census()
+        eng.set_census(False)
+        batched_hbx[fast] = sum(v for k, v in census.items() if k.startswith("hbx ") and " z=2 " in k)
+        params[fast] = {n: eng.get_param(1, n) for n in eng.trainable_names()}
+        eng.close()
+    assert batched_hbx["1"] > 0 and batched_hbx["0"] == 0, batched_hbx
+    for r in (0, 2):
+        for u in range(2):
+            assert np.array_equal(out["1"][r][u], out["0"][r][u]), (r, u)
+    for n, v in params["1"].items():
+        assert np.array_equal(v, params["0"][n]), n

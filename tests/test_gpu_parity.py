@@ -17,7 +17,7 @@ from suta_amd import synth
 from suta_amd.config import get_config
 from suta_amd.engine import SutaEngine, SutaHParams
 from suta_amd.weights import synth_weights
-from tests.parity import assert_params_close, logits_tol
+from tests.parity import assert_params_close, assert_sgd_params_close, logits_tol
 
 pytestmark = pytest.mark.gpu
 
@@ -212,10 +212,16 @@ def test_graph_replay_equals_eager(preset, n):
     names = eng.trainable_names()
     eng.set_graphs(False)
     a, ia, _ = eng.adapt(x, 4, hp, record=[1, 2, 4])
+    assert eng.graph_stats()["last"] == "eager"
     pa = [{k: eng.get_param(b, k) for k in names} for b in range(2)]
     eng.set_graphs(True)
+    g0 = eng.graph_stats()
     b, ib, _ = eng.adapt(x, 4, hp, record=[1, 2, 4])   # same key as the eager call: captured, then launched
+    g1 = eng.graph_stats()
     c, ic, _ = eng.adapt(x, 4, hp, record=[1, 2, 4])   # replayed
+    g2 = eng.graph_stats()
+    assert g1["last"] == "captured" and g1["captures"] == g0["captures"] + 1 and g1["launches"] == g0["launches"] + 1
+    assert g2["last"] == "replayed" and g2["captures"] == g1["captures"] and g2["launches"] == g1["launches"] + 1
     pc = [{k: eng.get_param(u, k) for k in names} for u in range(2)]
     for r in (1, 2, 4):
         assert np.array_equal(a[r], b[r]) and np.array_equal(a[r], c[r]), r
@@ -365,3 +371,36 @@ def test_branch_free_gelu_equals_erff_gelu(monkeypatch):
                                        err_msg=f"step {r} utt {u}")
         for n in names:
             assert_params_close(par["1"][u][n], par["0"][u][n], 2e-5, 3, name=f"utt {u} {n}")
+
+
+@pytest.mark.parametrize("variant", ["steplr_group", "steplr_layer", "sgd_group", "sgd_steplr_layer",
+                                     "steplr_group_nonepisodic"])
+def test_scheduler_and_sgd_match_reference(variant):
+    """--scheduler torch.optim.lr_scheduler.StepLR (lr * 0.7^i, restored by the episodic reset) and --opt SGD
+    against the reference driver loop's own runs (g9, main.py:308-348): logits after every step within
+    logits_tol, adapted tensors within the Adam budget (AdamW) or the SGD bound; the non-episodic variant carries
+    tensors, moments and the scheduler's step count into the second utterance."""
+    from tests.test_oracle_golden import g9_hparams
+    z = _load(f"g9_sched_{variant}.npz")
+    preset = "tiny-layer" if "layer" in variant else "tiny-group"
+    cfg = get_config(preset)
+    sd = synth_weights(cfg)
+    opt, lr, ss, episodic, steps = g9_hparams(z)
+    eng = SutaEngine(cfg, sd, max_batch=1)
+    hp = SutaHParams(lr=lr, optimizer=opt, lr_step_size=ss, episodic=episodic)
+    prev = {k: v.copy() for k, v in sd.items()}
+    for n in (8000, 12345):
+        logits, ids, T = eng.adapt(z[f"N{n}/x"], steps, hp, record=list(range(steps + 1)))
+        for i in range(steps + 1):
+            np.testing.assert_allclose(logits[i][0], z[f"N{n}/logits"][i], rtol=0, atol=logits_tol(5e-4),
+                                       err_msg=f"{variant} N{n} step {i}")
+        for key in z.files:
+            if key.startswith(f"N{n}/final/"):
+                name = key[len(f"N{n}/final/"):]
+                if opt == "SGD":
+                    assert_sgd_params_close(eng.get_param(0, name), z[key], prev[name], name=name)
+                else:
+                    assert_params_close(eng.get_param(0, name), z[key], lr, steps * (1 if episodic else 2), name=name)
+        if not episodic:
+            prev = {k[len(f"N{n}/final/"):]: z[k] for k in z.files if k.startswith(f"N{n}/final/")}
+    eng.close()

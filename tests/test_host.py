@@ -300,3 +300,30 @@ def test_legacy_weight_norm_names_in_safetensors(tmp_path):
     got = load_hf_checkpoint(str(tmp_path))
     assert sorted(got) == sorted(sd)
     assert np.array_equal(got[pre + "parametrizations.weight.original1"], sd[pre + "parametrizations.weight.original1"])
+
+
+def test_resolve_scheduler_and_optimizer_flags():
+    """--scheduler resolves the reference's eval'd dotted name (main.py:20-21) to StepLR's (step_size, gamma);
+    anything else is refused, as the reference's call with step_size / gamma keywords would fail for it."""
+    from suta_amd import main as M
+    from suta_amd.engine import SutaHParams
+    assert M.resolve_scheduler(None) == (0, 0.7)
+    assert M.resolve_scheduler("torch.optim.lr_scheduler.StepLR") == (1, 0.7)
+    for bad in ("StepLR", "torch.optim.lr_scheduler.ExponentialLR", "os.system"):
+        with pytest.raises(SystemExit):
+            M.resolve_scheduler(bad)
+    hp = SutaHParams(optimizer="SGD", lr_step_size=1).to_c()
+    assert (hp.optimizer, hp.lr_step_size, abs(hp.lr_gamma - 0.7) < 1e-7) == (1, 1, True)
+    with pytest.raises(ValueError):
+        SutaHParams(optimizer="RMSprop").to_c()
+
+
+def test_budget_clamped_to_free_device_memory():
+    """--gpu_budget_s defaults are sized for the 288 GB MI355X; on less free memory the driver clamps them."""
+    from suta_amd import main as M
+    base = get_config("wav2vec2-base")
+    assert M.workspace_bytes_per_audio_s(base) >= 0.36e9 / 8          # the measured 45 MB/s is covered
+    assert M.clamp_budget(1312.0, base, 280e9) == 1312.0             # an MI355X keeps the default
+    small = M.clamp_budget(1312.0, base, 16e9)
+    assert small < 1312.0 and small * M.workspace_bytes_per_audio_s(base) <= 0.7 * 16e9 + 1
+    assert M.clamp_budget(1312.0, base, None) == 1312.0

@@ -13,7 +13,8 @@ from oracle import w2v2_cpu as W
 from oracle.suta_loss_np import suta_loss_and_grad
 from suta_amd.config import get_config
 from suta_amd.weights import synth_weights
-from tests.parity import assert_params_close, logits_tol, same_pseudo_labels, sdpl_logits_tol
+from tests.parity import (assert_params_close, assert_sgd_params_close, logits_tol, same_pseudo_labels,
+                          sdpl_logits_tol)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 G = os.path.join(HERE, "golden")
@@ -191,3 +192,53 @@ def test_g6_sdpl_tiny_oracle_matches_reference(variant):
         if key.startswith("N8000/final/"):
             name = key[len("N8000/final/"):]
             assert_params_close(final[name].numpy(), z[key], lr, 5, max_frac=1.0, name=name, factor=2.0)
+
+
+# ---------------------------------------------------------------------------------------------
+# --scheduler StepLR / --opt SGD (reference main.py:8-23, 147-155, 207-208): g9 fixtures
+# ---------------------------------------------------------------------------------------------
+G9_VARIANTS = ["steplr_group", "steplr_layer", "sgd_group", "sgd_steplr_layer", "steplr_group_nonepisodic"]
+
+
+def g9_hparams(z):
+    """(opt, lr, lr_step_size, episodic, steps) of a g9 fixture: the reference's setup_optimizer passes
+    step_size 1 and gamma 0.7 to the scheduler (main.py:8, 21)."""
+    return (str(z["opt"]), float(z["lr"]), 1 if str(z["scheduler"]) != "None" else 0, bool(z["episodic"]),
+            int(z["steps"]))
+
+
+def test_step_lr_matches_reference_lr_sequence():
+    z = _load("g9_sched_steplr_group_nonepisodic.npz")
+    lrs = np.concatenate([z["N8000/lrs"], z["N12345/lrs"]])   # one scheduler across both utterances
+    got = [W.step_lr(float(z["lr"]), 0.7, 1, i) for i in range(len(lrs))]
+    assert np.array_equal(np.array(got, np.float64), lrs)
+    z = _load("g9_sched_steplr_group.npz")                   # episodic: restored per utterance
+    assert np.array_equal(z["N8000/lrs"], z["N12345/lrs"])
+
+
+@pytest.mark.parametrize("variant", G9_VARIANTS)
+def test_g9_scheduler_sgd_oracle_matches_reference(variant):
+    z = _load(f"g9_sched_{variant}.npz")
+    cfg = get_config("tiny-layer" if "layer" in variant else "tiny-group")
+    sd = synth_weights(cfg)
+    from tests.golden.make_golden import weights_digest  # noqa
+    assert weights_digest(sd) == str(z["weights_sha256"]), "seeded weight generator drifted"
+    assert W.trainable_entries(cfg, train_feature=True) == [str(s) for s in z["entries"]]
+    opt, lr, ss, episodic, steps = g9_hparams(z)
+    params = {k: torch.from_numpy(v) for k, v in sd.items()}
+    carry = None if episodic else W.OptCarry()
+    prev = {k: v.copy() for k, v in sd.items()}
+    for n in (8000, 12345):
+        x = torch.from_numpy(z[f"N{n}/x"])[None]
+        out, final = W.run_suta(params, cfg, x, steps, lr=lr, opt=opt, lr_step_size=ss, carry=carry)
+        for i in range(steps + 1):
+            np.testing.assert_allclose(out[i][0].numpy(), z[f"N{n}/logits"][i], rtol=0, atol=logits_tol(5e-4),
+                                       err_msg=f"{variant} N{n} step {i}")
+        for k, v in final.items():
+            ref = z[f"N{n}/final/{k}"]
+            if opt == "SGD":
+                assert_sgd_params_close(v.numpy(), ref, prev[k], name=k)
+            else:
+                assert_params_close(v.numpy(), ref, lr, steps * (1 if episodic else 2), name=k)
+        if not episodic:
+            prev = {k: z[f"N{n}/final/{k}"] for k in final}
