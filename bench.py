@@ -57,7 +57,7 @@ BATCH = 164        # utterances per engine call (see --batch); tests/test_gpu_be
 C4_BATCH = BATCH   # config C4's utterances per call (see --c4-batch)
 PMC_BATCH = 164    # the batch the committed headline PMC passes were taken at
 PMC_BATCH_C4 = 164  # the batch of the committed C4 passes
-C5_UTTERANCES = 96  # config C5's seeded TED-like length mix (see --c5-n)
+C5_UTTERANCES = 512  # config C5: a TED-LIUM-3-test-sized seeded length mix (see --c5-n; ~30 s per pass)
 GEMM_KERNELS = ("gemm_glds_kernel", "gemm_f32_kernel", "gemm_splitk_reduce", "attn_fwd_kernel", "attn_bwd_kernel",
                 "posconv_kernel", "flash_fwd_kernel", "flash_bwd_kernel", "flash_dq_reduce")
 # config C4's GEMM family (bf16 mode): every kernel its "gemm" + "attention" timing families launch.  Matched to the

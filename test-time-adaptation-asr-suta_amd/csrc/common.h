@@ -91,6 +91,8 @@ struct SutaSwitches {
     int hbx_t;            // SUTA_HBX_T (default 2): gemm_hbx accumulates C^T fragments with a row-per-lane epilogue whose
                           // outputs are staged through LDS into whole-line stores; 1 = direct 16-B row-per-lane stores,
                           // 0 = the column-per-lane form shared with the 128 x 128 kernel
+    int hbp_conv;         // SUTA_HBP_CONV (default 1): the conv stack's conv-seg input gradients on the four-phase 256 x 256
+                          // kernel (gemm.hip use_hbp_conv); 0 = the 128 x 128 kernel
     int epi_fast;         // SUTA_EPI_FAST (default 1): 32-bit-offset GEMM epilogue where every operand fits 4 GiB (p.off32);
                           // 0 = the general epilogue everywhere
 };

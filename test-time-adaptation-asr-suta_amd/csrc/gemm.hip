@@ -224,6 +224,16 @@ static bool use_hbx(const GemmParams& p) {
     return (long)((p.M + 255) / 256) * ((p.N + 255) / 256) * p.Z >= 256;
 }
 
+// the conv stack's input gradients (conv-A rows, per-tap weight segments: config C4's conv-seg GEMMs, Z = B) on the
+// four-phase 256 x 256 kernel's CONV form (gemm_hbx.hip hbp_conv_ok) on grids of at least one round of 256 tiles;
+// SUTA_HBP_CONV=0 keeps them on the 128 x 128 kernel (A/B runs), SUTA_HBX=2 forces them on every eligible grid
+static bool use_hbp_conv(const GemmParams& p) {
+    const SutaSwitches& sw = suta_switches();
+    if (!sw.hbx || !sw.hbp_conv || !hbp_conv_ok(p)) return false;
+    if (sw.hbx == 2) return true;
+    return (long)((p.M + 255) / 256) * ((p.N + 255) / 256) * p.Z >= 256;
+}
+
 // 32-bit epilogue offsets: M x ld elements of every operand the epilogue touches within 4 GiB
 // (SUTA_EPI_FAST=0 in the call's switch snapshot: the general epilogue everywhere, for A/B runs)
 static int epilogue_off32(const GemmParams& p) {
@@ -274,13 +284,15 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
         throw std::invalid_argument("gemm: bf16 pre-activation operands need the bf16-plane kernel with a Cb plane, ldc2 even");
     if (hb && p.segK > 0 && (p.segK % 8 || p.pad < 0 || (p.segB && (p.sBseg % 8))))
         throw std::invalid_argument("gemm: conv-A bf16 planes need segK and the tap stride % 8 == 0");
-    int tile = hbt || (hb && p.segK > 0) ? 0
+    int tile = hbt ? 0
+               : (hb && p.segK > 0) ? (g_force_tile < 0 && use_hbp_conv(p) ? 8 : 0)
                : g_force_tile >= 0 ? g_force_tile
                : hb            ? (use_hb8(p) ? 6 : use_hbx(p) ? 8 : choose_tile_hb(p.M, p.N, p.Z))
                : p.mode == 2   ? choose_tile_bf16(p.M, p.N, p.Z, !bf16_gbf)
                                : choose_tile(p.M, p.N, p.Z, p.K, p.mode);
     const bool glds_path = p.mode == 0 && g_nbuf == 3 && glds_ok;
-    if ((tile == 8 || tile == 9) && !(hb && p.K % 32 == 0 && p.K >= 128 && p.segK == 0 && (p.Z == 1 || (tile == 8 && hbx_batch_ok(p)))))
+    if ((tile == 8 || tile == 9) && !(hb && p.K % 32 == 0 && p.K >= 128 && p.segK == 0 && (p.Z == 1 || (tile == 8 && hbx_batch_ok(p)))) &&
+        !(tile == 8 && hb && p.segK > 0 && hbp_conv_ok(p)))
         tile = 0;
     if (tile == 7 && !glds_path) tile = 0;  // the 160-row tile exists only in the default LDS-DMA kernel
     if (tile == 6 && !(hb && p.K % 32 == 0)) tile = 0;  // the 256 x 256 tile is the bf16-plane ping-pong kernel only

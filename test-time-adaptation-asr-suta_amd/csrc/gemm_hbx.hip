@@ -648,7 +648,15 @@ constexpr int P_HALF = 16384;  // bytes per half-tile image (128 rows x 128 B)
 
 __device__ __forceinline__ int hbp_swz(int r) { return (r >> 1) & 7; }
 
-template <bool CB, int EM, bool STAG>
+// FORM 1: lockstep; 2: wave groups one barrier apart (STAG); 3: STAG with three half-tiles of DMA in flight and one
+// counted wait per K-tile (below).
+// CONV: conv-A rows with per-tap weight segments (the conv stack's input gradients, gemm.hip use_hbp_conv): A(m, k) =
+// Ab[(m + seg - pad) ldab + k - seg segK], zero unless 0 <= m + seg - pad < Mvalid (per utterance: zmvalid), B(k, n) =
+// Bb[n ldbb + k - seg segK + seg sBseg], seg = k / segK.  With ldab == segK the A address is linear in k (a segment
+// step is one row down and back to column 0), so only the row's validity changes per segment; the B address jumps by
+// sBseg - segK at each segment boundary.  Both are evaluated per DMA issue (segK % 64 == 0: a K-tile lies in one
+// segment), so the shifts live in the DMA pointers, not in per-element VALU work.
+template <bool CB, int EM, int FORM, bool CONV = false>
 __global__ __launch_bounds__(512, 1) void gemm_hbp_kernel(GemmParams p) {
     __shared__ __attribute__((aligned(16))) float smem[8 * P_HALF / 4];
     char* const lds = reinterpret_cast<char*>(smem);
@@ -663,10 +671,13 @@ __global__ __launch_bounds__(512, 1) void gemm_hbp_kernel(GemmParams p) {
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wr = wid >> 2, wc = wid & 3;
+    constexpr bool STAG = FORM >= 2;
 
     // DMA sources: half h (0 A0, 1 B0, 2 B1, 3 A1 -- the issue order), pieces wid and wid + 8 (8 LDS rows each)
     const __bf16* src[4][2];
     int inc[4][2];
+    int arow[2][2];  // CONV: source row m - pad of the A halves' pieces (segment 0)
+    const int mv = CONV ? (p.zmvalid ? p.zmvalid[z1] : p.Mvalid) : 0;
 #pragma unroll
     for (int h = 0; h < 4; ++h)
 #pragma unroll
@@ -676,11 +687,19 @@ __global__ __launch_bounds__(512, 1) void gemm_hbp_kernel(GemmParams p) {
             const bool isa = h == 0 || h == 3;
             const int q = h == 3 ? 1 : h == 2 ? 1 : 0;  // qm for A halves, qn for B halves
             const int grow = isa ? m0 + (lr >> 6) * 128 + q * 64 + (lr & 63) : n0 + (lr >> 5) * 64 + q * 32 + (lr & 31);
+            if (CONV && isa) {  // linear address of row grow - pad (validity decided per issue)
+                arow[h == 3 ? 1 : 0][i] = grow - p.pad;
+                src[h][i] = A + (long)(grow - p.pad) * p.ldab + 8 * c;
+                inc[h][i] = 64;
+                continue;
+            }
             const bool ok = grow < (isa ? p.M : p.N);
             const long ld = isa ? p.ldab : p.ldbb;
             src[h][i] = ok ? (isa ? A : B) + (long)grow * ld + 8 * c : reinterpret_cast<const __bf16*>(g_zero16);
             inc[h][i] = ok ? 64 : 0;
         }
+    const int spt = CONV ? p.segK / 64 : 1;          // K-tiles per segment
+    const long bjump = CONV ? p.sBseg - p.segK : 0;  // B address step at a segment boundary (bf16 elements)
     // LDS image of half h in buffer b (images in the order A0, A1, B0, B1)
     auto himg = [&](int b, int h) -> char* {
         const int slot = h == 0 ? 0 : h == 3 ? 1 : h == 1 ? 2 : 3;
@@ -688,6 +707,25 @@ __global__ __launch_bounds__(512, 1) void gemm_hbp_kernel(GemmParams p) {
     };
     auto issue = [&](int t, int h) {  // half h of K-tile t into buffer t & 1
         char* dst = himg(t & 1, h);
+        if constexpr (CONV) {
+            const int seg = t / spt;
+            const bool isa = h == 0 || h == 3;
+            if (!isa && t > 0 && t == seg * spt) {  // the next tap's weight slice
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+                    if (inc[h][i]) src[h][i] += bjump;
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const __bf16* g = src[h][i];
+                if (isa && (unsigned)(arow[h == 3 ? 1 : 0][i] + seg) >= (unsigned)mv)
+                    g = reinterpret_cast<const __bf16*>(g_zero16);  // conv padding row: zeros
+                __builtin_amdgcn_global_load_lds(reinterpret_cast<const float*>(g),
+                                                 (lds_ptr_t)(dst + (wid + 8 * i) * 1024), 16, 0, 0);
+                src[h][i] += inc[h][i];
+            }
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             __builtin_amdgcn_global_load_lds(reinterpret_cast<const float*>(src[h][i]),
@@ -729,7 +767,8 @@ __global__ __launch_bounds__(512, 1) void gemm_hbp_kernel(GemmParams p) {
     // counted wait of phase p: the halves issued at phases p - 1 and p (if any) may stay in flight
     auto wait_phase = [&](int n_out) {
         __builtin_amdgcn_sched_barrier(0);
-        if (n_out >= 2) wait_vm<4>();
+        if (n_out >= 3) wait_vm<6>();
+        else if (n_out >= 2) wait_vm<4>();
         else if (n_out == 1) wait_vm<2>();
         else wait_vm<0>();
     };
@@ -748,6 +787,60 @@ __global__ __launch_bounds__(512, 1) void gemm_hbp_kernel(GemmParams p) {
         barrier();
     };
 
+    if constexpr (FORM == 3) {
+        // Deep form (cdna_hip_programming.md's 256^2 template schedule): the halves of K-tile t + 2 go into buffer t & 1
+        // as soon as K-tile t is done with them, so three halves stay in flight and the wave waits once per K-tile.
+        //   phase 1  reads B0, A0 of t  (B first)  | issues A1 of t + 1 (last read: phase 3 of t - 1, two phases back)
+        //                                          | lgkmcnt(0) BEFORE the barrier: A0 / B0 of buffer t & 1 are free
+        //   phase 2  reads B1                      | issues A0 of t + 2 (read in phase 1, retired before its barrier)
+        //   phase 3  reads A1                      | issues B0 of t + 2 (read in phase 1)
+        //   phase 4  --                            | issues B1 of t + 2 (read in phase 2); vmcnt(6): all but the three
+        //                                          | halves of t + 2 retired -> K-tile t + 1 complete, read from phase 5
+        // With the groups one barrier apart a read of the lagging group still follows the other group's wait by a
+        // barrier, and an issue of the leading group follows the lagging group's retired reads by one (the phase
+        // bodies are placed so: reads and issues before the first barrier, the wait before it in phase 4).
+#pragma unroll
+        for (int h = 0; h < 4; ++h) issue(0, h);
+        if (nk > 1) {
+            issue(1, 0);
+            issue(1, 1);
+            issue(1, 2);
+            wait_vm<6>();
+        } else {
+            wait_vm<0>();
+        }
+        if (wr == 1) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier behind group 0
+        __builtin_amdgcn_s_barrier();
+        for (int t = 0; t < nk; ++t) {
+            const int b = t & 1;
+            const bool n1 = t + 1 < nk, n2 = t + 2 < nk;
+            // phase 1: quadrant (0,0)
+            read_b(b, 0, fb0);
+            __builtin_amdgcn_sched_barrier(0);
+            read_a(b, 0);
+            if (n1) issue(t + 1, 3);
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) before the barrier (WAR of phase 2's issue)
+            __builtin_amdgcn_sched_barrier(0);
+            barrier();
+            __builtin_amdgcn_s_setprio(1);
+            mfma_q(0, 0, fb0);
+            __builtin_amdgcn_s_setprio(0);
+            barrier();
+            // phase 2: quadrant (0,1)
+            read_b(b, 1, fb1);
+            if (n2) issue(t + 2, 0);
+            mfma_phase(0, 1, fb1);
+            // phase 3: quadrant (1,1)
+            read_a(b, 1);
+            if (n2) issue(t + 2, 1);
+            mfma_phase(1, 1, fb1);
+            // phase 4: quadrant (1,0)
+            if (n2) issue(t + 2, 2);
+            wait_phase(n2 ? 3 : 0);
+            mfma_phase(1, 0, fb0);
+        }
+    } else {
     // prologue: K-tile 0's four halves; A0 and B0 (phase 1's) retired
 #pragma unroll
     for (int h = 0; h < 4; ++h) issue(0, h);
@@ -779,6 +872,7 @@ __global__ __launch_bounds__(512, 1) void gemm_hbp_kernel(GemmParams p) {
         if (nxt) issue(t + 1, 3);
         wait_phase(nxt ? 2 : 0);
         mfma_phase(1, 0, fb0);
+    }
     }
     wait_vm<0>();
     if constexpr (STAG) {
@@ -838,6 +932,16 @@ bool hbx_t_ok(const GemmParams& p, bool check_off32) {
     return true;
 }
 
+// the conv stack's input-gradient GEMMs (conv-A rows, per-tap bf16 weight segments) on the four-phase 256 x 256 kernel:
+// k-contiguous planes whose A rows are the segments (ldab == segK, segK % 64 == 0, segmented B, no batch split inside a
+// plane), the staggered main loop (SUTA_HBX_FORM 2 / 3) with the staged C^T epilogue, the plain epilogue class
+bool hbp_conv_ok(const GemmParams& p) {
+    const SutaSwitches& sw = suta_switches();
+    return p.segK > 0 && p.segB && p.segK % 64 == 0 && p.ldab == p.segK && p.pad >= 0 && p.K % 64 == 0 && p.K >= 128 &&
+           p.zdiv == 1 && !p.ta && p.Ab && p.Bb && sw.hbx_form >= 2 && sw.hbx_t == 2 && !sw.hbx_dbg &&
+           (p.epi & ~(EPI_BIAS | EPI_RESID | EPI_ROWMASK)) == 0 && !p.preb && p.splits <= 1 && hbx_t_ok(p, true);
+}
+
 namespace {
 
 // epilogue classes of the bf16 linears (as gemm_hb_ep.hip): bias / residual, bias + GELU + pre-activation store,
@@ -858,6 +962,17 @@ void gemm_run_hbx(int variant, const GemmParams& p, dim3 grid, hipStream_t st) {
     if (p.Z != 1 && !(variant == 1 && suta_switches().hbx_form && suta_switches().hbx_t == 2 && p.K % 64 == 0 &&
                       hbx_t_ok(p, true) && !suta_switches().hbx_dbg))
         throw std::invalid_argument("hbx: batched GEMMs only on the four-phase form with the staged C^T epilogue");
+    if (p.segK > 0) {  // conv-A rows: the four-phase form's CONV instantiation (gemm.hip hbp_conv_ok)
+        if (!hbp_conv_ok(p)) throw std::invalid_argument("hbx: conv-A GEMM outside the four-phase CONV form's conditions");
+        if (suta_switches().hbx_form == 3) {
+            if (p.Cb) hipLaunchKernelGGL((gemm_hbp_kernel<true, XEM_A, 3, true>), grid, dim3(512), 0, st, p);
+            else hipLaunchKernelGGL((gemm_hbp_kernel<false, XEM_A, 3, true>), grid, dim3(512), 0, st, p);
+        } else {
+            if (p.Cb) hipLaunchKernelGGL((gemm_hbp_kernel<true, XEM_A, 2, true>), grid, dim3(512), 0, st, p);
+            else hipLaunchKernelGGL((gemm_hbp_kernel<false, XEM_A, 2, true>), grid, dim3(512), 0, st, p);
+        }
+        return;
+    }
     if ((e & EPI_DELTA) && !(variant == 1 && suta_switches().hbx_t && hbx_t_ok(p, true)))
         throw std::invalid_argument("hbx: EPI_DELTA needs the C^T epilogue and its operand conditions");
     if (variant == 2) {
@@ -874,12 +989,15 @@ void gemm_run_hbx(int variant, const GemmParams& p, dim3 grid, hipStream_t st) {
         const bool cb = p.Cb != nullptr;
 #define HBP(EM_)                                                                                                   \
         do {                                                                                                       \
-            if (form == 2) {                                                                                       \
-                if (cb) hipLaunchKernelGGL((gemm_hbp_kernel<true, EM_, true>), grid, dim3(512), 0, st, p);         \
-                else hipLaunchKernelGGL((gemm_hbp_kernel<false, EM_, true>), grid, dim3(512), 0, st, p);           \
+            if (form == 3) {                                                                                       \
+                if (cb) hipLaunchKernelGGL((gemm_hbp_kernel<true, EM_, 3>), grid, dim3(512), 0, st, p);            \
+                else hipLaunchKernelGGL((gemm_hbp_kernel<false, EM_, 3>), grid, dim3(512), 0, st, p);              \
+            } else if (form == 2) {                                                                                \
+                if (cb) hipLaunchKernelGGL((gemm_hbp_kernel<true, EM_, 2>), grid, dim3(512), 0, st, p);            \
+                else hipLaunchKernelGGL((gemm_hbp_kernel<false, EM_, 2>), grid, dim3(512), 0, st, p);              \
             } else {                                                                                               \
-                if (cb) hipLaunchKernelGGL((gemm_hbp_kernel<true, EM_, false>), grid, dim3(512), 0, st, p);        \
-                else hipLaunchKernelGGL((gemm_hbp_kernel<false, EM_, false>), grid, dim3(512), 0, st, p);          \
+                if (cb) hipLaunchKernelGGL((gemm_hbp_kernel<true, EM_, 1>), grid, dim3(512), 0, st, p);            \
+                else hipLaunchKernelGGL((gemm_hbp_kernel<false, EM_, 1>), grid, dim3(512), 0, st, p);              \
             }                                                                                                      \
             return;                                                                                                \
         } while (0)

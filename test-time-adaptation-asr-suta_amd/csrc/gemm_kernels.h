@@ -1981,3 +1981,5 @@ void gemm_run_hbt(const GemmParams& p, dim3 grid, hipStream_t st);              
 void gemm_run_hbx(int variant, const GemmParams& p, dim3 grid, hipStream_t st);                             // gemm_hbx.hip
 // the row-per-lane (C^T accumulator) epilogue's operand conditions (gemm_hbx.hip)
 bool hbx_t_ok(const GemmParams& p, bool check_off32);
+// conv-A GEMM (segK > 0) eligible for the four-phase 256 x 256 kernel's CONV form (gemm_hbx.hip; p.off32 set)
+bool hbp_conv_ok(const GemmParams& p);

@@ -1942,6 +1942,7 @@ void suta_latch_switches() {
     const char* fnw = std::getenv("SUTA_FLASH_FWD_NW");
     s.flash_fwd_nw = (fnw && atoi(fnw) == 8) ? 8 : 4;
     s.epi_fast = on("SUTA_EPI_FAST");
+    s.hbp_conv = on("SUTA_HBP_CONV");
     s.latched = 1;
     g_switches = s;
 }

@@ -53,8 +53,9 @@ int main(int argc, char** argv) {
     // (tile, ns, cb-capable, SUTA_HBX_T, SUTA_HBX_DBG): the DBG forms are diagnostics (wrong results): 1 no B DMA,
     // 2 no B fragment reads, 3 no DMA, 4 no fragment reads
     // + SUTA_HBX_FORM (6th): 1 the four-phase K-tile schedule (gemm_hbp_kernel), 2 the same with staggered wave groups
-    const int variants[][6] = {{8, 2, 1, 2, 0, 0}, {8, 2, 1, 2, 0, 1}, {8, 2, 1, 2, 0, 2}};
-    const char* vname[] = {"hbxTS", "hbp  ", "hbpS "};
+    // 3: the four-phase schedule with three half-tiles of DMA in flight and one counted wait per K-tile
+    const int variants[][6] = {{8, 2, 1, 2, 0, 0}, {8, 2, 1, 2, 0, 2}, {8, 2, 1, 2, 0, 3}};
+    const char* vname[] = {"hbxTS", "hbpS ", "hbpD "};
     constexpr int NV = 3;
     auto set_variant = [&](int v) {
         const char* tv[] = {"0", "1", "2", "3", "4", "5"};
