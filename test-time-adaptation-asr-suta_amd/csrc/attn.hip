@@ -357,6 +357,193 @@ __global__ __launch_bounds__(NW * 64) void flash_fwd_kernel(const float* __restr
 }
 
 
+// Software-pipelined exact-fp32 forward (the headline's; SUTA_FLASH_FWD_PIPE, default): iteration kt issues the S^T
+// MFMAs of key tile kt + 1 and then runs the softmax of tile kt (VALU) and its PV MFMAs.  The next tile's S chain does
+// not depend on this tile's softmax, so the wave keeps its MFMA pipe fed through its own softmax instead of waiting on
+// its S chain and then leaving the pipe idle during the exp / max / sum work.  K therefore runs one tile ahead of V
+// in LDS (still two buffers each: iteration kt reads K(kt + 1) and V(kt) and writes K(kt + 2) and V(kt + 1) into the
+// buffers iteration kt - 1 read, one barrier per iteration).  Per element the same operations as flash_fwd_kernel in
+// the same order (S chains, masks on the utterance's last tile only, online softmax, PV), so ctx and LSE are bitwise
+// equal; the three loop bodies (full next tile, next tile the last one, no next tile) are separate instantiations so
+// each is one basic block the scheduler can interleave.
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void flash_fwd_pipe_kernel(const float* __restrict__ qkv, float* __restrict__ ctx,
+                                                                 float* __restrict__ lse, int T, int NH, int H,
+                                                                 float scale, const int* __restrict__ tlen, int nqb,
+                                                                 __bf16* __restrict__ ctxb) {
+    constexpr int NT = NW * 64;
+    constexpr int ITEMS = FK * 16, NPT = (ITEMS + NT - 1) / NT;
+    __shared__ __attribute__((aligned(16))) float Ks[2][FK * FA_LD];
+    __shared__ __attribute__((aligned(16))) float Vt[2][64 * FK_LDT];
+    const int id = xcd_block();
+    const int qb = id % nqb, bh = id / nqb, hd = bh % NH, u = bh / NH;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, l32 = lane & 31,
+              h = lane >> 5;
+    const int tl = tlen ? tlen[u] : T;
+    const long ld = 3L * H;
+    const float* Qb = qkv + (long)u * T * ld + hd * 64;
+    const float* Kb = Qb + H;
+    const float* Vb = Qb + 2 * H;
+    const int q0 = (qb * NW + w) * 32;
+    if (tl <= 0) {
+        flash_fwd_no_keys(ctx, ctxb, lse, (long)u * T, (long)bh * T, T, H, hd, q0, l32, h);
+        return;
+    }
+    const bool active = q0 < T;
+    const float sl2 = scale * LOG2E;
+    RowReg<false> qv;
+    qv.load(Qb + (long)min(q0 + l32, T - 1) * ld, h);
+    auto vmap = [](int it, int& key, int& c4) {
+        const int l = it & 63, wi = it >> 6;
+        key = (l & 15) + 16 * (wi & 3);
+        c4 = 4 * ((l >> 4) + 4 * (wi >> 2));
+    };
+    f32x4 kr[NPT], vr[NPT];
+    auto fetch_k = [&](int kt) {
+#pragma unroll
+        for (int n = 0; n < NPT; ++n) {
+            const int it = threadIdx.x + n * NT, row = it >> 4, c4 = (it & 15) * 4, key = kt * FK + row;
+            kr[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (it < ITEMS && key < T) kr[n] = *reinterpret_cast<const f32x4*>(Kb + (long)key * ld + c4);
+        }
+    };
+    auto fetch_v = [&](int kt) {
+#pragma unroll
+        for (int n = 0; n < NPT; ++n) {
+            const int it = threadIdx.x + n * NT;
+            int vk, vc;
+            vmap(it, vk, vc);
+            vr[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (it < ITEMS && kt * FK + vk < T) vr[n] = *reinterpret_cast<const f32x4*>(Vb + (long)(kt * FK + vk) * ld + vc);
+        }
+    };
+    auto put_k = [&](int buf) {
+#pragma unroll
+        for (int n = 0; n < NPT; ++n) {
+            const int it = threadIdx.x + n * NT, row = it >> 4, c4 = (it & 15) * 4;
+            if (it < ITEMS) *reinterpret_cast<f32x4*>(&Ks[buf][row * FA_LD + c4]) = kr[n];
+        }
+    };
+    auto put_v = [&](int buf) {
+#pragma unroll
+        for (int n = 0; n < NPT; ++n) {
+            const int it = threadIdx.x + n * NT;
+            int vk, vc;
+            vmap(it, vk, vc);
+            if (it < ITEMS) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) Vt[buf][(vc + e) * FK_LDT + vk] = vr[n][e];
+            }
+        }
+    };
+
+    const int nkt = (tl + FK - 1) / FK;
+    f32x16 o[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) o[t][v] = 0.f;
+    float m_run = -INFINITY, l_run = 0.f;
+    // prologue: K(0), V(0) into buffer 0, K(1) into buffer 1; S of tile 0
+    fetch_k(0);
+    fetch_v(0);
+    put_k(0);
+    put_v(0);
+    if (nkt > 1) {
+        fetch_k(1);
+        put_k(1);
+    }
+    __syncthreads();
+    f32x16 sc[2];
+    auto s_tile = [&](f32x16 (&s)[2], int kt, bool two) {  // raw scores S^T of key tile kt (key r8(v,h), query l32)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+#pragma unroll
+            for (int v = 0; v < 16; ++v) s[j][v] = 0.f;
+            if (j == 0 || two) prod_rows<false>(s[j], Ks[kt & 1] + 32 * j * FA_LD, qv, l32, h);
+        }
+    };
+    if (active) s_tile(sc, 0, nkt > 1 || 32 < tl);
+    if (nkt > 2) __syncthreads();  // K(0) read by every wave before iteration 0 writes K(2) over it
+    // NEXT: 1 = the next tile is a full one, 2 = the next tile is the utterance's last (its second half may be empty),
+    // 0 = no next tile (this one is the last)
+    auto iter = [&](int kt, auto next_tag) {
+        constexpr int NEXT = decltype(next_tag)::value;
+        constexpr bool LAST = NEXT == 0;
+        if (NEXT == 1) fetch_k(kt + 2);
+        if (NEXT != 0) fetch_v(kt + 1);
+        if (active) {
+            f32x16 sn[2];
+            if constexpr (NEXT != 0) s_tile(sn, kt + 1, NEXT == 1 || (kt + 1) * FK + 32 < tl);
+            const bool two = !LAST || kt * FK + 32 < tl;
+            float mx = -INFINITY;
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int v = 0; v < 16; ++v) {
+                    const bool ok = !LAST || kt * FK + 32 * j + r8(v, h) < tl;
+                    sc[j][v] = ok ? sl2 * sc[j][v] : -INFINITY;
+                    mx = fmaxf(mx, sc[j][v]);
+                }
+            mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+            const float m_new = fmaxf(m_run, mx);
+            float ls = 0.f;
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int v = 0; v < 16; ++v) {
+                    sc[j][v] = __builtin_amdgcn_exp2f(sc[j][v] - m_new);
+                    ls += sc[j][v];
+                }
+            if (m_new != m_run) {
+                const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+                l_run *= alpha;
+#pragma unroll
+                for (int t = 0; t < 2; ++t)
+#pragma unroll
+                    for (int v = 0; v < 16; ++v) o[t][v] *= alpha;
+                m_run = m_new;
+            }
+            l_run += ls;
+            apply_cols<false, FK_LDT>(o, Vt[kt & 1], sc[0], l32, h);
+            if (two) apply_cols<false, FK_LDT>(o, Vt[kt & 1] + 32, sc[1], l32, h);
+            if constexpr (NEXT != 0) {
+#pragma unroll
+                for (int j = 0; j < 2; ++j) sc[j] = sn[j];
+            }
+        }
+        if (NEXT == 1) put_k(kt & 1);
+        if (NEXT != 0) put_v((kt + 1) & 1);
+        if (!LAST) __syncthreads();
+    };
+    int kt = 0;
+    for (; kt + 2 < nkt; ++kt) iter(kt, std::integral_constant<int, 1>{});
+    if (kt + 1 < nkt) iter(kt++, std::integral_constant<int, 2>{});
+    iter(kt, std::integral_constant<int, 0>{});
+    if (!active) return;
+    const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+    const int q = q0 + l32;
+    if (q >= T) return;
+    const float inv = 1.0f / l_tot;
+    float* cr = ctx + ((long)u * T + q) * H + hd * 64 + 4 * h;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+            f32x4 r;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) r[b] = o[t][4 * a + b] * inv;
+            *reinterpret_cast<f32x4*>(cr + 32 * t + 8 * a) = r;
+            if (ctxb) {
+                fbf16x4 b;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) b[e] = (__bf16)r[e];
+                *reinterpret_cast<fbf16x4*>(ctxb + ((long)u * T + q) * H + hd * 64 + 4 * h + 32 * t + 8 * a) = b;
+            }
+        }
+    if (h == 0) lse[(long)bh * T + q] = (m_run + log2f(l_tot)) * (1.0f / LOG2E);
+}
+
 // In-launch combination of a head's dQ partials (replaces the flash_dq_reduce pass when cnt is given): every key
 // block of the head publishes its partial (cdna_hip_programming.md's split-K seam protocol: stores drained, block
 // barrier, an agent-scope release, then a ticket on the head's counter); the block drawing nkb - 1 acquires and sums
@@ -1231,7 +1418,9 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
     float* Dl = Ls + 64;                          // [2][32]
     const int id = xcd_block();
     const int kb = id % nkb, bh = id / nkb, hd = bh % NH, u = bh / NH;
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, l32 = lane & 31, h = lane >> 5;
+    // the wave index as a scalar: every per-wave condition below (active, kall) is then a scalar branch
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, l32 = lane & 31,
+              h = lane >> 5;
     const int tl = tlen ? tlen[u] : T;
     const int ng = (T + 31) >> 5;
     const int g0 = kb * gpb, ngb = min(gpb, ng - g0);
@@ -1307,10 +1496,13 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
     // (the dQ product's K^T fragments are read from the K^T image per tile: holding them in registers, 32 VGPRs,
     // made the two-stage prefetch spill)
     const __bf16* kfrow = Kt + (16 * di + l16) * FBB_KB + 8 * g;
-    const bool odd = lane & 1;
-    // tile qt: fetch tile qt+2 into fx (its previous content, tile qt, is in LDS), put tile qt+1 from py
-    auto tile = [&](int qt, Stg& fx, const Stg& py) {
-        const int q0 = qt * 32, buf = qt & 1;
+    // the lane's dS column in the tile image: row r8(v, h), key 32 w + l32
+    __bf16* const srow = Ss + 32 * w + l32;
+    // tile qt: fetch tile qt+2 into fx (its previous content, tile qt, is in LDS), put tile qt+1 from py; BUF = qt & 1
+    // as a constant (the two unrolled instances), so the LDS image addresses fold
+    auto tile = [&](int qt, Stg& fx, const Stg& py, auto buf_tag) {
+        constexpr int buf = decltype(buf_tag)::value;
+        const int q0 = qt * 32;
         if (qt + 2 < nqt) fetch(qt + 2, fx);
         const float* Lt = Ls + buf * 32;
         const float* Dlt = Dl + buf * 32;
@@ -1349,15 +1541,12 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
                 pv_tr<FB_RS>(dv, Dt, 16 * c, pb[c], lane);  // dV^T += dO^T P
                 pv_tr<FB_RS>(dk, Qt, 16 * c, sb[c], lane);  // dK^T += Q^T dS
             }
+            // dS into LDS: the lane's 16 query rows of its key column, 2-byte stores of the packed bf16 pairs (low /
+            // high halves), no lane exchange
 #pragma unroll
             for (int v = 0; v < 16; v += 2) {
-                const float a = dp[v], b = dp[v + 1];
-                const float recv = __int_as_float(
-                    __builtin_amdgcn_mov_dpp(__float_as_int(odd ? a : b), 0xB1, 0xF, 0xF, false));
-                fbf16x2 pr;
-                pr[0] = (__bf16)(odd ? recv : a);
-                pr[1] = (__bf16)(odd ? b : recv);
-                *reinterpret_cast<fbf16x2*>(Ss + (r8(v, h) + (odd ? 1 : 0)) * FBB_KB + 32 * w + (l32 & ~1)) = pr;
+                srow[r8(v, h) * FBB_KB] = sb[v >> 3][v & 7];
+                srow[r8(v + 1, h) * FBB_KB] = sb[v >> 3][(v & 7) + 1];
             }
         }
         __syncthreads();  // dS tile complete
@@ -1379,12 +1568,14 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
         if (qt + 1 < nqt) put(buf ^ 1, py);
         __syncthreads();
     };
+    using B0 = std::integral_constant<int, 0>;
+    using B1 = std::integral_constant<int, 1>;
     int qt = 0;
     for (; qt + 1 < nqt; qt += 2) {
-        tile(qt, sa, sb);
-        tile(qt + 1, sb, sa);
+        tile(qt, sa, sb, B0{});
+        tile(qt + 1, sb, sa, B1{});
     }
-    if (qt < nqt) tile(qt, sa, sb);
+    if (qt < nqt) tile(qt, sa, sb, B0{});
     if (w < ngb && key < T) {  // dK, dV rows of this wave's keys
         float* dkr = dqkv + ((long)u * T + key) * ld + H + hd * 64 + 4 * h;
         float* dvr = dkr + H;
@@ -1494,6 +1685,9 @@ bool launch_flash_fwd(const float* qkv, float* ctx, float* lse, int B, int T, in
     } else if (bf16)
         hipLaunchKernelGGL((flash_fwd_kernel<FF_NW, true>), grid, dim3(FF_NW * 64), 0, st, qkv, ctx, lse, T, NH, H,
                            scale, tlen, nqb, ctxb);
+    else if (suta_switches().flash_fwd_pipe)
+        hipLaunchKernelGGL((flash_fwd_pipe_kernel<FF_NW>), grid, dim3(FF_NW * 64), 0, st, qkv, ctx, lse, T, NH, H, scale,
+                           tlen, nqb, ctxb);
     else
         hipLaunchKernelGGL((flash_fwd_kernel<FF_NW, false>), grid, dim3(FF_NW * 64), 0, st, qkv, ctx, lse, T, NH, H,
                            scale, tlen, nqb, ctxb);

@@ -1943,6 +1943,7 @@ void suta_latch_switches() {
     s.flash_fwd_nw = (fnw && atoi(fnw) == 8) ? 8 : 4;
     s.epi_fast = on("SUTA_EPI_FAST");
     s.hbp_conv = on("SUTA_HBP_CONV");
+    s.flash_fwd_pipe = on("SUTA_FLASH_FWD_PIPE");
     s.latched = 1;
     g_switches = s;
 }

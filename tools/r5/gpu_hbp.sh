@@ -11,6 +11,7 @@ grep -E "hbx|hbp|epi" $O/hb_bench.log
 timeout -k 10 1000 python -u -m pytest -x -v --timeout 600 --timeout-method thread -m gpu \
   "tests/test_gpu_large_bf16.py::test_bf16_hbx_slice_ring_kernel_bitwise_equals_128_tile" \
   "tests/test_gpu_large_bf16.py::test_conv_input_gradients_on_256_tile_bitwise" \
+  "tests/test_gpu_parity.py::test_pipelined_fp32_flash_forward_bitwise" \
   "tests/test_gpu_parity.py::test_scheduler_and_sgd_match_reference" \
   "tests/test_gpu_parity.py::test_graph_replay_equals_eager" \
   "tests/test_gpu_large_bf16.py::test_batched_gemm_without_off32_epilogue_falls_back" \
