@@ -2217,6 +2217,10 @@ static void adapt_impl(suta_engine* e, const float* wav, int32_t on_dev, int32_t
     key.sw = suta_switches();
     const bool graph_ok = e->graph_key_repeats(key);
     e->run_adapt_loop(batch, *hp, steps, rec, nrec, rec_logits, rec_ids, graph_ok);
+    // the loop ran to completion with this key, so every buffer it needs is allocated now: a lazy allocation during
+    // it (drop_graph) must not cost the next call of the key its capture (config C4 allocated its bf16 conversion
+    // buffer in the first call, which pushed the capture to the third)
+    e->gkey_seen = true;
     if (logits_out && nrec)
         HIPCHK(hipMemcpyAsync(logits_out, rec_logits, rl * 4, logits_on_dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost,
                               e->st));

@@ -1934,7 +1934,7 @@ void suta_latch_switches() {
     const char* lrpw = std::getenv("SUTA_LN_RPW");
     s.ln_rpw = lrpw ? atoi(lrpw) : 2;
     const char* hform = std::getenv("SUTA_HBX_FORM");
-    s.hbx_form = hform ? atoi(hform) : 2;
+    s.hbx_form = hform ? atoi(hform) : 3;
     const char* hdbg = std::getenv("SUTA_HBX_DBG");
     s.hbx_dbg = hdbg ? atoi(hdbg) : 0;
     const char* hb8 = std::getenv("SUTA_HB8");
