@@ -485,7 +485,11 @@ __global__ __launch_bounds__(NW * 64) void flash_fwd_pipe_kernel(const float* __
                     sc[j][v] = ok ? sl2 * sc[j][v] : -INFINITY;
                     mx = fmaxf(mx, sc[j][v]);
                 }
-            mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+            {  // the other half-wave's maximum by v_permlane32_swap (no LDS round trip: a ds_bpermute's lgkmcnt wait
+               // would also wait for the S MFMAs' fragment reads); max is exact, so this is __shfl_xor's result
+                const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+                mx = fmaxf(mx, __uint_as_float(h ? sw[0] : sw[1]));
+            }
             const float m_new = fmaxf(m_run, mx);
             float ls = 0.f;
 #pragma unroll
@@ -495,7 +499,9 @@ __global__ __launch_bounds__(NW * 64) void flash_fwd_pipe_kernel(const float* __
                     sc[j][v] = __builtin_amdgcn_exp2f(sc[j][v] - m_new);
                     ls += sc[j][v];
                 }
-            if (m_new != m_run) {
+            {  // rescale unconditionally: alpha is exactly 1 when the maximum did not move (and 0 on the first tile, where
+               // o and l are 0), so this is bitwise flash_fwd_kernel's conditional rescale -- and it leaves no branch
+               // between the next tile's S MFMAs and this tile's softmax, which the scheduler can then interleave
                 const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
                 l_run *= alpha;
 #pragma unroll
@@ -505,6 +511,16 @@ __global__ __launch_bounds__(NW * 64) void flash_fwd_pipe_kernel(const float* __
                 m_run = m_new;
             }
             l_run += ls;
+            if constexpr (NEXT != 0) {
+                // in-order issue: this tile's softmax VALU has to sit BETWEEN the next tile's S MFMAs in program order
+                // to run under them (the scheduler alone put the max after ~48 of the 64); 3 VALU per MFMA gap (a
+                // 64-cycle v_mfma_f32_32x32x2_f32 hides ~12 issue slots of 4 cycles)
+#pragma unroll
+                for (int i = 0; i < 64; ++i) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+                    __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);  // VALU
+                }
+            }
             apply_cols<false, FK_LDT>(o, Vt[kt & 1], sc[0], l32, h);
             if (two) apply_cols<false, FK_LDT>(o, Vt[kt & 1] + 32, sc[1], l32, h);
             if constexpr (NEXT != 0) {

@@ -1940,6 +1940,9 @@ int32_t suta_create(const suta_model_config* cfg, const char* const* names, cons
         if (const char* af = std::getenv("SUTA_ATTN_FUSED")) e->attn_fused = af[0] != '0';
         if (const char* pc = std::getenv("SUTA_POSCONV")) e->posconv_kernel = pc[0] != '0';
         if (const char* bp = std::getenv("SUTA_BF16_PLANES")) e->bf16_planes = bp[0] != '0';
+        // SUTA_GRAPHS=0: no graph capture (as suta_set_graphs(e, 0)); profiling runs under rocprofv3 --pmc, which
+        // crashes (SIGSEGV in a profiler thread) once a captured graph is launched -- the kernels are the same
+        if (const char* gr = std::getenv("SUTA_GRAPHS")) e->use_graphs = gr[0] != '0';
         HIPCHK(hipSetDevice(device));
         HIPCHK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
         e->d_step = reinterpret_cast<int*>(e->dalloc(1));
