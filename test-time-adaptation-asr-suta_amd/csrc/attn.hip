@@ -485,11 +485,7 @@ __global__ __launch_bounds__(NW * 64) void flash_fwd_pipe_kernel(const float* __
                     sc[j][v] = ok ? sl2 * sc[j][v] : -INFINITY;
                     mx = fmaxf(mx, sc[j][v]);
                 }
-            {  // the other half-wave's maximum by v_permlane32_swap (no LDS round trip: a ds_bpermute's lgkmcnt wait
-               // would also wait for the S MFMAs' fragment reads); max is exact, so this is __shfl_xor's result
-                const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-                mx = fmaxf(mx, __uint_as_float(h ? sw[0] : sw[1]));
-            }
+            mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
             const float m_new = fmaxf(m_run, mx);
             float ls = 0.f;
 #pragma unroll
@@ -499,10 +495,10 @@ __global__ __launch_bounds__(NW * 64) void flash_fwd_pipe_kernel(const float* __
                     sc[j][v] = __builtin_amdgcn_exp2f(sc[j][v] - m_new);
                     ls += sc[j][v];
                 }
-            {  // rescale unconditionally: alpha is exactly 1 when the maximum did not move (and 0 on the first tile, where
-               // o and l are 0), so this is bitwise flash_fwd_kernel's conditional rescale -- and it leaves no branch
-               // between the next tile's S MFMAs and this tile's softmax, which the scheduler can then interleave
-                const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+            {  // rescale without a branch: alpha is selected as exactly 1 when the maximum did not move (v_exp_f32 is
+               // not guaranteed exact at 0), so this is bitwise flash_fwd_kernel's conditional rescale -- and it leaves
+               // no branch between the next tile's S MFMAs and this tile's softmax, which the scheduler can interleave
+                const float alpha = m_new == m_run ? 1.0f : __builtin_amdgcn_exp2f(m_run - m_new);
                 l_run *= alpha;
 #pragma unroll
                 for (int t = 0; t < 2; ++t)
@@ -511,16 +507,6 @@ __global__ __launch_bounds__(NW * 64) void flash_fwd_pipe_kernel(const float* __
                 m_run = m_new;
             }
             l_run += ls;
-            if constexpr (NEXT != 0) {
-                // in-order issue: this tile's softmax VALU has to sit BETWEEN the next tile's S MFMAs in program order
-                // to run under them (the scheduler alone put the max after ~48 of the 64); 3 VALU per MFMA gap (a
-                // 64-cycle v_mfma_f32_32x32x2_f32 hides ~12 issue slots of 4 cycles)
-#pragma unroll
-                for (int i = 0; i < 64; ++i) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-                    __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);  // VALU
-                }
-            }
             apply_cols<false, FK_LDT>(o, Vt[kt & 1], sc[0], l32, h);
             if (two) apply_cols<false, FK_LDT>(o, Vt[kt & 1] + 32, sc[1], l32, h);
             if constexpr (NEXT != 0) {
@@ -1619,6 +1605,244 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
     if (dq_cnt) dq_combine(dqp, dqkv, dqkvb, dq_cnt, reinterpret_cast<int*>(Ls), bh, u, hd, T, NH, H, nkb, tl, B);
 }
 
+// Software-pipelined form of flash_bwd_bf16p_kernel (SUTA_FLASH_BWD_PIPE, default): iteration qt issues the S and dP
+// MFMAs of query tile qt + 1 first and then runs tile qt's softmax / dS (VALU), its dV^T / dK^T MFMAs and the dS
+// store, so a wave's MFMA pipe works through its own softmax instead of idling on it (the unpipelined tile ran S/dP,
+// waited on them, did the VALU work, then the second MFMA group: MFMA busy 0.17).  Three Q / dO row images (tile
+// qt + 1 must be resident while tile qt is consumed; tile qt + 2 is written after tile qt's dQ into the image tile
+// qt - 1 left), one register stage for the copy (issued a whole iteration ahead).  Per element the same operations in
+// the same order as flash_bwd_bf16p_kernel -- S / dP chains, exponent, masks, dS, the dV / dK / dQ MFMA orders -- so
+// dQ / dK / dV are bitwise equal.  Loop bodies are instantiated per (next tile exists, wave's keys masked) so each is
+// one basic block the scheduler can interleave; the tile past T (the layout's last) masks its rows in the peeled body.
+// LDS: K^T image, dS tile, 3 x (Q, dO) row images, the block's K and V rows (row-major: the S / dP products read the
+// wave's key rows from here instead of holding them in 32 VGPRs), LSE / delta
+constexpr size_t fbbpp_lds_bytes() {
+    return 2 * ((size_t)(64 + 32) * FBB_KB + 3 * 2 * 32 * FB_RS + 2 * FBB_NW * 32 * FB_RS) + 6 * 128;
+}
+
+__global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16pp_kernel(
+    const __bf16* __restrict__ qkvb, const __bf16* __restrict__ dob, const float* __restrict__ lse,
+    const float* __restrict__ delta, float* __restrict__ dqkv, float* __restrict__ dqp, int T, int NH, int H,
+    float scale, const int* __restrict__ tlen, int nkb, int gpb, int B, __bf16* __restrict__ dqkvb,
+    int* __restrict__ dq_cnt) {
+    constexpr int NW = FBB_NW, NT = NW * 64;
+    extern __shared__ __attribute__((aligned(16))) __bf16 sm16[];
+    __bf16* Kt = sm16;                            // [64][FBB_KB]   K^T of the block's keys
+    __bf16* Ss = Kt + 64 * FBB_KB;                // [32][FBB_KB]   dS of the query tile
+    __bf16* Qr = Ss + 32 * FBB_KB;                // [3][32][FB_RS] Q rows
+    __bf16* Dr = Qr + 3 * 32 * FB_RS;             // [3][32][FB_RS] dO rows
+    __bf16* Kr = Dr + 3 * 32 * FB_RS;             // [NW * 32][FB_RS] K rows of the block's keys
+    __bf16* Vr = Kr + NW * 32 * FB_RS;            // [NW * 32][FB_RS] V rows
+    float* Ls = reinterpret_cast<float*>(Vr + NW * 32 * FB_RS);  // [3][32]
+    float* Dl = Ls + 96;                          // [3][32]
+    const int id = xcd_block();
+    const int kb = id % nkb, bh = id / nkb, hd = bh % NH, u = bh / NH;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, l32 = lane & 31,
+              h = lane >> 5;
+    const int tl = tlen ? tlen[u] : T;
+    const int ng = (T + 31) >> 5;
+    const int g0 = kb * gpb, ngb = min(gpb, ng - g0);
+    const int kbase = g0 * 32;
+    const long ld = 3L * H;
+    const __bf16* Qb = qkvb + (long)u * T * ld + hd * 64;
+    const __bf16* Kb = Qb + H;
+    const __bf16* Vb = Qb + 2 * H;
+    const __bf16* Ob = dob + (long)u * T * H + hd * 64;
+    const float* lb = lse + (long)bh * T;
+    const float* db = delta + (long)bh * T;
+    const bool active = w < ngb && kbase + 32 * w < tl;
+    const bool kall = kbase + 32 * w + 32 <= tl;
+    const int key = kbase + 32 * w + l32;
+    const float sl2 = scale * LOG2E;
+    for (int it = threadIdx.x; it < ngb * 32 * 8; it += NT) {  // K^T, K rows, V rows of the block's keys (0 past T)
+        const int row = it >> 3, c8 = (it & 7) * 8, k = kbase + row;
+        fbf16x8 x = {}, y = {};
+        if (k < T) {
+            x = *reinterpret_cast<const fbf16x8*>(Kb + (long)k * ld + c8);
+            y = *reinterpret_cast<const fbf16x8*>(Vb + (long)k * ld + c8);
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) Kt[(c8 + e) * FBB_KB + row] = x[e];
+        *reinterpret_cast<fbf16x8*>(Kr + row * FB_RS + c8) = x;
+        *reinterpret_cast<fbf16x8*>(Vr + row * FB_RS + c8) = y;
+    }
+    // the wave's key row (the B operand of S = Q K^T and dP = dO V^T): key min(key, T - 1) as the register form
+    // read it -- rows past T hold zeros here, but those keys are masked (s = 0) and their dK / dV never stored
+    const __bf16* krow = Kr + (32 * w + l32) * FB_RS + 8 * h;
+    const __bf16* vrow = Vr + (32 * w + l32) * FB_RS + 8 * h;
+    const bool isq = threadIdx.x < 256;
+    const int crow = (threadIdx.x & 255) >> 3, ccol = (threadIdx.x & 7) * 8;
+    fbf16x8 sx;  // the one register stage of the query-tile copy
+    float slr;
+    auto fetch = [&](int qt) {
+        const int q = qt * 32 + crow;
+        sx = fbf16x8{};
+        if (q < T) sx = *reinterpret_cast<const fbf16x8*>(isq ? Qb + (long)q * ld + ccol : Ob + (long)q * H + ccol);
+        slr = 0.f;
+        const int qq = qt * 32 + (threadIdx.x & 31);
+        if (threadIdx.x < 64 && qq < T) slr = threadIdx.x < 32 ? lb[qq] : db[qq];
+    };
+    auto put = [&](int buf) {
+        *reinterpret_cast<fbf16x8*>((isq ? Qr : Dr) + (buf * 32 + crow) * FB_RS + ccol) = sx;
+        if (threadIdx.x < 32) Ls[buf * 32 + threadIdx.x] = slr;
+        else if (threadIdx.x < 64) Dl[buf * 32 + threadIdx.x - 32] = slr;
+    };
+    f32x16 dv[2], dk[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) dv[t][v] = dk[t][v] = 0.f;
+    const int g = lane >> 4, l16 = lane & 15;
+    const int qi = w & 1, di = w >> 1;
+    const int kq = ngb * 32;
+    const long dq_stride = (long)B * NH * T * 64;
+    float* dqb = dqp + kb * dq_stride + (long)bh * T * 64;
+    const int nqt = (tl + 31) >> 5;
+    if (!active && w < ngb)
+        for (int r = 0; r < 32; ++r)
+            if (h == 0) Ss[r * FBB_KB + 32 * w + l32] = (__bf16)0.f;
+    // prologue: tiles 0 and 1 resident, tile 2 in registers, S / dP of tile 0
+    fetch(0);
+    put(0);
+    if (nqt > 1) {
+        fetch(1);
+        put(1);
+    }
+    __syncthreads();
+    if (nqt > 2) fetch(2);
+    const __bf16* kfrow = Kt + (16 * di + l16) * FBB_KB + 8 * g;
+    __bf16* const srow = Ss + 32 * w + l32;
+    // S = Q K^T of a tile (issued one tile ahead) and dP = dO V^T of the current one: prod_rows_b's k order
+    f32x16 s;
+    auto s_of = [&](f32x16& s_, int buf) {
+#pragma unroll
+        for (int v = 0; v < 16; ++v) s_[v] = 0.f;
+        const __bf16* qr = Qr + (buf * 32 + l32) * FB_RS + 8 * h;
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            s_ = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const fbf16x8*>(qr + 16 * c),
+                                                         *reinterpret_cast<const fbf16x8*>(krow + 16 * c), s_, 0, 0, 0);
+    };
+    auto dp_of = [&](f32x16& dp_, int buf) {
+#pragma unroll
+        for (int v = 0; v < 16; ++v) dp_[v] = 0.f;
+        const __bf16* dr = Dr + (buf * 32 + l32) * FB_RS + 8 * h;
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            dp_ = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const fbf16x8*>(dr + 16 * c),
+                                                          *reinterpret_cast<const fbf16x8*>(vrow + 16 * c), dp_, 0, 0, 0);
+    };
+    if (active) s_of(s, 0);
+    // one tile: NEXT = tile qt + 1 exists (its S issued first, under this tile's exponentials), MASKK = this wave's keys reach past the length,
+    // MASKQ = this tile reaches past T (the layout's last tile)
+    auto tile = [&](int qt, auto next_tag, auto maskk_tag, auto maskq_tag) {
+        constexpr bool NEXT = decltype(next_tag)::value, MASKK = decltype(maskk_tag)::value,
+                       MASKQ = decltype(maskq_tag)::value;
+        const int q0 = qt * 32, buf = qt % 3;
+        if (active) {
+            f32x16 sn, dp;
+            if constexpr (NEXT) s_of(sn, (qt + 1) % 3);
+            dp_of(dp, buf);
+            const __bf16* Qt = Qr + buf * 32 * FB_RS;
+            const __bf16* Dt = Dr + buf * 32 * FB_RS;
+            const float* Lt = Ls + buf * 32;
+            const float* Dlt = Dl + buf * 32;
+            // LSE / delta of the lane's rows r8(v, h), one run of 4 rows at a time (registers: the next tile's S / dP
+            // accumulators are live here)
+            const bool kok = key < tl;
+#pragma unroll
+            for (int a = 0; a < 4; ++a) {
+                const f32x4 lq = *reinterpret_cast<const f32x4*>(Lt + 8 * a + 4 * h);
+                const f32x4 dq = *reinterpret_cast<const f32x4*>(Dlt + 8 * a + 4 * h);
+#pragma unroll
+                for (int b2 = 0; b2 < 4; ++b2) {
+                    const int v = 4 * a + b2;
+                    float p = __builtin_amdgcn_exp2f(fmaf(s[v], sl2, -LOG2E * lq[b2]));
+                    if constexpr (MASKK || MASKQ) {
+                        if (!(kok && q0 + r8(v, h) < T)) p = 0.f;
+                    }
+                    s[v] = p;
+                    dp[v] = scale * (p * (dp[v] - dq[b2]));
+                }
+            }
+            fbf16x8 pb[2], sb[2];
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                pb[v >> 3][v & 7] = (__bf16)s[v];
+                sb[v >> 3][v & 7] = (__bf16)dp[v];
+            }
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                pv_tr<FB_RS>(dv, Dt, 16 * c, pb[c], lane);  // dV^T += dO^T P
+                pv_tr<FB_RS>(dk, Qt, 16 * c, sb[c], lane);  // dK^T += Q^T dS
+            }
+#pragma unroll
+            for (int v = 0; v < 16; v += 2) {
+                srow[r8(v, h) * FBB_KB] = sb[v >> 3][v & 7];
+                srow[r8(v + 1, h) * FBB_KB] = sb[v >> 3][(v & 7) + 1];
+            }
+            if constexpr (NEXT) s = sn;
+        }
+        __syncthreads();  // dS tile complete
+        {
+            const __bf16* ar = Ss + (16 * qi + l16) * FBB_KB + 8 * g;
+            f32x4 c[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (32 * j < kq)
+                    c[j & 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                        *reinterpret_cast<const fbf16x8*>(ar + 32 * j),
+                        *reinterpret_cast<const fbf16x8*>(kfrow + 32 * j), c[j & 1], 0, 0, 0);
+            const f32x4 c0 = c[0], c1 = c[1];
+            float* dr = dqb + (long)(q0 + 16 * qi + 4 * g) * 64 + 16 * di + l16;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (q0 + 16 * qi + 4 * g + r < T) dr[r * 64] = c0[r] + c1[r];
+        }
+        if constexpr (NEXT) {
+            if (qt + 2 < nqt) put((qt + 2) % 3);
+            __syncthreads();  // tile qt + 2 visible; the dS image free
+            if (qt + 3 < nqt) fetch(qt + 3);
+        }
+    };
+    using TT = std::true_type;
+    using FF = std::false_type;
+    const bool mq = (nqt - 1) * 32 + 32 > T;  // the last tile reaches past T
+    if (kall) {
+        for (int qt = 0; qt + 1 < nqt; ++qt) tile(qt, TT{}, FF{}, FF{});
+        if (mq) tile(nqt - 1, FF{}, FF{}, TT{});
+        else tile(nqt - 1, FF{}, FF{}, FF{});
+    } else {
+        for (int qt = 0; qt + 1 < nqt; ++qt) tile(qt, TT{}, TT{}, FF{});
+        tile(nqt - 1, FF{}, TT{}, TT{});
+    }
+    if (w < ngb && key < T) {
+        float* dkr = dqkv + ((long)u * T + key) * ld + H + hd * 64 + 4 * h;
+        float* dvr = dkr + H;
+    #pragma unroll
+        for (int t = 0; t < 2; ++t)
+    #pragma unroll
+            for (int a = 0; a < 4; ++a) {
+                f32x4 x, y;
+    #pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    x[b] = dk[t][4 * a + b];
+                    y[b] = dv[t][4 * a + b];
+                }
+                if (dqkv) {
+                    *reinterpret_cast<f32x4*>(dkr + 32 * t + 8 * a) = x;
+                    *reinterpret_cast<f32x4*>(dvr + 32 * t + 8 * a) = y;
+                }
+                if (dqkvb) {
+                    __bf16* kb2 = dqkvb + ((long)u * T + key) * ld + H + hd * 64 + 4 * h + 32 * t + 8 * a;
+                    *reinterpret_cast<fbf16x4*>(kb2) = cvt4(x);
+                    *reinterpret_cast<fbf16x4*>(kb2 + H) = cvt4(y);
+                }
+            }
+    }
+    if (dq_cnt) dq_combine(dqp, dqkv, dqkvb, dq_cnt, reinterpret_cast<int*>(Ls), bh, u, hd, T, NH, H, nkb, tl, B);
+}
+
 // dQ = sum over key blocks in order (query rows < tl; rows past it get 0, as their dS is 0)
 __global__ __launch_bounds__(256) void flash_dq_reduce(const float* __restrict__ dqp, float* __restrict__ dqkv, int B,
                                                        int T, int NH, int H, int nkb, const int* __restrict__ tlen,
@@ -1759,17 +1983,31 @@ bool launch_flash_bwd(const float* qkv, const float* dctx, const float* lse, con
     if (on_planes) {
         if ((reinterpret_cast<uintptr_t>(qkvb) | reinterpret_cast<uintptr_t>(dctxb)) & 15)
             throw std::invalid_argument("flash_bwd: bf16 planes not 16-B aligned");
-        constexpr size_t lds = fbbp_lds_bytes();
-        static bool attr = false;
-        if (!attr) {
-            if (hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_bwd_bf16p_kernel),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-                throw std::runtime_error("hipFuncSetAttribute(flash_bwd_bf16p_kernel) failed");
-            attr = true;
+        if (suta_switches().flash_bwd_pipe) {  // the software-pipelined form (bitwise the same results)
+            constexpr size_t lds = fbbpp_lds_bytes();
+            static bool attr = false;
+            if (!attr) {
+                if (hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_bwd_bf16pp_kernel),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+                    throw std::runtime_error("hipFuncSetAttribute(flash_bwd_bf16pp_kernel) failed");
+                attr = true;
+            }
+            hipLaunchKernelGGL(flash_bwd_bf16pp_kernel, grid, dim3(FBB_NW * 64), lds, st,
+                               reinterpret_cast<const __bf16*>(qkvb), reinterpret_cast<const __bf16*>(dctxb), lse, delta,
+                               dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb, cnt);
+        } else {
+            constexpr size_t lds = fbbp_lds_bytes();
+            static bool attr = false;
+            if (!attr) {
+                if (hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_bwd_bf16p_kernel),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+                    throw std::runtime_error("hipFuncSetAttribute(flash_bwd_bf16p_kernel) failed");
+                attr = true;
+            }
+            hipLaunchKernelGGL(flash_bwd_bf16p_kernel, grid, dim3(FBB_NW * 64), lds, st,
+                               reinterpret_cast<const __bf16*>(qkvb), reinterpret_cast<const __bf16*>(dctxb), lse, delta,
+                               dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb, cnt);
         }
-        hipLaunchKernelGGL(flash_bwd_bf16p_kernel, grid, dim3(FBB_NW * 64), lds, st,
-                           reinterpret_cast<const __bf16*>(qkvb), reinterpret_cast<const __bf16*>(dctxb), lse, delta,
-                           dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb, cnt);
     } else if (bf16 && nw == FBB_NW && fb_img()) {
         constexpr size_t lds = fbb_lds_bytes();
         static bool attr = false;

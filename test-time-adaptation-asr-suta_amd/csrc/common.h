@@ -93,8 +93,10 @@ struct SutaSwitches {
                           // 0 = the column-per-lane form shared with the 128 x 128 kernel
     int hbp_conv;         // SUTA_HBP_CONV (default 1): the conv stack's conv-seg input gradients on the four-phase 256 x 256
                           // kernel (gemm.hip use_hbp_conv); 0 = the 128 x 128 kernel
-    int flash_fwd_pipe;   // SUTA_FLASH_FWD_PIPE (default 1): the exact-fp32 flash forward software-pipelined (S of the next
+    int flash_fwd_pipe;   // SUTA_FLASH_FWD_PIPE (default 0, measured neutral): the exact-fp32 flash forward software-pipelined (S of the next
                           // key tile under this tile's softmax, attn.hip flash_fwd_pipe_kernel; bitwise equal); 0 = not
+    int flash_bwd_pipe;   // SUTA_FLASH_BWD_PIPE (default 0, measured 18 % slower): the bf16-plane flash backward software-pipelined (S / dP of the
+                          // next query tile under this tile's softmax, attn.hip flash_bwd_bf16pp_kernel; bitwise equal)
     int epi_fast;         // SUTA_EPI_FAST (default 1): 32-bit-offset GEMM epilogue where every operand fits 4 GiB (p.off32);
                           // 0 = the general epilogue everywhere
 };

@@ -1943,7 +1943,12 @@ void suta_latch_switches() {
     s.flash_fwd_nw = (fnw && atoi(fnw) == 8) ? 8 : 4;
     s.epi_fast = on("SUTA_EPI_FAST");
     s.hbp_conv = on("SUTA_HBP_CONV");
-    s.flash_fwd_pipe = on("SUTA_FLASH_FWD_PIPE");
+    // the software-pipelined flash kernels measured no faster (fp32 forward 119.0 vs 117.3 ms per C2 batch) or slower
+    // (bf16 backward 826 vs 701 ms per two C4 calls, profiles/r5): opt-in (=1) for A/B runs
+    const char* ffp = std::getenv("SUTA_FLASH_FWD_PIPE");
+    s.flash_fwd_pipe = ffp ? atoi(ffp) : 0;
+    const char* fbp = std::getenv("SUTA_FLASH_BWD_PIPE");
+    s.flash_bwd_pipe = fbp ? atoi(fbp) : 0;
     s.latched = 1;
     g_switches = s;
 }
