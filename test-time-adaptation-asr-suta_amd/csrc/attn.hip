@@ -495,10 +495,9 @@ __global__ __launch_bounds__(NW * 64) void flash_fwd_pipe_kernel(const float* __
                     sc[j][v] = __builtin_amdgcn_exp2f(sc[j][v] - m_new);
                     ls += sc[j][v];
                 }
-            {  // rescale without a branch: alpha is selected as exactly 1 when the maximum did not move (v_exp_f32 is
-               // not guaranteed exact at 0), so this is bitwise flash_fwd_kernel's conditional rescale -- and it leaves
-               // no branch between the next tile's S MFMAs and this tile's softmax, which the scheduler can interleave
-                const float alpha = m_new == m_run ? 1.0f : __builtin_amdgcn_exp2f(m_run - m_new);
+            if (m_new != m_run) {  // rescale only when the maximum moved, exactly as flash_fwd_kernel (an unconditional
+                                   // l_run * alpha + ls is fused into one fma under -ffp-contract=fast: not bitwise)
+                const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
                 l_run *= alpha;
 #pragma unroll
                 for (int t = 0; t < 2; ++t)
@@ -1403,18 +1402,31 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16_kernel(
 // One row image per query tile serves the S / dP products (row reads) and the dV^T / dK^T products
 // (ds_read_b64_tr_b16 transposed reads, as the forward's PV): no transposed tiles are written.  Masks only
 // on a wave whose keys pass the utterance's length or on a query tile past T.
-constexpr size_t fbbp_lds_bytes() { return 2 * ((size_t)(64 + 32) * FBB_KB + 2 * 2 * 32 * FB_RS) + 4 * 128; }
+//
+// ONEB (SUTA_FLASH_BWD_ONEB): one barrier per query tile instead of two.  The dS image is double-buffered (tile qt
+// writes Ss[qt & 1]) and tile qt + 1's Q / dO rows are put into their image BEFORE tile qt's barrier, so that one
+// barrier both completes tile qt's dS image (RAW for its dQ) and publishes tile qt + 1 (RAW for its S / dP).  WAR:
+// the Q / dO image tile qt + 1 overwrites held tile qt - 1, whose last reads (its S / dP / dV / dK products) every
+// wave finished before tile qt - 1's barrier; Ss[qt & 1] is rewritten by tile qt + 2 after tile qt + 1's barrier,
+// which every wave reaches only after its dQ reads of tile qt.  Per element the same operations in the same order:
+// bitwise equal to the two-barrier form.
+template <bool ONEB>
+constexpr size_t fbbp_lds_bytes() {
+    return 2 * ((size_t)(64 + (ONEB ? 64 : 32)) * FBB_KB + 2 * 2 * 32 * FB_RS) + 4 * 128;
+}
 
+template <bool ONEB>
 __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
     const __bf16* __restrict__ qkvb, const __bf16* __restrict__ dob, const float* __restrict__ lse,
     const float* __restrict__ delta, float* __restrict__ dqkv, float* __restrict__ dqp, int T, int NH, int H,
     float scale, const int* __restrict__ tlen, int nkb, int gpb, int B, __bf16* __restrict__ dqkvb,
     int* __restrict__ dq_cnt) {
     constexpr int NW = FBB_NW, NT = NW * 64;
+    constexpr int NSS = ONEB ? 2 : 1;             // dS images
     extern __shared__ __attribute__((aligned(16))) __bf16 sm16[];
     __bf16* Kt = sm16;                            // [64][FBB_KB]   K^T of the block's keys
-    __bf16* Ss = Kt + 64 * FBB_KB;                // [32][FBB_KB]   dS of the query tile
-    __bf16* Qr = Ss + 32 * FBB_KB;                // [2][32][FB_RS] Q rows
+    __bf16* Ss = Kt + 64 * FBB_KB;                // [NSS][32][FBB_KB] dS of the query tile
+    __bf16* Qr = Ss + NSS * 32 * FBB_KB;          // [2][32][FB_RS] Q rows
     __bf16* Dr = Qr + 2 * 32 * FB_RS;             // [2][32][FB_RS] dO rows
     float* Ls = reinterpret_cast<float*>(Dr + 2 * 32 * FB_RS);  // [2][32]
     float* Dl = Ls + 64;                          // [2][32]
@@ -1488,7 +1500,7 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
     float* dqb = dqp + kb * dq_stride + (long)bh * T * 64;
     const int nqt = (tl + 31) >> 5;
     if (!active && w < ngb)
-        for (int r = 0; r < 32; ++r)
+        for (int r = 0; r < NSS * 32; ++r)
             if (h == 0) Ss[r * FBB_KB + 32 * w + l32] = (__bf16)0.f;
     Stg sa, sb;
     fetch(0, sa);
@@ -1499,11 +1511,12 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
     // made the two-stage prefetch spill)
     const __bf16* kfrow = Kt + (16 * di + l16) * FBB_KB + 8 * g;
     // the lane's dS column in the tile image: row r8(v, h), key 32 w + l32
-    __bf16* const srow = Ss + 32 * w + l32;
     // tile qt: fetch tile qt+2 into fx (its previous content, tile qt, is in LDS), put tile qt+1 from py; BUF = qt & 1
     // as a constant (the two unrolled instances), so the LDS image addresses fold
     auto tile = [&](int qt, Stg& fx, const Stg& py, auto buf_tag) {
         constexpr int buf = decltype(buf_tag)::value;
+        __bf16* const Sb = Ss + (ONEB ? buf : 0) * 32 * FBB_KB;  // this tile's dS image
+        __bf16* const srow = Sb + 32 * w + l32;
         const int q0 = qt * 32;
         if (qt + 2 < nqt) fetch(qt + 2, fx);
         const float* Lt = Ls + buf * 32;
@@ -1551,9 +1564,12 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
                 srow[r8(v + 1, h) * FBB_KB] = sb[v >> 3][(v & 7) + 1];
             }
         }
+        if constexpr (ONEB) {
+            if (qt + 1 < nqt) put(buf ^ 1, py);  // published by the barrier below
+        }
         __syncthreads();  // dS tile complete
         {
-            const __bf16* ar = Ss + (16 * qi + l16) * FBB_KB + 8 * g;
+            const __bf16* ar = Sb + (16 * qi + l16) * FBB_KB + 8 * g;
             f32x4 c[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
             for (int j = 0; j < 8; ++j)
@@ -1567,8 +1583,10 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
             for (int r = 0; r < 4; ++r)
                 if (q0 + 16 * qi + 4 * g + r < T) dr[r * 64] = c0[r] + c1[r];
         }
-        if (qt + 1 < nqt) put(buf ^ 1, py);
-        __syncthreads();
+        if constexpr (!ONEB) {
+            if (qt + 1 < nqt) put(buf ^ 1, py);
+            __syncthreads();
+        }
     };
     using B0 = std::integral_constant<int, 0>;
     using B1 = std::integral_constant<int, 1>;
@@ -1601,6 +1619,9 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
                     *reinterpret_cast<fbf16x4*>(kb2 + H) = cvt4(y);
                 }
             }
+    }
+    if constexpr (ONEB) {
+        if (dq_cnt) __syncthreads();  // (dq_combine's ticket scratch aliases Ls, still read by the last tile's waves)
     }
     if (dq_cnt) dq_combine(dqp, dqkv, dqkvb, dq_cnt, reinterpret_cast<int*>(Ls), bh, u, hd, T, NH, H, nkb, tl, B);
 }
@@ -1950,6 +1971,23 @@ static void flash_bwd_go(dim3 grid, hipStream_t st, const float* qkv, const floa
                        T, NH, H, scale, tlen, nkb, gpb, B, dqkvb, cnt);
 }
 
+template <bool ONEB>
+static void flash_bwd_bf16p_go(dim3 grid, hipStream_t st, const void* qkvb, const void* dctxb, const float* lse,
+                               const float* delta, float* dqkv, float* dqp, int T, int NH, int H, float scale,
+                               const int* tlen, int nkb, int gpb, int B, __bf16* dqkvb, int* cnt) {
+    constexpr size_t lds = fbbp_lds_bytes<ONEB>();
+    static bool attr = false;
+    if (!attr) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_bwd_bf16p_kernel<ONEB>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+            throw std::runtime_error("hipFuncSetAttribute(flash_bwd_bf16p_kernel) failed");
+        attr = true;
+    }
+    hipLaunchKernelGGL(flash_bwd_bf16p_kernel<ONEB>, grid, dim3(FBB_NW * 64), lds, st,
+                       reinterpret_cast<const __bf16*>(qkvb), reinterpret_cast<const __bf16*>(dctxb), lse, delta, dqkv,
+                       dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb, cnt);
+}
+
 // bf16 mode, bf16 planes of qkv and dctx given: flash_bwd_bf16p_kernel (env SUTA_FLASH_BWD_PLANE=0 keeps the
 // fp32-row kernels for A/B runs; from the call's switch snapshot)
 static bool fb_plane() { return suta_switches().flash_bwd_plane != 0; }
@@ -1995,18 +2033,12 @@ bool launch_flash_bwd(const float* qkv, const float* dctx, const float* lse, con
             hipLaunchKernelGGL(flash_bwd_bf16pp_kernel, grid, dim3(FBB_NW * 64), lds, st,
                                reinterpret_cast<const __bf16*>(qkvb), reinterpret_cast<const __bf16*>(dctxb), lse, delta,
                                dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb, cnt);
+        } else if (suta_switches().flash_bwd_oneb) {
+            flash_bwd_bf16p_go<true>(grid, st, qkvb, dctxb, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B,
+                                     dqkvb, cnt);
         } else {
-            constexpr size_t lds = fbbp_lds_bytes();
-            static bool attr = false;
-            if (!attr) {
-                if (hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_bwd_bf16p_kernel),
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-                    throw std::runtime_error("hipFuncSetAttribute(flash_bwd_bf16p_kernel) failed");
-                attr = true;
-            }
-            hipLaunchKernelGGL(flash_bwd_bf16p_kernel, grid, dim3(FBB_NW * 64), lds, st,
-                               reinterpret_cast<const __bf16*>(qkvb), reinterpret_cast<const __bf16*>(dctxb), lse, delta,
-                               dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb, cnt);
+            flash_bwd_bf16p_go<false>(grid, st, qkvb, dctxb, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B,
+                                      dqkvb, cnt);
         }
     } else if (bf16 && nw == FBB_NW && fb_img()) {
         constexpr size_t lds = fbb_lds_bytes();

@@ -1949,6 +1949,8 @@ void suta_latch_switches() {
     s.flash_fwd_pipe = ffp ? atoi(ffp) : 0;
     const char* fbp = std::getenv("SUTA_FLASH_BWD_PIPE");
     s.flash_bwd_pipe = fbp ? atoi(fbp) : 0;
+    const char* fob = std::getenv("SUTA_FLASH_BWD_ONEB");
+    s.flash_bwd_oneb = fob ? atoi(fob) : 0;
     s.latched = 1;
     g_switches = s;
 }

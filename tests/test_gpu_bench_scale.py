@@ -187,7 +187,8 @@ def test_c4_bench_layout_bf16():
     and 20.  The launch census of the first (eager) call shows the schedules this layout reaches: the linears on
     the 256 x 256 bf16-plane kernel (hbx) over ceil(B x 399 / 256) row tiles, the K = 32 lm_head input gradient on
     the 128 x 128 one over ceil(B x 399 / 128), the conv stack's per-utterance (Z = B) GEMMs on bf16 planes --
-    forward on the 256 x 256 kernel, input gradients (conv-A rows, per-tap weight segments), weight gradients on
+    forward and input gradients (conv-A rows, per-tap weight segments) on the four-phase 256 x 256 kernel (no
+    conv-seg launch left on the 128 x 128 one), weight gradients on
     the MN-contiguous hbt kernel -- and the per-utterance feature-projection weight gradient.
     Reference main.py:181,205 (forward and backward through the encoder)."""
     from oracle import w2v2_cpu as W
@@ -216,8 +217,11 @@ def test_c4_bench_layout_bf16():
                    for k in census), (gx, txt)
     # the K = 32 lm_head input gradient (below hbx's K >= 128) on the 128 x 128 kernel
     assert any(k.startswith("grid hb 128x128 ") and f" gx=8 gy={gy} z=1 " in k for k in census), (gy, txt)
-    assert any(k.startswith(("hb ", "hbx ")) and z in k and k.endswith(" conv-seg") for k in census), txt   # conv dX
-    assert any(k.startswith(("hb ", "hbx ")) and z in k and "conv" not in k for k in census), txt  # conv forward
+    # conv dX (conv-A rows, per-tap weight segments) and the conv forward: both on the four-phase 256 x 256 kernel
+    # (round 5: the conv-seg input gradients left the 128 x 128 kernel), none of them on the 128 x 128 one
+    assert any(k.startswith("hbx 256x256 ") and z in k and k.endswith(" conv-seg") for k in census), txt
+    assert not any(k.startswith("hb ") and z in k and k.endswith(" conv-seg") for k in census), txt
+    assert any(k.startswith("hbx 256x256 ") and z in k and "conv" not in k for k in census), txt
     assert any(k.startswith("hbt ") and z in k for k in census), txt                        # conv dW
     assert any(z in k and k.startswith(("gbf", "x6_1plane")) for k in census), txt
     eng.set_precision("fp32")
