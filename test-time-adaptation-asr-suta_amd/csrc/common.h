@@ -97,8 +97,8 @@ struct SutaSwitches {
                           // key tile under this tile's softmax, attn.hip flash_fwd_pipe_kernel; bitwise equal); 0 = not
     int flash_bwd_pipe;   // SUTA_FLASH_BWD_PIPE (default 0, measured 18 % slower): the bf16-plane flash backward software-pipelined (S / dP of the
                           // next query tile under this tile's softmax, attn.hip flash_bwd_bf16pp_kernel; bitwise equal)
-    int flash_bwd_oneb;   // SUTA_FLASH_BWD_ONEB: the bf16-plane flash backward with one barrier per query tile (dS image
-                          // double-buffered, the next tile's Q / dO put before the barrier); bitwise equal; 0 = two barriers
+    int flash_bwd_oneb;   // SUTA_FLASH_BWD_ONEB (default 1): the bf16-plane flash backward with one barrier per query tile (dS
+                          // image double-buffered, the next tile's Q / dO put before the barrier); bitwise equal; 0 = two
     int epi_fast;         // SUTA_EPI_FAST (default 1): 32-bit-offset GEMM epilogue where every operand fits 4 GiB (p.off32);
                           // 0 = the general epilogue everywhere
 };

@@ -1949,8 +1949,9 @@ void suta_latch_switches() {
     s.flash_fwd_pipe = ffp ? atoi(ffp) : 0;
     const char* fbp = std::getenv("SUTA_FLASH_BWD_PIPE");
     s.flash_bwd_pipe = fbp ? atoi(fbp) : 0;
-    const char* fob = std::getenv("SUTA_FLASH_BWD_ONEB");
-    s.flash_bwd_oneb = fob ? atoi(fob) : 0;
+    // one barrier per query tile in the bf16-plane flash backward: C4 attention 543-546 -> 534-535 ms per call, same box
+    // (profiles/r5/oneb_ab.txt); =0 the two-barrier form
+    s.flash_bwd_oneb = on("SUTA_FLASH_BWD_ONEB");
     s.latched = 1;
     g_switches = s;
 }
