@@ -45,7 +45,7 @@ HBM_PEAK_TBS = 8.0             # MI355X_MICROARCH.md: HBM3E peak
 RECORD = [0, 1, 3, 5, 10]
 C4_RECORD = [0, 1, 5, 10, 20]   # config C4 (20 steps): greedy ids recorded at these steps
 # newest committed rocprofv3 PMC reduction of each workload (tools/pmc_traffic.py; profiles/<round>/README.md)
-ROUNDS = ("r4", "r3", "r2", "r1")
+ROUNDS = ("r5", "r4", "r3", "r2", "r1")
 PMC_TRAFFIC = next((p for p in (os.path.join(ROOT, "profiles", r, "pmc_traffic.json") for r in ROUNDS)
                     if os.path.exists(p)), None)
 PMC_TRAFFIC_C4 = next((p for p in (os.path.join(ROOT, "profiles", r, "pmc_traffic_c4.json") for r in ROUNDS)

@@ -67,10 +67,11 @@ def build_parser(sdpl: bool = False):
                    help="max utterances adapted together as one ragged batch (episodic runs; 1 = one per call)")
     p.add_argument("--gpu_budget_s", type=float, default=1312.0,
                    help="max padded audio seconds per ragged batch (utterances x longest)")
-    p.add_argument("--gpu_min_fill", type=float, default=0.2,
+    p.add_argument("--gpu_min_fill", type=float, default=0.3,
                    help="ragged grouping: 0 = greedy; > 0 = padding-minimising partition charging a batch at least "
-                        "this fraction of --gpu_budget_s (bench.py c5, TED-like mix at --gpu_batch 164 / --gpu_budget_s "
-                        "1312: 0.35 / 0.2 / 0.1 / 0.05 -> 15.5 / 16.8 / 16.5 / 15.5 utt/s, profiles/r4/c5_mf*.json)")
+                        "this fraction of --gpu_budget_s (bench.py c5, TED-like mix of 512 utterances at --gpu_batch 164 "
+                        "/ --gpu_budget_s 1312: 0.2 / 0.3 / 0.4 / 0.5 / 0.7 -> 20.8 / 21.6 / 21.5-21.6 / 20.9 / 20.8 "
+                        "utt/s, profiles/r5/c5_mf*.json; on round 4's 96-utterance mix 0.15-0.25 was the optimum)")
     p.add_argument("--dist_backend", default="auto", choices=["auto", "nccl", "gloo"],
                    help="torch.distributed backend under torchrun (auto: nccl = RCCL when a GPU is visible)")
     p.add_argument("--num_workers", type=int, default=4,
