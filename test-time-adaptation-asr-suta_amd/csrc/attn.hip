@@ -177,6 +177,19 @@ __device__ __forceinline__ void apply_cols(f32x16 (&o)[2], const float* __restri
     }
 }
 
+// max / sum with the other half-wave's value (lane l and l ^ 32) through v_permlane32_swap (no LDS round trip, as
+// __shfl_xor's ds_bpermute is): swapping two copies of x leaves {x[l], x[l + 32]} in the lower half's pair and
+// {x[l - 32], x[l]} in the upper's, so one op of the pair is op(x[l], x[l ^ 32]) -- bitwise the shuffle form (fmax
+// and a two-term sum are commutative)
+__device__ __forceinline__ float half_swap_max(float x) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float half_swap_sum(float x) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 constexpr float LOG2E = 1.4426950408889634f;
 
 // ------------------------------------------------------------------------------------------------
@@ -304,7 +317,7 @@ __global__ __launch_bounds__(NW * 64) void flash_fwd_kernel(const float* __restr
                     s[j][v] = ok ? sl2 * s[j][v] : -INFINITY;
                     mx = fmaxf(mx, s[j][v]);
                 }
-            mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+            mx = half_swap_max(mx);
             const float m_new = fmaxf(m_run, mx);
             float ls = 0.f;
 #pragma unroll
@@ -333,7 +346,7 @@ __global__ __launch_bounds__(NW * 64) void flash_fwd_kernel(const float* __restr
     for (int kt = 0; kt + 1 < nkt; ++kt) tile(kt, std::false_type{});
     tile(nkt - 1, std::true_type{});
     if (!active) return;
-    const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+    const float l_tot = half_swap_sum(l_run);
     const int q = q0 + l32;
     if (q >= T) return;
     const float inv = 1.0f / l_tot;
@@ -485,7 +498,7 @@ __global__ __launch_bounds__(NW * 64) void flash_fwd_pipe_kernel(const float* __
                     sc[j][v] = ok ? sl2 * sc[j][v] : -INFINITY;
                     mx = fmaxf(mx, sc[j][v]);
                 }
-            mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+            mx = half_swap_max(mx);
             const float m_new = fmaxf(m_run, mx);
             float ls = 0.f;
 #pragma unroll
@@ -522,7 +535,7 @@ __global__ __launch_bounds__(NW * 64) void flash_fwd_pipe_kernel(const float* __
     if (kt + 1 < nkt) iter(kt++, std::integral_constant<int, 2>{});
     iter(kt, std::integral_constant<int, 0>{});
     if (!active) return;
-    const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+    const float l_tot = half_swap_sum(l_run);
     const int q = q0 + l32;
     if (q >= T) return;
     const float inv = 1.0f / l_tot;
@@ -974,7 +987,7 @@ __global__ __launch_bounds__(FF_NW_BF * 64) void flash_fwd_bf16_kernel(
                     s[j][v] = ok ? sl2 * s[j][v] : -INFINITY;
                     mx = fmaxf(mx, s[j][v]);
                 }
-            mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+            mx = half_swap_max(mx);
             const float m_new = fmaxf(m_run, mx);
             float ls = 0.f;
 #pragma unroll
@@ -1001,7 +1014,7 @@ __global__ __launch_bounds__(FF_NW_BF * 64) void flash_fwd_bf16_kernel(
         __syncthreads();
     }
     if (!active) return;
-    const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+    const float l_tot = half_swap_sum(l_run);
     const int q = q0 + l32;
     if (q >= T) return;
     const float inv = 1.0f / l_tot;
@@ -1149,7 +1162,7 @@ __global__ __launch_bounds__(NW * 64) void flash_fwd_bf16p_kernel(
             if (two)
 #pragma unroll
                 for (int v = 0; v < 16; ++v) mx = fmaxf(mx, s[1][v]);
-            mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+            mx = half_swap_max(mx);
             const float m_new = fmaxf(m_run, sl2 * mx);
             float ls = 0.f;
             fbf16x8 pb[2][2];
@@ -1183,7 +1196,7 @@ __global__ __launch_bounds__(NW * 64) void flash_fwd_bf16p_kernel(
     for (int kt = 0; kt + 1 < nkt; ++kt) tile(kt, std::false_type{});
     tile(nkt - 1, std::true_type{});
     if (!active) return;
-    const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+    const float l_tot = half_swap_sum(l_run);
     const int q = q0 + l32;
     if (q >= T) return;
     const float inv = 1.0f / l_tot;

@@ -571,14 +571,15 @@ def test_conv_input_gradients_on_256_tile_bitwise(monkeypatch, form):
         assert np.array_equal(v, params["0"][n]), n
 
 
-@pytest.mark.parametrize("switch", ["SUTA_FLASH_BWD_PIPE", "SUTA_FLASH_BWD_ONEB"])
+@pytest.mark.parametrize("switch", ["SUTA_FLASH_BWD_PIPE", "SUTA_FLASH_BWD_ONEB", "SUTA_CONV_DW_SIDE"])
 @pytest.mark.parametrize("model", ["wav2vec2-large", "wav2vec2-base"])
 def test_pipelined_bf16_flash_backward_bitwise(monkeypatch, model, switch):
     """Two alternative forms of the bf16-plane flash backward against flash_bwd_bf16p_kernel (switch = 0): the
     software-pipelined one (SUTA_FLASH_BWD_PIPE=1: S of query tile qt + 1 issued under tile qt's exponentials, K / V
     rows read from LDS, three Q / dO images) and the one-barrier one (SUTA_FLASH_BWD_ONEB=1: double-buffered dS image,
     the next tile's rows put before the tile's single barrier).  Both do the same operations per element in the same
-    order, so logits and adapted tensors are bitwise equal.  bf16 mode, a ragged batch with T = 399 (13 key groups: two
+    order, so logits and adapted tensors are bitwise equal.  SUTA_CONV_DW_SIDE=1 (the conv stack's weight-gradient
+    GEMMs on a side stream, alternating dz planes) runs the same kernels in another order: bitwise equal as well.  bf16 mode, a ragged batch with T = 399 (13 key groups: two
     key blocks, a half-empty last query tile), 262 (keys past the length inside a wave) and 49 (one query tile), 2 SUTA
     steps."""
     cfg = get_config(model)
