@@ -1428,12 +1428,17 @@ constexpr size_t fbbp_lds_bytes() {
     return 2 * ((size_t)(64 + (ONEB ? 64 : 32)) * FBB_KB + 2 * 2 * 32 * FB_RS) + 4 * 128;
 }
 
+//
+// Chained dQ (kbl >= 0, SUTA_DQ_CHAIN): one launch per key block, kbl = 0 .. nkb - 1 in stream order, grid = one block
+// per (utterance, head).  Launch kbl adds its dQ contribution to a single fp32 accumulator per head -- launch 0 writes
+// it, later ones read-add-write it -- and the last launch writes dQ itself (rows past the utterance's length 0), so no
+// per-key-block partials and no flash_dq_reduce pass: the sums run in key-block order, as the reduce pass's.
 template <bool ONEB>
 __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
     const __bf16* __restrict__ qkvb, const __bf16* __restrict__ dob, const float* __restrict__ lse,
     const float* __restrict__ delta, float* __restrict__ dqkv, float* __restrict__ dqp, int T, int NH, int H,
     float scale, const int* __restrict__ tlen, int nkb, int gpb, int B, __bf16* __restrict__ dqkvb,
-    int* __restrict__ dq_cnt) {
+    int* __restrict__ dq_cnt, int kbl) {
     constexpr int NW = FBB_NW, NT = NW * 64;
     constexpr int NSS = ONEB ? 2 : 1;             // dS images
     extern __shared__ __attribute__((aligned(16))) __bf16 sm16[];
@@ -1444,7 +1449,8 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
     float* Ls = reinterpret_cast<float*>(Dr + 2 * 32 * FB_RS);  // [2][32]
     float* Dl = Ls + 64;                          // [2][32]
     const int id = xcd_block();
-    const int kb = id % nkb, bh = id / nkb, hd = bh % NH, u = bh / NH;
+    const bool chain = kbl >= 0;
+    const int kb = chain ? kbl : id % nkb, bh = chain ? id : id / nkb, hd = bh % NH, u = bh / NH;
     // the wave index as a scalar: every per-wave condition below (active, kall) is then a scalar branch
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, l32 = lane & 31,
               h = lane >> 5;
@@ -1510,7 +1516,8 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
     const int qi = w & 1, di = w >> 1;
     const int kq = ngb * 32;
     const long dq_stride = (long)B * NH * T * 64;
-    float* dqb = dqp + kb * dq_stride + (long)bh * T * 64;
+    float* dqb = dqp + (chain ? 0 : kb * dq_stride) + (long)bh * T * 64;
+    const bool dq_last = chain && kb + 1 == nkb;  // this launch writes dQ itself
     const int nqt = (tl + 31) >> 5;
     if (!active && w < ngb)
         for (int r = 0; r < NSS * 32; ++r)
@@ -1592,9 +1599,26 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
                         *reinterpret_cast<const fbf16x8*>(kfrow + 32 * j), c[j & 1], 0, 0, 0);
             const f32x4 c0 = c[0], c1 = c[1];
             float* dr = dqb + (long)(q0 + 16 * qi + 4 * g) * 64 + 16 * di + l16;
+            if (!chain) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
-                if (q0 + 16 * qi + 4 * g + r < T) dr[r * 64] = c0[r] + c1[r];
+                for (int r = 0; r < 4; ++r)
+                    if (q0 + 16 * qi + 4 * g + r < T) dr[r * 64] = c0[r] + c1[r];
+            } else if (!dq_last) {  // the head's accumulator: written by key block 0, read-add-written by later ones
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if (q0 + 16 * qi + 4 * g + r < T) dr[r * 64] = kb == 0 ? c0[r] + c1[r] : dr[r * 64] + (c0[r] + c1[r]);
+            } else {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int q = q0 + 16 * qi + 4 * g + r;
+                    if (q < T) {
+                        const float v = q < tl ? (kb == 0 ? c0[r] + c1[r] : dr[r * 64] + (c0[r] + c1[r])) : 0.f;
+                        const long o = ((long)u * T + q) * ld + hd * 64 + 16 * di + l16;
+                        if (dqkv) dqkv[o] = v;
+                        if (dqkvb) dqkvb[o] = (__bf16)v;
+                    }
+                }
+            }
         }
         if constexpr (!ONEB) {
             if (qt + 1 < nqt) put(buf ^ 1, py);
@@ -1632,6 +1656,13 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
                     *reinterpret_cast<fbf16x4*>(kb2 + H) = cvt4(y);
                 }
             }
+    }
+    if (dq_last) {  // query rows of tiles past the utterance's length (never computed): dQ = 0
+        for (int i = nqt * 32 * 64 + threadIdx.x; i < T * 64; i += NT) {
+            const long o = ((long)u * T + (i >> 6)) * ld + hd * 64 + (i & 63);
+            if (dqkv) dqkv[o] = 0.f;
+            if (dqkvb) dqkvb[o] = (__bf16)0.f;
+        }
     }
     if constexpr (ONEB) {
         if (dq_cnt) __syncthreads();  // (dq_combine's ticket scratch aliases Ls, still read by the last tile's waves)
@@ -1987,7 +2018,7 @@ static void flash_bwd_go(dim3 grid, hipStream_t st, const float* qkv, const floa
 template <bool ONEB>
 static void flash_bwd_bf16p_go(dim3 grid, hipStream_t st, const void* qkvb, const void* dctxb, const float* lse,
                                const float* delta, float* dqkv, float* dqp, int T, int NH, int H, float scale,
-                               const int* tlen, int nkb, int gpb, int B, __bf16* dqkvb, int* cnt) {
+                               const int* tlen, int nkb, int gpb, int B, __bf16* dqkvb, int* cnt, int kbl = -1) {
     constexpr size_t lds = fbbp_lds_bytes<ONEB>();
     static bool attr = false;
     if (!attr) {
@@ -1998,7 +2029,7 @@ static void flash_bwd_bf16p_go(dim3 grid, hipStream_t st, const void* qkvb, cons
     }
     hipLaunchKernelGGL(flash_bwd_bf16p_kernel<ONEB>, grid, dim3(FBB_NW * 64), lds, st,
                        reinterpret_cast<const __bf16*>(qkvb), reinterpret_cast<const __bf16*>(dctxb), lse, delta, dqkv,
-                       dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb, cnt);
+                       dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb, cnt, kbl);
 }
 
 // bf16 mode, bf16 planes of qkv and dctx given: flash_bwd_bf16p_kernel (env SUTA_FLASH_BWD_PLANE=0 keeps the
@@ -2031,6 +2062,11 @@ bool launch_flash_bwd(const float* qkv, const float* dctx, const float* lse, con
             throw std::runtime_error("flash_bwd: ticket memset failed");
     }
     if (!qkv && !on_planes) throw std::invalid_argument("flash_bwd: fp32 qkv not written and the plane kernel not taken");
+    // SUTA_DQ_CHAIN (bf16 planes, the plain two-pass form): one launch per key block adding into one accumulator per
+    // head, where each launch still fills the chip (>= 4 rounds of blocks) or there is one key block
+    // (2: at any grid size -- tests)
+    const bool dq_chain = on_planes && !cnt && !suta_switches().flash_bwd_pipe && suta_switches().dq_chain &&
+                          (nkb == 1 || (long)B * NH >= 1024 || suta_switches().dq_chain == 2);
     if (on_planes) {
         if ((reinterpret_cast<uintptr_t>(qkvb) | reinterpret_cast<uintptr_t>(dctxb)) & 15)
             throw std::invalid_argument("flash_bwd: bf16 planes not 16-B aligned");
@@ -2046,6 +2082,15 @@ bool launch_flash_bwd(const float* qkv, const float* dctx, const float* lse, con
             hipLaunchKernelGGL(flash_bwd_bf16pp_kernel, grid, dim3(FBB_NW * 64), lds, st,
                                reinterpret_cast<const __bf16*>(qkvb), reinterpret_cast<const __bf16*>(dctxb), lse, delta,
                                dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb, cnt);
+        } else if (dq_chain) {  // one launch per key block, dQ written by the last (no partials, no reduce pass)
+            for (int kbl = 0; kbl < nkb; ++kbl) {
+                if (suta_switches().flash_bwd_oneb)
+                    flash_bwd_bf16p_go<true>(dim3((unsigned)((long)B * NH)), st, qkvb, dctxb, lse, delta, dqkv, dqp, T,
+                                             NH, H, scale, tlen, nkb, gpb, B, dqkvb, nullptr, kbl);
+                else
+                    flash_bwd_bf16p_go<false>(dim3((unsigned)((long)B * NH)), st, qkvb, dctxb, lse, delta, dqkv, dqp,
+                                              T, NH, H, scale, tlen, nkb, gpb, B, dqkvb, nullptr, kbl);
+            }
         } else if (suta_switches().flash_bwd_oneb) {
             flash_bwd_bf16p_go<true>(grid, st, qkvb, dctxb, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B,
                                      dqkvb, cnt);
@@ -2071,7 +2116,7 @@ bool launch_flash_bwd(const float* qkv, const float* dctx, const float* lse, con
         if (bf16) flash_bwd_go<8, true>(grid, st, qkv, dctx, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb, cnt);
         else flash_bwd_go<8, false>(grid, st, qkv, dctx, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb, cnt);
     }
-    if (!cnt) {
+    if (!cnt && !dq_chain) {
         const long n4 = (long)B * NH * T * 16;
         hipLaunchKernelGGL(flash_dq_reduce, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, dqp, dqkv, B, T, NH, H,
                            nkb, tlen, dqkvb);

@@ -99,6 +99,8 @@ struct SutaSwitches {
                           // next query tile under this tile's softmax, attn.hip flash_bwd_bf16pp_kernel; bitwise equal)
     int flash_bwd_oneb;   // SUTA_FLASH_BWD_ONEB (default 1): the bf16-plane flash backward with one barrier per query tile (dS
                           // image double-buffered, the next tile's Q / dO put before the barrier); bitwise equal; 0 = two
+    int dq_chain;         // SUTA_DQ_CHAIN: the bf16-plane flash backward as one launch per key block adding dQ into one
+                          // accumulator per head, the last launch writing dQ (no partials, no flash_dq_reduce pass)
     int conv_dw_side;     // SUTA_CONV_DW_SIDE: the layer-mode conv stack's weight-gradient GEMMs on a side stream (engine.hip
                           // backward: fork after the layer's LayerNorm backward, join before its dz plane is rewritten)
     int epi_fast;         // SUTA_EPI_FAST (default 1): 32-bit-offset GEMM epilogue where every operand fits 4 GiB (p.off32);

@@ -1952,6 +1952,8 @@ void suta_latch_switches() {
     // one barrier per query tile in the bf16-plane flash backward: C4 attention 543-546 -> 534-535 ms per call, same box
     // (profiles/r5/oneb_ab.txt); =0 the two-barrier form
     s.flash_bwd_oneb = on("SUTA_FLASH_BWD_ONEB");
+    const char* dqc = std::getenv("SUTA_DQ_CHAIN");
+    s.dq_chain = dqc ? atoi(dqc) : 0;
     const char* cds = std::getenv("SUTA_CONV_DW_SIDE");
     s.conv_dw_side = cds ? atoi(cds) : 0;
     s.latched = 1;

@@ -571,7 +571,7 @@ def test_conv_input_gradients_on_256_tile_bitwise(monkeypatch, form):
         assert np.array_equal(v, params["0"][n]), n
 
 
-@pytest.mark.parametrize("switch", ["SUTA_FLASH_BWD_PIPE", "SUTA_FLASH_BWD_ONEB", "SUTA_CONV_DW_SIDE"])
+@pytest.mark.parametrize("switch", ["SUTA_FLASH_BWD_PIPE", "SUTA_FLASH_BWD_ONEB", "SUTA_CONV_DW_SIDE", "SUTA_DQ_CHAIN"])
 @pytest.mark.parametrize("model", ["wav2vec2-large", "wav2vec2-base"])
 def test_pipelined_bf16_flash_backward_bitwise(monkeypatch, model, switch):
     """Two alternative forms of the bf16-plane flash backward against flash_bwd_bf16p_kernel (switch = 0): the
@@ -579,7 +579,9 @@ def test_pipelined_bf16_flash_backward_bitwise(monkeypatch, model, switch):
     rows read from LDS, three Q / dO images) and the one-barrier one (SUTA_FLASH_BWD_ONEB=1: double-buffered dS image,
     the next tile's rows put before the tile's single barrier).  Both do the same operations per element in the same
     order, so logits and adapted tensors are bitwise equal.  SUTA_CONV_DW_SIDE=1 (the conv stack's weight-gradient
-    GEMMs on a side stream, alternating dz planes) runs the same kernels in another order: bitwise equal as well.  bf16 mode, a ragged batch with T = 399 (13 key groups: two
+    GEMMs on a side stream, alternating dz planes) runs the same kernels in another order, and SUTA_DQ_CHAIN (one
+    launch per key block summing dQ into one accumulator in key-block order, the last launch writing dQ and the zero
+    rows past each utterance's length) the reduce pass's sums: bitwise equal as well.  bf16 mode, a ragged batch with T = 399 (13 key groups: two
     key blocks, a half-empty last query tile), 262 (keys past the length inside a wave) and 49 (one query tile), 2 SUTA
     steps."""
     cfg = get_config(model)
@@ -587,7 +589,8 @@ def test_pipelined_bf16_flash_backward_bitwise(monkeypatch, model, switch):
     waves = [synth.wave(n, 70 + i) for i, n in enumerate((128000, 84000, 16000))]
     out, params = {}, {}
     for pipe in ("1", "0"):
-        monkeypatch.setenv(switch, pipe)
+        # (SUTA_DQ_CHAIN=2: the chained launches at this small grid too)
+        monkeypatch.setenv(switch, "2" if (switch == "SUTA_DQ_CHAIN" and pipe == "1") else pipe)
         eng = SutaEngine(cfg, sd, max_batch=3, max_samples=128000)
         eng.set_precision("bf16")
         out[pipe], _, t = eng.adapt_varlen(waves, 2, SutaHParams(), record=[0, 1, 2])
