@@ -450,8 +450,11 @@ def bench_c5(args, dev):
                                                   drv.gpu_min_fill)]
     q = LAYOUT_QUANTUM
     widths = [-(-int(ns[g].max()) // q) * q for g in groups]
-    eng = SutaEngine(cfg, synth_weights(cfg), device=dev, max_batch=max(len(g) for g in groups),
-                     max_samples=max(widths))
+    sd = synth_weights(cfg)
+    E = max(1, getattr(args, "c5_engines", 1) or 1)
+    engs = [SutaEngine(cfg, sd, device=dev, max_batch=max(len(g) for g in groups), max_samples=max(widths))
+            for _ in range(E)]
+    eng = engs[0]
     hp = SutaHParams()
     pads = []
     for g, w in zip(groups, widths):
@@ -461,14 +464,34 @@ def bench_c5(args, dev):
         pads.append(torch.from_numpy(p).to(f"cuda:{dev}"))
     lens = [[int(ns[i]) for i in g] for g in groups]
     big = int(np.argmax([len(g) * w for g, w in zip(groups, widths)]))
-    eng.adapt_varlen(pads[big], 1, hp, record=[1], lengths=lens[big], want_logits=False)   # workspace at its max
+    for e in engs:
+        e.adapt_varlen(pads[big], 1, hp, record=[1], lengths=lens[big], want_logits=False)   # workspace at its max
+        e.sync()
     torch.cuda.synchronize()
-    eng.sync()
+    # --c5-engines E > 1: E engines (own streams, workspaces) in E host threads, the groups dealt longest-processing-
+    # time first by padded frames (an experiment on concurrency between ragged groups; the driver runs one engine)
+    shares = [[] for _ in range(E)]
+    load = [0] * E
+    for j in sorted(range(len(groups)), key=lambda j: -len(groups[j]) * widths[j]):
+        e = int(np.argmin(load))
+        shares[e].append(j)
+        load[e] += len(groups[j]) * widths[j]
+
+    def run_share(e, js):
+        for j in js:
+            engs[e].adapt_varlen(pads[j], S, hp, record=RECORD, lengths=lens[j], want_logits=False)
+        engs[e].sync()
 
     def one_pass():
-        for p, ln in zip(pads, lens):
-            eng.adapt_varlen(p, S, hp, record=RECORD, lengths=ln, want_logits=False)
-        eng.sync()
+        if E == 1:
+            run_share(0, range(len(groups)))
+            return
+        import threading
+        th = [threading.Thread(target=run_share, args=(e, shares[e])) for e in range(E)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
     t0 = time.perf_counter()
     one_pass()
     el = time.perf_counter() - t0
@@ -485,9 +508,11 @@ def bench_c5(args, dev):
            "max_seconds": round(float(ns.max()) / 16000, 2), "n_batches": len(groups),
            "batch_sizes": [len(g) for g in groups], "padded_frame_fraction": round(1.0 - T_true / T_pad, 4),
            "algorithmic_tflops": round(flops / el / 1e12, 3)}
+    if E > 1:
+        res["engines"] = E
     if not args.no_timing:
         eng.set_timing(True)
-        one_pass()
+        run_share(0, range(len(groups)))   # (one engine: per-launch events on its stream)
         t = eng.get_timing()
         eng.set_timing(False)
         gms, gn = t["gemm"]
@@ -496,7 +521,8 @@ def bench_c5(args, dev):
                            "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
                            "kernel": "fp32 MFMA GEMM family (as the headline), FLOPs on true lengths",
                            "launches": int(gn), "avg_launch_ms": round(gms / max(1, gn), 5)}
-    eng.close()
+    for e in engs:
+        e.close()
     return res
 
 
@@ -529,6 +555,7 @@ def build_parser():
     ap.add_argument("--c5-gpu-batch", type=int, default=None, help="C5 grouping override (default: the driver's)")
     ap.add_argument("--c5-gpu-budget-s", type=float, default=None, help="C5 grouping override (default: the driver's)")
     ap.add_argument("--c5-gpu-min-fill", type=float, default=None, help="C5 grouping override (default: the driver's)")
+    ap.add_argument("--c5-engines", type=int, default=1, help="C5: engines (streams, host threads) sharing the groups")
     ap.add_argument("--no-batch64", dest="batch64", action="store_false",
                     help="skip the 64-utterances-per-call line")
     ap.add_argument("--no-split", dest="also_split", action="store_false",
