@@ -18,13 +18,17 @@ ARGV = ["--gpus", "2", "--dist-backend", "gloo", "--model", "tiny-group", "--bat
         "--no-c5", "--no-batch64", "--no-split"]
 
 
-def test_bench_two_ranks_shard_time_and_print(tmp_path):
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_two_ranks_shard_time_and_print(tmp_path, world):
+    """World sizes 2 and 4 (the driver's SCALE run launches 1 / 2 / 4 / 8 ranks; 8 processes are not started here)."""
     from tests import _bench_dist_worker as W
     from suta_amd import synth
-    world, port = 2, free_port()
+    port = free_port()
+    argv = list(ARGV)
+    argv[argv.index("--gpus") + 1] = str(world)
     ctx = mp.get_context("spawn")
     outs = [str(tmp_path / f"rank{r}.json") for r in range(world)]
-    procs = [ctx.Process(target=W.bench_rank, args=(r, world, port, outs[r], ARGV)) for r in range(world)]
+    procs = [ctx.Process(target=W.bench_rank, args=(r, world, port, outs[r], argv)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -32,18 +36,19 @@ def test_bench_two_ranks_shard_time_and_print(tmp_path):
         assert p.exitcode == 0, p.exitcode
     res = [json.load(open(o)) for o in outs]
     # rank 0 alone prints, one JSON line
-    assert res[1]["stdout"] == "" and res[1]["ret"] is None
+    for r in range(1, world):
+        assert res[r]["stdout"] == "" and res[r]["ret"] is None
     lines = [ln for ln in res[0]["stdout"].splitlines() if ln.strip()]
     assert len(lines) == 1
     out = json.loads(lines[0])
     assert out == res[0]["ret"]
     B, steps, warmup = 3, 3, 1
     nb = steps + warmup
-    assert out["n_gpus"] == 2 and out["scaling"] == "weak" and out["dist"]["backend"] == "gloo"
+    assert out["n_gpus"] == world and out["scaling"] == "weak" and out["dist"]["backend"] == "gloo"
     # value = utterances of all ranks / max elapsed over ranks
     el = out["dist"]["rank_elapsed_s"]
     # the closing barrier holds every rank until the slowest has finished: rank 1's stand-in sleeps 0.1 s per call
-    assert len(el) == 2 and min(el) >= steps * 0.1
+    assert len(el) == world and min(el) >= steps * 0.1
     assert out["value"] == pytest.approx(B * steps * world / max(el), rel=1e-3)
     assert out["ms_per_step"] == pytest.approx(1000 * max(el) / steps, rel=1e-3)
     # disjoint utterance ranges, and each rank adapted exactly its own utterances
@@ -52,7 +57,8 @@ def test_bench_two_ranks_shard_time_and_print(tmp_path):
     for r in range(world):
         want = [float(synth.wave(4000, i)[0]) for i in range(r * nb * B, (r + 1) * nb * B)]
         np.testing.assert_array_equal(np.array(res[r]["seen"], np.float32), np.array(want, np.float32))
-    assert not set(res[0]["seen"]) & set(res[1]["seen"])
+    for r in range(1, world):
+        assert not set(res[0]["seen"]) & set(res[r]["seen"])
 
 
 def test_driver_defaults_run_the_bench_layout():
