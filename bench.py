@@ -451,7 +451,7 @@ def bench_c5(args, dev):
     q = LAYOUT_QUANTUM
     widths = [-(-int(ns[g].max()) // q) * q for g in groups]
     sd = synth_weights(cfg)
-    E = max(1, getattr(args, "c5_engines", 1) or 1)
+    E = max(1, getattr(args, "c5_engines", None) or drv.gpu_engines)   # the driver's --gpu_engines unless overridden
     engs = [SutaEngine(cfg, sd, device=dev, max_batch=max(len(g) for g in groups), max_samples=max(widths))
             for _ in range(E)]
     eng = engs[0]
@@ -468,8 +468,8 @@ def bench_c5(args, dev):
         e.adapt_varlen(pads[big], 1, hp, record=[1], lengths=lens[big], want_logits=False)   # workspace at its max
         e.sync()
     torch.cuda.synchronize()
-    # --c5-engines E > 1: E engines (own streams, workspaces) in E host threads, the groups dealt longest-processing-
-    # time first by padded frames (an experiment on concurrency between ragged groups; the driver runs one engine)
+    # E engines (own streams, workspaces) in E host threads, the groups dealt longest-processing-time first by padded
+    # samples -- as suta_amd/main.py adapt_window deals them (--gpu_engines, default 2)
     shares = [[] for _ in range(E)]
     load = [0] * E
     for j in sorted(range(len(groups)), key=lambda j: -len(groups[j]) * widths[j]):
@@ -501,15 +501,14 @@ def bench_c5(args, dev):
     res = {"workload": f"wav2vec2-base SUTA {S} steps, {len(ns)} TED-like utterances (log-normal around 10 s, "
                        "2-37.5 s, seeded), length-sorted ragged batches grouped by the driver's ragged_groups "
                        f"(--gpu_batch {drv.gpu_batch}, --gpu_budget_s {drv.gpu_budget_s:g}, --gpu_min_fill "
-                       f"{drv.gpu_min_fill:g}), scripts/LS.sh flags, fp32",
+                       f"{drv.gpu_min_fill:g}, {E} engine(s)), scripts/LS.sh flags, fp32",
            "config": "C5", "precision": "fp32", "value": round(len(ns) / el, 4), "unit": "utt/s",
            "audio_s_per_s": round(float(ns.sum()) / 16000 / el, 2), "seconds": round(el, 3),
            "n_utterances": len(ns), "mean_seconds": round(float(ns.mean()) / 16000, 2),
            "max_seconds": round(float(ns.max()) / 16000, 2), "n_batches": len(groups),
            "batch_sizes": [len(g) for g in groups], "padded_frame_fraction": round(1.0 - T_true / T_pad, 4),
            "algorithmic_tflops": round(flops / el / 1e12, 3)}
-    if E > 1:
-        res["engines"] = E
+    res["engines"] = E
     if not args.no_timing:
         eng.set_timing(True)
         run_share(0, range(len(groups)))   # (one engine: per-launch events on its stream)
@@ -555,7 +554,8 @@ def build_parser():
     ap.add_argument("--c5-gpu-batch", type=int, default=None, help="C5 grouping override (default: the driver's)")
     ap.add_argument("--c5-gpu-budget-s", type=float, default=None, help="C5 grouping override (default: the driver's)")
     ap.add_argument("--c5-gpu-min-fill", type=float, default=None, help="C5 grouping override (default: the driver's)")
-    ap.add_argument("--c5-engines", type=int, default=1, help="C5: engines (streams, host threads) sharing the groups")
+    ap.add_argument("--c5-engines", type=int, default=None,
+                    help="C5: engines (streams, host threads) sharing the groups (default: the driver's --gpu_engines)")
     ap.add_argument("--no-batch64", dest="batch64", action="store_false",
                     help="skip the 64-utterances-per-call line")
     ap.add_argument("--no-split", dest="also_split", action="store_false",

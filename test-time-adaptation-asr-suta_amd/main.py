@@ -72,6 +72,10 @@ def build_parser(sdpl: bool = False):
                         "this fraction of --gpu_budget_s (bench.py c5, TED-like mix of 512 utterances at --gpu_batch 164 "
                         "/ --gpu_budget_s 1312: 0.2 / 0.3 / 0.4 / 0.5 / 0.7 -> 20.8 / 21.6 / 21.5-21.6 / 20.9 / 20.8 "
                         "utt/s, profiles/r5/c5_mf*.json; on round 4's 96-utterance mix 0.15-0.25 was the optimum)")
+    p.add_argument("--gpu_engines", type=int, default=2,
+                   help="episodic runs: engines per GPU (own HIP stream, workspace and host thread) adapting ragged "
+                        "groups concurrently; the padded-audio budget is per engine (bench.py c5, 512 TED-like "
+                        "utterances: 1 / 2 engines 21.60 / 22.93 utt/s, profiles/r5/c5_e*.json)")
     p.add_argument("--dist_backend", default="auto", choices=["auto", "nccl", "gloo"],
                    help="torch.distributed backend under torchrun (auto: nccl = RCCL when a GPU is visible)")
     p.add_argument("--num_workers", type=int, default=4,
@@ -247,13 +251,18 @@ def main(argv=None, sdpl: bool = False):
     say(f"[INFO]    scheduler: {a.scheduler}")
     say(param_names)
     gb = max(1, a.gpu_batch) if a.episodic else 1  # non-episodic adaptation is sequential
+    # non-episodic adaptation carries state across utterances in one engine's slot: one engine
+    n_eng = max(1, a.gpu_engines) if (a.episodic and gb > 1) else 1
     if torch.cuda.is_available():
-        budget = clamp_budget(a.gpu_budget_s, cfg, torch.cuda.mem_get_info(device)[0])
+        budget = clamp_budget(a.gpu_budget_s, cfg, torch.cuda.mem_get_info(device)[0], frac=0.7 / n_eng)
         if budget < a.gpu_budget_s:
-            say(f"[suta_amd] --gpu_budget_s {a.gpu_budget_s} exceeds 70 % of the free device memory; using {budget:.0f} s")
+            say(f"[suta_amd] --gpu_budget_s {a.gpu_budget_s} x {n_eng} engine(s) exceeds 70 % of the free device "
+                f"memory; using {budget:.0f} s")
             a.gpu_budget_s = budget
-    engine = SutaEngine(cfg, weights, device=device, max_batch=gb)
-    engine.set_precision(a.precision)
+    engines = [SutaEngine(cfg, weights, device=device, max_batch=gb) for _ in range(n_eng)]
+    for e in engines:
+        e.set_precision(a.precision)
+    engine = engines[0]
     hp = SutaHParams(lr=a.lr, temp=a.temp, em_coef=a.em_coef, div_coef=0.0 if sdpl else a.div_coef,
                      reweight=a.reweight, non_blank=a.non_blank, train_feature=a.train_feature,
                      bias_only=a.bias_only, episodic=a.episodic, pl_coef=1.0 if sdpl else 0.0, optimizer=a.opt,
@@ -273,20 +282,48 @@ def main(argv=None, sdpl: bool = False):
         mine = list(range(len(batches)))
 
     def adapt_window(items):
-        """ids {record step: (T,)} per item, adapting length-sorted groups of gb as ragged batches."""
+        """ids {record step: (T,)} per item, adapting length-sorted groups of gb as ragged batches.  With several
+        engines the groups are dealt longest-first to the least-loaded engine (padded samples) and each engine's
+        share runs in its own host thread on its own stream; every utterance's result is the same whichever engine
+        adapts it (episodic: the slot starts from the pristine tensors)."""
         order = sorted(range(len(items)), key=lambda i: len(items[i][1])) if gb > 1 else list(range(len(items)))
         out = [None] * len(items)
-        for grp in ragged_groups([len(items[i][1]) for i in order], gb, a.gpu_budget_s * SAMPLE_RATE,
-                                   a.gpu_min_fill):
-            grp = [order[j] for j in grp]
-            if gb == 1:
-                _, ids, _ = engine.adapt(items[grp[0]][1], a.steps, hp, record=record, want_logits=False)
-                out[grp[0]] = {r: ids[r][0] for r in record}
-            else:  # layout rounded up to LAYOUT_QUANTUM: equal layouts replay one captured step
-                _, ids, _ = engine.adapt_varlen([items[i][1] for i in grp], a.steps, hp, record=record,
-                                                want_logits=False, quantum=LAYOUT_QUANTUM)
-                for j, i in enumerate(grp):
-                    out[i] = {r: ids[r][j] for r in record}
+        groups = [[order[j] for j in grp] for grp in ragged_groups([len(items[i][1]) for i in order], gb,
+                                                                   a.gpu_budget_s * SAMPLE_RATE, a.gpu_min_fill)]
+
+        def run(eng, grps):
+            for grp in grps:
+                if gb == 1:
+                    _, ids, _ = eng.adapt(items[grp[0]][1], a.steps, hp, record=record, want_logits=False)
+                    out[grp[0]] = {r: ids[r][0] for r in record}
+                else:  # layout rounded up to LAYOUT_QUANTUM: equal layouts replay one captured step
+                    _, ids, _ = eng.adapt_varlen([items[i][1] for i in grp], a.steps, hp, record=record,
+                                                 want_logits=False, quantum=LAYOUT_QUANTUM)
+                    for j, i in enumerate(grp):
+                        out[i] = {r: ids[r][j] for r in record}
+        if n_eng == 1 or len(groups) == 1:
+            run(engine, groups)
+            return out
+        import threading
+        shares, load = [[] for _ in range(n_eng)], [0] * n_eng
+        for grp in sorted(groups, key=lambda g: -len(g) * max(len(items[i][1]) for i in g)):
+            e = load.index(min(load))
+            shares[e].append(grp)
+            load[e] += len(grp) * max(len(items[i][1]) for i in grp)
+        errs = []
+
+        def guarded(eng, grps):
+            try:
+                run(eng, grps)
+            except BaseException as exc:   # re-raised in the calling thread
+                errs.append(exc)
+        th = [threading.Thread(target=guarded, args=(engines[e], shares[e])) for e in range(n_eng) if shares[e]]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        if errs:
+            raise errs[0]
         return out
 
     results = []
@@ -377,7 +414,8 @@ def main(argv=None, sdpl: bool = False):
             durations = [r["duration"] for r in allres]
             werrs = [r.get("werr", np.nan) for r in allres]
             pd.DataFrame({"duration": durations, "WERR": werrs}).to_csv(os.path.join(a.log_dir, exp_name + ".csv"))
-    engine.close()
+    for e in engines:
+        e.close()
     if world > 1:
         import torch.distributed as tdist
         tdist.destroy_process_group()

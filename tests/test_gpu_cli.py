@@ -36,14 +36,15 @@ def _corpus(root, n=4):
         (tpath / f"U{i}.trn").write_text(f"U{i} " + " ".join(rng.choice(words, size=3 + i)) + "\n")
 
 
-@pytest.mark.parametrize("gpu_batch", [1, 16])
-def test_cli_end_to_end_matches_oracle(tmp_path, capsys, gpu_batch):
-    """gpu_batch 16: the 4 utterances (different lengths) run as one ragged batch."""
+@pytest.mark.parametrize("gpu_batch,engines", [(1, 1), (16, 2), (2, 2), (2, 3)])
+def test_cli_end_to_end_matches_oracle(tmp_path, capsys, gpu_batch, engines):
+    """gpu_batch 16: the 4 utterances (different lengths) run as one ragged batch; gpu_batch 2 with 2 / 3 engines:
+    the ragged groups adapted concurrently by several engines (own streams, host threads), results by utterance."""
     from oracle import w2v2_cpu as W
     _corpus(tmp_path)
     args = (f"--asr tiny-group --synthetic_weights --steps 10 --dataset_name chime --dataset_dir {tmp_path} "
             f"--temp 2.5 --episodic --em_coef 0.3 --reweight --log_dir {tmp_path}/exps --lr 5e-4 --non_blank "
-            f"--train_feature --extra_noise 0 --gpu_batch {gpu_batch}").split()
+            f"--train_feature --extra_noise 0 --gpu_batch {gpu_batch} --gpu_engines {engines}").split()
     counts = M.main(args)
     out = capsys.readouterr().out
     assert "original WER: " in out and "adapt-10 WER: " in out and "TTA-10 WER:" in out
