@@ -6,7 +6,9 @@ scripts/LS.sh flags (episodic reset, vanilla forward, greedy ids recorded at ste
 Waveforms are resident in HBM before the timed region.  Seeded random weights of the
 w2v2-base architecture (no checkpoints offline).
 
-Multi-GPU: one process per GPU (torchrun); every rank adapts its own utterances (no data-path
+Multi-GPU: one process per GPU -- `python bench.py --gpus N` starts the N rank processes itself (torchrun env
+contract, before this process touches the GPU; `self_launch`), and the torchrun form works unchanged; every
+rank adapts its own utterances (no data-path
 collective, weak scaling); a barrier + device sync brackets the timed region and the max
 elapsed time over ranks is used.  value = utterances of all ranks / that time.  The collectives
 (barrier, max, gather of per-rank facts) go through `Comm` on `--dist-backend` (nccl = RCCL over
@@ -164,6 +166,11 @@ class Comm:
         if self.world > 1:
             self.tdist.barrier()
 
+    def world_seen(self):
+        """get_world_size() of the live process group (1 without one): the ranks that actually joined."""
+        import torch.distributed as tdist
+        return tdist.get_world_size() if tdist.is_available() and tdist.is_initialized() else 1
+
     def max(self, x):
         if self.world == 1:
             return x
@@ -266,8 +273,9 @@ def run(args, rank, world, comm, dev, make_engine):
                    "batch_note": "164 utterances x 399 frames = 512 row tiles of 128 (tuned to the bench's fixed "
                                  "length); see batch64 for the 64-per-call line"},
         "algorithmic_tflops": round(flops_utt * utts / el / 1e12, 3),
-        "dist": {"backend": comm.backend if world > 1 else None, "rank_elapsed_s": rank_el,
-                 "utterance_shards": shards},
+        "dist": {"backend": comm.backend if world > 1 else None, "world_seen": comm.world_seen(),
+                 "rank_elapsed_s": rank_el, "utterance_shards": shards,
+                 "rccl_measured": bool(world > 1 and comm.backend == "nccl")},
     }
     if timing:
         gms, gn = timing["gemm"]
@@ -563,20 +571,80 @@ def build_parser():
     return ap
 
 
-def main():
-    args = build_parser().parse_args()
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def self_launch(n: int, argv, script: str = None, timeout_s: float = None) -> int:
+    """`--gpus N` (N > 1) without a torchrun environment: start N rank processes of `script` (this file) with the
+    torchrun contract -- RANK, WORLD_SIZE, LOCAL_RANK, LOCAL_WORLD_SIZE, MASTER_ADDR 127.0.0.1, MASTER_PORT -- and
+    return the worst exit status.  This process never touches the GPU (no HIP call before or after the children
+    start); rank 0's JSON line reaches stdout through the inherited descriptor.  When one rank fails, the others
+    (which would wait in a barrier forever) are terminated."""
+    import subprocess
+    port = free_port()
+    script = script or os.path.abspath(__file__)
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PYTHONUNBUFFERED="1")
+        procs.append(subprocess.Popen([sys.executable, script] + list(argv), env=env))
+    t0, worst = time.time(), 0
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c not in (None, 0)]
+        late = timeout_s is not None and time.time() - t0 > timeout_s
+        if bad or late:
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(15)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+            worst = bad[0] if bad else 124
+            print(f"bench.py: self-launched rank failed (exit {worst}); stopped the other ranks", file=sys.stderr)
+            return worst
+        if all(c == 0 for c in codes):
+            return 0
+        time.sleep(0.2)
+
+
+def main(argv=None, engine_factory=None, script=None):
+    """argv: bench flags (default sys.argv[1:]).  engine_factory / script: the CPU plumbing test's stand-in engine
+    (called as engine_factory(rank) -> make_engine) and the script its self-launched ranks run; None = the real
+    engine on the GPU and this file."""
+    argv = sys.argv[1:] if argv is None else list(argv)
+    args = build_parser().parse_args(argv)
     if args.only_c4 or args.only_c5:
         torch.cuda.set_device(0)
         print(json.dumps(bench_c4(args, 0) if args.only_c4 else bench_c5(args, 0)), flush=True)
-        return
+        return 0
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # the plain `python bench.py --gpus N` form: one rank process per GPU, launched here
+        return self_launch(args.gpus, argv, script=script)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world:
-        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: launch N > 1 with "
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: launch N > 1 as `python bench.py --gpus N` or "
               f"`python -m torch.distributed.run --nproc-per-node {args.gpus} bench.py --gpus {args.gpus}`",
               file=sys.stderr)
-        sys.exit(2)
+        return 2
+    if engine_factory is not None:   # CPU plumbing test: stand-in engine, host "device", gloo only
+        if world > 1:
+            import torch.distributed as tdist
+            tdist.init_process_group("gloo")
+        comm = Comm(rank, world, "gloo", None)
+        run(args, rank, world, comm, Device(None), engine_factory(rank))
+        if world > 1:
+            tdist.destroy_process_group()
+        return 0
     ndev = torch.cuda.device_count()
     if ndev < 1:
         raise SystemExit("bench.py needs a GPU (the engine has no CPU path)")
@@ -600,7 +668,8 @@ def main():
     if world > 1:
         import torch.distributed as tdist
         tdist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -12,6 +12,7 @@
  *   suta_forward         `model(input_values).logits` under no_grad (main.py:331-332)
  *   suta_step            forward_and_adapt(...) — one SUTA step, reference schedule
  *                        (main.py:172-215)
+ *   suta_step_ex         the same with forward_and_adapt's repeat_inference argument (main.py:211-215)
  *   suta_adapt           the per-utterance loop: vanilla forward + `steps` x forward_and_adapt
  *                        with recorded checkpoints (main.py:327-398), minimal schedule
  *                        ((S+1) forwards + S backwards), batched over utterances
@@ -128,6 +129,14 @@ int32_t suta_forward(suta_engine* e, const float* wav, int32_t wav_on_device, in
 int32_t suta_step(suta_engine* e, const float* wav, int32_t wav_on_device, int32_t normalize,
                   int32_t batch, int64_t n_samples, const suta_hparams* hp, float* logits_out,
                   float* loss_out);
+
+/* suta_step with forward_and_adapt's `repeat_inference` argument (main.py:172-173, 211-215): != 0 returns the
+ * no-grad re-inference logits after the update (suta_step), 0 returns the grad forward's logits -- the ones the
+ * loss was taken on -- and skips the re-forward.  logits_out is a device pointer when logits_on_device != 0.
+ * The forward_and_adapt-compatible Python shim (suta_amd/suta.py) calls this entry. */
+int32_t suta_step_ex(suta_engine* e, const float* wav, int32_t wav_on_device, int32_t normalize,
+                     int32_t batch, int64_t n_samples, const suta_hparams* hp, int32_t repeat_inference,
+                     float* logits_out, int32_t logits_on_device, float* loss_out);
 
 /* Episodic SUTA on `batch` utterances: (reset if hp->episodic), vanilla forward, `steps`
  * adaptation steps.  record_steps[0..n_record) are step counts r in [0, steps] (0 = vanilla);

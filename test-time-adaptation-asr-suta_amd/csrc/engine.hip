@@ -260,7 +260,14 @@ struct suta_engine {
     long adam_tab_cap = 0;
     int* d_step = nullptr;
     int h_step = 0;
+    // host rows [0, h_lr.size()) of the table for the optimizer scalars in tab_hp (h_lr = each step's scheduled lr,
+    // the StepLR chained product carried row to row); rows [0, dev_rows) are on the device.  A non-episodic run
+    // grows them by `steps` rows per call instead of rebuilding every row since its start (advisor r5)
     std::vector<float> h_tab;
+    std::vector<double> h_lr;
+    long dev_rows = 0;
+    suta_hparams tab_hp{};
+    double lr_at(const suta_hparams& hp, long i);
     // the whole S-step loop of one suta_adapt call (slot reset, forward, S x (backward + Adam + forward),
     // recorded argmax ids and logits into device staging) captured as one graph per key
     struct GraphKey {
@@ -1667,17 +1674,32 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
     }
 }
 
+// The optimizer scalars a table row depends on (the rest of suta_hparams only shapes the loss)
+static bool same_opt_scalars(const suta_hparams& a, const suta_hparams& b) {
+    return a.lr == b.lr && a.beta1 == b.beta1 && a.beta2 == b.beta2 && a.weight_decay == b.weight_decay &&
+           a.optimizer == b.optimizer && a.lr_step_size == b.lr_step_size && a.lr_gamma == b.lr_gamma;
+}
+
 // lr of optimizer step i counted from the last reset: torch.optim.lr_scheduler.StepLR (main.py:20-21, step_size 1 and
 // gamma 0.7 there) multiplies the group's lr by gamma, in double, each time its step count (advanced after every
 // optimizer step, main.py:207-208) reaches a multiple of step_size (StepLR.get_lr, the chained form); the episodic
-// reset restores it (main.py:147-152)
-static double scheduled_lr(const suta_hparams& hp, long i) {
-    double lr = py_double(hp.lr);
-    if (hp.lr_step_size <= 0) return lr;
+// reset restores it (main.py:147-152).  Carried as a running product over h_lr (rows are only ever appended while
+// the scalars stay the same), so step i costs O(1) amortised and equals the chained loop bitwise.
+double suta_engine::lr_at(const suta_hparams& hp, long i) {
+    if (h_lr.empty() || !same_opt_scalars(hp, tab_hp)) {
+        h_lr.clear();
+        h_tab.clear();
+        dev_rows = 0;
+        tab_hp = hp;
+        h_lr.push_back(py_double(hp.lr));
+    }
     const double g = py_double(hp.lr_gamma);
-    for (long e = 1; e <= i; ++e)
-        if (e % hp.lr_step_size == 0) lr = lr * g;
-    return lr;
+    while ((long)h_lr.size() <= i) {
+        const long e = (long)h_lr.size();
+        const double prev = h_lr.back();
+        h_lr.push_back(hp.lr_step_size > 0 && e % hp.lr_step_size == 0 ? prev * g : prev);
+    }
+    return h_lr[i];
 }
 
 static void check_optimizer(const suta_hparams& hp) {
@@ -1691,7 +1713,7 @@ void suta_engine::adam(int B, const suta_hparams& hp) {
     check_optimizer(hp);
     // Python floats are doubles: recover the decimal the caller meant (0.9f -> 0.9) so the
     // scalars match torch's double-precision host arithmetic (adam.py:495-510)
-    const double lr = scheduled_lr(hp, opt_steps), b1 = py_double(hp.beta1), b2 = py_double(hp.beta2);
+    const double lr = lr_at(hp, opt_steps), b1 = py_double(hp.beta1), b2 = py_double(hp.beta2);
     a.beta1 = (float)b1;
     a.beta2 = (float)b2;
     a.omb1 = (float)(1.0 - b1);
@@ -1735,17 +1757,20 @@ void suta_engine::adam(int B, const suta_hparams& hp) {
 void suta_engine::prepare_adam(const suta_hparams& hp, int steps) {
     check_optimizer(hp);
     const long need = opt_steps + std::max(steps, 1);
+    (void)lr_at(hp, need - 1);  // (re)starts the host rows when the optimizer scalars changed
     if (need > adam_tab_cap) {
         const long cap = std::max<long>(need, 2 * adam_tab_cap);
         if (d_adam_tab) HIPCHK(hipFree(d_adam_tab));
         HIPCHK(hipMalloc(&d_adam_tab, cap * ADAM_TAB * sizeof(float)));
         adam_tab_cap = cap;
+        dev_rows = 0;
         drop_graph();  // captured steps point at the old table
     }
     const double b1 = py_double(hp.beta1), b2 = py_double(hp.beta2), wd = py_double(hp.weight_decay);
-    h_tab.assign(need * ADAM_TAB, 0.f);
-    for (long s0 = 0; s0 < need; ++s0) {
-        const double lr = scheduled_lr(hp, s0);
+    const long have = (long)(h_tab.size() / ADAM_TAB);
+    if (need > have) h_tab.resize(need * ADAM_TAB, 0.f);
+    for (long s0 = have; s0 < need; ++s0) {
+        const double lr = h_lr[s0];
         float* row = h_tab.data() + s0 * ADAM_TAB;
         for (int kk = 1; kk <= 5; ++kk)
             for (int j = 1; j <= kk; ++j) {
@@ -1757,7 +1782,11 @@ void suta_engine::prepare_adam(const suta_hparams& hp, int steps) {
         row[51] = (float)(-lr);
     }
     h_step = (int)opt_steps;
-    HIPCHK(hipMemcpyAsync(d_adam_tab, h_tab.data(), h_tab.size() * sizeof(float), hipMemcpyHostToDevice, st));
+    if (need > dev_rows) {  // rows already on the device hold the same values: only the new ones go up
+        HIPCHK(hipMemcpyAsync(d_adam_tab + dev_rows * ADAM_TAB, h_tab.data() + dev_rows * ADAM_TAB,
+                              (need - dev_rows) * ADAM_TAB * sizeof(float), hipMemcpyHostToDevice, st));
+        dev_rows = need;
+    }
     HIPCHK(hipMemcpyAsync(d_step, &h_step, sizeof(int), hipMemcpyHostToDevice, st));
     HIPCHK(hipStreamSynchronize(st));  // pageable sources
 }
@@ -2191,28 +2220,41 @@ int32_t suta_forward(suta_engine* e, const float* wav, int32_t on_dev, int32_t n
     });
 }
 
-int32_t suta_step(suta_engine* e, const float* wav, int32_t on_dev, int32_t norm, int32_t batch, int64_t n,
-                  const suta_hparams* hp, float* logits_out, float* loss_out) {
+int32_t suta_step_ex(suta_engine* e, const float* wav, int32_t on_dev, int32_t norm, int32_t batch, int64_t n,
+                     const suta_hparams* hp, int32_t repeat_inference, float* logits_out, int32_t logits_on_dev,
+                     float* loss_out) {
     return guard([&] {
         check_batch(e, batch, n);
+        if (!logits_out) throw SutaError(SUTA_ERR_ARG, "logits_out is null");
         HIPCHK(hipSetDevice(e->device));
         suta_latch_switches();
         e->build_plan(batch, n);
         e->set_lengths(batch, nullptr);
         e->stage_input(wav, on_dev, norm, batch, n);
         e->prepare_adam(*hp, 1);
+        const size_t lbytes = (size_t)batch * e->plan.T * e->c.V * 4;
+        const hipMemcpyKind lk = logits_on_dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
         e->forward(batch);
+        // repeat_inference == False (main.py:212-215): the caller gets the grad forward's logits, taken before the
+        // backward reuses any buffer
+        if (!repeat_inference) HIPCHK(hipMemcpyAsync(logits_out, e->plan.logits, lbytes, lk, e->st));
         e->backward(batch, *hp);
         e->adam(batch, *hp);
-        e->forward(batch);
+        if (repeat_inference) {
+            e->forward(batch);
+            HIPCHK(hipMemcpyAsync(logits_out, e->plan.logits, lbytes, lk, e->st));
+        }
         if (loss_out)
             HIPCHK(hipMemcpyAsync(loss_out, e->plan.loss, (size_t)batch * 4, hipMemcpyDeviceToHost, e->st));
-        HIPCHK(hipMemcpyAsync(logits_out, e->plan.logits, (size_t)batch * e->plan.T * e->c.V * 4, hipMemcpyDeviceToHost,
-                              e->st));
         HIPCHK(hipStreamSynchronize(e->st));
         if (e->timing) e->collect_timing();
         e->check_sdpl();
     });
+}
+
+int32_t suta_step(suta_engine* e, const float* wav, int32_t on_dev, int32_t norm, int32_t batch, int64_t n,
+                  const suta_hparams* hp, float* logits_out, float* loss_out) {
+    return suta_step_ex(e, wav, on_dev, norm, batch, n, hp, 1, logits_out, 0, loss_out);
 }
 
 }  // extern "C"

@@ -24,7 +24,7 @@ import os
 import re
 import wave as _wave
 from pathlib import Path
-from typing import Iterator, List, Sequence, Tuple
+from typing import Iterator, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -164,13 +164,22 @@ def _say(*a):
         print(*a)
 
 
-def create_dataset(split, name, path, batch_size=1):
-    """data.py:48-68."""
+def create_dataset(split, name, path, batch_size=1, chime_subsets: Optional[Sequence[str]] = None):
+    """data.py:48-68.  chime_subsets: the CHiME et05 subsets to read (None = the reference's hard-coded 7,
+    corpus/CHiME.py:27; config C3 "eval-real" = the three *_real ones); refused for other corpora."""
     n = name.lower()
     table = {"librispeech": LibriDataset, "chime": CHiMEDataset, "ted": TedDataset, "commonvoice": CVDataset}
     if n not in table:
         raise NotImplementedError(name)
-    ds = table[n](split, batch_size, path)
+    if chime_subsets:
+        if n != "chime":
+            raise ValueError(f"chime_subsets given for dataset {name!r}")
+        bad = [s for s in chime_subsets if s not in CHiMEDataset.SUBSETS]
+        if bad:
+            raise ValueError(f"unknown CHiME subset(s) {bad}: the reference reads {CHiMEDataset.SUBSETS}")
+        ds = CHiMEDataset(split, batch_size, path, subsets=list(chime_subsets))
+    else:
+        ds = table[n](split, batch_size, path)
     _say(f"[INFO]    There are {len(ds)} samples.")
     return ds, batch_size
 
@@ -486,10 +495,10 @@ def collect_audio_batch(batch, reader: AudioReader, decoded=None, indices=None, 
     return lens, wavs, texts, files
 
 
-def load_dataset(split=None, name="librispeech", path=None, batch_size=1, extra_noise=0.0, num_workers=0
-                 ) -> Iterator:
+def load_dataset(split=None, name="librispeech", path=None, batch_size=1, extra_noise=0.0, num_workers=0,
+                 chime_subsets: Optional[Sequence[str]] = None) -> Iterator:
     """data.py:71-78 as a plain iterator (batches of `batch_size` consecutive items)."""
-    ds, bs = create_dataset(split, name, path, batch_size)
+    ds, bs = create_dataset(split, name, path, batch_size, chime_subsets)
     reader = AudioReader(extra_noise)
 
     class _Loader:

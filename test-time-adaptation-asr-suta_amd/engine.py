@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("SUTA_LIB") or os.path.join(os.path.dirname(os.path.ab
 MAX_CONV = 8
 
 # exported symbols (kept in sync with include/suta.h; tests/test_abi.py checks both)
-EXPORTS = ("suta_create", "suta_destroy", "suta_reset", "suta_num_frames", "suta_forward", "suta_step",
+EXPORTS = ("suta_create", "suta_destroy", "suta_reset", "suta_num_frames", "suta_forward", "suta_step", "suta_step_ex",
            "suta_adapt", "suta_adapt_varlen", "suta_loss_grad", "suta_get_param", "suta_param_info", "suta_sync", "suta_stream", "suta_set_timing",
            "suta_get_timing", "suta_get_timing_ex", "suta_set_precision", "suta_set_graphs", "suta_set_census",
            "suta_get_census", "suta_get_graph_stats", "suta_last_error")
@@ -69,6 +69,9 @@ class SutaHParams:
             raise ValueError(f"optimizer {self.optimizer!r}: the engine implements {sorted(OPTIMIZERS)}")
         if self.optimizer == "Adam" and self.weight_decay != 0:
             raise ValueError("Adam with weight decay (L2 in the gradient) is not AdamW; the reference passes 0")
+        if self.optimizer == "SGD" and self.weight_decay != 0:
+            raise ValueError("SGD with weight decay (wd * p added to the gradient) is not implemented; the reference "
+                             "passes 0 (main.py:18)")
         return HParamsC(self.lr, self.temp, self.em_coef, self.div_coef, self.betas[0], self.betas[1], self.eps,
                         self.weight_decay, int(self.reweight), int(self.non_blank), int(self.train_feature),
                         int(self.bias_only), int(self.episodic), float(self.pl_coef), OPTIMIZERS[self.optimizer],
@@ -96,6 +99,8 @@ def load_library(path: str = LIB_PATH):
     lib.suta_forward.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int64, C.c_void_p]
     lib.suta_step.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int64, P(HParamsC),
                               C.c_void_p, C.c_void_p]
+    lib.suta_step_ex.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int64, P(HParamsC),
+                                 C.c_int32, C.c_void_p, C.c_int32, C.c_void_p]
     lib.suta_adapt.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int64, C.c_int32,
                                P(HParamsC), i32p, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p, i64p]
     lib.suta_loss_grad.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int64, P(HParamsC), C.c_void_p,
@@ -228,6 +233,22 @@ class SutaEngine:
         loss = np.empty((B,), np.float32)
         _check(self.lib.suta_step(self.handle, p, dev, int(normalize), B, N, C.byref(hp.to_c()), _ptr(out),
                                   _ptr(loss)))
+        return out, loss
+
+    def step_ex(self, wav, hp: SutaHParams, repeat_inference: bool = True, normalize: bool = False,
+                logits_device_ptr: Optional[int] = None):
+        """suta_step_ex: one forward_and_adapt step; returns (logits (B,T,V) numpy or None when written to
+        `logits_device_ptr`, loss (B,)).  repeat_inference=False returns the grad forward's logits."""
+        p, dev, B, N, keep = self._wav(wav)
+        T = self.num_frames(N)
+        loss = np.empty((B,), np.float32)
+        if logits_device_ptr is not None:
+            out, lp, ldev = None, C.c_void_p(logits_device_ptr), 1
+        else:
+            out = np.empty((B, T, self.V), np.float32)
+            lp, ldev = _ptr(out), 0
+        _check(self.lib.suta_step_ex(self.handle, p, dev, int(normalize), B, N, C.byref(hp.to_c()),
+                                     int(bool(repeat_inference)), lp, ldev, _ptr(loss)))
         return out, loss
 
     def adapt(self, wav, steps: int, hp: SutaHParams, record: Sequence[int] = (), normalize: bool = False,

@@ -80,6 +80,10 @@ def build_parser(sdpl: bool = False):
                    help="torch.distributed backend under torchrun (auto: nccl = RCCL when a GPU is visible)")
     p.add_argument("--num_workers", type=int, default=4,
                    help="audio decode threads (FLAC/WAV decode + resample ahead of the engine)")
+    p.add_argument("--chime_subsets", default=None,
+                   help="--dataset_name chime: comma-separated et05 subsets (default: the reference's 7 of "
+                        "corpus/CHiME.py:27, real and simu); config C3 'eval-real' = "
+                        "et05_bus_real,et05_caf_real,et05_str_real")
     p.add_argument("--precision", default="fp32", choices=["fp32", "fp32-split-bf16", "bf16"],
                    help="GEMM arithmetic (fp32 = the reference's; bf16 = BASELINE config C4)")
     return p
@@ -228,7 +232,9 @@ def main(argv=None, sdpl: bool = False):
     if sdpl:
         from .decode import VOCAB
         say({t: i for i, t in enumerate(VOCAB)})  # main_SDPL.py:269-271 prints vocab.json
-    dataset = load_dataset(a.split, a.dataset_name, a.dataset_dir, a.batch_size, a.extra_noise)
+    subsets = [x for x in a.chime_subsets.split(",") if x] if a.chime_subsets else None
+    dataset = load_dataset(a.split, a.dataset_name, a.dataset_dir, a.batch_size, a.extra_noise,
+                           chime_subsets=subsets)
     say("------------------------------------")
     say(f"exp: {exp_name}")
     tail = ((f"pl_coef = {a.pl_coef}",) if sdpl else (f"train_all = {a.train_all}", f"train_LN = {True}"))

@@ -7,6 +7,7 @@ sharing device 0, the real engine) is tests/test_gpu_bench_dist.py.  Reference: 
 the sharding is the build's own."""
 import json
 import multiprocessing as mp
+import os
 
 import numpy as np
 import pytest
@@ -18,9 +19,9 @@ ARGV = ["--gpus", "2", "--dist-backend", "gloo", "--model", "tiny-group", "--bat
         "--no-c5", "--no-batch64", "--no-split"]
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_bench_two_ranks_shard_time_and_print(tmp_path, world):
-    """World sizes 2 and 4 (the driver's SCALE run launches 1 / 2 / 4 / 8 ranks; 8 processes are not started here)."""
+    """World sizes 2, 4 and 8 (the driver's SCALE run launches 1 / 2 / 4 / 8 ranks)."""
     from tests import _bench_dist_worker as W
     from suta_amd import synth
     port = free_port()
@@ -45,6 +46,7 @@ def test_bench_two_ranks_shard_time_and_print(tmp_path, world):
     B, steps, warmup = 3, 3, 1
     nb = steps + warmup
     assert out["n_gpus"] == world and out["scaling"] == "weak" and out["dist"]["backend"] == "gloo"
+    assert out["dist"]["world_seen"] == world and out["dist"]["rccl_measured"] is False
     # value = utterances of all ranks / max elapsed over ranks
     el = out["dist"]["rank_elapsed_s"]
     # the closing barrier holds every rank until the slowest has finished: rank 1's stand-in sleeps 0.1 s per call
@@ -59,6 +61,46 @@ def test_bench_two_ranks_shard_time_and_print(tmp_path, world):
         np.testing.assert_array_equal(np.array(res[r]["seen"], np.float32), np.array(want, np.float32))
     for r in range(1, world):
         assert not set(res[0]["seen"]) & set(res[r]["seen"])
+
+
+def _selflaunch(tmp_path, world, extra_env=None):
+    import subprocess
+    import sys
+    from tests.multirank import REPO
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR",
+                                                             "MASTER_PORT", "LOCAL_WORLD_SIZE")}
+    env.update(BENCH_SEEN_DIR=str(tmp_path), **(extra_env or {}))
+    argv = list(ARGV)
+    argv[argv.index("--gpus") + 1] = str(world)
+    return subprocess.run([sys.executable, os.path.join(REPO, "tests", "_bench_selflaunch_worker.py")] + argv,
+                          env=env, capture_output=True, text=True, timeout=300)
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_bench_self_launches_ranks_without_torchrun_env(tmp_path, world):
+    """`python bench.py --gpus N` with no torchrun environment (the plain form of the driver's BENCH command) starts
+    the N ranks itself (bench.self_launch): one JSON line from rank 0 with n_gpus = world_seen = N, every rank
+    adapting its own shard."""
+    from suta_amd import synth
+    p = _selflaunch(tmp_path, world)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == world and out["dist"]["world_seen"] == world and out["dist"]["backend"] == "gloo"
+    B, nb = 3, 4
+    for r in range(world):
+        seen = json.load(open(tmp_path / f"seen{r}.json"))
+        want = [float(synth.wave(4000, i)[0]) for i in range(r * nb * B, (r + 1) * nb * B)]
+        np.testing.assert_array_equal(np.array(seen, np.float32), np.array(want, np.float32))
+
+
+def test_bench_self_launch_stops_ranks_when_one_fails(tmp_path):
+    """A rank that dies leaves the others waiting for it in the rendezvous / a barrier: the launcher terminates them
+    and returns the failing rank's status."""
+    p = _selflaunch(tmp_path, 2, {"BENCH_FAIL_RANK": "1"})
+    assert p.returncode == 3, (p.returncode, p.stderr[-2000:])
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
 
 
 def test_driver_defaults_run_the_bench_layout():

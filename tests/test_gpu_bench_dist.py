@@ -46,3 +46,23 @@ def test_bench_two_gloo_ranks_on_one_gpu():
     nb = steps + warmup
     assert out["dist"]["utterance_shards"] == [[(r * nb + warmup) * B, (r * nb + nb) * B] for r in range(world)]
     assert out["roofline"]["frac"] > 0 and out["attention"]["tflops"] > 0
+
+
+def test_bench_self_launch_two_gloo_ranks_on_one_gpu():
+    """The plain `python bench.py --gpus 2` form with no torchrun environment: bench.py starts the two rank
+    processes itself (bench.self_launch) before touching the GPU; rank 0 prints the one JSON line with the live
+    process group's size."""
+    B, steps, warmup = 4, 2, 1
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR",
+                                                             "MASTER_PORT", "LOCAL_WORLD_SIZE")}
+    argv = [sys.executable, "-u", os.path.join(REPO, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+            "--batch", str(B), "--n-samples", "32000", "--steps", str(steps), "--warmup", str(warmup),
+            "--no-cpu-baseline", "--no-c4", "--no-c5", "--no-split", "--no-batch64", "--no-timing"]
+    p = subprocess.run(argv, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, f"{p.stdout[-2000:]}\n{p.stderr[-3000:]}"
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["dist"]["world_seen"] == 2 and out["dist"]["backend"] == "gloo"
+    el = out["dist"]["rank_elapsed_s"]
+    assert out["value"] == pytest.approx(B * steps * 2 / max(el), rel=1e-3)

@@ -71,6 +71,35 @@ def test_chime_loader_order_and_texts(tmp_path):
         assert texts[f.stem] == t
 
 
+def test_chime_subsets_flag(tmp_path):
+    """Config C3 'eval-real' (BASELINE.json): --chime_subsets restricts the reference's hard-coded 7 et05 subsets
+    (corpus/CHiME.py:27); the default is exactly that list."""
+    assert D.CHiMEDataset.SUBSETS == ["et05_bus_real", "et05_bus_simu", "et05_caf_real", "et05_caf_simu",
+                                      "et05_ped_simu", "et05_str_real", "et05_str_simu"]
+    assert build_parser().parse_args([]).chime_subsets is None
+    apath = tmp_path / "data/audio/16kHz/enhanced"
+    tpath = tmp_path / "data/transcriptions"
+    rng = np.random.default_rng(5)
+    for sub in D.CHiMEDataset.SUBSETS:
+        (apath / sub).mkdir(parents=True)
+        (tpath / sub).mkdir(parents=True)
+        name = f"F01_{sub[5:8].upper()}_{sub[-4:]}"
+        _write_wav(apath / sub / f"{name}.wav", rng.standard_normal(1600) * 0.1)
+        (tpath / sub / f"{name}.trn").write_text(f"{name} A WORD\n")
+    everything, _ = D.create_dataset(None, "chime", str(tmp_path), 1)
+    assert len(everything) == 7
+    real = "et05_bus_real,et05_caf_real,et05_str_real"
+    a = build_parser().parse_args(["--dataset_name", "chime", "--chime_subsets", real])
+    ds, _ = D.create_dataset(None, "chime", str(tmp_path), 1, a.chime_subsets.split(","))
+    assert sorted(f.parent.name for f in ds.file_list) == real.split(",")
+    ld = D.load_dataset(None, "chime", str(tmp_path), 1, 0.0, chime_subsets=["et05_ped_simu"])
+    assert [os.path.basename(os.path.dirname(str(it[0][0]))) for it in ld.raw_batches()] == ["et05_ped_simu"]
+    with pytest.raises(ValueError):
+        D.create_dataset(None, "chime", str(tmp_path), 1, ["et05_ped_real"])     # not a reference subset
+    with pytest.raises(ValueError):
+        D.create_dataset(None, "librispeech", str(tmp_path), 1, ["et05_bus_real"])
+
+
 def test_audio_reader_truncates_and_noise_is_deterministic(tmp_path):
     x = np.random.default_rng(1).standard_normal(700000) * 0.05
     _write_wav(tmp_path / "a.wav", x)
