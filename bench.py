@@ -64,7 +64,7 @@ GEMM_KERNELS = ("gemm_glds_kernel", "gemm_f32_kernel", "gemm_splitk_reduce", "at
                 "posconv_kernel", "flash_fwd_kernel", "flash_bwd_kernel", "flash_dq_reduce")
 # config C4's GEMM family (bf16 mode): every kernel its "gemm" + "attention" timing families launch.  Matched to the
 # PMC table by base name (pmc_kernel_bytes: the trace may hold mangled names).
-GEMM_KERNELS_C4 = ("gemm_hb_kernel", "gemm_hb8_kernel", "gemm_hbx_kernel", "gemm_hbp_kernel", "gemm_hbt_kernel",
+GEMM_KERNELS_C4 = ("gemm_hb_kernel", "gemm_hbx_kernel", "gemm_hbp_kernel", "gemm_hbt_kernel",
                    "gemm_x6_kernel", "gemm_gbf_kernel",
                    "gemm_splitk_reduce", "to_bf16_kernel", "posconv_bf16_kernel", "flash_fwd_bf16p_kernel",
                    "flash_bwd_bf16p_kernel", "flash_fwd_bf16_kernel", "flash_bwd_bf16_kernel", "flash_dq_reduce")

@@ -370,235 +370,6 @@ __global__ __launch_bounds__(NW * 64) void flash_fwd_kernel(const float* __restr
 }
 
 
-// Software-pipelined exact-fp32 forward (the headline's; SUTA_FLASH_FWD_PIPE, default): iteration kt issues the S^T
-// MFMAs of key tile kt + 1 and then runs the softmax of tile kt (VALU) and its PV MFMAs.  The next tile's S chain does
-// not depend on this tile's softmax, so the wave keeps its MFMA pipe fed through its own softmax instead of waiting on
-// its S chain and then leaving the pipe idle during the exp / max / sum work.  K therefore runs one tile ahead of V
-// in LDS (still two buffers each: iteration kt reads K(kt + 1) and V(kt) and writes K(kt + 2) and V(kt + 1) into the
-// buffers iteration kt - 1 read, one barrier per iteration).  Per element the same operations as flash_fwd_kernel in
-// the same order (S chains, masks on the utterance's last tile only, online softmax, PV), so ctx and LSE are bitwise
-// equal; the three loop bodies (full next tile, next tile the last one, no next tile) are separate instantiations so
-// each is one basic block the scheduler can interleave.
-template <int NW>
-__global__ __launch_bounds__(NW * 64) void flash_fwd_pipe_kernel(const float* __restrict__ qkv, float* __restrict__ ctx,
-                                                                 float* __restrict__ lse, int T, int NH, int H,
-                                                                 float scale, const int* __restrict__ tlen, int nqb,
-                                                                 __bf16* __restrict__ ctxb) {
-    constexpr int NT = NW * 64;
-    constexpr int ITEMS = FK * 16, NPT = (ITEMS + NT - 1) / NT;
-    __shared__ __attribute__((aligned(16))) float Ks[2][FK * FA_LD];
-    __shared__ __attribute__((aligned(16))) float Vt[2][64 * FK_LDT];
-    const int id = xcd_block();
-    const int qb = id % nqb, bh = id / nqb, hd = bh % NH, u = bh / NH;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, l32 = lane & 31,
-              h = lane >> 5;
-    const int tl = tlen ? tlen[u] : T;
-    const long ld = 3L * H;
-    const float* Qb = qkv + (long)u * T * ld + hd * 64;
-    const float* Kb = Qb + H;
-    const float* Vb = Qb + 2 * H;
-    const int q0 = (qb * NW + w) * 32;
-    if (tl <= 0) {
-        flash_fwd_no_keys(ctx, ctxb, lse, (long)u * T, (long)bh * T, T, H, hd, q0, l32, h);
-        return;
-    }
-    const bool active = q0 < T;
-    const float sl2 = scale * LOG2E;
-    RowReg<false> qv;
-    qv.load(Qb + (long)min(q0 + l32, T - 1) * ld, h);
-    auto vmap = [](int it, int& key, int& c4) {
-        const int l = it & 63, wi = it >> 6;
-        key = (l & 15) + 16 * (wi & 3);
-        c4 = 4 * ((l >> 4) + 4 * (wi >> 2));
-    };
-    f32x4 kr[NPT], vr[NPT];
-    auto fetch_k = [&](int kt) {
-#pragma unroll
-        for (int n = 0; n < NPT; ++n) {
-            const int it = threadIdx.x + n * NT, row = it >> 4, c4 = (it & 15) * 4, key = kt * FK + row;
-            kr[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (it < ITEMS && key < T) kr[n] = *reinterpret_cast<const f32x4*>(Kb + (long)key * ld + c4);
-        }
-    };
-    auto fetch_v = [&](int kt) {
-#pragma unroll
-        for (int n = 0; n < NPT; ++n) {
-            const int it = threadIdx.x + n * NT;
-            int vk, vc;
-            vmap(it, vk, vc);
-            vr[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (it < ITEMS && kt * FK + vk < T) vr[n] = *reinterpret_cast<const f32x4*>(Vb + (long)(kt * FK + vk) * ld + vc);
-        }
-    };
-    auto put_k = [&](int buf) {
-#pragma unroll
-        for (int n = 0; n < NPT; ++n) {
-            const int it = threadIdx.x + n * NT, row = it >> 4, c4 = (it & 15) * 4;
-            if (it < ITEMS) *reinterpret_cast<f32x4*>(&Ks[buf][row * FA_LD + c4]) = kr[n];
-        }
-    };
-    auto put_v = [&](int buf) {
-#pragma unroll
-        for (int n = 0; n < NPT; ++n) {
-            const int it = threadIdx.x + n * NT;
-            int vk, vc;
-            vmap(it, vk, vc);
-            if (it < ITEMS) {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) Vt[buf][(vc + e) * FK_LDT + vk] = vr[n][e];
-            }
-        }
-    };
-
-    const int nkt = (tl + FK - 1) / FK;
-    f32x16 o[2];
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int v = 0; v < 16; ++v) o[t][v] = 0.f;
-    float m_run = -INFINITY, l_run = 0.f;
-    // prologue: K(0), V(0) into buffer 0, K(1) into buffer 1; S of tile 0
-    fetch_k(0);
-    fetch_v(0);
-    put_k(0);
-    put_v(0);
-    if (nkt > 1) {
-        fetch_k(1);
-        put_k(1);
-    }
-    __syncthreads();
-    f32x16 sc[2];
-    auto s_tile = [&](f32x16 (&s)[2], int kt, bool two) {  // raw scores S^T of key tile kt (key r8(v,h), query l32)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-#pragma unroll
-            for (int v = 0; v < 16; ++v) s[j][v] = 0.f;
-            if (j == 0 || two) prod_rows<false>(s[j], Ks[kt & 1] + 32 * j * FA_LD, qv, l32, h);
-        }
-    };
-    if (active) s_tile(sc, 0, nkt > 1 || 32 < tl);
-    if (nkt > 2) __syncthreads();  // K(0) read by every wave before iteration 0 writes K(2) over it
-    // NEXT: 1 = the next tile is a full one, 2 = the next tile is the utterance's last (its second half may be empty),
-    // 0 = no next tile (this one is the last)
-    auto iter = [&](int kt, auto next_tag) {
-        constexpr int NEXT = decltype(next_tag)::value;
-        constexpr bool LAST = NEXT == 0;
-        if (NEXT == 1) fetch_k(kt + 2);
-        if (NEXT != 0) fetch_v(kt + 1);
-        if (active) {
-            f32x16 sn[2];
-            if constexpr (NEXT != 0) s_tile(sn, kt + 1, NEXT == 1 || (kt + 1) * FK + 32 < tl);
-            const bool two = !LAST || kt * FK + 32 < tl;
-            float mx = -INFINITY;
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-#pragma unroll
-                for (int v = 0; v < 16; ++v) {
-                    const bool ok = !LAST || kt * FK + 32 * j + r8(v, h) < tl;
-                    sc[j][v] = ok ? sl2 * sc[j][v] : -INFINITY;
-                    mx = fmaxf(mx, sc[j][v]);
-                }
-            mx = half_swap_max(mx);
-            const float m_new = fmaxf(m_run, mx);
-            float ls = 0.f;
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-#pragma unroll
-                for (int v = 0; v < 16; ++v) {
-                    sc[j][v] = __builtin_amdgcn_exp2f(sc[j][v] - m_new);
-                    ls += sc[j][v];
-                }
-            if (m_new != m_run) {  // rescale only when the maximum moved, exactly as flash_fwd_kernel (an unconditional
-                                   // l_run * alpha + ls is fused into one fma under -ffp-contract=fast: not bitwise)
-                const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
-                l_run *= alpha;
-#pragma unroll
-                for (int t = 0; t < 2; ++t)
-#pragma unroll
-                    for (int v = 0; v < 16; ++v) o[t][v] *= alpha;
-                m_run = m_new;
-            }
-            l_run += ls;
-            apply_cols<false, FK_LDT>(o, Vt[kt & 1], sc[0], l32, h);
-            if (two) apply_cols<false, FK_LDT>(o, Vt[kt & 1] + 32, sc[1], l32, h);
-            if constexpr (NEXT != 0) {
-#pragma unroll
-                for (int j = 0; j < 2; ++j) sc[j] = sn[j];
-            }
-        }
-        if (NEXT == 1) put_k(kt & 1);
-        if (NEXT != 0) put_v((kt + 1) & 1);
-        if (!LAST) __syncthreads();
-    };
-    int kt = 0;
-    for (; kt + 2 < nkt; ++kt) iter(kt, std::integral_constant<int, 1>{});
-    if (kt + 1 < nkt) iter(kt++, std::integral_constant<int, 2>{});
-    iter(kt, std::integral_constant<int, 0>{});
-    if (!active) return;
-    const float l_tot = half_swap_sum(l_run);
-    const int q = q0 + l32;
-    if (q >= T) return;
-    const float inv = 1.0f / l_tot;
-    float* cr = ctx + ((long)u * T + q) * H + hd * 64 + 4 * h;
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int a = 0; a < 4; ++a) {
-            f32x4 r;
-#pragma unroll
-            for (int b = 0; b < 4; ++b) r[b] = o[t][4 * a + b] * inv;
-            *reinterpret_cast<f32x4*>(cr + 32 * t + 8 * a) = r;
-            if (ctxb) {
-                fbf16x4 b;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) b[e] = (__bf16)r[e];
-                *reinterpret_cast<fbf16x4*>(ctxb + ((long)u * T + q) * H + hd * 64 + 4 * h + 32 * t + 8 * a) = b;
-            }
-        }
-    if (h == 0) lse[(long)bh * T + q] = (m_run + log2f(l_tot)) * (1.0f / LOG2E);
-}
-
-// In-launch combination of a head's dQ partials (replaces the flash_dq_reduce pass when cnt is given): every key
-// block of the head publishes its partial (cdna_hip_programming.md's split-K seam protocol: stores drained, block
-// barrier, an agent-scope release, then a ticket on the head's counter); the block drawing nkb - 1 acquires and sums
-// the nkb partials in key-block order -- flash_dq_reduce's order, so dQ is bitwise the same -- into dqkv's Q columns
-// and / or their bf16 plane (rows past the utterance's length get 0, as their dS is 0).  The counters are zeroed
-// by a memset node ahead of every launch.  Every thread of the block must reach this call.
-__device__ __forceinline__ void dq_combine(const float* __restrict__ dqp, float* __restrict__ dqkv,
-                                           __bf16* __restrict__ dqkvb, int* __restrict__ cnt, int* flag, int bh,
-                                           int u, int hd, int T, int NH, int H, int nkb, int tl, int B) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int prev = __hip_atomic_fetch_add(cnt + bh, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int last = prev == nkb - 1;
-        if (last) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        *flag = last;
-    }
-    __syncthreads();
-    if (!*flag) return;
-    const long stride4 = (long)B * NH * T * 16;  // one key block's partials, in float4
-    const f32x4* pp = reinterpret_cast<const f32x4*>(dqp + (long)bh * T * 64);
-    for (int i = threadIdx.x; i < T * 16; i += blockDim.x) {
-        const int q = i >> 4, c4 = (i & 15) * 4;
-        f32x4 sum = {0.f, 0.f, 0.f, 0.f};
-        if (q < tl)
-            for (int k = 0; k < nkb; ++k) sum += pp[k * stride4 + i];
-        if (dqkv) *reinterpret_cast<f32x4*>(dqkv + ((long)u * T + q) * 3 * H + hd * 64 + c4) = sum;
-        if (dqkvb) {
-            fbf16x4 b4;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) b4[e] = (__bf16)sum[e];
-            *reinterpret_cast<fbf16x4*>(dqkvb + ((long)u * T + q) * 3 * H + hd * 64 + c4) = b4;
-        }
-    }
-}
-
 // ------------------------------------------------------------------------------------------------
 // backward
 // ------------------------------------------------------------------------------------------------
@@ -616,8 +387,7 @@ template <int NW, bool BF16>
 __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void flash_bwd_kernel(
     const float* __restrict__ qkv, const float* __restrict__ dctx, const float* __restrict__ lse,
     const float* __restrict__ delta, float* __restrict__ dqkv, float* __restrict__ dqp, int T, int NH, int H,
-    float scale, const int* __restrict__ tlen, int nkb, int gpb, int B, __bf16* __restrict__ dqkvb,
-    int* __restrict__ dq_cnt) {
+    float scale, const int* __restrict__ tlen, int nkb, int gpb, int B, __bf16* __restrict__ dqkvb) {
     constexpr int NT = NW * 64;
     constexpr int KBP = fb_kbp<NW>();
     constexpr int QPT = 512 / NT;       // float4 of a 32 x 64 tile per thread
@@ -832,7 +602,6 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void flash_bwd_kernel(
                 }
             }
     }
-    if (dq_cnt) dq_combine(dqp, dqkv, dqkvb, dq_cnt, reinterpret_cast<int*>(Ls), bh, u, hd, T, NH, H, nkb, tl, B);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1226,8 +995,7 @@ constexpr size_t fbb_lds_bytes() {
 __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16_kernel(
     const float* __restrict__ qkv, const float* __restrict__ dctx, const float* __restrict__ lse,
     const float* __restrict__ delta, float* __restrict__ dqkv, float* __restrict__ dqp, int T, int NH, int H,
-    float scale, const int* __restrict__ tlen, int nkb, int gpb, int B, __bf16* __restrict__ dqkvb,
-    int* __restrict__ dq_cnt) {
+    float scale, const int* __restrict__ tlen, int nkb, int gpb, int B, __bf16* __restrict__ dqkvb) {
     constexpr int NW = FBB_NW, NT = NW * 64;
     constexpr int QPT = 512 / NT;
     extern __shared__ __attribute__((aligned(16))) __bf16 sm16[];
@@ -1406,7 +1174,6 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16_kernel(
                 }
             }
     }
-    if (dq_cnt) dq_combine(dqp, dqkv, dqkvb, dq_cnt, reinterpret_cast<int*>(Ls), bh, u, hd, T, NH, H, nkb, tl, B);
 }
 
 // backward on bf16 operand planes (config C4 with bf16 planes): K and V rows of the wave's keys, the
@@ -1428,17 +1195,11 @@ constexpr size_t fbbp_lds_bytes() {
     return 2 * ((size_t)(64 + (ONEB ? 64 : 32)) * FBB_KB + 2 * 2 * 32 * FB_RS) + 4 * 128;
 }
 
-//
-// Chained dQ (kbl >= 0, SUTA_DQ_CHAIN): one launch per key block, kbl = 0 .. nkb - 1 in stream order, grid = one block
-// per (utterance, head).  Launch kbl adds its dQ contribution to a single fp32 accumulator per head -- launch 0 writes
-// it, later ones read-add-write it -- and the last launch writes dQ itself (rows past the utterance's length 0), so no
-// per-key-block partials and no flash_dq_reduce pass: the sums run in key-block order, as the reduce pass's.
 template <bool ONEB>
 __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
     const __bf16* __restrict__ qkvb, const __bf16* __restrict__ dob, const float* __restrict__ lse,
     const float* __restrict__ delta, float* __restrict__ dqkv, float* __restrict__ dqp, int T, int NH, int H,
-    float scale, const int* __restrict__ tlen, int nkb, int gpb, int B, __bf16* __restrict__ dqkvb,
-    int* __restrict__ dq_cnt, int kbl) {
+    float scale, const int* __restrict__ tlen, int nkb, int gpb, int B, __bf16* __restrict__ dqkvb) {
     constexpr int NW = FBB_NW, NT = NW * 64;
     constexpr int NSS = ONEB ? 2 : 1;             // dS images
     extern __shared__ __attribute__((aligned(16))) __bf16 sm16[];
@@ -1449,8 +1210,7 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
     float* Ls = reinterpret_cast<float*>(Dr + 2 * 32 * FB_RS);  // [2][32]
     float* Dl = Ls + 64;                          // [2][32]
     const int id = xcd_block();
-    const bool chain = kbl >= 0;
-    const int kb = chain ? kbl : id % nkb, bh = chain ? id : id / nkb, hd = bh % NH, u = bh / NH;
+    const int kb = id % nkb, bh = id / nkb, hd = bh % NH, u = bh / NH;
     // the wave index as a scalar: every per-wave condition below (active, kall) is then a scalar branch
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, l32 = lane & 31,
               h = lane >> 5;
@@ -1516,8 +1276,7 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
     const int qi = w & 1, di = w >> 1;
     const int kq = ngb * 32;
     const long dq_stride = (long)B * NH * T * 64;
-    float* dqb = dqp + (chain ? 0 : kb * dq_stride) + (long)bh * T * 64;
-    const bool dq_last = chain && kb + 1 == nkb;  // this launch writes dQ itself
+    float* dqb = dqp + kb * dq_stride + (long)bh * T * 64;
     const int nqt = (tl + 31) >> 5;
     if (!active && w < ngb)
         for (int r = 0; r < NSS * 32; ++r)
@@ -1599,26 +1358,9 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
                         *reinterpret_cast<const fbf16x8*>(kfrow + 32 * j), c[j & 1], 0, 0, 0);
             const f32x4 c0 = c[0], c1 = c[1];
             float* dr = dqb + (long)(q0 + 16 * qi + 4 * g) * 64 + 16 * di + l16;
-            if (!chain) {
 #pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    if (q0 + 16 * qi + 4 * g + r < T) dr[r * 64] = c0[r] + c1[r];
-            } else if (!dq_last) {  // the head's accumulator: written by key block 0, read-add-written by later ones
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    if (q0 + 16 * qi + 4 * g + r < T) dr[r * 64] = kb == 0 ? c0[r] + c1[r] : dr[r * 64] + (c0[r] + c1[r]);
-            } else {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int q = q0 + 16 * qi + 4 * g + r;
-                    if (q < T) {
-                        const float v = q < tl ? (kb == 0 ? c0[r] + c1[r] : dr[r * 64] + (c0[r] + c1[r])) : 0.f;
-                        const long o = ((long)u * T + q) * ld + hd * 64 + 16 * di + l16;
-                        if (dqkv) dqkv[o] = v;
-                        if (dqkvb) dqkvb[o] = (__bf16)v;
-                    }
-                }
-            }
+            for (int r = 0; r < 4; ++r)
+                if (q0 + 16 * qi + 4 * g + r < T) dr[r * 64] = c0[r] + c1[r];
         }
         if constexpr (!ONEB) {
             if (qt + 1 < nqt) put(buf ^ 1, py);
@@ -1657,255 +1399,6 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
                 }
             }
     }
-    if (dq_last) {  // query rows of tiles past the utterance's length (never computed): dQ = 0
-        for (int i = nqt * 32 * 64 + threadIdx.x; i < T * 64; i += NT) {
-            const long o = ((long)u * T + (i >> 6)) * ld + hd * 64 + (i & 63);
-            if (dqkv) dqkv[o] = 0.f;
-            if (dqkvb) dqkvb[o] = (__bf16)0.f;
-        }
-    }
-    if constexpr (ONEB) {
-        if (dq_cnt) __syncthreads();  // (dq_combine's ticket scratch aliases Ls, still read by the last tile's waves)
-    }
-    if (dq_cnt) dq_combine(dqp, dqkv, dqkvb, dq_cnt, reinterpret_cast<int*>(Ls), bh, u, hd, T, NH, H, nkb, tl, B);
-}
-
-// Software-pipelined form of flash_bwd_bf16p_kernel (SUTA_FLASH_BWD_PIPE, default): iteration qt issues the S and dP
-// MFMAs of query tile qt + 1 first and then runs tile qt's softmax / dS (VALU), its dV^T / dK^T MFMAs and the dS
-// store, so a wave's MFMA pipe works through its own softmax instead of idling on it (the unpipelined tile ran S/dP,
-// waited on them, did the VALU work, then the second MFMA group: MFMA busy 0.17).  Three Q / dO row images (tile
-// qt + 1 must be resident while tile qt is consumed; tile qt + 2 is written after tile qt's dQ into the image tile
-// qt - 1 left), one register stage for the copy (issued a whole iteration ahead).  Per element the same operations in
-// the same order as flash_bwd_bf16p_kernel -- S / dP chains, exponent, masks, dS, the dV / dK / dQ MFMA orders -- so
-// dQ / dK / dV are bitwise equal.  Loop bodies are instantiated per (next tile exists, wave's keys masked) so each is
-// one basic block the scheduler can interleave; the tile past T (the layout's last) masks its rows in the peeled body.
-// LDS: K^T image, dS tile, 3 x (Q, dO) row images, the block's K and V rows (row-major: the S / dP products read the
-// wave's key rows from here instead of holding them in 32 VGPRs), LSE / delta
-constexpr size_t fbbpp_lds_bytes() {
-    return 2 * ((size_t)(64 + 32) * FBB_KB + 3 * 2 * 32 * FB_RS + 2 * FBB_NW * 32 * FB_RS) + 6 * 128;
-}
-
-__global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16pp_kernel(
-    const __bf16* __restrict__ qkvb, const __bf16* __restrict__ dob, const float* __restrict__ lse,
-    const float* __restrict__ delta, float* __restrict__ dqkv, float* __restrict__ dqp, int T, int NH, int H,
-    float scale, const int* __restrict__ tlen, int nkb, int gpb, int B, __bf16* __restrict__ dqkvb,
-    int* __restrict__ dq_cnt) {
-    constexpr int NW = FBB_NW, NT = NW * 64;
-    extern __shared__ __attribute__((aligned(16))) __bf16 sm16[];
-    __bf16* Kt = sm16;                            // [64][FBB_KB]   K^T of the block's keys
-    __bf16* Ss = Kt + 64 * FBB_KB;                // [32][FBB_KB]   dS of the query tile
-    __bf16* Qr = Ss + 32 * FBB_KB;                // [3][32][FB_RS] Q rows
-    __bf16* Dr = Qr + 3 * 32 * FB_RS;             // [3][32][FB_RS] dO rows
-    __bf16* Kr = Dr + 3 * 32 * FB_RS;             // [NW * 32][FB_RS] K rows of the block's keys
-    __bf16* Vr = Kr + NW * 32 * FB_RS;            // [NW * 32][FB_RS] V rows
-    float* Ls = reinterpret_cast<float*>(Vr + NW * 32 * FB_RS);  // [3][32]
-    float* Dl = Ls + 96;                          // [3][32]
-    const int id = xcd_block();
-    const int kb = id % nkb, bh = id / nkb, hd = bh % NH, u = bh / NH;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, l32 = lane & 31,
-              h = lane >> 5;
-    const int tl = tlen ? tlen[u] : T;
-    const int ng = (T + 31) >> 5;
-    const int g0 = kb * gpb, ngb = min(gpb, ng - g0);
-    const int kbase = g0 * 32;
-    const long ld = 3L * H;
-    const __bf16* Qb = qkvb + (long)u * T * ld + hd * 64;
-    const __bf16* Kb = Qb + H;
-    const __bf16* Vb = Qb + 2 * H;
-    const __bf16* Ob = dob + (long)u * T * H + hd * 64;
-    const float* lb = lse + (long)bh * T;
-    const float* db = delta + (long)bh * T;
-    const bool active = w < ngb && kbase + 32 * w < tl;
-    const bool kall = kbase + 32 * w + 32 <= tl;
-    const int key = kbase + 32 * w + l32;
-    const float sl2 = scale * LOG2E;
-    for (int it = threadIdx.x; it < ngb * 32 * 8; it += NT) {  // K^T, K rows, V rows of the block's keys (0 past T)
-        const int row = it >> 3, c8 = (it & 7) * 8, k = kbase + row;
-        fbf16x8 x = {}, y = {};
-        if (k < T) {
-            x = *reinterpret_cast<const fbf16x8*>(Kb + (long)k * ld + c8);
-            y = *reinterpret_cast<const fbf16x8*>(Vb + (long)k * ld + c8);
-        }
-#pragma unroll
-        for (int e = 0; e < 8; ++e) Kt[(c8 + e) * FBB_KB + row] = x[e];
-        *reinterpret_cast<fbf16x8*>(Kr + row * FB_RS + c8) = x;
-        *reinterpret_cast<fbf16x8*>(Vr + row * FB_RS + c8) = y;
-    }
-    // the wave's key row (the B operand of S = Q K^T and dP = dO V^T): key min(key, T - 1) as the register form
-    // read it -- rows past T hold zeros here, but those keys are masked (s = 0) and their dK / dV never stored
-    const __bf16* krow = Kr + (32 * w + l32) * FB_RS + 8 * h;
-    const __bf16* vrow = Vr + (32 * w + l32) * FB_RS + 8 * h;
-    const bool isq = threadIdx.x < 256;
-    const int crow = (threadIdx.x & 255) >> 3, ccol = (threadIdx.x & 7) * 8;
-    fbf16x8 sx;  // the one register stage of the query-tile copy
-    float slr;
-    auto fetch = [&](int qt) {
-        const int q = qt * 32 + crow;
-        sx = fbf16x8{};
-        if (q < T) sx = *reinterpret_cast<const fbf16x8*>(isq ? Qb + (long)q * ld + ccol : Ob + (long)q * H + ccol);
-        slr = 0.f;
-        const int qq = qt * 32 + (threadIdx.x & 31);
-        if (threadIdx.x < 64 && qq < T) slr = threadIdx.x < 32 ? lb[qq] : db[qq];
-    };
-    auto put = [&](int buf) {
-        *reinterpret_cast<fbf16x8*>((isq ? Qr : Dr) + (buf * 32 + crow) * FB_RS + ccol) = sx;
-        if (threadIdx.x < 32) Ls[buf * 32 + threadIdx.x] = slr;
-        else if (threadIdx.x < 64) Dl[buf * 32 + threadIdx.x - 32] = slr;
-    };
-    f32x16 dv[2], dk[2];
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int v = 0; v < 16; ++v) dv[t][v] = dk[t][v] = 0.f;
-    const int g = lane >> 4, l16 = lane & 15;
-    const int qi = w & 1, di = w >> 1;
-    const int kq = ngb * 32;
-    const long dq_stride = (long)B * NH * T * 64;
-    float* dqb = dqp + kb * dq_stride + (long)bh * T * 64;
-    const int nqt = (tl + 31) >> 5;
-    if (!active && w < ngb)
-        for (int r = 0; r < 32; ++r)
-            if (h == 0) Ss[r * FBB_KB + 32 * w + l32] = (__bf16)0.f;
-    // prologue: tiles 0 and 1 resident, tile 2 in registers, S / dP of tile 0
-    fetch(0);
-    put(0);
-    if (nqt > 1) {
-        fetch(1);
-        put(1);
-    }
-    __syncthreads();
-    if (nqt > 2) fetch(2);
-    const __bf16* kfrow = Kt + (16 * di + l16) * FBB_KB + 8 * g;
-    __bf16* const srow = Ss + 32 * w + l32;
-    // S = Q K^T of a tile (issued one tile ahead) and dP = dO V^T of the current one: prod_rows_b's k order
-    f32x16 s;
-    auto s_of = [&](f32x16& s_, int buf) {
-#pragma unroll
-        for (int v = 0; v < 16; ++v) s_[v] = 0.f;
-        const __bf16* qr = Qr + (buf * 32 + l32) * FB_RS + 8 * h;
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-            s_ = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const fbf16x8*>(qr + 16 * c),
-                                                         *reinterpret_cast<const fbf16x8*>(krow + 16 * c), s_, 0, 0, 0);
-    };
-    auto dp_of = [&](f32x16& dp_, int buf) {
-#pragma unroll
-        for (int v = 0; v < 16; ++v) dp_[v] = 0.f;
-        const __bf16* dr = Dr + (buf * 32 + l32) * FB_RS + 8 * h;
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-            dp_ = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const fbf16x8*>(dr + 16 * c),
-                                                          *reinterpret_cast<const fbf16x8*>(vrow + 16 * c), dp_, 0, 0, 0);
-    };
-    if (active) s_of(s, 0);
-    // one tile: NEXT = tile qt + 1 exists (its S issued first, under this tile's exponentials), MASKK = this wave's keys reach past the length,
-    // MASKQ = this tile reaches past T (the layout's last tile)
-    auto tile = [&](int qt, auto next_tag, auto maskk_tag, auto maskq_tag) {
-        constexpr bool NEXT = decltype(next_tag)::value, MASKK = decltype(maskk_tag)::value,
-                       MASKQ = decltype(maskq_tag)::value;
-        const int q0 = qt * 32, buf = qt % 3;
-        if (active) {
-            f32x16 sn, dp;
-            if constexpr (NEXT) s_of(sn, (qt + 1) % 3);
-            dp_of(dp, buf);
-            const __bf16* Qt = Qr + buf * 32 * FB_RS;
-            const __bf16* Dt = Dr + buf * 32 * FB_RS;
-            const float* Lt = Ls + buf * 32;
-            const float* Dlt = Dl + buf * 32;
-            // LSE / delta of the lane's rows r8(v, h), one run of 4 rows at a time (registers: the next tile's S / dP
-            // accumulators are live here)
-            const bool kok = key < tl;
-#pragma unroll
-            for (int a = 0; a < 4; ++a) {
-                const f32x4 lq = *reinterpret_cast<const f32x4*>(Lt + 8 * a + 4 * h);
-                const f32x4 dq = *reinterpret_cast<const f32x4*>(Dlt + 8 * a + 4 * h);
-#pragma unroll
-                for (int b2 = 0; b2 < 4; ++b2) {
-                    const int v = 4 * a + b2;
-                    float p = __builtin_amdgcn_exp2f(fmaf(s[v], sl2, -LOG2E * lq[b2]));
-                    if constexpr (MASKK || MASKQ) {
-                        if (!(kok && q0 + r8(v, h) < T)) p = 0.f;
-                    }
-                    s[v] = p;
-                    dp[v] = scale * (p * (dp[v] - dq[b2]));
-                }
-            }
-            fbf16x8 pb[2], sb[2];
-#pragma unroll
-            for (int v = 0; v < 16; ++v) {
-                pb[v >> 3][v & 7] = (__bf16)s[v];
-                sb[v >> 3][v & 7] = (__bf16)dp[v];
-            }
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                pv_tr<FB_RS>(dv, Dt, 16 * c, pb[c], lane);  // dV^T += dO^T P
-                pv_tr<FB_RS>(dk, Qt, 16 * c, sb[c], lane);  // dK^T += Q^T dS
-            }
-#pragma unroll
-            for (int v = 0; v < 16; v += 2) {
-                srow[r8(v, h) * FBB_KB] = sb[v >> 3][v & 7];
-                srow[r8(v + 1, h) * FBB_KB] = sb[v >> 3][(v & 7) + 1];
-            }
-            if constexpr (NEXT) s = sn;
-        }
-        __syncthreads();  // dS tile complete
-        {
-            const __bf16* ar = Ss + (16 * qi + l16) * FBB_KB + 8 * g;
-            f32x4 c[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-                if (32 * j < kq)
-                    c[j & 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                        *reinterpret_cast<const fbf16x8*>(ar + 32 * j),
-                        *reinterpret_cast<const fbf16x8*>(kfrow + 32 * j), c[j & 1], 0, 0, 0);
-            const f32x4 c0 = c[0], c1 = c[1];
-            float* dr = dqb + (long)(q0 + 16 * qi + 4 * g) * 64 + 16 * di + l16;
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                if (q0 + 16 * qi + 4 * g + r < T) dr[r * 64] = c0[r] + c1[r];
-        }
-        if constexpr (NEXT) {
-            if (qt + 2 < nqt) put((qt + 2) % 3);
-            __syncthreads();  // tile qt + 2 visible; the dS image free
-            if (qt + 3 < nqt) fetch(qt + 3);
-        }
-    };
-    using TT = std::true_type;
-    using FF = std::false_type;
-    const bool mq = (nqt - 1) * 32 + 32 > T;  // the last tile reaches past T
-    if (kall) {
-        for (int qt = 0; qt + 1 < nqt; ++qt) tile(qt, TT{}, FF{}, FF{});
-        if (mq) tile(nqt - 1, FF{}, FF{}, TT{});
-        else tile(nqt - 1, FF{}, FF{}, FF{});
-    } else {
-        for (int qt = 0; qt + 1 < nqt; ++qt) tile(qt, TT{}, TT{}, FF{});
-        tile(nqt - 1, FF{}, TT{}, TT{});
-    }
-    if (w < ngb && key < T) {
-        float* dkr = dqkv + ((long)u * T + key) * ld + H + hd * 64 + 4 * h;
-        float* dvr = dkr + H;
-    #pragma unroll
-        for (int t = 0; t < 2; ++t)
-    #pragma unroll
-            for (int a = 0; a < 4; ++a) {
-                f32x4 x, y;
-    #pragma unroll
-                for (int b = 0; b < 4; ++b) {
-                    x[b] = dk[t][4 * a + b];
-                    y[b] = dv[t][4 * a + b];
-                }
-                if (dqkv) {
-                    *reinterpret_cast<f32x4*>(dkr + 32 * t + 8 * a) = x;
-                    *reinterpret_cast<f32x4*>(dvr + 32 * t + 8 * a) = y;
-                }
-                if (dqkvb) {
-                    __bf16* kb2 = dqkvb + ((long)u * T + key) * ld + H + hd * 64 + 4 * h + 32 * t + 8 * a;
-                    *reinterpret_cast<fbf16x4*>(kb2) = cvt4(x);
-                    *reinterpret_cast<fbf16x4*>(kb2 + H) = cvt4(y);
-                }
-            }
-    }
-    if (dq_cnt) dq_combine(dqp, dqkv, dqkvb, dq_cnt, reinterpret_cast<int*>(Ls), bh, u, hd, T, NH, H, nkb, tl, B);
 }
 
 // dQ = sum over key blocks in order (query rows < tl; rows past it get 0, as their dS is 0)
@@ -1940,13 +1433,13 @@ __global__ __launch_bounds__(256) void flash_dq_reduce(const float* __restrict__
 
 constexpr int FF_NW = 4;
 
-static int g_fb_nw = 0;  // backward block width: 4 or 8 waves (0 = unset: env SUTA_FLASH_BWD_NW, default 8)
+// backward block width: 4 or 8 waves (env SUTA_FLASH_BWD_NW, default 8), read once (thread-safe initialisation)
 static int fb_nw() {
-    if (!g_fb_nw) {
+    static const int nw = [] {
         const char* e = std::getenv("SUTA_FLASH_BWD_NW");
-        g_fb_nw = (e && atoi(e) == 4) ? 4 : 8;
-    }
-    return g_fb_nw;
+        return (e && atoi(e) == 4) ? 4 : 8;
+    }();
+    return nw;
 }
 
 // bf16 mode: LDS images in bf16 (flash_*_bf16_kernel; env SUTA_FLASH_BF16_IMG=0 selects the fp32-image
@@ -1955,7 +1448,7 @@ static bool fb_img() { return suta_switches().flash_bf16_img != 0; }
 
 long flash_dq_scratch_floats(int B, int T, int NH) {
     const int ng = (T + 31) / 32, nkb = (ng + fb_nw() - 1) / fb_nw();
-    return (long)nkb * B * NH * T * 64 + (long)B * NH + 64;  // partials, then the per-head tickets (dq_combine)
+    return (long)nkb * B * NH * T * 64 + 64;  // the per-key-block dQ partials
 }
 
 // bf16 mode, bf16 qkv plane given: flash_fwd_bf16p_kernel (env SUTA_FLASH_FWD_PLANE=0 keeps the fp32-row
@@ -1990,9 +1483,6 @@ bool launch_flash_fwd(const float* qkv, float* ctx, float* lse, int B, int T, in
     } else if (bf16)
         hipLaunchKernelGGL((flash_fwd_kernel<FF_NW, true>), grid, dim3(FF_NW * 64), 0, st, qkv, ctx, lse, T, NH, H,
                            scale, tlen, nqb, ctxb);
-    else if (suta_switches().flash_fwd_pipe)
-        hipLaunchKernelGGL((flash_fwd_pipe_kernel<FF_NW>), grid, dim3(FF_NW * 64), 0, st, qkv, ctx, lse, T, NH, H, scale,
-                           tlen, nqb, ctxb);
     else
         hipLaunchKernelGGL((flash_fwd_kernel<FF_NW, false>), grid, dim3(FF_NW * 64), 0, st, qkv, ctx, lse, T, NH, H,
                            scale, tlen, nqb, ctxb);
@@ -2002,34 +1492,22 @@ bool launch_flash_fwd(const float* qkv, float* ctx, float* lse, int B, int T, in
 template <int NW, bool BF16>
 static void flash_bwd_go(dim3 grid, hipStream_t st, const float* qkv, const float* dctx, const float* lse,
                          const float* delta, float* dqkv, float* dqp, int T, int NH, int H, float scale,
-                         const int* tlen, int nkb, int gpb, int B, __bf16* dqkvb, int* cnt) {
+                         const int* tlen, int nkb, int gpb, int B, __bf16* dqkvb) {
     constexpr size_t lds = fb_lds_bytes<NW>();
-    static bool attr = false;
-    if (!attr) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_bwd_kernel<NW, BF16>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-            throw std::runtime_error("hipFuncSetAttribute(flash_bwd_kernel) failed");
-        attr = true;
-    }
+    set_max_lds_once(reinterpret_cast<const void*>(&flash_bwd_kernel<NW, BF16>), lds, "flash_bwd_kernel");
     hipLaunchKernelGGL((flash_bwd_kernel<NW, BF16>), grid, dim3(NW * 64), lds, st, qkv, dctx, lse, delta, dqkv, dqp,
-                       T, NH, H, scale, tlen, nkb, gpb, B, dqkvb, cnt);
+                       T, NH, H, scale, tlen, nkb, gpb, B, dqkvb);
 }
 
 template <bool ONEB>
 static void flash_bwd_bf16p_go(dim3 grid, hipStream_t st, const void* qkvb, const void* dctxb, const float* lse,
                                const float* delta, float* dqkv, float* dqp, int T, int NH, int H, float scale,
-                               const int* tlen, int nkb, int gpb, int B, __bf16* dqkvb, int* cnt, int kbl = -1) {
+                               const int* tlen, int nkb, int gpb, int B, __bf16* dqkvb) {
     constexpr size_t lds = fbbp_lds_bytes<ONEB>();
-    static bool attr = false;
-    if (!attr) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_bwd_bf16p_kernel<ONEB>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-            throw std::runtime_error("hipFuncSetAttribute(flash_bwd_bf16p_kernel) failed");
-        attr = true;
-    }
+    set_max_lds_once(reinterpret_cast<const void*>(&flash_bwd_bf16p_kernel<ONEB>), lds, "flash_bwd_bf16p_kernel");
     hipLaunchKernelGGL(flash_bwd_bf16p_kernel<ONEB>, grid, dim3(FBB_NW * 64), lds, st,
                        reinterpret_cast<const __bf16*>(qkvb), reinterpret_cast<const __bf16*>(dctxb), lse, delta, dqkv,
-                       dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb, cnt, kbl);
+                       dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb);
 }
 
 // bf16 mode, bf16 planes of qkv and dctx given: flash_bwd_bf16p_kernel (env SUTA_FLASH_BWD_PLANE=0 keeps the
@@ -2051,75 +1529,30 @@ bool launch_flash_bwd(const float* qkv, const float* dctx, const float* lse, con
     const int gpb = (ng + nkb - 1) / nkb;  // key groups per block (balanced)
     const dim3 grid((unsigned)((long)B * NH * nkb));
     const bool on_planes = flash_bwd_reads_planes(bf16, qkvb, dctxb, H);
-    // SUTA_DQ_INLAUNCH=1: the dQ partials combined by the last key block of each head (dq_combine), the per-head
-    // tickets zeroed ahead of the launch; default 0: the separate flash_dq_reduce pass (same-box C4: attention 544 vs
-    // 675 ms per call with the combine -- the reducing block reads both 102-KB partials of its head serially, the
-    // guide's "worth it when the slabs are a few tens of KB" bound)
-    int* cnt = nullptr;
-    if (suta_switches().dq_inlaunch) {
-        cnt = reinterpret_cast<int*>(dqp + (long)nkb * B * NH * T * 64);
-        if (hipMemsetAsync(cnt, 0, sizeof(int) * (size_t)B * NH, st) != hipSuccess)
-            throw std::runtime_error("flash_bwd: ticket memset failed");
-    }
     if (!qkv && !on_planes) throw std::invalid_argument("flash_bwd: fp32 qkv not written and the plane kernel not taken");
-    // SUTA_DQ_CHAIN (bf16 planes, the plain two-pass form): one launch per key block adding into one accumulator per
-    // head, where each launch still fills the chip (>= 4 rounds of blocks) or there is one key block
-    // (2: at any grid size -- tests)
-    const bool dq_chain = on_planes && !cnt && !suta_switches().flash_bwd_pipe && suta_switches().dq_chain &&
-                          (nkb == 1 || (long)B * NH >= 1024 || suta_switches().dq_chain == 2);
     if (on_planes) {
         if ((reinterpret_cast<uintptr_t>(qkvb) | reinterpret_cast<uintptr_t>(dctxb)) & 15)
             throw std::invalid_argument("flash_bwd: bf16 planes not 16-B aligned");
-        if (suta_switches().flash_bwd_pipe) {  // the software-pipelined form (bitwise the same results)
-            constexpr size_t lds = fbbpp_lds_bytes();
-            static bool attr = false;
-            if (!attr) {
-                if (hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_bwd_bf16pp_kernel),
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-                    throw std::runtime_error("hipFuncSetAttribute(flash_bwd_bf16pp_kernel) failed");
-                attr = true;
-            }
-            hipLaunchKernelGGL(flash_bwd_bf16pp_kernel, grid, dim3(FBB_NW * 64), lds, st,
-                               reinterpret_cast<const __bf16*>(qkvb), reinterpret_cast<const __bf16*>(dctxb), lse, delta,
-                               dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb, cnt);
-        } else if (dq_chain) {  // one launch per key block, dQ written by the last (no partials, no reduce pass)
-            for (int kbl = 0; kbl < nkb; ++kbl) {
-                if (suta_switches().flash_bwd_oneb)
-                    flash_bwd_bf16p_go<true>(dim3((unsigned)((long)B * NH)), st, qkvb, dctxb, lse, delta, dqkv, dqp, T,
-                                             NH, H, scale, tlen, nkb, gpb, B, dqkvb, nullptr, kbl);
-                else
-                    flash_bwd_bf16p_go<false>(dim3((unsigned)((long)B * NH)), st, qkvb, dctxb, lse, delta, dqkv, dqp,
-                                              T, NH, H, scale, tlen, nkb, gpb, B, dqkvb, nullptr, kbl);
-            }
-        } else if (suta_switches().flash_bwd_oneb) {
+        if (suta_switches().flash_bwd_oneb)
             flash_bwd_bf16p_go<true>(grid, st, qkvb, dctxb, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B,
-                                     dqkvb, cnt);
-        } else {
+                                     dqkvb);
+        else
             flash_bwd_bf16p_go<false>(grid, st, qkvb, dctxb, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B,
-                                      dqkvb, cnt);
-        }
+                                      dqkvb);
     } else if (bf16 && nw == FBB_NW && fb_img()) {
         constexpr size_t lds = fbb_lds_bytes();
-        static bool attr = false;
-        if (!attr) {
-            if (hipFuncSetAttribute(reinterpret_cast<const void*>(&flash_bwd_bf16_kernel),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-                throw std::runtime_error("hipFuncSetAttribute(flash_bwd_bf16_kernel) failed");
-            attr = true;
-        }
+        set_max_lds_once(reinterpret_cast<const void*>(&flash_bwd_bf16_kernel), lds, "flash_bwd_bf16_kernel");
         hipLaunchKernelGGL(flash_bwd_bf16_kernel, grid, dim3(FBB_NW * 64), lds, st, qkv, dctx, lse, delta, dqkv, dqp,
-                           T, NH, H, scale, tlen, nkb, gpb, B, dqkvb, cnt);
+                           T, NH, H, scale, tlen, nkb, gpb, B, dqkvb);
     } else if (nw == 4) {
-        if (bf16) flash_bwd_go<4, true>(grid, st, qkv, dctx, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb, cnt);
-        else flash_bwd_go<4, false>(grid, st, qkv, dctx, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb, cnt);
+        if (bf16) flash_bwd_go<4, true>(grid, st, qkv, dctx, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb);
+        else flash_bwd_go<4, false>(grid, st, qkv, dctx, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb);
     } else {
-        if (bf16) flash_bwd_go<8, true>(grid, st, qkv, dctx, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb, cnt);
-        else flash_bwd_go<8, false>(grid, st, qkv, dctx, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb, cnt);
+        if (bf16) flash_bwd_go<8, true>(grid, st, qkv, dctx, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb);
+        else flash_bwd_go<8, false>(grid, st, qkv, dctx, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb);
     }
-    if (!cnt && !dq_chain) {
-        const long n4 = (long)B * NH * T * 16;
-        hipLaunchKernelGGL(flash_dq_reduce, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, dqp, dqkv, B, T, NH, H,
-                           nkb, tlen, dqkvb);
-    }
+    const long n4 = (long)B * NH * T * 16;
+    hipLaunchKernelGGL(flash_dq_reduce, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, dqp, dqkv, B, T, NH, H,
+                       nkb, tlen, dqkvb);
     return true;
 }

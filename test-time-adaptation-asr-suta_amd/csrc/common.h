@@ -73,7 +73,6 @@ struct SutaSwitches {
     int dy_planes;        // SUTA_DY_PLANES
     int conv_dx_planes;   // SUTA_CONV_DX_PLANES
     int fused_conv_ln;    // SUTA_FUSED_CONV_LN
-    int hb8;              // SUTA_HB8 (default 0): 256 x 256 ping-pong bf16-plane GEMM selection mode
     int flash_fwd_nw;     // SUTA_FLASH_FWD_NW (default 4): waves per block of the bf16-plane flash forward
     int hbx;              // SUTA_HBX (default 1): the 256 x 256 slice-ring bf16-plane GEMM for plain-epilogue linears
                           // on full grids; 2: on every eligible bf16-plane linear (tests: small grids, edge tiles)
@@ -83,30 +82,22 @@ struct SutaSwitches {
                           // (SUTA_HBX_T=2) and K % 64 == 0: 2 four-phase 64-deep K-tiles with two wave groups one
                           // barrier apart + s_setprio (gemm_hbp_kernel), 1 the same in lockstep, 0 the 32-deep slice ring
     int ln_rpw;           // SUTA_LN_RPW (default 2): rows per wave of the bf16-input (conv stack) LayerNorm forward; 1 = one
-    int dq_inlaunch;      // SUTA_DQ_INLAUNCH (default 0): 1 = flash-backward dQ partials combined in-launch by each head's
-                          // last key block (measured slower: C4 attention 544 -> 675 ms per call, the last block reads
-                          // 2 x 102 KB of partials serially); 0 = the separate flash_dq_reduce pass
-    int hbx_dbg;          // SUTA_HBX_DBG (tools/hb_bench diagnostics; wrong results): gemm_hbx with parts of its loop removed
+    int hbx_dbg;          // SUTA_HBX_DBG (tools/hb_bench diagnostics; wrong results): gemm_hbx with parts of its loop removed;
+                          // honoured only by the tools build of gemm_hbx.hip (-DSUTA_HBX_DIAG), ignored by libsuta.so
     int fused_delta;      // SUTA_FUSED_DELTA (default 1): the flash backward's delta in the dctx GEMM's epilogue
     int hbx_t;            // SUTA_HBX_T (default 2): gemm_hbx accumulates C^T fragments with a row-per-lane epilogue whose
                           // outputs are staged through LDS into whole-line stores; 1 = direct 16-B row-per-lane stores,
                           // 0 = the column-per-lane form shared with the 128 x 128 kernel
     int hbp_conv;         // SUTA_HBP_CONV (default 1): the conv stack's conv-seg input gradients on the four-phase 256 x 256
                           // kernel (gemm.hip use_hbp_conv); 0 = the 128 x 128 kernel
-    int flash_fwd_pipe;   // SUTA_FLASH_FWD_PIPE (default 0, measured neutral): the exact-fp32 flash forward software-pipelined (S of the next
-                          // key tile under this tile's softmax, attn.hip flash_fwd_pipe_kernel; bitwise equal); 0 = not
-    int flash_bwd_pipe;   // SUTA_FLASH_BWD_PIPE (default 0, measured 18 % slower): the bf16-plane flash backward software-pipelined (S / dP of the
-                          // next query tile under this tile's softmax, attn.hip flash_bwd_bf16pp_kernel; bitwise equal)
     int flash_bwd_oneb;   // SUTA_FLASH_BWD_ONEB (default 1): the bf16-plane flash backward with one barrier per query tile (dS
                           // image double-buffered, the next tile's Q / dO put before the barrier); bitwise equal; 0 = two
-    int dq_chain;         // SUTA_DQ_CHAIN: the bf16-plane flash backward as one launch per key block adding dQ into one
-                          // accumulator per head, the last launch writing dQ (no partials, no flash_dq_reduce pass)
-    int conv_dw_side;     // SUTA_CONV_DW_SIDE: the layer-mode conv stack's weight-gradient GEMMs on a side stream (engine.hip
-                          // backward: fork after the layer's LayerNorm backward, join before its dz plane is rewritten)
     int epi_fast;         // SUTA_EPI_FAST (default 1): 32-bit-offset GEMM epilogue where every operand fits 4 GiB (p.off32);
                           // 0 = the general epilogue everywhere
 };
 void suta_latch_switches();
+// hipFuncSetAttribute(fn, MaxDynamicSharedMemorySize, bytes) once per kernel, thread-safe (ops.hip)
+void set_max_lds_once(const void* fn, size_t bytes, const char* name);
 const SutaSwitches& suta_switches();  // the snapshot (taken now if none was)
 
 // GELU / GELU' of the bf16-plane GEMM epilogues (config C4: the result is rounded to a bf16 plane), two elements per

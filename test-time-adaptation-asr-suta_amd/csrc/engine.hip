@@ -201,12 +201,6 @@ struct suta_engine {
     Cfg c;
     int device = 0;
     hipStream_t st = nullptr;
-    // side stream of the layer-mode conv stack's weight-gradient GEMMs (SUTA_CONV_DW_SIDE): dW_i forks off the engine
-    // stream after layer i's LayerNorm backward and joins before the dz plane it read is rewritten (layer i - 2) or the
-    // backward ends; its own split-K workspace
-    hipStream_t st2 = nullptr;
-    hipEvent_t conv_fork[16] = {}, conv_join[16] = {};
-    DevBuf splitws2;
     int max_batch = 0;
     long max_samples = 0;
     bool attn_fused = true;  // fused attention fwd/bwd kernels where their shape holds; env SUTA_ATTN_FUSED=0 off
@@ -385,15 +379,13 @@ struct suta_engine {
         if (convact.alloc(tot)) drop_graph();
         return reinterpret_cast<char*>(convact.p) + off;
     }
-    DevBuf convdz, convdz2;
-    // bf16 plane of the current conv layer's dz (the weight gradient's B operand); parity 1: the second plane (layers
-    // alternate planes while their weight gradients run on the side stream)
-    void* conv_dz_plane(int parity = 0) {
+    DevBuf convdz;
+    // bf16 plane of the current conv layer's dz (the weight gradient's B operand)
+    void* conv_dz_plane() {
         size_t n = 0;
         for (int j = 1; j < c.nconv; ++j) n = std::max(n, (size_t)rup((long)plan.B * plan.Lc[j] * c.C[j] * 2, 256));
-        DevBuf& b = parity ? convdz2 : convdz;
-        if (b.alloc(n)) drop_graph();
-        return b.p;
+        if (convdz.alloc(n)) drop_graph();
+        return convdz.p;
     }
     // layer i >= 1, native = 0: [B][C_i][K_i * C_{i-1}] bf16 (forward B operand); native = 1: the source layout
     // [B][K_i][C_{i-1}][C_i] (the input gradient's per-tap B segments)
@@ -533,11 +525,6 @@ suta_engine::~suta_engine() {
         (void)hipEventDestroy(pe.second.second);
     }
     for (auto e : evpool) (void)hipEventDestroy(e);
-    for (int i = 0; i < 16; ++i) {
-        if (conv_fork[i]) (void)hipEventDestroy(conv_fork[i]);
-        if (conv_join[i]) (void)hipEventDestroy(conv_join[i]);
-    }
-    if (st2) (void)hipStreamDestroy(st2);
     if (st) (void)hipStreamDestroy(st);
 }
 
@@ -1488,17 +1475,10 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
     float* other = pl.dzc;
     // bf16 conv storage: z_i and (below the last layer) da_i are bf16 planes in place in their fp32 buffers
     const bool zbf = k.layer_mode && conv_z_bf16();
-    // weight gradients on the side stream (SUTA_CONV_DW_SIDE, layer mode with bf16 planes, not in the per-kernel timing
-    // pass): dW_i runs beside dX_i and the LayerNorm backward of layer i - 1 (a memory / VALU-bound kernel that
-    // co-resides with the GEMM's blocks); layer i's dz plane is parity i & 1, rewritten by layer i - 2 after dW_i joined
-    const bool dw_side = k.layer_mode && conv_planes() && suta_switches().conv_dw_side && !timing && last < 16;
-    if (dw_side && splitws2.alloc(sizeof(float) * (size_t)plan.splitws_floats)) drop_graph();
     for (int i = last; i >= 1; --i) {
         // cur: group mode -> dz_i ; layer mode -> da_i
         bool bias_done = false;
         const bool cpl = conv_planes();
-        const int dzp = dw_side ? (i & 1) : 0;
-        if (dw_side && i + 2 <= last) HIPCHK(hipStreamWaitEvent(st, conv_join[i + 2], 0));
         if (k.layer_mode) {
             timed(F_NORM, [&] {
                 // fused: the LayerNorm backward also sums the conv bias gradient (one read of dz_i)
@@ -1510,7 +1490,7 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
                                               cpl && conv_dx_planes() ? nullptr : other, G + o_cg[i], G + o_cbeta[i],
                                               k.conv_bias ? G + o_cb[i] : nullptr,
                                               nullptr, Pn, pl.lnpart, st, pl.z[i], pl.cmean[i], nullptr, 0, 0, 0,
-                                              cpl ? conv_dz_plane(dzp) : nullptr, bfin)) {
+                                              cpl ? conv_dz_plane() : nullptr, bfin)) {
                     bias_done = true;
                 } else if (zbf) {
                     throw SutaError(SUTA_ERR_UNSUPPORTED, "conv stack in bf16: the fused LayerNorm backward is required");
@@ -1547,18 +1527,10 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
                 g.A = nullptr;
                 g.Ab = conv_act_plane(i - 1);
                 g.ldab = g.lda;
-                g.Bb = conv_dz_plane(dzp);
+                g.Bb = conv_dz_plane();
                 g.ldbb = g.ldb;
             }
-            if (dw_side) {  // fork: the side stream waits for layer i's LayerNorm backward (the dz plane)
-                HIPCHK(hipEventRecord(conv_fork[i], st));
-                HIPCHK(hipStreamWaitEvent(st2, conv_fork[i], 0));
-                g.mode = gemm_mode;
-                gemm_launch(g, st2, splitws2.p, plan.splitws_floats);
-                HIPCHK(hipEventRecord(conv_join[i], st2));
-            } else {
-                gemm(g);
-            }
+            gemm(g);
         }
         {  // da_{i-1} = conv_i^T(dz_i): one GEMM per output-row residue rho (rows S*m + rho), whose K
            // runs over the taps k = rho + S*j (segment seg = nj-1-j reads dz row m - j and weight tap k)
@@ -1602,7 +1574,7 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
                     if (!bias_done) throw SutaError(SUTA_ERR_UNSUPPORTED, "conv planes: dz plane not written");
                     g.A = nullptr;
                     g.B = nullptr;
-                    g.Ab = conv_dz_plane(dzp);
+                    g.Ab = conv_dz_plane();
                     g.ldab = Cout;
                     g.Bb = static_cast<char*>(conv_wt_plane(i, 1)) + (long)(rho + S_ * (nj - 1)) * Cin * Cout * 2;
                     g.ldbb = Cout;
@@ -1620,8 +1592,6 @@ void suta_engine::backward(int B, const suta_hparams& hp) {
         }
         std::swap(cur, other);
     }
-    // join: the side stream's last weight gradient (dW_1; in stream order every earlier one) before anything later
-    if (dw_side && last >= 1) HIPCHK(hipStreamWaitEvent(st, conv_join[1], 0));
     // conv0: cur = da0
     if (!k.layer_mode) {
         timed(F_FRONT, [&] {
@@ -2005,11 +1975,6 @@ int32_t suta_create(const suta_model_config* cfg, const char* const* names, cons
         if (const char* gr = std::getenv("SUTA_GRAPHS")) e->use_graphs = gr[0] != '0';
         HIPCHK(hipSetDevice(device));
         HIPCHK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
-        HIPCHK(hipStreamCreateWithFlags(&e->st2, hipStreamNonBlocking));
-        for (int i = 0; i < 16; ++i) {
-            HIPCHK(hipEventCreateWithFlags(&e->conv_fork[i], hipEventDisableTiming));
-            HIPCHK(hipEventCreateWithFlags(&e->conv_join[i], hipEventDisableTiming));
-        }
         e->d_step = reinterpret_cast<int*>(e->dalloc(1));
         HIPCHK(hipMemset(e->d_step, 0, sizeof(int)));
         std::map<std::string, std::pair<const float*, long>> w;

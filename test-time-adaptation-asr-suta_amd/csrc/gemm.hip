@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <atomic>
 #include <map>
 #include <mutex>
 #include <stdexcept>
@@ -28,7 +29,7 @@ void gemm_set_variant(int tile, int nbuf) {
 // layout reaches.  Counted when a launch is issued (eager or while a graph is captured), not on replay.
 static std::mutex g_census_mu;
 static std::map<std::string, long> g_census;
-static bool g_census_on = false;
+static std::atomic<bool> g_census_on{false};
 // with engine timing on as well: per GEMM shape, the summed HIP-event time of its launches ("ms|<shape>|n=<n>"
 // entries, value in microseconds)
 static std::map<std::string, std::pair<double, long>> g_census_ms;
@@ -163,40 +164,6 @@ static int choose_tile_hb(long M, long N, long Z) {
     return best;
 }
 
-// 160 x 128 tile (exact mode, LDS-DMA kernel, 1 x 4 waves): on the M = B*T linears whose 128 x 128 grid
-// ends in a mostly empty round of the 512 resident blocks (N = 768: 1200 tiles = 2.34 rounds; N = 2304:
-// 3600 = 7.03), the 160-row tile covers the same padded area in fewer rounds (960 = 1.88; 2880 = 5.6).
-// Measured (tools/gemm_bench, same box): equal to 128 x 128 within 1.4 % on every such shape (ffn2 1.123 vs
-// 1.138 ms, dqkv->dx 0.870 vs 0.876) and the bench within noise (35.70 vs 35.78 utt/s): the linears are not
-// tail-bound.  Opt-in: SUTA_GEMM160=1.
-static bool use_tile160(long M, long N, long Z) {
-    static int env = -1;
-    if (env < 0) {
-        const char* e = std::getenv("SUTA_GEMM160");
-        env = (e && atoi(e) == 1) ? 1 : 0;
-    }
-    if (!env) return false;
-    const long t128 = ((M + 127) / 128) * ((N + 127) / 128) * Z;
-    const long t160 = ((M + 159) / 160) * ((N + 127) / 128) * Z;
-    return t128 >= 512 && (t160 + 511) / 512 < (t128 + 511) / 512;
-}
-
-// 256 x 256 ping-pong bf16-plane kernel (gemm_hb8_kernel): K % 32 == 0 and a grid of >= 256 tiles (one block
-// per CU, no split-K).  Opt-in (tools/hb_bench: 5-13 % faster than 128 x 128 on the bare C4 shapes, yet config
-// C4 measured 1.3 % slower with it on every eligible linear -- at one block per CU the fused epilogues are
-// exposed).  SUTA_HB8=1: every eligible GEMM; =2: forced on every K % 32 == 0 (tests: small grids, edge tiles);
-// =3: only GEMMs whose epilogue reads no second operand and writes no extra output; =4: only without a bf16 C
-// copy.  From the call's switch snapshot (common.h SutaSwitches).
-static int use_hb8(const GemmParams& p) {
-    const int mode = suta_switches().hb8;
-    if (p.K % 32 != 0 || mode == 0 || p.Z != 1 || p.segK > 0) return 0;
-    if (mode == 2) return 1;
-    if (mode == 3 && ((p.epi & (EPI_GELU | EPI_RESID | EPI_STORE_PRE | EPI_DGELU | EPI_ACCUM | EPI_SMBWD)) || p.Cb))
-        return 0;
-    if (mode == 4 && p.Cb) return 0;
-    return ((p.M + 255) / 256) * ((p.N + 255) / 256) >= 256;
-}
-
 // 256 x 256 slice-ring bf16-plane kernel (gemm_hbx.hip, v_mfma_f32_32x32x16_bf16; bitwise the 128 x 128 kernel's
 // results: same MFMA products, same k order) for the linears on grids of at least one full round of 256 tiles.
 // tools/hb_bench (C4 shapes at M = 164 x 399, same box; profiles/r4/hbx_epilogue_hb_bench.log): qkv 729 -> 875 TF,
@@ -212,7 +179,7 @@ static int use_hb8(const GemmParams& p) {
 // operand over 4 GiB, or SUTA_EPI_FAST=0 -- must stay on the 128 x 128 kernel)
 static bool hbx_batch_ok(const GemmParams& p) {
     const SutaSwitches& sw = suta_switches();
-    return p.Z == 1 || (sw.hbx_form && sw.hbx_t == 2 && !sw.hbx_dbg && p.K % 64 == 0 && hbx_t_ok(p, true));
+    return p.Z == 1 || (sw.hbx_form && sw.hbx_t == 2 && p.K % 64 == 0 && hbx_t_ok(p, true));
 }
 
 static bool use_hbx(const GemmParams& p) {
@@ -250,7 +217,7 @@ bool gemm_hbx_t_selected(const GemmParams& p0) {
     GemmParams p = p0;
     p.off32 = epilogue_off32(p);
     const bool hb = p.mode == 2 && p.Ab && p.Bb && !p.ta && p.segK == 0;
-    return hb && g_force_tile < 0 && !use_hb8(p) && use_hbx(p) && suta_switches().hbx_t && hbx_t_ok(p, true);
+    return hb && g_force_tile < 0 && use_hbx(p) && suta_switches().hbx_t && hbx_t_ok(p, true);
 }
 
 void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
@@ -280,37 +247,32 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
     const bool bf16_gbf = p.mode == 2 && glds_ok && p.ta;  // bf16 weight gradients: LDS-DMA fp32 stages
     p.off32 = epilogue_off32(p);  // before the tile choice: the 256 x 256 kernel's batched form needs it
     p.fgelu = suta_switches().fast_gelu;  // (the engine call's switch snapshot)
-    if (p.preb && (!hb || !p.Cb || (p.ldc2 & 1)))  // (gemm_hb8_kernel shares the epilogue)
+    if (p.preb && (!hb || !p.Cb || (p.ldc2 & 1)))
         throw std::invalid_argument("gemm: bf16 pre-activation operands need the bf16-plane kernel with a Cb plane, ldc2 even");
     if (hb && p.segK > 0 && (p.segK % 8 || p.pad < 0 || (p.segB && (p.sBseg % 8))))
         throw std::invalid_argument("gemm: conv-A bf16 planes need segK and the tap stride % 8 == 0");
     int tile = hbt ? 0
                : (hb && p.segK > 0) ? (g_force_tile < 0 && use_hbp_conv(p) ? 8 : 0)
                : g_force_tile >= 0 ? g_force_tile
-               : hb            ? (use_hb8(p) ? 6 : use_hbx(p) ? 8 : choose_tile_hb(p.M, p.N, p.Z))
+               : hb            ? (use_hbx(p) ? 8 : choose_tile_hb(p.M, p.N, p.Z))
                : p.mode == 2   ? choose_tile_bf16(p.M, p.N, p.Z, !bf16_gbf)
                                : choose_tile(p.M, p.N, p.Z, p.K, p.mode);
-    const bool glds_path = p.mode == 0 && g_nbuf == 3 && glds_ok;
     if ((tile == 8 || tile == 9) && !(hb && p.K % 32 == 0 && p.K >= 128 && p.segK == 0 && (p.Z == 1 || (tile == 8 && hbx_batch_ok(p)))) &&
         !(tile == 8 && hb && p.segK > 0 && hbp_conv_ok(p)))
         tile = 0;
-    if (tile == 7 && !glds_path) tile = 0;  // the 160-row tile exists only in the default LDS-DMA kernel
-    if (tile == 6 && !(hb && p.K % 32 == 0)) tile = 0;  // the 256 x 256 tile is the bf16-plane ping-pong kernel only
-    if (g_force_tile < 0 && tile == 0 && glds_path && use_tile160(p.M, p.N, p.Z)) tile = 7;
-    // tiles 0 = 128x128, 1 = 128x64, 2 = 64x128, 3 = 64x64, 7 = 160x128; bf16 mode also 4 = 256x128,
-    // 5 = 128x256
+    if (tile == 6 || tile == 7) tile = 0;  // (the removed 256 x 256 ping-pong and 160 x 128 tiles: DESIGN.md 8)
+    // tiles 0 = 128x128, 1 = 128x64, 2 = 64x128, 3 = 64x64; bf16 mode also 4 = 256x128, 5 = 128x256
     // 8 / 9: the 256 x 256 slice-ring bf16-plane kernel (gemm_hbx.hip) on v_mfma_f32_32x32x16_bf16 / 16x16x32
-    const bool big = tile == 4 || tile == 6 || tile == 8 || tile == 9;
-    const int BM = tile == 7 ? 160 : big ? 256 : (tile == 0 || tile == 1 || tile == 5) ? 128 : 64;
-    const int BN = (tile == 5 || tile == 6 || tile == 8 || tile == 9) ? 256
-                   : (tile == 0 || tile == 2 || tile == 4 || tile == 7) ? 128 : 64;
+    const bool big = tile == 4 || tile == 8 || tile == 9;
+    const int BM = big ? 256 : (tile == 0 || tile == 1 || tile == 5) ? 128 : 64;
+    const int BN = (tile == 5 || tile == 8 || tile == 9) ? 256 : (tile == 0 || tile == 2 || tile == 4) ? 128 : 64;
     const int gx = (p.N + BN - 1) / BN, gy = (p.M + BM - 1) / BM;
     const long blocks = (long)gx * gy * p.Z;
 
     // split-K when the grid cannot fill 256 CUs and K is long
     int splits = 1;
     // (the split-K reduce has no bf16 pre store and no batched bf16 C plane)
-    if (ws && suta_switches().splitk && p.K >= 1024 && blocks < 256 && tile != 6 && tile != 8 && tile != 9 && !p.preb &&
+    if (ws && suta_switches().splitk && p.K >= 1024 && blocks < 256 && tile != 8 && tile != 9 && !p.preb &&
         !(p.Cb && p.Z > 1)) {
         splits = (int)std::min<long>(16, (512 + blocks - 1) / blocks);
         while (splits > 1 && (long)splits * p.Z * p.M * (long)p.N > ws_floats) --splits;
@@ -323,39 +285,35 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
     if ((p.epi & EPI_DELTA) && !(tile == 8 && suta_switches().hbx_t && hbx_t_ok(p, true)))
         throw std::invalid_argument("gemm: EPI_DELTA needs the 256 x 256 bf16-plane kernel's C^T epilogue (gemm_hbx_t_selected)");
     {
-        static int ord = -1;  // SUTA_GEMM_ORDER=1: m-fastest; =G >= 2: bands of G tile rows (A/B runs)
-        if (ord < 0) {
-            const char* e = std::getenv("SUTA_GEMM_ORDER");
-            ord = e ? std::max(0, atoi(e)) : 0;
-        }
-        p.order = (ord >= 1 && p.Z == 1 && splits == 1) ? ord : 0;
-        // bf16-plane GEMMs: bands of 8 tile rows (N >= 2048) or 4 walked column by column keep both operand
+        // tile order (xcd_tile): n-fastest by default (m-fastest and other band widths measured 1-4 % slower on the
+        // fp32 linears).  bf16-plane GEMMs: bands of 8 tile rows (N >= 2048) or 4 walked column by column keep both operand
         // panels L2-resident (tools/hb_bench, M = 25 536: qkv 543 -> 598 TF, ffn1 525 -> 590, the N = 1024
         // shapes within +-2 %); the fp32 kernels measured neutral and keep the n-fastest order
-        if (hb && ord == 0 && splits == 1) p.order = gx >= 16 ? 8 : 4;
+        p.order = 0;
+        if (hb && splits == 1) p.order = gx >= 16 ? 8 : 4;
         // fp32 linears with >= 16 column tiles (QKV, FFN1 and their input-gradient GEMMs): their weight panels do
         // not stay in an XCD's 4 MB L2 across a band of rows in n-fastest order; bands of 8 tile rows walked
         // column by column halve their HBM reads (FFN1 forward 1.43 -> 0.72 GB per launch, PMC) at equal time
         // (37.05 vs 37.13 utt/s, within noise); narrow GEMMs (6 column tiles) keep the n-fastest order, which
         // reads less for them
-        if (!hb && p.mode == 0 && ord == 0 && splits == 1 && p.Z == 1 && gx >= 16) p.order = 8;
+        if (!hb && p.mode == 0 && splits == 1 && p.Z == 1 && gx >= 16) p.order = 8;
     }
     dim3 grid(gx, gy, p.Z * splits);
     if (hbt) {
         census("hbt", BM, BN, p, splits);
         gemm_run_hbt(p, grid, st);
     } else if (hb) {
-        static int hbns = -1;  // SUTA_HB_NS: stage variant of the 128 x 128 bf16-plane kernel (A/B runs; 2 default)
-        if (hbns < 0) {
+        // SUTA_HB_NS: stage variant of the 128 x 128 bf16-plane kernel (A/B runs; 2 default), read once (thread-safe)
+        static const int hbns = [] {
             const char* ev = std::getenv("SUTA_HB_NS");
-            hbns = ev ? std::max(2, atoi(ev)) : 2;
-        }
+            return ev ? std::max(2, atoi(ev)) : 2;
+        }();
         const int ns = g_force_tile >= 0 ? g_nbuf : (tile == 0 ? hbns : 2);
         if (tile == 8 || tile == 9) {
             census(tile == 8 ? "hbx" : "hbx16", BM, BN, p, splits);
             gemm_run_hbx(tile == 8 ? 1 : 2, p, grid, st);
         } else {
-            census(tile == 6 ? "hb8" : "hb", BM, BN, p, splits);
+            census("hb", BM, BN, p, splits);
             gemm_run_hb(tile, ns, p, grid, st);
         }
     } else if (p.mode == 2) {

@@ -10,11 +10,6 @@ void gemm_run_hb(int tile, int ns, const GemmParams& p, dim3 grid, hipStream_t s
         else launch_hb<128, 128, 2, 32, 4, true, false>(p, grid, st);
         return;
     }
-    if (tile == 6) {  // 256 x 256 ping-pong (K % 32 == 0, no split-K)
-        const char* e = std::getenv("SUTA_HB8_PF");  // 1: fragments read one phase ahead
-        launch_hb8(p, grid, st, e && atoi(e) == 1);
-        return;
-    }
     if (tile == 4) {
         launch_hb<256, 128, 2>(p, grid, st);
         return;

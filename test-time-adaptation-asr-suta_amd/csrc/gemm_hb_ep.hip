@@ -19,11 +19,10 @@ void launch_class(const GemmParams& p, dim3 grid, hipStream_t st) {
 }  // namespace
 
 bool gemm_run_hb_class(const GemmParams& p, dim3 grid, hipStream_t st) {
-    static int on = -1;  // SUTA_HB_EPI_CLASS=0: the generic kernel for every epilogue (A/B runs)
-    if (on < 0) {
+    static const int on = [] {  // SUTA_HB_EPI_CLASS=0: the generic kernel for every epilogue (A/B runs); read once
         const char* e = std::getenv("SUTA_HB_EPI_CLASS");
-        on = (e && atoi(e) == 0) ? 0 : 1;
-    }
+        return (e && atoi(e) == 0) ? 0 : 1;
+    }();
     if (!on || p.segK > 0) return false;
     const int e = p.epi;
     if ((e & ~EM_A) == 0) launch_class<EM_A>(p, grid, st);

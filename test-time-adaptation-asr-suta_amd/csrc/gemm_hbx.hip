@@ -935,10 +935,20 @@ bool hbx_t_ok(const GemmParams& p, bool check_off32) {
 // the conv stack's input-gradient GEMMs (conv-A rows, per-tap bf16 weight segments) on the four-phase 256 x 256 kernel:
 // k-contiguous planes whose A rows are the segments (ldab == segK, segK % 64 == 0, segmented B, no batch split inside a
 // plane), the staggered main loop (SUTA_HBX_FORM 2 / 3) with the staged C^T epilogue, the plain epilogue class
+// SUTA_HBX_DBG: gemm_hbx_kernel with parts of its main loop removed (wrong results; tools/hb_bench diagnostics of
+// where the loop's time goes).  Compiled only into the tools build (-DSUTA_HBX_DIAG), never into libsuta.so.
+static int hbx_diag() {
+#ifdef SUTA_HBX_DIAG
+    return suta_switches().hbx_dbg;
+#else
+    return 0;
+#endif
+}
+
 bool hbp_conv_ok(const GemmParams& p) {
     const SutaSwitches& sw = suta_switches();
     return p.segK > 0 && p.segB && p.segK % 64 == 0 && p.ldab == p.segK && p.pad >= 0 && p.K % 64 == 0 && p.K >= 128 &&
-           p.zdiv == 1 && !p.ta && p.Ab && p.Bb && sw.hbx_form >= 2 && sw.hbx_t == 2 && !sw.hbx_dbg &&
+           p.zdiv == 1 && !p.ta && p.Ab && p.Bb && sw.hbx_form >= 2 && sw.hbx_t == 2 && !hbx_diag() &&
            (p.epi & ~(EPI_BIAS | EPI_RESID | EPI_ROWMASK)) == 0 && !p.preb && p.splits <= 1 && hbx_t_ok(p, true);
 }
 
@@ -960,7 +970,7 @@ void gemm_run_hbx(int variant, const GemmParams& p, dim3 grid, hipStream_t st) {
     if (p.splits > 1 || (e & (EPI_ACCUM | EPI_SMBWD)))
         throw std::invalid_argument("hbx: no split-K, ACCUM or SMBWD");
     if (p.Z != 1 && !(variant == 1 && suta_switches().hbx_form && suta_switches().hbx_t == 2 && p.K % 64 == 0 &&
-                      hbx_t_ok(p, true) && !suta_switches().hbx_dbg))
+                      hbx_t_ok(p, true) && !hbx_diag()))
         throw std::invalid_argument("hbx: batched GEMMs only on the four-phase form with the staged C^T epilogue");
     if (p.segK > 0) {  // conv-A rows: the four-phase form's CONV instantiation (gemm.hip hbp_conv_ok)
         if (!hbp_conv_ok(p)) throw std::invalid_argument("hbx: conv-A GEMM outside the four-phase CONV form's conditions");
@@ -983,7 +993,7 @@ void gemm_run_hbx(int variant, const GemmParams& p, dim3 grid, hipStream_t st) {
         return;
     }
     const int tr = suta_switches().hbx_t;
-    const int dbg = suta_switches().hbx_dbg;
+    const int dbg = hbx_diag();
     const int form = suta_switches().hbx_form;
     if (form && tr == 2 && p.K % 64 == 0 && hbx_t_ok(p, true) && !dbg) {  // the four-phase K-tile schedule
         const bool cb = p.Cb != nullptr;
@@ -1007,6 +1017,7 @@ void gemm_run_hbx(int variant, const GemmParams& p, dim3 grid, hipStream_t st) {
         if ((e & ~XEM_D) == 0) HBP(XEM_D);
 #undef HBP
     }
+#ifdef SUTA_HBX_DIAG
     if (dbg && tr == 2 && hbx_t_ok(p, true) && (e & ~XEM_A) == 0) {  // tools/hb_bench diagnostics
         const bool cb = p.Cb != nullptr;
 #define HBX_DBG(D)                                                                                                 \
@@ -1022,6 +1033,7 @@ void gemm_run_hbx(int variant, const GemmParams& p, dim3 grid, hipStream_t st) {
 #undef HBX_DBG
         return;
     }
+#endif
     if (tr && hbx_t_ok(p, true)) {  // C^T accumulators, row-per-lane epilogue (2: LDS-staged whole-line stores)
         if (tr == 2) {
             if (e == XEM_L) return launch_hbx_em<32, XEM_L, 2>(p, grid, st);

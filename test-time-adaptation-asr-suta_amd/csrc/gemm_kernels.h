@@ -1509,10 +1509,6 @@ void launch_glds(const GemmParams& p, dim3 grid, hipStream_t st) {
 template <int BKS, int NS>
 void launch_glds_tile(int tile, const GemmParams& p, dim3 grid, hipStream_t st) {
     if (tile == 0) launch_glds<128, 128, BKS, NS>(p, grid, st);
-    else if (tile == 7) {
-        if constexpr (BKS == 32 && NS == 2) launch_glds<160, 128, BKS, NS>(p, grid, st);  // default variant only
-        else launch_glds<128, 128, BKS, NS>(p, grid, st);
-    }
     else if (tile == 1) launch_glds<128, 64, BKS, NS>(p, grid, st);
     else if (tile == 2) launch_glds<64, 128, BKS, NS>(p, grid, st);
     else launch_glds<64, 64, BKS, NS>(p, grid, st);
@@ -1661,186 +1657,6 @@ template <int BM, int BN, int NS, int BKS = 32, int NWV = 4, bool CONV = false, 
           int EM = -1>
 void launch_hb(const GemmParams& p, dim3 grid, hipStream_t st) {
     hipLaunchKernelGGL((gemm_hb_kernel<BM, BN, NS, BKS, NWV, CONV, SEGB, CBT, EM>), grid, dim3(64 * NWV), 0, st, p);
-}
-
-// 256 x 256 bf16-plane GEMM on one block per CU with a ping-pong schedule (cdna_hip_programming.md,
-// "256^2 8-phase template": wave groups offset by one barrier).  8 waves = 2 groups (wr: A rows
-// 128 wr..) x 4 (wc: B rows 64 wc..), wave tile 128 x 64 = 4 x 2 fragments of v_mfma_f32_32x32x16_bf16;
-// four 32-deep K-tile buffers (A 256 x 32 + B 256 x 32 bf16 = 32 KB each, the hb stage image), three
-// K-tiles of LDS-DMA in flight ahead of the one being read.
-// Every 16-deep K slice is one phase: ds_read the slice's 6 fragments, [LDS-DMA], barrier, 8 MFMAs at
-// raised priority, barrier.  Group 1 enters one barrier late, so each barrier releases one group into
-// its MFMAs and the other into its reads: a SIMD's two waves (one per group) alternate on the matrix
-// pipe.  Hazards, with group 0's phase-p barriers numbered 2p+1 / 2p+2 and group 1's 2p+2 / 2p+3:
-//   WAR -- K-tile s+3 is staged into the buffer of tile s-1 in phase kc = 1 of tile s (phase 2s+1):
-//          group 0 has passed barrier 4s+2, so group 1 has finished phase 2s-1 (its last read of s-1);
-//   RAW -- every wave retires tile s+1's DMA (counted vmcnt: tiles s+2, s+3 may stay in flight) before
-//          its first barrier of phase 2s+1; group 0 reads tile s+1 after barrier 4s+4 (group 1's first
-//          barrier of 2s+1), group 1 after 4s+5.
-// Requires K % 32 == 0, no split-K (the dispatcher guarantees both).
-// PF: fragments read one phase ahead (after the phase's first barrier, into a second register set) so the
-// MFMAs never wait on this phase's LDS reads; tile s+1 is then retired one phase earlier (kc = 0 of tile s).
-template <bool CB, bool PF>
-__global__ __launch_bounds__(512, 1) void gemm_hb8_kernel(GemmParams p) {
-    constexpr int BM = 256, BN = 256, BKS = 16, NWV = 8, NB = 4;
-    constexpr int NPW = (BM + BN) * BKS / (256 * NWV);  // DMA instructions per wave per K-tile (4)
-    constexpr int BUF = (BM + BN) * BKS;                 // 4-byte units per K-tile buffer
-    __shared__ __attribute__((aligned(16))) float smem[NB * BUF];
-
-    const TileId tid = xcd_tile(p.order);
-    const float* A = reinterpret_cast<const float*>(p.Ab);
-    const float* B = reinterpret_cast<const float*>(p.Bb);
-    const long lda = p.ldab / 2, ldb = p.ldbb / 2;  // in 4-byte units
-    const int m0 = tid.y * BM, n0 = tid.x * BN;
-    const int nst = p.K / 32;
-    const int lane = threadIdx.x & 63;
-    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wr = wid >> 2, wc = wid & 3;
-    const int h = lane >> 5, l32 = lane & 31;
-
-    f32x16 acc[4][2];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-    GldsStream<BM, BKS, true, NWV> sa;
-    GldsStream<BN, BKS, true, NWV> sb;
-    sa.init(A, lda, m0, p.M, 0, wid, lane);
-    sb.init(B, ldb, n0, p.N, 0, wid, lane);
-#pragma unroll
-    for (int t = 0; t < NB - 1; ++t)
-        if (t < nst) {
-            glds_stream_issue(sa, smem + t * BUF, wid);
-            glds_stream_issue(sb, smem + t * BUF + BM * BKS, wid);
-        }
-    if (nst >= 3) wait_vm<2 * NPW>();
-    else if (nst == 2) wait_vm<NPW>();
-    else wait_vm<0>();
-    __builtin_amdgcn_s_barrier();
-    if (wr == 1) __builtin_amdgcn_s_barrier();  // the stagger
-    __builtin_amdgcn_sched_barrier(0);
-
-    auto frag = [&](const float* lds, int row, int kc) {
-        const int c = 2 * kc + h;
-        return *reinterpret_cast<const bf16x8*>(lds + row * BKS + ((c ^ glds_swz<BKS>(row)) * 4));
-    };
-    if constexpr (PF) {
-        bf16x8 xa[4], xb[2], ya[4], yb[2];  // X: slice kc = 0, Y: slice kc = 1 of the current tile
-#pragma unroll
-        for (int j = 0; j < 2; ++j) xb[j] = frag(smem + BM * BKS, wc * 64 + j * 32 + l32, 0);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) xa[i] = frag(smem, wr * 128 + i * 32 + l32, 0);
-        for (int s = 0; s < nst; ++s) {
-            const float* As = smem + (s % NB) * BUF;
-            const float* Bs = As + BM * BKS;
-            const float* An = smem + ((s + 1) % NB) * BUF;
-            const float* Bn = An + BM * BKS;
-            // phase kc = 0: retire tile s+1 (read from the next phase on), MFMAs on X, read Y
-            if (s + 2 < nst) wait_vm<NPW>();
-            else wait_vm<0>();
-            __builtin_amdgcn_sched_barrier(0);
-            __builtin_amdgcn_s_barrier();
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int j = 0; j < 2; ++j) yb[j] = frag(Bs, wc * 64 + j * 32 + l32, 1);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) ya[i] = frag(As, wr * 128 + i * 32 + l32, 1);
-            __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < 2; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa[i], xb[j], acc[i][j], 0, 0, 0);
-            __builtin_amdgcn_s_setprio(0);
-            __builtin_amdgcn_sched_barrier(0);
-            __builtin_amdgcn_s_barrier();
-            __builtin_amdgcn_sched_barrier(0);
-            // phase kc = 1: stage tile s+3, MFMAs on Y, read X of tile s+1
-            if (s + 3 < nst) {
-                float* nxt = smem + ((s + 3) % NB) * BUF;
-                glds_stream_issue(sa, nxt, wid);
-                glds_stream_issue(sb, nxt + BM * BKS, wid);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            __builtin_amdgcn_s_barrier();
-            __builtin_amdgcn_sched_barrier(0);
-            if (s + 1 < nst) {
-#pragma unroll
-                for (int j = 0; j < 2; ++j) xb[j] = frag(Bn, wc * 64 + j * 32 + l32, 0);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) xa[i] = frag(An, wr * 128 + i * 32 + l32, 0);
-            }
-            __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < 2; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ya[i], yb[j], acc[i][j], 0, 0, 0);
-            __builtin_amdgcn_s_setprio(0);
-            __builtin_amdgcn_sched_barrier(0);
-            __builtin_amdgcn_s_barrier();
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    } else {
-    for (int s = 0; s < nst; ++s) {
-            const float* As = smem + (s % NB) * BUF;
-            const float* Bs = As + BM * BKS;
-    #pragma unroll
-            for (int kc = 0; kc < 2; ++kc) {
-                bf16x8 af[4], bf[2];
-    #pragma unroll
-                for (int j = 0; j < 2; ++j) bf[j] = frag(Bs, wc * 64 + j * 32 + l32, kc);
-    #pragma unroll
-                for (int i = 0; i < 4; ++i) af[i] = frag(As, wr * 128 + i * 32 + l32, kc);
-                if (kc == 1) {
-                    if (s + 3 < nst) {
-                        float* nxt = smem + ((s + 3) % NB) * BUF;
-                        glds_stream_issue(sa, nxt, wid);
-                        glds_stream_issue(sb, nxt + BM * BKS, wid);
-                        wait_vm<2 * NPW>();  // tile s+1 landed; s+2, s+3 in flight
-                    } else if (s + 2 < nst) {
-                        wait_vm<NPW>();
-                    } else {
-                        wait_vm<0>();
-                    }
-                }
-                __builtin_amdgcn_sched_barrier(0);
-                __builtin_amdgcn_s_barrier();
-                __builtin_amdgcn_sched_barrier(0);
-                __builtin_amdgcn_s_setprio(1);
-    #pragma unroll
-                for (int i = 0; i < 4; ++i)
-    #pragma unroll
-                    for (int j = 0; j < 2; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
-                __builtin_amdgcn_s_setprio(0);
-                __builtin_amdgcn_sched_barrier(0);
-                __builtin_amdgcn_s_barrier();
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        }
-    }
-    if (wr == 0) __builtin_amdgcn_s_barrier();  // equal barrier counts in both groups
-    wait_vm<0>();
-    // two 64-row halves: bounds the epilogue's live temporaries beside the 128 accumulator registers
-    const bool interior = m0 + BM <= p.M && n0 + BN <= p.N;
-    gemm_epilogue<2, 2, CB>(p, reinterpret_cast<const f32x16(&)[2][2]>(acc[0]), 0, 0, m0 + wr * 128, n0 + wc * 64, h,
-                            l32, interior, tid.z);
-    gemm_epilogue<2, 2, CB>(p, reinterpret_cast<const f32x16(&)[2][2]>(acc[2]), 0, 0, m0 + wr * 128 + 64,
-                            n0 + wc * 64, h, l32, interior, tid.z);
-}
-
-inline void launch_hb8(const GemmParams& p, dim3 grid, hipStream_t st, bool pf) {
-    if (pf) {
-        if (p.Cb) hipLaunchKernelGGL((gemm_hb8_kernel<true, true>), grid, dim3(512), 0, st, p);
-        else hipLaunchKernelGGL((gemm_hb8_kernel<false, true>), grid, dim3(512), 0, st, p);
-    } else {
-        if (p.Cb) hipLaunchKernelGGL((gemm_hb8_kernel<true, false>), grid, dim3(512), 0, st, p);
-        else hipLaunchKernelGGL((gemm_hb8_kernel<false, false>), grid, dim3(512), 0, st, p);
-    }
 }
 
 }  // namespace

@@ -4,7 +4,10 @@
 // duplicate-entry multiplicity.  All reductions are fixed-order (bitwise reproducible).
 #include "ops.h"
 #include <algorithm>
+#include <map>
+#include <mutex>
 #include <stdexcept>
+#include <string>
 
 namespace {
 
@@ -1761,12 +1764,8 @@ static void posconv_go(int WB, dim3 grid, size_t lds, hipStream_t st, const floa
     // > 64 KiB of dynamic LDS must be allowed per kernel (once per instantiation)
 #define PC(WB_)                                                                                                   \
     do {                                                                                                          \
-        static bool attr = false;                                                                                 \
-        if (!attr) {                                                                                              \
-            HIPCHK_OPS(hipFuncSetAttribute(reinterpret_cast<const void*>(&posconv_kernel<CG, WB_, PC_CHT, FWD>),   \
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));              \
-            attr = true;                                                                                          \
-        }                                                                                                         \
+        set_max_lds_once(reinterpret_cast<const void*>(&posconv_kernel<CG, WB_, PC_CHT, FWD>), 160 * 1024,       \
+                         "posconv_kernel");                                                                       \
         hipLaunchKernelGGL((posconv_kernel<CG, WB_, PC_CHT, FWD>), grid, dim3(WB_ * 64), lds, st, x, W, bias, R, C, \
                            C2, T, H, G, K, pad, tlen, ntile, B);                                                  \
     } while (0)
@@ -1816,12 +1815,8 @@ static void posconv_bf16_go(int WB, dim3 grid, size_t lds, hipStream_t st, const
                             const int* tlen, int ntile, int B) {
 #define PCB(WB_)                                                                                                  \
     do {                                                                                                          \
-        static bool attr = false;                                                                                 \
-        if (!attr) {                                                                                              \
-            HIPCHK_OPS(hipFuncSetAttribute(reinterpret_cast<const void*>(&posconv_bf16_kernel<WB_, FWD>),          \
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));              \
-            attr = true;                                                                                          \
-        }                                                                                                         \
+        set_max_lds_once(reinterpret_cast<const void*>(&posconv_bf16_kernel<WB_, FWD>), 160 * 1024,              \
+                         "posconv_bf16_kernel");                                                                  \
         hipLaunchKernelGGL((posconv_bf16_kernel<WB_, FWD>), grid, dim3(WB_ * 64), lds, st, x, W, bias, R, C, C2, T, \
                            H, G, K, pad, tlen, ntile, B);                                                         \
     } while (0)
@@ -1905,6 +1900,19 @@ void launch_adam(float* P, const float* G, float* M, float* V, long pstride, int
     hipLaunchKernelGGL(adam_kernel, dim3((unsigned)nblk, B), dim3(256), 0, st, P, G, M, V, pstride, aa);
 }
 
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per kernel.  Several engines' host threads launch concurrently
+// (--gpu_engines), so the "done" set is guarded (advisor r5: the former per-call-site static flags were data races).
+void set_max_lds_once(const void* fn, size_t bytes, const char* name) {
+    static std::mutex mu;
+    static std::map<const void*, size_t> done;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = done.find(fn);
+    if (it != done.end() && it->second >= bytes) return;
+    if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) != hipSuccess)
+        throw std::runtime_error(std::string("hipFuncSetAttribute(") + name + ") failed");
+    done[fn] = bytes;
+}
+
 static thread_local SutaSwitches g_switches{};  // per host thread (common.h)
 
 void suta_latch_switches() {
@@ -1929,33 +1937,19 @@ void suta_latch_switches() {
     const char* hbxt = std::getenv("SUTA_HBX_T");
     s.hbx_t = hbxt ? std::min(2, std::max(0, atoi(hbxt))) : 2;
     s.fused_delta = on("SUTA_FUSED_DELTA");
-    const char* dqi = std::getenv("SUTA_DQ_INLAUNCH");
-    s.dq_inlaunch = dqi ? atoi(dqi) : 0;
     const char* lrpw = std::getenv("SUTA_LN_RPW");
     s.ln_rpw = lrpw ? atoi(lrpw) : 2;
     const char* hform = std::getenv("SUTA_HBX_FORM");
     s.hbx_form = hform ? atoi(hform) : 3;
     const char* hdbg = std::getenv("SUTA_HBX_DBG");
     s.hbx_dbg = hdbg ? atoi(hdbg) : 0;
-    const char* hb8 = std::getenv("SUTA_HB8");
-    s.hb8 = hb8 ? atoi(hb8) : 0;
     const char* fnw = std::getenv("SUTA_FLASH_FWD_NW");
     s.flash_fwd_nw = (fnw && atoi(fnw) == 8) ? 8 : 4;
     s.epi_fast = on("SUTA_EPI_FAST");
     s.hbp_conv = on("SUTA_HBP_CONV");
-    // the software-pipelined flash kernels measured no faster (fp32 forward 119.0 vs 117.3 ms per C2 batch) or slower
-    // (bf16 backward 826 vs 701 ms per two C4 calls, profiles/r5): opt-in (=1) for A/B runs
-    const char* ffp = std::getenv("SUTA_FLASH_FWD_PIPE");
-    s.flash_fwd_pipe = ffp ? atoi(ffp) : 0;
-    const char* fbp = std::getenv("SUTA_FLASH_BWD_PIPE");
-    s.flash_bwd_pipe = fbp ? atoi(fbp) : 0;
     // one barrier per query tile in the bf16-plane flash backward: C4 attention 543-546 -> 534-535 ms per call, same box
     // (profiles/r5/oneb_ab.txt); =0 the two-barrier form
     s.flash_bwd_oneb = on("SUTA_FLASH_BWD_ONEB");
-    const char* dqc = std::getenv("SUTA_DQ_CHAIN");
-    s.dq_chain = dqc ? atoi(dqc) : 0;
-    const char* cds = std::getenv("SUTA_CONV_DW_SIDE");
-    s.conv_dw_side = cds ? atoi(cds) : 0;
     s.latched = 1;
     g_switches = s;
 }

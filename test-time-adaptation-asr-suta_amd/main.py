@@ -151,6 +151,19 @@ def workspace_bytes_per_audio_s(cfg) -> float:
     return 50 * 4 * cfg["num_hidden_layers"] * 14 * cfg["hidden_size"] + 6350 * 512 * 4 * 3
 
 
+def engine_fixed_bytes(cfg, weights, max_batch: int, precision: str = "fp32") -> float:
+    """Device bytes an engine holds whatever its batch layout (advisor r5): its fp32 copy of the weights, the bf16
+    planes of the frozen linear weights in bf16 mode (W and W^T: one fp32 copy's worth), and per utterance slot the
+    trainable tensors, their gradients and both Adam moments (plus the pristine copy)."""
+    from .config import param_shapes
+    from .modules import collect_params
+    wbytes = 4.0 * sum(int(np.asarray(v).size) for v in weights.values())
+    shapes = dict(param_shapes(cfg))
+    _, names = collect_params(cfg, bias_only=False, train_feature=True)
+    pn = sum(int(np.prod(shapes[n])) for n in dict.fromkeys(names) if n in shapes)
+    return wbytes * (2.0 if precision == "bf16" else 1.0) + 4.0 * pn * (4 * max_batch + 1)
+
+
 def clamp_budget(budget_s: float, cfg, free_bytes, frac: float = 0.7) -> float:
     """The ragged-batch audio budget limited to `frac` of the device's free memory (the defaults are sized for the
     288 GB of an MI355X; a smaller GPU would otherwise fail its first allocation)."""
@@ -260,7 +273,9 @@ def main(argv=None, sdpl: bool = False):
     # non-episodic adaptation carries state across utterances in one engine's slot: one engine
     n_eng = max(1, a.gpu_engines) if (a.episodic and gb > 1) else 1
     if torch.cuda.is_available():
-        budget = clamp_budget(a.gpu_budget_s, cfg, torch.cuda.mem_get_info(device)[0], frac=0.7 / n_eng)
+        # the engines' fixed footprint (weights, bf16 weight planes, per-slot state) comes off the free memory first
+        free = torch.cuda.mem_get_info(device)[0] - n_eng * engine_fixed_bytes(cfg, weights, gb, a.precision)
+        budget = clamp_budget(a.gpu_budget_s, cfg, max(1.0, free), frac=0.7 / n_eng)
         if budget < a.gpu_budget_s:
             say(f"[suta_amd] --gpu_budget_s {a.gpu_budget_s} x {n_eng} engine(s) exceeds 70 % of the free device "
                 f"memory; using {budget:.0f} s")

@@ -182,39 +182,6 @@ def test_bf16_posconv_kernel_equals_conv_a_path(monkeypatch):
     eng.close()
 
 
-def test_bf16_hb8_pingpong_kernel(monkeypatch):
-    """gemm_hb8_kernel (256 x 256 tile, two wave groups one barrier apart) forced on every bf16-plane linear
-    with K % 32 == 0 (SUTA_HB8=2; by default it runs only where the grid has >= 256 tiles, i.e. config C4's
-    64 x 8 s batches): the large model's 20-step SUTA against the reference goldens g7, reruns bitwise
-    identical, and a ragged pair (edge tiles: 198 and 124 rows of a 256-row tile) against the 128 x 128
-    kernel (SUTA_HB8=0) to bf16 tolerance (same operand roundings, another fp32 summation order)."""
-    z = _load("g7_large_16000.npz")
-    cfg = get_config("wav2vec2-large")
-    sd = synth_weights(cfg)
-    steps = [int(s) for s in z["steps"]]
-    waves = [synth.wave(32000, 80), synth.wave(20000, 81)]
-    out = {}
-    for mode in ("2", "0"):
-        monkeypatch.setenv("SUTA_HB8", mode)
-        eng = SutaEngine(cfg, sd, max_batch=2, max_samples=32000)
-        eng.set_precision("bf16")
-        if mode == "2":
-            logits, _, _ = eng.adapt(_g7_wave(), 20, SutaHParams(), record=steps)
-            for j, s in enumerate(steps):
-                assert_bf16_close(logits[s][0], z["logits"][j], 0.97, f"hb8 large step {s}",
-                                  rtol=BF16_LOGITS_RTOL_LARGE)
-        a, _, _ = eng.adapt_varlen(waves, 3, SutaHParams(), record=[0, 3])
-        b, _, _ = eng.adapt_varlen(waves, 3, SutaHParams(), record=[0, 3])
-        for u in range(2):
-            assert np.array_equal(a[3][u], b[3][u]), (mode, u)
-        out[mode] = a
-        eng.close()
-    for r in (0, 3):
-        for u in range(2):
-            assert_bf16_close(out["2"][r][u], out["0"][r][u], 0.97, f"hb8 vs 128x128 step {r} utt {u}",
-                              rtol=BF16_LOGITS_RTOL_LARGE)
-
-
 def test_bf16_hbx_slice_ring_kernel_bitwise_equals_128_tile(monkeypatch):
     """gemm_hbx_kernel (256 x 256 tile, 32-deep slice ring, v_mfma_f32_32x32x16_bf16) forced on every bf16-plane linear
     (SUTA_HBX=2: every epilogue class -- bias / residual, bias + GELU + bf16 pre-activation, GELU' -- small grids and
@@ -286,31 +253,6 @@ def test_bf16_fused_delta_bitwise_equals_separate_pass(monkeypatch):
     assert delta_launches["1"] == 3 * cfg["num_hidden_layers"], delta_launches   # one dctx GEMM per layer-backward
     assert delta_launches["0"] == 0, delta_launches
     for r in (0, 3):
-        for u in range(2):
-            assert np.array_equal(out["1"][r][u], out["0"][r][u]), (r, u)
-    for n, v in params["1"].items():
-        assert np.array_equal(v, params["0"][n]), n
-
-
-@pytest.mark.parametrize("model,precision", [("wav2vec2-base", "fp32"), ("wav2vec2-large", "bf16")])
-def test_dq_inlaunch_bitwise_equals_reduce_pass(monkeypatch, model, precision):
-    """The flash backward's dQ partials combined in-launch by each head's last-arriving key block (dq_combine: release
-    fence, ticket, acquire; SUTA_DQ_INLAUNCH=1, opt-in) against the separate flash_dq_reduce pass (=0, default): both sum the
-    key blocks' partials in block order, so logits and adapted tensors are bitwise equal.  A ragged pair whose longer
-    utterance (T = 474: 15 key groups -> two key blocks per head) exercises the multi-block combination; exact fp32
-    (flash_bwd_kernel) and bf16 planes (flash_bwd_bf16p_kernel)."""
-    cfg = get_config(model)
-    sd = synth_weights(cfg)
-    waves = [synth.wave(152000, 88), synth.wave(64000, 89)]
-    out, params = {}, {}
-    for v in ("1", "0"):
-        monkeypatch.setenv("SUTA_DQ_INLAUNCH", v)
-        eng = SutaEngine(cfg, sd, max_batch=2, max_samples=152000)
-        eng.set_precision(precision)
-        out[v], _, _ = eng.adapt_varlen(waves, 2, SutaHParams(), record=[0, 2])
-        params[v] = {n: eng.get_param(1, n) for n in eng.trainable_names()}
-        eng.close()
-    for r in (0, 2):
         for u in range(2):
             assert np.array_equal(out["1"][r][u], out["0"][r][u]), (r, u)
     for n, v in params["1"].items():
@@ -571,26 +513,20 @@ def test_conv_input_gradients_on_256_tile_bitwise(monkeypatch, form):
         assert np.array_equal(v, params["0"][n]), n
 
 
-@pytest.mark.parametrize("switch", ["SUTA_FLASH_BWD_PIPE", "SUTA_FLASH_BWD_ONEB", "SUTA_CONV_DW_SIDE", "SUTA_DQ_CHAIN"])
+@pytest.mark.parametrize("switch", ["SUTA_FLASH_BWD_ONEB"])
 @pytest.mark.parametrize("model", ["wav2vec2-large", "wav2vec2-base"])
 def test_pipelined_bf16_flash_backward_bitwise(monkeypatch, model, switch):
-    """Two alternative forms of the bf16-plane flash backward against flash_bwd_bf16p_kernel (switch = 0): the
-    software-pipelined one (SUTA_FLASH_BWD_PIPE=1: S of query tile qt + 1 issued under tile qt's exponentials, K / V
-    rows read from LDS, three Q / dO images) and the one-barrier one (SUTA_FLASH_BWD_ONEB=1: double-buffered dS image,
-    the next tile's rows put before the tile's single barrier).  Both do the same operations per element in the same
-    order, so logits and adapted tensors are bitwise equal.  SUTA_CONV_DW_SIDE=1 (the conv stack's weight-gradient
-    GEMMs on a side stream, alternating dz planes) runs the same kernels in another order, and SUTA_DQ_CHAIN (one
-    launch per key block summing dQ into one accumulator in key-block order, the last launch writing dQ and the zero
-    rows past each utterance's length) the reduce pass's sums: bitwise equal as well.  bf16 mode, a ragged batch with T = 399 (13 key groups: two
-    key blocks, a half-empty last query tile), 262 (keys past the length inside a wave) and 49 (one query tile), 2 SUTA
-    steps."""
+    """The one-barrier form of the bf16-plane flash backward (SUTA_FLASH_BWD_ONEB=1, default: double-buffered dS
+    image, the next tile's rows put before the tile's single barrier) against the two-barrier one (=0): the same
+    operations per element in the same order, so logits and adapted tensors are bitwise equal.  bf16 mode, a ragged
+    batch with T = 399 (13 key groups: two key blocks, a half-empty last query tile), 262 (keys past the length inside a
+    wave) and 49 (one query tile), 2 SUTA steps."""
     cfg = get_config(model)
     sd = synth_weights(cfg)
     waves = [synth.wave(n, 70 + i) for i, n in enumerate((128000, 84000, 16000))]
     out, params = {}, {}
     for pipe in ("1", "0"):
-        # (SUTA_DQ_CHAIN=2: the chained launches at this small grid too)
-        monkeypatch.setenv(switch, "2" if (switch == "SUTA_DQ_CHAIN" and pipe == "1") else pipe)
+        monkeypatch.setenv(switch, pipe)
         eng = SutaEngine(cfg, sd, max_batch=3, max_samples=128000)
         eng.set_precision("bf16")
         out[pipe], _, t = eng.adapt_varlen(waves, 2, SutaHParams(), record=[0, 1, 2])

@@ -404,27 +404,3 @@ def test_scheduler_and_sgd_match_reference(variant):
         if not episodic:
             prev = {k[len(f"N{n}/final/"):]: z[k] for k in z.files if k.startswith(f"N{n}/final/")}
     eng.close()
-
-
-def test_pipelined_fp32_flash_forward_bitwise(monkeypatch):
-    """The software-pipelined exact-fp32 flash forward (S of key tile kt + 1 issued before the softmax of tile kt;
-    SUTA_FLASH_FWD_PIPE=1, default) against the unpipelined kernel (=0): the same operations per element in the same
-    order, so logits and adapted tensors are bitwise equal.  Ragged batch whose utterances have 1, 2, 3 and 7 key tiles
-    of 64 (T = 49, 99, 149, 399: the peeled bodies for a last tile, a next-is-last tile and full tiles, half-empty
-    last tiles), 2 SUTA steps (the backward reads the forward's LSE)."""
-    cfg = get_config("wav2vec2-base")
-    sd = synth_weights(cfg)
-    waves = [synth.wave(n, 60 + i) for i, n in enumerate((16000, 32000, 48000, 128000))]
-    out, params = {}, {}
-    for pipe in ("1", "0"):
-        monkeypatch.setenv("SUTA_FLASH_FWD_PIPE", pipe)
-        eng = SutaEngine(cfg, sd, max_batch=4, max_samples=128000)
-        out[pipe], _, t = eng.adapt_varlen(waves, 2, SutaHParams(), record=[0, 1, 2])
-        params[pipe] = {n: eng.get_param(3, n) for n in eng.trainable_names()}
-        eng.close()
-    assert list(t) == [49, 99, 149, 399]
-    for r in (0, 1, 2):
-        for u in range(4):
-            assert np.array_equal(out["1"][r][u], out["0"][r][u]), (r, u)
-    for n, v in params["1"].items():
-        assert np.array_equal(v, params["0"][n]), n

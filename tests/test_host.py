@@ -356,3 +356,19 @@ def test_budget_clamped_to_free_device_memory():
     small = M.clamp_budget(1312.0, base, 16e9)
     assert small < 1312.0 and small * M.workspace_bytes_per_audio_s(base) <= 0.7 * 16e9 + 1
     assert M.clamp_budget(1312.0, base, None) == 1312.0
+
+
+def test_engine_fixed_footprint_counts_weights_planes_and_slots():
+    """The budget clamp first subtracts each engine's fixed device footprint (advisor r5): the fp32 weights, the bf16
+    weight planes in bf16 mode, and per slot the trainable tensors, gradients and Adam moments."""
+    from suta_amd import main as M
+    from suta_amd.weights import synth_weights
+    cfg = get_config("tiny-group")
+    w = synth_weights(cfg)
+    wb = 4.0 * sum(v.size for v in w.values())
+    f1 = M.engine_fixed_bytes(cfg, w, 1)
+    f8 = M.engine_fixed_bytes(cfg, w, 8)
+    assert f1 > wb and f8 > f1
+    slot = (f8 - f1) / 7                                      # 4 fp32 arrays per slot of the trainable tensors
+    assert slot % 16 == 0 and slot > 0
+    assert M.engine_fixed_bytes(cfg, w, 1, "bf16") == pytest.approx(f1 + wb)

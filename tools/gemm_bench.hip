@@ -90,12 +90,12 @@ int main(int argc, char** argv) {
     hipStream_t st; CK(hipStreamCreate(&st));
     hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     const int variants[][2] = {{-1, 1}, {-1, 3}, {0, 3}, {0, 7}, {0, 5}, {0, 6}, {1, 3}, {1, 7},
-                               {3, 3}, {3, 7}, {2, 3}, {2, 7}, {0, 1}, {3, 1}, {-1, 7}, {-1, 8}, {-1, 9}, {-1, 10}, {0, 11}, {4, 11}, {5, 11}, {7, 3}};
+                               {3, 3}, {3, 7}, {2, 3}, {2, 7}, {0, 1}, {3, 1}, {-1, 7}, {-1, 8}, {-1, 9}, {-1, 10}, {0, 11}, {4, 11}, {5, 11}};
     const char* vname[] = {"auto/1buf", "auto/g32x2", "128/g32x2", "128/g64x2", "128/g16x3", "128/g32x3",
                            "128x64/g32x2", "128x64/g64x2", "64/g32x2", "64/g64x2", "64x128/g32", "64x128/g64",
                            "128/1buf", "64/1buf", "auto/g64x2", "auto/v8", "auto/v9", "auto/v10",
-                           "x1-128", "x1-256x128", "x1-128x256", "160x128/g32"};
-    const int NV = 22;
+                           "x1-128", "x1-256x128", "x1-128x256"};
+    const int NV = 21;
     bool check = argc < 2 || atoi(argv[1]) != 0;
     int only_v = argc >= 3 ? atoi(argv[2]) : -1;
     int only_s = argc >= 4 ? atoi(argv[3]) : -1;

@@ -1,9 +1,12 @@
 // bf16-plane GEMM microbenchmark + check on the C4 linear shapes (w2v2-large, M = 164 x 399 rows: bench.py's layout):
 // gemm_hb_kernel (128 x 128), gemm_hbx_kernel (256 x 256 slice ring) with its two epilogue forms (column-per-lane
 // accumulators, and C^T accumulators with 16-B row-per-lane stores).  Variants run interleaved, `rounds` times each (median reported).
-// Build: hipcc -O3 --offload-arch=gfx950 -I test-time-adaptation-asr-suta_amd/csrc -c tools/hb_bench.hip -o /tmp/hb.o
-//        && hipcc --offload-arch=gfx950 /tmp/hb.o test-time-adaptation-asr-suta_amd/csrc/gemm*.o \
-//           test-time-adaptation-asr-suta_amd/csrc/ops.o -o tools/hb_bench
+// Build (the SUTA_HBX_DBG diagnostic forms exist only in this tools build of gemm_hbx.hip, -DSUTA_HBX_DIAG):
+//   C=test-time-adaptation-asr-suta_amd/csrc
+//   hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -DSUTA_HBX_DIAG -c $C/gemm_hbx.hip -o /tmp/gemm_hbx_diag.o
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I $C -c tools/hb_bench.hip -o /tmp/hb.o
+//   hipcc --offload-arch=gfx950 /tmp/hb.o /tmp/gemm_hbx_diag.o $(ls $C/gemm*.o | grep -v gemm_hbx.o) $C/ops.o \
+//         -o tools/hb_bench
 #include <hip/hip_runtime.h>
 #include <cmath>
 #include <cstdio>
@@ -67,7 +70,6 @@ int main(int argc, char** argv) {
     };
     __bf16* Cb;
     CK(hipMalloc(&Cb, (size_t)M * 4096 * 2));
-    setenv("SUTA_HB8_PF", "0", 1);
     for (auto& s : shapes) {
         GemmParams p;
         gemm_init(p);
