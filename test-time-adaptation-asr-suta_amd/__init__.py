@@ -3,7 +3,8 @@
 The hot path (reference main.py:172-215 `forward_and_adapt`, run `steps` times per
 utterance by main.py:347-348) executes in `libsuta.so`: hand-written gfx950 HIP kernels
 behind the C ABI declared in `include/suta.h`.  This package is the Python host:
-ctypes binding (`engine`), the `forward_and_adapt`-compatible shim (`suta`), model
+ctypes binding (`engine`), the `forward_and_adapt`-compatible drop-in (`suta`: the reference loop body of
+main.py:302-348 runs on its objects), model
 geometry (`config`), seeded weights (`weights`), CTC decode / WER (`decode`), and the
 main.py-compatible driver (`main`).
 """

@@ -1190,12 +1190,79 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16_kernel(
 // wave finished before tile qt - 1's barrier; Ss[qt & 1] is rewritten by tile qt + 2 after tile qt + 1's barrier,
 // which every wave reaches only after its dQ reads of tile qt.  Per element the same operations in the same order:
 // bitwise equal to the two-barrier form.
-template <bool ONEB>
-constexpr size_t fbbp_lds_bytes() {
-    return 2 * ((size_t)(64 + (ONEB ? 64 : 32)) * FBB_KB + 2 * 2 * 32 * FB_RS) + 4 * 128;
+//
+// The dS image is KEY-major (round 6; cdna_hip_programming.md section 3, "an accumulator tile whose column index a
+// later product sums over"): the lane holds dS for its key (the lane) and 16 query rows (registers 4a .. 4a + 3 =
+// rows 8a + 4h + 0..3, four consecutive rows), so it stores 4 packed 8-byte words at [its key][8a + 4h] -- 4
+// ds_write_b64 per lane and tile instead of 16 two-byte stores (the former query-major image: 1.87 bank-conflict
+// cycles per LDS instruction).  The dQ product's A operand (16 queries x 32 keys of the 16x16x32 MFMA)
+// is read back with ds_read_b64_tr_b16 (T10: per 16-lane group 4 key rows x 16 query columns delivered column-
+// major).  Rows of 72 B (FBS_RS = 36 bf16): the 16 consecutive keys of a store's lane group land on 16 distinct
+// 2-dword bank pairs (18 k mod 32), and a transposed read's 32-lane half takes the 8 keys {4m + c} of a 32-key
+// chunk (72 m mod 64 = 8 m: 8 disjoint 8-dword windows).  The MFMA's k-slot 8 gg + jj (gg = lane >> 4) therefore
+// holds key fbs_key(gg, jj) of the chunk, and the K^T image stores each chunk's keys in that order (fbs_pos), so the
+// B operand stays one contiguous 16-B read.
+constexpr int FBS_RS = 36;
+__device__ __forceinline__ int fbs_key(int gg, int jj) { return 16 * (gg & 1) + 4 * (jj & 3) + 2 * (gg >> 1) + (jj >> 2); }
+__device__ __forceinline__ int fbs_pos(int kl) {  // inverse of fbs_key within a 32-key chunk
+    const int gg = ((kl >> 4) & 1) | (((kl >> 1) & 1) << 1), jj = ((kl >> 2) & 3) | ((kl & 1) << 2);
+    return 8 * gg + jj;
+}
+
+// The Q / dO row images of the bf16-plane backward (round 6): query row q of a tile at image row fq_row(q) (a
+// permutation of the 5 row bits: image bits 0, 1, 2, 3 = row bits 2, 3, 0, 1), rows padded to FB_RS = 72 bf16.  With
+// rows in natural order the transposed reads were 2-way conflicted (36 r mod 64 puts rows r and r + 2 of a read's four
+// rows on overlapping 16-bank windows); with this order both reads of the tile body are conflict-free (searched over
+// every bit permutation and padded stride):
+//   row reads (prod_rows_q: ds_read_b128, lane l32 -> query l32, 16 B at column 8h + 16s) -- each 16-lane group's 16
+//     rows cover the 64 banks once;
+//   transposed reads (pv_tr_q: ds_read_b64_tr_b16 of queries R0 .. R0 + 3, R0 = 0 mod 4, 16 columns per 32-lane half)
+//     -- the four image rows' 16-dword windows are disjoint mod 64.
+// Rows R0 + 8 and R0 + 16 are image rows fq_row(R0) + 2 and + 16, and a column step is a constant too, so every read
+// is one address register plus an immediate offset.
+__device__ __forceinline__ int fq_row(int q) {
+    return ((q >> 2) & 1) | (((q >> 3) & 1) << 1) | ((q & 1) << 2) | (((q >> 1) & 1) << 3) | (q & 16);
+}
+
+// prod_rows_b on a permuted image
+__device__ __forceinline__ void prod_rows_q(f32x16& acc, const __bf16* __restrict__ L, const RowReg<true>& x, int l32,
+                                            int h) {
+    const __bf16* lr = L + fq_row(l32) * FB_RS + 8 * h;
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const fbf16x8*>(lr + 16 * s), x.v[s], acc, 0,
+                                                      0, 0);
+}
+
+// pv_tr on a permuted image: o[t] += L^T(rows 32t.. = columns of L, contraction over 16 queries from kb) b
+__device__ __forceinline__ void pv_tr_q(f32x16 (&o)[2], const __bf16* __restrict__ L, int kb, const fbf16x8& b,
+                                        int lane) {
+    const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+    const int k0 = kb + 4 * (g >> 1) + q;  // (bit 3 clear: query k0 + 8 is image row fq_row(k0) + 2)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const __bf16* a0 = L + fq_row(k0) * FB_RS + 32 * t + 16 * (g & 1) + 4 * pp;
+        const fbf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_b4p)(a0));
+        const fbf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_b4p)(a0 + 2 * FB_RS));
+        fbf16x8 a;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            a[j] = lo[j];
+            a[4 + j] = hi[j];
+        }
+        o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, o[t], 0, 0, 0);
+    }
 }
 
 template <bool ONEB>
+constexpr size_t fbbp_lds_bytes() {
+    return 2 * ((size_t)64 * FBB_KB + (ONEB ? 2 : 1) * FBB_NW * 32 * FBS_RS + 2 * 2 * 32 * FB_RS) + 4 * 128;
+}
+
+// DG (tools build only, SUTA_FB_DIAG; wrong results): parts of the tile body removed to locate its time -- 1 the dQ
+// product, 2 the softmax / dS arithmetic, 4 the dV / dK products, 8 the S / dP products, 16 the query-tile prefetch,
+// 32 the dS stores.  libsuta.so instantiates DG = 0 only.
+template <bool ONEB, int DG = 0>
 __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
     const __bf16* __restrict__ qkvb, const __bf16* __restrict__ dob, const float* __restrict__ lse,
     const float* __restrict__ delta, float* __restrict__ dqkv, float* __restrict__ dqp, int T, int NH, int H,
@@ -1203,10 +1270,10 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
     constexpr int NW = FBB_NW, NT = NW * 64;
     constexpr int NSS = ONEB ? 2 : 1;             // dS images
     extern __shared__ __attribute__((aligned(16))) __bf16 sm16[];
-    __bf16* Kt = sm16;                            // [64][FBB_KB]   K^T of the block's keys
-    __bf16* Ss = Kt + 64 * FBB_KB;                // [NSS][32][FBB_KB] dS of the query tile
-    __bf16* Qr = Ss + NSS * 32 * FBB_KB;          // [2][32][FB_RS] Q rows
-    __bf16* Dr = Qr + 2 * 32 * FB_RS;             // [2][32][FB_RS] dO rows
+    __bf16* Kt = sm16;                            // [64][FBB_KB]   K^T of the block's keys (fbs_pos order per chunk)
+    __bf16* Ss = Kt + 64 * FBB_KB;                // [NSS][NW * 32][FBS_RS] dS of the query tile, key-major
+    __bf16* Qr = Ss + NSS * NW * 32 * FBS_RS;     // [2][32][FB_RS] Q rows (query q at image row fq_row(q))
+    __bf16* Dr = Qr + 2 * 32 * FB_RS;             // [2][32][FB_RS] dO rows (likewise)
     float* Ls = reinterpret_cast<float*>(Dr + 2 * 32 * FB_RS);  // [2][32]
     float* Dl = Ls + 64;                          // [2][32]
     const int id = xcd_block();
@@ -1242,8 +1309,9 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
         const int row = it >> 3, c8 = (it & 7) * 8, k = kbase + row;
         fbf16x8 x = {};
         if (k < T) x = *reinterpret_cast<const fbf16x8*>(Kb + (long)k * ld + c8);
+        const int pos = (row & ~31) | fbs_pos(row & 31);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) Kt[(c8 + e) * FBB_KB + row] = x[e];
+        for (int e = 0; e < 8; ++e) Kt[(c8 + e) * FBB_KB + pos] = x[e];
     }
     // query-tile copy: threads 0..255 one 16-B chunk of the Q rows, 256..511 one of the dO rows.  Two register
     // stages: the loads of tile qt+2 are issued at the start of tile qt and written to LDS at the end of tile qt+1,
@@ -1263,7 +1331,7 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
         if (threadIdx.x < 64 && qq < T) sg.lr = threadIdx.x < 32 ? lb[qq] : db[qq];
     };
     auto put = [&](int buf, const Stg& sg) {
-        *reinterpret_cast<fbf16x8*>((isq ? Qr : Dr) + (buf * 32 + crow) * FB_RS + ccol) = sg.xr;
+        *reinterpret_cast<fbf16x8*>((isq ? Qr : Dr) + (buf * 32 + fq_row(crow)) * FB_RS + ccol) = sg.xr;
         if (threadIdx.x < 32) Ls[buf * 32 + threadIdx.x] = sg.lr;
         else if (threadIdx.x < 64) Dl[buf * 32 + threadIdx.x - 32] = sg.lr;
     };
@@ -1278,9 +1346,11 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
     const long dq_stride = (long)B * NH * T * 64;
     float* dqb = dqp + kb * dq_stride + (long)bh * T * 64;
     const int nqt = (tl + 31) >> 5;
-    if (!active && w < ngb)
-        for (int r = 0; r < NSS * 32; ++r)
-            if (h == 0) Ss[r * FBB_KB + 32 * w + l32] = (__bf16)0.f;
+    if (!active && w < ngb)  // keys past the length: zero dS rows in every image
+        for (int i = 0; i < NSS; ++i)
+#pragma unroll
+            for (int c = 0; c < 32; c += 8)
+                *reinterpret_cast<fbf16x4*>(Ss + (i * NW * 32 + 32 * w + l32) * FBS_RS + c + 4 * h) = fbf16x4{};
     Stg sa, sb;
     fetch(0, sa);
     put(0, sa);
@@ -1289,15 +1359,19 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
     // (the dQ product's K^T fragments are read from the K^T image per tile: holding them in registers, 32 VGPRs,
     // made the two-stage prefetch spill)
     const __bf16* kfrow = Kt + (16 * di + l16) * FBB_KB + 8 * g;
-    // the lane's dS column in the tile image: row r8(v, h), key 32 w + l32
+    // the dQ A operand's transposed reads: lane 4 q' + p of 16-lane group g reads key rows fbs_key(g, q') and
+    // fbs_key(g, 4 + q') of each 32-key chunk, query columns 16 qi + 4 p .. + 3
+    const int trq = (lane >> 2) & 3, trp = lane & 3;
+    const int tr_off0 = fbs_key(g, trq) * FBS_RS + 16 * qi + 4 * trp;
+    const int tr_off1 = fbs_key(g, 4 + trq) * FBS_RS + 16 * qi + 4 * trp;
     // tile qt: fetch tile qt+2 into fx (its previous content, tile qt, is in LDS), put tile qt+1 from py; BUF = qt & 1
     // as a constant (the two unrolled instances), so the LDS image addresses fold
     auto tile = [&](int qt, Stg& fx, const Stg& py, auto buf_tag) {
         constexpr int buf = decltype(buf_tag)::value;
-        __bf16* const Sb = Ss + (ONEB ? buf : 0) * 32 * FBB_KB;  // this tile's dS image
-        __bf16* const srow = Sb + 32 * w + l32;
+        __bf16* const Sb = Ss + (ONEB ? buf : 0) * NW * 32 * FBS_RS;  // this tile's dS image (key-major)
+        __bf16* const srow = Sb + (32 * w + l32) * FBS_RS + 4 * h;       // the lane's key row, its half's columns
         const int q0 = qt * 32;
-        if (qt + 2 < nqt) fetch(qt + 2, fx);
+        if (!(DG & 16) && qt + 2 < nqt) fetch(qt + 2, fx);
         const float* Lt = Ls + buf * 32;
         const float* Dlt = Dl + buf * 32;
         if (active) {
@@ -1306,14 +1380,17 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
             f32x16 s, dp;
 #pragma unroll
             for (int v = 0; v < 16; ++v) s[v] = dp[v] = 0.f;
-            prod_rows_b(s, Qt, kv, l32, h);
-            prod_rows_b(dp, Dt, vv, l32, h);
+            if constexpr (!(DG & 8)) {
+                prod_rows_q(s, Qt, kv, l32, h);
+                prod_rows_q(dp, Dt, vv, l32, h);
+            }
             f32x4 lq[4], dq[4];
 #pragma unroll
             for (int a = 0; a < 4; ++a) {
                 lq[a] = *reinterpret_cast<const f32x4*>(Lt + 8 * a + 4 * h);
                 dq[a] = *reinterpret_cast<const f32x4*>(Dlt + 8 * a + 4 * h);
             }
+            if constexpr (!(DG & 2)) {
 #pragma unroll
             for (int v = 0; v < 16; ++v) s[v] = __builtin_amdgcn_exp2f(fmaf(s[v], sl2, -LOG2E * lq[v >> 2][v & 3]));
             if (!kall || q0 + 32 > T) {  // keys past the length, query rows past T: probability 0
@@ -1324,38 +1401,51 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
             }
 #pragma unroll
             for (int v = 0; v < 16; ++v) dp[v] = scale * (s[v] * (dp[v] - dq[v >> 2][v & 3]));
+            }
             fbf16x8 pb[2], sb[2];
 #pragma unroll
             for (int v = 0; v < 16; ++v) {
                 pb[v >> 3][v & 7] = (__bf16)s[v];
                 sb[v >> 3][v & 7] = (__bf16)dp[v];
             }
+            if constexpr (!(DG & 4)) {
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
-                pv_tr<FB_RS>(dv, Dt, 16 * c, pb[c], lane);  // dV^T += dO^T P
-                pv_tr<FB_RS>(dk, Qt, 16 * c, sb[c], lane);  // dK^T += Q^T dS
+                pv_tr_q(dv, Dt, 16 * c, pb[c], lane);  // dV^T += dO^T P
+                pv_tr_q(dk, Qt, 16 * c, sb[c], lane);  // dK^T += Q^T dS
             }
-            // dS into LDS: the lane's 16 query rows of its key column, 2-byte stores of the packed bf16 pairs (low /
-            // high halves), no lane exchange
+            }
+            // dS into the key-major image: registers 4a .. 4a + 3 (query rows 8a + 4h + 0..3) as one 8-byte store each
 #pragma unroll
-            for (int v = 0; v < 16; v += 2) {
-                srow[r8(v, h) * FBB_KB] = sb[v >> 3][v & 7];
-                srow[r8(v + 1, h) * FBB_KB] = sb[v >> 3][(v & 7) + 1];
+            for (int a = 0; a < 4; ++a) {
+                if constexpr (DG & 32) break;
+                fbf16x4 w4;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) w4[e] = sb[a >> 1][4 * (a & 1) + e];
+                *reinterpret_cast<fbf16x4*>(srow + 8 * a) = w4;
             }
         }
         if constexpr (ONEB) {
             if (qt + 1 < nqt) put(buf ^ 1, py);  // published by the barrier below
         }
         __syncthreads();  // dS tile complete
-        {
-            const __bf16* ar = Sb + (16 * qi + l16) * FBB_KB + 8 * g;
+        if constexpr (!(DG & 1)) {
             f32x4 c[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
             for (int j = 0; j < 8; ++j)
-                if (32 * j < kq)
+                if (32 * j < kq) {  // (wave-uniform: EXEC stays all ones for the transposed reads)
+                    const __bf16* a0 = Sb + 32 * j * FBS_RS;
+                    const fbf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_b4p)(a0 + tr_off0));
+                    const fbf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_b4p)(a0 + tr_off1));
+                    fbf16x8 a;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        a[e] = lo[e];
+                        a[4 + e] = hi[e];
+                    }
                     c[j & 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                        *reinterpret_cast<const fbf16x8*>(ar + 32 * j),
-                        *reinterpret_cast<const fbf16x8*>(kfrow + 32 * j), c[j & 1], 0, 0, 0);
+                        a, *reinterpret_cast<const fbf16x8*>(kfrow + 32 * j), c[j & 1], 0, 0, 0);
+                }
             const f32x4 c0 = c[0], c1 = c[1];
             float* dr = dqb + (long)(q0 + 16 * qi + 4 * g) * 64 + 16 * di + l16;
 #pragma unroll
@@ -1499,13 +1589,22 @@ static void flash_bwd_go(dim3 grid, hipStream_t st, const float* qkv, const floa
                        T, NH, H, scale, tlen, nkb, gpb, B, dqkvb);
 }
 
-template <bool ONEB>
+template <bool ONEB, int DG = 0>
 static void flash_bwd_bf16p_go(dim3 grid, hipStream_t st, const void* qkvb, const void* dctxb, const float* lse,
                                const float* delta, float* dqkv, float* dqp, int T, int NH, int H, float scale,
                                const int* tlen, int nkb, int gpb, int B, __bf16* dqkvb) {
+#ifdef SUTA_FB_DIAG
+    if constexpr (DG == 0) {  // tools build: SUTA_FB_DIAG=<bits> selects a diagnostic form (wrong results)
+        const char* e = std::getenv("SUTA_FB_DIAG");
+        const int dg = e ? atoi(e) : 0;
+#define FBD(D_) if (dg == D_) return flash_bwd_bf16p_go<ONEB, D_>(grid, st, qkvb, dctxb, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb)
+        FBD(1); FBD(2); FBD(4); FBD(8); FBD(16); FBD(32); FBD(3); FBD(7); FBD(15); FBD(31); FBD(63); FBD(14); FBD(6);
+#undef FBD
+    }
+#endif
     constexpr size_t lds = fbbp_lds_bytes<ONEB>();
-    set_max_lds_once(reinterpret_cast<const void*>(&flash_bwd_bf16p_kernel<ONEB>), lds, "flash_bwd_bf16p_kernel");
-    hipLaunchKernelGGL(flash_bwd_bf16p_kernel<ONEB>, grid, dim3(FBB_NW * 64), lds, st,
+    set_max_lds_once(reinterpret_cast<const void*>(&flash_bwd_bf16p_kernel<ONEB, DG>), lds, "flash_bwd_bf16p_kernel");
+    hipLaunchKernelGGL((flash_bwd_bf16p_kernel<ONEB, DG>), grid, dim3(FBB_NW * 64), lds, st,
                        reinterpret_cast<const __bf16*>(qkvb), reinterpret_cast<const __bf16*>(dctxb), lse, delta, dqkv,
                        dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb);
 }
