@@ -1183,7 +1183,7 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16_kernel(
 // (ds_read_b64_tr_b16 transposed reads, as the forward's PV): no transposed tiles are written.  Masks only
 // on a wave whose keys pass the utterance's length or on a query tile past T.
 //
-// ONEB (SUTA_FLASH_BWD_ONEB): one barrier per query tile instead of two.  The dS image is double-buffered (tile qt
+// One barrier per query tile (round 5; the two-barrier form was removed in round 6).  The dS image is double-buffered (tile qt
 // writes Ss[qt & 1]) and tile qt + 1's Q / dO rows are put into their image BEFORE tile qt's barrier, so that one
 // barrier both completes tile qt's dS image (RAW for its dQ) and publishes tile qt + 1 (RAW for its S / dP).  WAR:
 // the Q / dO image tile qt + 1 overwrites held tile qt - 1, whose last reads (its S / dP / dV / dK products) every
@@ -1254,21 +1254,21 @@ __device__ __forceinline__ void pv_tr_q(f32x16 (&o)[2], const __bf16* __restrict
     }
 }
 
-template <bool ONEB>
 constexpr size_t fbbp_lds_bytes() {
-    return 2 * ((size_t)64 * FBB_KB + (ONEB ? 2 : 1) * FBB_NW * 32 * FBS_RS + 2 * 2 * 32 * FB_RS) + 4 * 128;
+    return 2 * ((size_t)64 * FBB_KB + 2 * FBB_NW * 32 * FBS_RS + 2 * 2 * 32 * FB_RS) + 4 * 128;
 }
+constexpr int FBB_DKS = 72;  // bf16 row stride of the dK / dV staging images at the end of the kernel
 
 // DG (tools build only, SUTA_FB_DIAG; wrong results): parts of the tile body removed to locate its time -- 1 the dQ
 // product, 2 the softmax / dS arithmetic, 4 the dV / dK products, 8 the S / dP products, 16 the query-tile prefetch,
-// 32 the dS stores.  libsuta.so instantiates DG = 0 only.
-template <bool ONEB, int DG = 0>
+// 32 the dS stores, 64 the K^T image, 128 the dK / dV stores.  libsuta.so instantiates DG = 0 only.
+template <int DG = 0>
 __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
     const __bf16* __restrict__ qkvb, const __bf16* __restrict__ dob, const float* __restrict__ lse,
     const float* __restrict__ delta, float* __restrict__ dqkv, float* __restrict__ dqp, int T, int NH, int H,
     float scale, const int* __restrict__ tlen, int nkb, int gpb, int B, __bf16* __restrict__ dqkvb) {
     constexpr int NW = FBB_NW, NT = NW * 64;
-    constexpr int NSS = ONEB ? 2 : 1;             // dS images
+    constexpr int NSS = 2;                        // dS images (one barrier per query tile)
     extern __shared__ __attribute__((aligned(16))) __bf16 sm16[];
     __bf16* Kt = sm16;                            // [64][FBB_KB]   K^T of the block's keys (fbs_pos order per chunk)
     __bf16* Ss = Kt + 64 * FBB_KB;                // [NSS][NW * 32][FBS_RS] dS of the query tile, key-major
@@ -1305,7 +1305,7 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
             vv.v[s] = *reinterpret_cast<const fbf16x8*>(Vb + kr + 16 * s);
         }
     }
-    for (int it = threadIdx.x; it < ngb * 32 * 8; it += NT) {  // K^T image of the block's keys (0 past T)
+    for (int it = threadIdx.x; it < ((DG & 64) ? 0 : ngb * 32 * 8); it += NT) {  // K^T image of the block's keys
         const int row = it >> 3, c8 = (it & 7) * 8, k = kbase + row;
         fbf16x8 x = {};
         if (k < T) x = *reinterpret_cast<const fbf16x8*>(Kb + (long)k * ld + c8);
@@ -1343,8 +1343,9 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
     const int g = lane >> 4, l16 = lane & 15;
     const int qi = w & 1, di = w >> 1;
     const int kq = ngb * 32;
-    const long dq_stride = (long)B * NH * T * 64;
-    float* dqb = dqp + kb * dq_stride + (long)bh * T * 64;
+    const int NQT = (T + 31) >> 5;                     // query tiles of the layout
+    const long dq_stride = (long)B * NH * NQT * 2048;  // one key block's partials: [B * NH][NQT][NW][64 lanes][4]
+    float* dqb = dqp + kb * dq_stride + (long)bh * NQT * 2048;
     const int nqt = (tl + 31) >> 5;
     if (!active && w < ngb)  // keys past the length: zero dS rows in every image
         for (int i = 0; i < NSS; ++i)
@@ -1368,7 +1369,7 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
     // as a constant (the two unrolled instances), so the LDS image addresses fold
     auto tile = [&](int qt, Stg& fx, const Stg& py, auto buf_tag) {
         constexpr int buf = decltype(buf_tag)::value;
-        __bf16* const Sb = Ss + (ONEB ? buf : 0) * NW * 32 * FBS_RS;  // this tile's dS image (key-major)
+        __bf16* const Sb = Ss + buf * NW * 32 * FBS_RS;  // this tile's dS image (key-major)
         __bf16* const srow = Sb + (32 * w + l32) * FBS_RS + 4 * h;       // the lane's key row, its half's columns
         const int q0 = qt * 32;
         if (!(DG & 16) && qt + 2 < nqt) fetch(qt + 2, fx);
@@ -1425,9 +1426,7 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
                 *reinterpret_cast<fbf16x4*>(srow + 8 * a) = w4;
             }
         }
-        if constexpr (ONEB) {
-            if (qt + 1 < nqt) put(buf ^ 1, py);  // published by the barrier below
-        }
+        if (qt + 1 < nqt) put(buf ^ 1, py);  // published by the barrier below
         __syncthreads();  // dS tile complete
         if constexpr (!(DG & 1)) {
             f32x4 c[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
@@ -1446,15 +1445,9 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
                     c[j & 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                         a, *reinterpret_cast<const fbf16x8*>(kfrow + 32 * j), c[j & 1], 0, 0, 0);
                 }
-            const f32x4 c0 = c[0], c1 = c[1];
-            float* dr = dqb + (long)(q0 + 16 * qi + 4 * g) * 64 + 16 * di + l16;
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                if (q0 + 16 * qi + 4 * g + r < T) dr[r * 64] = c0[r] + c1[r];
-        }
-        if constexpr (!ONEB) {
-            if (qt + 1 < nqt) put(buf ^ 1, py);
-            __syncthreads();
+            // the block's dQ partial of this tile in fragment order (flash_dq_reduce_frag transposes): one 16-B store
+            // per lane, the wave's 1 KB contiguous (the row layout took four stores of 64-B pieces)
+            *reinterpret_cast<f32x4*>(dqb + ((long)qt * NW + w) * 256 + lane * 4) = c[0] + c[1];
         }
     };
     using B0 = std::integral_constant<int, 0>;
@@ -1465,33 +1458,67 @@ __global__ __launch_bounds__(FBB_NW * 64, 1) void flash_bwd_bf16p_kernel(
         tile(qt + 1, sb, sa, B1{});
     }
     if (qt < nqt) tile(qt, sa, sb, B0{});
-    if (w < ngb && key < T) {  // dK, dV rows of this wave's keys
+    // dK, dV rows of this wave's keys.  fp32 (when requested; in bf16 mode null when only the bf16 plane is read, the
+    // QKV input-gradient GEMM): direct 16-B stores
+    if (!(DG & 128) && dqkv && w < ngb && key < T) {
         float* dkr = dqkv + ((long)u * T + key) * ld + H + hd * 64 + 4 * h;
         float* dvr = dkr + H;
-    #pragma unroll
+#pragma unroll
         for (int t = 0; t < 2; ++t)
-    #pragma unroll
+#pragma unroll
             for (int a = 0; a < 4; ++a) {
                 f32x4 x, y;
-    #pragma unroll
+#pragma unroll
                 for (int b = 0; b < 4; ++b) {
                     x[b] = dk[t][4 * a + b];
                     y[b] = dv[t][4 * a + b];
                 }
-                if (dqkv) {  // null in bf16 mode when only the bf16 plane is read (the QKV input-gradient GEMM)
-                    *reinterpret_cast<f32x4*>(dkr + 32 * t + 8 * a) = x;
-                    *reinterpret_cast<f32x4*>(dvr + 32 * t + 8 * a) = y;
+                *reinterpret_cast<f32x4*>(dkr + 32 * t + 8 * a) = x;
+                *reinterpret_cast<f32x4*>(dvr + 32 * t + 8 * a) = y;
+            }
+    }
+    // the bf16 plane: each wave's 32 x 64 dK and dV tiles staged through LDS (rows of FBB_DKS; the K^T / dS / Q / dO
+    // images are free once every wave is past the last tile's dQ reads) and stored as whole 128-B rows, 16 B per lane
+    // (the accumulator layout gave 8-byte stores one 6-KB row apart: ~0.1 ms of a 0.8-ms C4 layer backward,
+    // tools/attn_bench SUTA_FB_DIAG=128)
+    if (!(DG & 128) && dqkvb) {
+        static_assert(FBB_NW * 2 * 32 * FBB_DKS <= 64 * FBB_KB + 2 * FBB_NW * 32 * FBS_RS + 4 * 32 * FB_RS,
+                      "dK / dV staging must fit the K^T, dS and Q / dO images");
+        __syncthreads();
+        __bf16* const stk = sm16 + w * 2 * 32 * FBB_DKS;  // this wave's dK image [32][FBB_DKS], then its dV image
+        __bf16* const stv = stk + 32 * FBB_DKS;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int a = 0; a < 4; ++a) {
+                fbf16x4 x, y;
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    x[b] = (__bf16)dk[t][4 * a + b];
+                    y[b] = (__bf16)dv[t][4 * a + b];
                 }
-                if (dqkvb) {
-                    __bf16* kb2 = dqkvb + ((long)u * T + key) * ld + H + hd * 64 + 4 * h + 32 * t + 8 * a;
-                    *reinterpret_cast<fbf16x4*>(kb2) = cvt4(x);
-                    *reinterpret_cast<fbf16x4*>(kb2 + H) = cvt4(y);
+                *reinterpret_cast<fbf16x4*>(stk + l32 * FBB_DKS + 32 * t + 8 * a + 4 * h) = x;
+                *reinterpret_cast<fbf16x4*>(stv + l32 * FBB_DKS + 32 * t + 8 * a + 4 * h) = y;
+            }
+        __syncthreads();
+        if (w < ngb) {
+            __bf16* const ob = dqkvb + (long)u * T * ld + H + hd * 64;
+#pragma unroll
+            for (int it = 0; it < 4; ++it) {  // 8 rows x 8 chunks of 16 B per instruction
+                const int r = 8 * it + (lane >> 3), c8 = (lane & 7) * 8, k2 = kbase + 32 * w + r;
+                const fbf16x8 x = *reinterpret_cast<const fbf16x8*>(stk + r * FBB_DKS + c8);
+                const fbf16x8 y = *reinterpret_cast<const fbf16x8*>(stv + r * FBB_DKS + c8);
+                if (k2 < T) {
+                    *reinterpret_cast<fbf16x8*>(ob + ((unsigned)k2 * (unsigned)ld + c8)) = x;
+                    *reinterpret_cast<fbf16x8*>(ob + ((unsigned)k2 * (unsigned)ld + H + c8)) = y;
                 }
             }
+        }
     }
 }
 
-// dQ = sum over key blocks in order (query rows < tl; rows past it get 0, as their dS is 0)
+// dQ = sum over key blocks in order (query rows < tl; rows past it get 0, as their dS is 0).  Row-layout partials
+// (flash_bwd_kernel, flash_bwd_bf16_kernel): one thread per 4 columns of a row.
 __global__ __launch_bounds__(256) void flash_dq_reduce(const float* __restrict__ dqp, float* __restrict__ dqkv, int B,
                                                        int T, int NH, int H, int nkb, const int* __restrict__ tlen,
                                                        __bf16* __restrict__ dqkvb) {
@@ -1519,6 +1546,51 @@ __global__ __launch_bounds__(256) void flash_dq_reduce(const float* __restrict__
     }
 }
 
+// The same for the fragment-order partials of flash_bwd_bf16p_kernel ([kb][B * NH][NQT][8 waves][64 lanes][4]: lane
+// (g, l16) of wave w = qi + 2 di holds rows 16 qi + 4 g + 0..3, column 16 di + l16 of its 32 x 64 tile): one block per
+// (head, query tile) sums the key blocks' 8-KB tiles in key-block order (per element the row-layout pass's order, so
+// the results are bitwise the same), transposes them through LDS and writes the tile's dQ rows whole.
+__global__ __launch_bounds__(256) void flash_dq_reduce_frag(const float* __restrict__ dqp, float* __restrict__ dqkv,
+                                                            int B, int T, int NH, int H, int nkb,
+                                                            const int* __restrict__ tlen, __bf16* __restrict__ dqkvb) {
+    __shared__ __attribute__((aligned(16))) float tile[32][64 + 4];
+    const int NQT = (T + 31) >> 5;
+    const long bt = blockIdx.x;  // bh * NQT + qt
+    const int qt = (int)(bt % NQT);
+    const long bh = bt / NQT;
+    const int hd = (int)(bh % NH), u = (int)(bh / NH);
+    const int tl = tlen ? tlen[u] : T;
+    const int q0 = qt * 32;
+    if (q0 < tl) {  // (block-uniform)
+        const long stride = (long)B * NH * NQT * 2048;
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            const int f = half * 256 + threadIdx.x;  // fragment = wave * 64 + lane
+            const f32x4* p = reinterpret_cast<const f32x4*>(dqp + bt * 2048) + f;
+            f32x4 s = {0.f, 0.f, 0.f, 0.f};
+            for (int k = 0; k < nkb; ++k) s += p[k * (stride / 4)];
+            const int wv = f >> 6, ln = f & 63, qi = wv & 1, di = wv >> 1, g = ln >> 4, l16 = ln & 15;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) tile[16 * qi + 4 * g + r][16 * di + l16] = s[r];
+        }
+    }
+    __syncthreads();
+    // 32 rows x 64 columns: thread -> row threadIdx / 8, columns (threadIdx % 8) * 8 .. + 7
+    const int r = threadIdx.x >> 3, c8 = (threadIdx.x & 7) * 8, q = q0 + r;
+    if (q >= T) return;
+    f32x4 lo = {0.f, 0.f, 0.f, 0.f}, hi = {0.f, 0.f, 0.f, 0.f};
+    if (q < tl) {
+        lo = *reinterpret_cast<const f32x4*>(&tile[r][c8]);
+        hi = *reinterpret_cast<const f32x4*>(&tile[r][c8 + 4]);
+    }
+    const long o = ((long)u * T + q) * 3 * H + hd * 64 + c8;
+    if (dqkv) {
+        *reinterpret_cast<f32x4*>(dqkv + o) = lo;
+        *reinterpret_cast<f32x4*>(dqkv + o + 4) = hi;
+    }
+    if (dqkvb) *reinterpret_cast<fbf16x8*>(dqkvb + o) = cvt8(lo, hi);
+}
+
 }  // namespace
 
 constexpr int FF_NW = 4;
@@ -1538,7 +1610,9 @@ static bool fb_img() { return suta_switches().flash_bf16_img != 0; }
 
 long flash_dq_scratch_floats(int B, int T, int NH) {
     const int ng = (T + 31) / 32, nkb = (ng + fb_nw() - 1) / fb_nw();
-    return (long)nkb * B * NH * T * 64 + 64;  // the per-key-block dQ partials
+    // the per-key-block dQ partials (row layout: T rows per head; fragment layout of the bf16-plane kernel: whole
+    // 32-row query tiles)
+    return (long)nkb * B * NH * ((T + 31) / 32) * 32 * 64 + 64;
 }
 
 // bf16 mode, bf16 qkv plane given: flash_fwd_bf16p_kernel (env SUTA_FLASH_FWD_PLANE=0 keeps the fp32-row
@@ -1589,7 +1663,7 @@ static void flash_bwd_go(dim3 grid, hipStream_t st, const float* qkv, const floa
                        T, NH, H, scale, tlen, nkb, gpb, B, dqkvb);
 }
 
-template <bool ONEB, int DG = 0>
+template <int DG = 0>
 static void flash_bwd_bf16p_go(dim3 grid, hipStream_t st, const void* qkvb, const void* dctxb, const float* lse,
                                const float* delta, float* dqkv, float* dqp, int T, int NH, int H, float scale,
                                const int* tlen, int nkb, int gpb, int B, __bf16* dqkvb) {
@@ -1597,14 +1671,15 @@ static void flash_bwd_bf16p_go(dim3 grid, hipStream_t st, const void* qkvb, cons
     if constexpr (DG == 0) {  // tools build: SUTA_FB_DIAG=<bits> selects a diagnostic form (wrong results)
         const char* e = std::getenv("SUTA_FB_DIAG");
         const int dg = e ? atoi(e) : 0;
-#define FBD(D_) if (dg == D_) return flash_bwd_bf16p_go<ONEB, D_>(grid, st, qkvb, dctxb, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb)
+#define FBD(D_) if (dg == D_) return flash_bwd_bf16p_go<D_>(grid, st, qkvb, dctxb, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb)
         FBD(1); FBD(2); FBD(4); FBD(8); FBD(16); FBD(32); FBD(3); FBD(7); FBD(15); FBD(31); FBD(63); FBD(14); FBD(6);
+        FBD(64); FBD(128); FBD(127); FBD(191); FBD(255);
 #undef FBD
     }
 #endif
-    constexpr size_t lds = fbbp_lds_bytes<ONEB>();
-    set_max_lds_once(reinterpret_cast<const void*>(&flash_bwd_bf16p_kernel<ONEB, DG>), lds, "flash_bwd_bf16p_kernel");
-    hipLaunchKernelGGL((flash_bwd_bf16p_kernel<ONEB, DG>), grid, dim3(FBB_NW * 64), lds, st,
+    constexpr size_t lds = fbbp_lds_bytes();
+    set_max_lds_once(reinterpret_cast<const void*>(&flash_bwd_bf16p_kernel<DG>), lds, "flash_bwd_bf16p_kernel");
+    hipLaunchKernelGGL((flash_bwd_bf16p_kernel<DG>), grid, dim3(FBB_NW * 64), lds, st,
                        reinterpret_cast<const __bf16*>(qkvb), reinterpret_cast<const __bf16*>(dctxb), lse, delta, dqkv,
                        dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb);
 }
@@ -1632,12 +1707,10 @@ bool launch_flash_bwd(const float* qkv, const float* dctx, const float* lse, con
     if (on_planes) {
         if ((reinterpret_cast<uintptr_t>(qkvb) | reinterpret_cast<uintptr_t>(dctxb)) & 15)
             throw std::invalid_argument("flash_bwd: bf16 planes not 16-B aligned");
-        if (suta_switches().flash_bwd_oneb)
-            flash_bwd_bf16p_go<true>(grid, st, qkvb, dctxb, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B,
-                                     dqkvb);
-        else
-            flash_bwd_bf16p_go<false>(grid, st, qkvb, dctxb, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B,
-                                      dqkvb);
+        flash_bwd_bf16p_go(grid, st, qkvb, dctxb, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb);
+        hipLaunchKernelGGL(flash_dq_reduce_frag, dim3((unsigned)((long)B * NH * ((T + 31) / 32))), dim3(256), 0, st, dqp,
+                           dqkv, B, T, NH, H, nkb, tlen, dqkvb);
+        return true;
     } else if (bf16 && nw == FBB_NW && fb_img()) {
         constexpr size_t lds = fbb_lds_bytes();
         set_max_lds_once(reinterpret_cast<const void*>(&flash_bwd_bf16_kernel), lds, "flash_bwd_bf16_kernel");

@@ -90,8 +90,6 @@ struct SutaSwitches {
                           // 0 = the column-per-lane form shared with the 128 x 128 kernel
     int hbp_conv;         // SUTA_HBP_CONV (default 1): the conv stack's conv-seg input gradients on the four-phase 256 x 256
                           // kernel (gemm.hip use_hbp_conv); 0 = the 128 x 128 kernel
-    int flash_bwd_oneb;   // SUTA_FLASH_BWD_ONEB (default 1): the bf16-plane flash backward with one barrier per query tile (dS
-                          // image double-buffered, the next tile's Q / dO put before the barrier); bitwise equal; 0 = two
     int epi_fast;         // SUTA_EPI_FAST (default 1): 32-bit-offset GEMM epilogue where every operand fits 4 GiB (p.off32);
                           // 0 = the general epilogue everywhere
 };

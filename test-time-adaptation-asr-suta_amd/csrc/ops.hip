@@ -1947,9 +1947,6 @@ void suta_latch_switches() {
     s.flash_fwd_nw = (fnw && atoi(fnw) == 8) ? 8 : 4;
     s.epi_fast = on("SUTA_EPI_FAST");
     s.hbp_conv = on("SUTA_HBP_CONV");
-    // one barrier per query tile in the bf16-plane flash backward: C4 attention 543-546 -> 534-535 ms per call, same box
-    // (profiles/r5/oneb_ab.txt); =0 the two-barrier form
-    s.flash_bwd_oneb = on("SUTA_FLASH_BWD_ONEB");
     s.latched = 1;
     g_switches = s;
 }
