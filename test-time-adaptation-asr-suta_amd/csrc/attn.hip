@@ -466,8 +466,9 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void flash_bwd_kernel(
         for (int v = 0; v < 16; ++v) dv[t][v] = dk[t][v] = 0.f;
     const int g = lane >> 4, l16 = lane & 15;
     const int kq = ngb * 32;  // contraction length of the dQ product
-    const long dq_stride = (long)B * NH * T * 64;
-    float* dqb = dqp + kb * dq_stride + (long)bh * T * 64;
+    const int NQT = (T + 31) >> 5;                     // query tiles of the layout
+    const long dq_stride = (long)B * NH * NQT * 2048;  // one key block's partials: [B * NH][NQT][8 sub-tiles][64][4]
+    float* dqb = dqp + kb * dq_stride + (long)bh * NQT * 2048;
 
     const int nqt = (tl + 31) >> 5;  // query tiles past the length: dO rows are 0, nothing to add
     if (!active && w < ngb)         // keys past the length: their dS columns stay 0 for the dQ product
@@ -553,10 +554,9 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void flash_bwd_kernel(
                     c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c0, 0, 0, 0);
                 }
             }
-            float* dr = dqb + (long)(q0 + 16 * qi + 4 * g) * 64 + 16 * di + l16;
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                if (q0 + 16 * qi + 4 * g + r < T) dr[r * 64] = c0[r] + c1[r];
+            // the block's dQ partial of sub-tile st in fragment order (flash_dq_reduce_frag transposes): one 16-B
+            // store per lane, 1 KB contiguous per wave
+            *reinterpret_cast<f32x4*>(dqb + ((long)qt * 8 + st) * 256 + lane * 4) = c0 + c1;
         }
         if (qt + 1 < nqt) put(buf ^ 1, py);
         __syncthreads();  // next tile visible; dS tile free
@@ -1716,12 +1716,18 @@ bool launch_flash_bwd(const float* qkv, const float* dctx, const float* lse, con
         set_max_lds_once(reinterpret_cast<const void*>(&flash_bwd_bf16_kernel), lds, "flash_bwd_bf16_kernel");
         hipLaunchKernelGGL(flash_bwd_bf16_kernel, grid, dim3(FBB_NW * 64), lds, st, qkv, dctx, lse, delta, dqkv, dqp,
                            T, NH, H, scale, tlen, nkb, gpb, B, dqkvb);
-    } else if (nw == 4) {
-        if (bf16) flash_bwd_go<4, true>(grid, st, qkv, dctx, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb);
-        else flash_bwd_go<4, false>(grid, st, qkv, dctx, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb);
     } else {
-        if (bf16) flash_bwd_go<8, true>(grid, st, qkv, dctx, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb);
-        else flash_bwd_go<8, false>(grid, st, qkv, dctx, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb);
+        // flash_bwd_kernel: dQ partials in fragment order, as the bf16-plane kernel's
+        if (nw == 4) {
+            if (bf16) flash_bwd_go<4, true>(grid, st, qkv, dctx, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb);
+            else flash_bwd_go<4, false>(grid, st, qkv, dctx, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb);
+        } else {
+            if (bf16) flash_bwd_go<8, true>(grid, st, qkv, dctx, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb);
+            else flash_bwd_go<8, false>(grid, st, qkv, dctx, lse, delta, dqkv, dqp, T, NH, H, scale, tlen, nkb, gpb, B, dqkvb);
+        }
+        hipLaunchKernelGGL(flash_dq_reduce_frag, dim3((unsigned)((long)B * NH * ((T + 31) / 32))), dim3(256), 0, st, dqp,
+                           dqkv, B, T, NH, H, nkb, tlen, dqkvb);
+        return true;
     }
     const long n4 = (long)B * NH * T * 16;
     hipLaunchKernelGGL(flash_dq_reduce, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, dqp, dqkv, B, T, NH, H,
