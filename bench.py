@@ -47,7 +47,7 @@ HBM_PEAK_TBS = 8.0             # MI355X_MICROARCH.md: HBM3E peak
 RECORD = [0, 1, 3, 5, 10]
 C4_RECORD = [0, 1, 5, 10, 20]   # config C4 (20 steps): greedy ids recorded at these steps
 # newest committed rocprofv3 PMC reduction of each workload (tools/pmc_traffic.py; profiles/<round>/README.md)
-ROUNDS = ("r5", "r4", "r3", "r2", "r1")
+ROUNDS = ("r6", "r5", "r4", "r3", "r2", "r1")
 PMC_TRAFFIC = next((p for p in (os.path.join(ROOT, "profiles", r, "pmc_traffic.json") for r in ROUNDS)
                     if os.path.exists(p)), None)
 PMC_TRAFFIC_C4 = next((p for p in (os.path.join(ROOT, "profiles", r, "pmc_traffic_c4.json") for r in ROUNDS)
@@ -61,16 +61,17 @@ PMC_BATCH = 164    # the batch the committed headline PMC passes were taken at
 PMC_BATCH_C4 = 164  # the batch of the committed C4 passes
 C5_UTTERANCES = 512  # config C5: a TED-LIUM-3-test-sized seeded length mix (see --c5-n; ~30 s per pass)
 GEMM_KERNELS = ("gemm_glds_kernel", "gemm_f32_kernel", "gemm_splitk_reduce", "attn_fwd_kernel", "attn_bwd_kernel",
-                "posconv_kernel", "flash_fwd_kernel", "flash_bwd_kernel", "flash_dq_reduce")
+                "posconv_kernel", "flash_fwd_kernel", "flash_bwd_kernel", "flash_dq_reduce", "flash_dq_reduce_frag")
 # config C4's GEMM family (bf16 mode): every kernel its "gemm" + "attention" timing families launch.  Matched to the
 # PMC table by base name (pmc_kernel_bytes: the trace may hold mangled names).
 GEMM_KERNELS_C4 = ("gemm_hb_kernel", "gemm_hbx_kernel", "gemm_hbp_kernel", "gemm_hbt_kernel",
                    "gemm_x6_kernel", "gemm_gbf_kernel",
                    "gemm_splitk_reduce", "to_bf16_kernel", "posconv_bf16_kernel", "flash_fwd_bf16p_kernel",
-                   "flash_bwd_bf16p_kernel", "flash_fwd_bf16_kernel", "flash_bwd_bf16_kernel", "flash_dq_reduce")
+                   "flash_bwd_bf16p_kernel", "flash_fwd_bf16_kernel", "flash_bwd_bf16_kernel", "flash_dq_reduce",
+                   "flash_dq_reduce_frag")
 # kernels of each family the C4 bench layout must have launched (a missing entry means a stale PMC table)
 C4_REQUIRED = ("gemm_hb_kernel", "gemm_hbp_kernel", "gemm_hbt_kernel", "flash_fwd_bf16p_kernel", "flash_bwd_bf16p_kernel",
-               "flash_dq_reduce")
+               "flash_dq_reduce_frag")
 FRONT_KERNELS = ("conv0_gn_kernel", "col_stats_final", "gn_bwd_final", "conv0_dw_reduce")
 
 
@@ -299,7 +300,7 @@ def run(args, rank, world, comm, dev, make_engine):
                                               "distinct slice, C written, epilogue operands), no tile re-reads or "
                                               "split-K partials",
                            "traffic_ratio": round(traffic / traffic_alg, 3) if traffic and traffic_alg else None,
-                           "kernel": "fp32 MFMA GEMM family: gemm_glds_kernel + gemm_f32_kernel + posconv_kernel + flash attention (flash_fwd_kernel, flash_bwd_kernel + flash_dq_reduce) (all launches)",
+                           "kernel": "fp32 MFMA GEMM family: gemm_glds_kernel + gemm_f32_kernel + posconv_kernel + flash attention (flash_fwd_kernel, flash_bwd_kernel + flash_dq_reduce_frag) (all launches)",
                            "launches": int(gn), "avg_launch_ms": round(gms / max(1, gn), 5),
                            "measured": f"HIP events around every GEMM-family launch on the engine stream, separate "
                                        f"pass of {tsteps} batch(es) after the timed region (eager path: "

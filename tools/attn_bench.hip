@@ -98,7 +98,9 @@ int main(int argc, char** argv) {
                          bf16 ? ctxb : nullptr, bf16 ? qkvb : nullptr);
     };
     auto bwd = [&] {
-        launch_flash_bwd(bf16 ? nullptr : qkv, dctx, lse, delta, dqkv, dqp, B, T, NH, H, 64, scale, nullptr, bf16, st,
+        // bf16 mode as the engine runs it: dQ / dK / dV only as the bf16 plane (the fp32 dqkv is not written)
+        launch_flash_bwd(bf16 ? nullptr : qkv, dctx, lse, delta, bf16 ? nullptr : dqkv, dqp, B, T, NH, H, 64, scale,
+                         nullptr, bf16, st,
                          bf16 ? dqkvb : nullptr, bf16 ? qkvb : nullptr, bf16 ? dctxb : nullptr);
     };
     fwd();

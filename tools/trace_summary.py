@@ -25,7 +25,7 @@ def main():
         base = n.replace('void ', '').replace('(anonymous namespace)::', '')
         fam[base.split('(')[0].split('<')[0]] += t
         if any(q in n for q in ('gemm_f32_kernel', 'gemm_x6_kernel', 'gemm_glds_kernel', 'gemm_hb_kernel', 'gemm_gbf_kernel',
-                                'gemm_hb8_kernel', 'gemm_hbx_kernel', 'gemm_hbp_kernel', 'gemm_hbt_kernel')):
+                                'gemm_hbx_kernel', 'gemm_hbp_kernel', 'gemm_hbt_kernel')):
             tmpl = base.split("<")[0][5:9] + ":" + n[n.find('<') + 1:n.find('>')]
             k = (tmpl, gx // max(1, wx), gy, gz)  # grid in blocks (workgroups of wx threads)
             g[k][0] += 1
