@@ -6,8 +6,8 @@ O=gpurun_out/r6${1:-attnab}
 R=/tmp/r6attn_raw
 mkdir -p $O $R
 for m in 1 0; do for r in 1 2; do
-  timeout -k 10 120 ./tools/ab/attn_bench_old $m >> $O/ab.txt 2>&1; echo -n "old " >> $O/ab.txt
-  timeout -k 10 120 ./tools/attn_bench $m >> $O/ab.txt 2>&1; echo "^new" >> $O/ab.txt
+  echo -n "old " >> $O/ab.txt; timeout -k 10 120 ./tools/ab/attn_bench_old $m >> $O/ab.txt 2>&1
+  echo -n "new " >> $O/ab.txt; timeout -k 10 120 ./tools/attn_bench $m >> $O/ab.txt 2>&1
 done; done
 cat $O/ab.txt
 if [ -n "$2" ]; then
