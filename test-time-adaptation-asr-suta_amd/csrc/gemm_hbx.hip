@@ -649,7 +649,9 @@ constexpr int P_HALF = 16384;  // bytes per half-tile image (128 rows x 128 B)
 __device__ __forceinline__ int hbp_swz(int r) { return (r >> 1) & 7; }
 
 // FORM 1: lockstep; 2: wave groups one barrier apart (STAG); 3: STAG with three half-tiles of DMA in flight and one
-// counted wait per K-tile (below).
+// counted wait per K-tile (below); 4: form 3's schedule on v_mfma_f32_16x16x32_bf16 (16 MFMAs per phase instead of 8
+// of 32x32x16, the guide's 256^2 template shape), accumulators remapped through LDS to the 32x32 C^T layout of
+// epilogue_t after the main loop (round 6).
 // CONV: conv-A rows with per-tap weight segments (the conv stack's input gradients, gemm.hip use_hbp_conv): A(m, k) =
 // Ab[(m + seg - pad) ldab + k - seg segK], zero unless 0 <= m + seg - pad < Mvalid (per utterance: zmvalid), B(k, n) =
 // Bb[n ldbb + k - seg segK + seg sBseg], seg = k / segK.  With ldab == segK the A address is linear in k (a segment
@@ -737,32 +739,73 @@ __global__ __launch_bounds__(512, 1) void gemm_hbp_kernel(GemmParams p) {
         const int c = 2 * kk + (lane >> 5);
         return *reinterpret_cast<const bf16x8*>(img + lr * 128 + ((c ^ hbp_swz(lr)) << 4));
     };
+    constexpr bool M16 = FORM == 4;
     f32x16 acc[4][2];
+    f32x4 acc16[8][4];  // M16: acc16[bm][bn] = C^T fragment of rows 16 bm .. of the wave tile, columns 16 bn ..
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    if constexpr (M16) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc16[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
     bf16x8 fa[2][4], fb0[4], fb1[4];
+    // M16 fragments (16x16x32: lane -> row lane & 15 of a 16-row block, 8 k at 32 kk2 + 8 (lane >> 4) = chunk
+    // 4 kk2 + (lane >> 4); the same registers as the 32x32 form: fa[bi][kk] = 16-row block bi, kk2 = kk & 1 for
+    // bi < 4 ... stored as fa[bm >> 1][2 (bm & 1) + kk2], fb[2 bn + kk2])
+    auto frag16 = [&](const char* img, int lr, int kk2) {
+        const int c = 4 * kk2 + (lane >> 4);
+        return *reinterpret_cast<const bf16x8*>(img + lr * 128 + ((c ^ hbp_swz(lr)) << 4));
+    };
     auto read_a = [&](int b, int qm) {
         const char* img = lds + (b * 4 + qm) * P_HALF;
+        if constexpr (M16) {
 #pragma unroll
-        for (int bi = 0; bi < 2; ++bi)
+            for (int bm = 0; bm < 4; ++bm)
 #pragma unroll
-            for (int kk = 0; kk < 4; ++kk) fa[bi][kk] = frag(img, wr * 64 + 32 * bi + (lane & 31), kk);
+                for (int kk2 = 0; kk2 < 2; ++kk2)
+                    fa[bm >> 1][2 * (bm & 1) + kk2] = frag16(img, wr * 64 + 16 * bm + (lane & 15), kk2);
+        } else {
+#pragma unroll
+            for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) fa[bi][kk] = frag(img, wr * 64 + 32 * bi + (lane & 31), kk);
+        }
     };
     auto read_b = [&](int b, int qn, bf16x8 (&fb)[4]) {
         const char* img = lds + (b * 4 + 2 + qn) * P_HALF;
+        if constexpr (M16) {
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk) fb[kk] = frag(img, wc * 32 + (lane & 31), kk);
+            for (int bn = 0; bn < 2; ++bn)
+#pragma unroll
+                for (int kk2 = 0; kk2 < 2; ++kk2) fb[2 * bn + kk2] = frag16(img, wc * 32 + 16 * bn + (lane & 15), kk2);
+        } else {
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) fb[kk] = frag(img, wc * 32 + (lane & 31), kk);
+        }
     };
     auto mfma_q = [&](int qm, int qn, const bf16x8 (&fb)[4]) {
+        if constexpr (M16) {
 #pragma unroll
-        for (int bi = 0; bi < 2; ++bi)
+            for (int bm = 0; bm < 4; ++bm)
 #pragma unroll
-            for (int kk = 0; kk < 4; ++kk)
-                acc[2 * qm + bi][qn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[kk], fa[bi][kk], acc[2 * qm + bi][qn], 0, 0, 0);
+                for (int bn = 0; bn < 2; ++bn)
+#pragma unroll
+                    for (int kk2 = 0; kk2 < 2; ++kk2)
+                        acc16[4 * qm + bm][2 * qn + bn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                            fb[2 * bn + kk2], fa[bm >> 1][2 * (bm & 1) + kk2], acc16[4 * qm + bm][2 * qn + bn], 0, 0, 0);
+        } else {
+#pragma unroll
+            for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk)
+                    acc[2 * qm + bi][qn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[kk], fa[bi][kk], acc[2 * qm + bi][qn], 0, 0, 0);
+        }
     };
     // counted wait of phase p: the halves issued at phases p - 1 and p (if any) may stay in flight
     auto wait_phase = [&](int n_out) {
@@ -787,7 +830,7 @@ __global__ __launch_bounds__(512, 1) void gemm_hbp_kernel(GemmParams p) {
         barrier();
     };
 
-    if constexpr (FORM == 3) {
+    if constexpr (FORM >= 3) {
         // Deep form (cdna_hip_programming.md's 256^2 template schedule): the halves of K-tile t + 2 go into buffer t & 1
         // as soon as K-tile t is done with them, so three halves stay in flight and the wave waits once per K-tile.
         //   phase 1  reads B0, A0 of t  (B first)  | issues A1 of t + 1 (last read: phase 3 of t - 1, two phases back)
@@ -879,6 +922,39 @@ __global__ __launch_bounds__(512, 1) void gemm_hbp_kernel(GemmParams p) {
         if (wr == 0) __builtin_amdgcn_s_barrier();  // the leading group's matching barrier
     }
     __syncthreads();  // every wave is done with the buffers: wave-private 16-KB staging images
+    if constexpr (M16) {
+        // 16x16 C^T fragments -> the 32x32 C^T layout (lane l: row 32 i + (l & 31), register 4 g + k: column 32 j + 8 g +
+        // 4 (l >> 5) + k), one 32-row band at a time through the wave's staging image: fp32 [32][64], 16-B chunk c of
+        // row r at slot c ^ (r & 15) (conflict-free 16-B writes and reads)
+        char* const tb = lds + wid * 16384;
+        const int l16 = lane & 15, g4 = lane >> 4, l32 = lane & 31, hh = lane >> 5;
+        auto wave_sync = [] {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        };
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+            for (int b2 = 0; b2 < 2; ++b2)
+#pragma unroll
+                for (int bn = 0; bn < 4; ++bn) {
+                    const int r = 16 * b2 + l16, c = 4 * bn + g4;
+                    *reinterpret_cast<f32x4*>(tb + r * 256 + ((c ^ (r & 15)) << 4)) = acc16[2 * i + b2][bn];
+                }
+            wave_sync();
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int c = 8 * j + 2 * g + hh;
+                    const f32x4 v = *reinterpret_cast<const f32x4*>(tb + l32 * 256 + ((c ^ (l32 & 15)) << 4));
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) acc[i][j][4 * g + k] = v[k];
+                }
+            wave_sync();
+        }
+    }
     {  // (one epilogue instantiation: for Z = 1 the rebase adds zero)
         GemmParams q = p;
         const bool preb = CB && p.preb;
@@ -974,7 +1050,7 @@ void gemm_run_hbx(int variant, const GemmParams& p, dim3 grid, hipStream_t st) {
         throw std::invalid_argument("hbx: batched GEMMs only on the four-phase form with the staged C^T epilogue");
     if (p.segK > 0) {  // conv-A rows: the four-phase form's CONV instantiation (gemm.hip hbp_conv_ok)
         if (!hbp_conv_ok(p)) throw std::invalid_argument("hbx: conv-A GEMM outside the four-phase CONV form's conditions");
-        if (suta_switches().hbx_form == 3) {
+        if (suta_switches().hbx_form >= 3) {  // (form 4's 16x16x32 shape only on the plain linears)
             if (p.Cb) hipLaunchKernelGGL((gemm_hbp_kernel<true, XEM_A, 3, true>), grid, dim3(512), 0, st, p);
             else hipLaunchKernelGGL((gemm_hbp_kernel<false, XEM_A, 3, true>), grid, dim3(512), 0, st, p);
         } else {
@@ -994,12 +1070,20 @@ void gemm_run_hbx(int variant, const GemmParams& p, dim3 grid, hipStream_t st) {
     }
     const int tr = suta_switches().hbx_t;
     const int dbg = hbx_diag();
-    const int form = suta_switches().hbx_form;
+    // SUTA_HBX_FORM 4 (default): the 16x16x32 form where it measured faster (tools/hb_bench, profiles/r6/hb16.txt:
+    // +8-14 % on the QKV, FFN1, FFN2 and dQKV shapes; the N = K = 1024 out-projection -4 %, which keeps form 3);
+    // 5: the 16x16x32 form on every shape (tests)
+    int form = suta_switches().hbx_form;
+    if (form == 4 && p.N <= 1024 && p.K <= 1024) form = 3;
+    else if (form == 5) form = 4;
     if (form && tr == 2 && p.K % 64 == 0 && hbx_t_ok(p, true) && !dbg) {  // the four-phase K-tile schedule
         const bool cb = p.Cb != nullptr;
 #define HBP(EM_)                                                                                                   \
         do {                                                                                                       \
-            if (form == 3) {                                                                                       \
+            if (form == 4) {                                                                                       \
+                if (cb) hipLaunchKernelGGL((gemm_hbp_kernel<true, EM_, 4>), grid, dim3(512), 0, st, p);            \
+                else hipLaunchKernelGGL((gemm_hbp_kernel<false, EM_, 4>), grid, dim3(512), 0, st, p);              \
+            } else if (form == 3) {                                                                                \
                 if (cb) hipLaunchKernelGGL((gemm_hbp_kernel<true, EM_, 3>), grid, dim3(512), 0, st, p);            \
                 else hipLaunchKernelGGL((gemm_hbp_kernel<false, EM_, 3>), grid, dim3(512), 0, st, p);              \
             } else if (form == 2) {                                                                                \

@@ -1940,7 +1940,7 @@ void suta_latch_switches() {
     const char* lrpw = std::getenv("SUTA_LN_RPW");
     s.ln_rpw = lrpw ? atoi(lrpw) : 2;
     const char* hform = std::getenv("SUTA_HBX_FORM");
-    s.hbx_form = hform ? atoi(hform) : 3;
+    s.hbx_form = hform ? atoi(hform) : 4;
     const char* hdbg = std::getenv("SUTA_HBX_DBG");
     s.hbx_dbg = hdbg ? atoi(hdbg) : 0;
     const char* fnw = std::getenv("SUTA_FLASH_FWD_NW");

@@ -188,7 +188,8 @@ def test_bf16_hbx_slice_ring_kernel_bitwise_equals_128_tile(monkeypatch):
     edge tiles of a ragged pair: 198 and 124 rows of a 256-row tile), in every epilogue form (SUTA_HBX_T=1: C^T
     accumulators, row-per-lane 16-B stores; 2: the same staged through LDS into whole-line stores; 0: the
     column-per-lane form) and main loop (SUTA_HBX_FORM=2: four-phase 64-deep K-tiles, staggered wave groups; 3 the same
-    with three half-tiles of DMA in flight and one wait per K-tile; 1 the four phases in lockstep; 0 the 32-deep slice
+    with three half-tiles of DMA in flight and one wait per K-tile; 5 form 3 on v_mfma_f32_16x16x32_bf16 with the
+    accumulators remapped to the C^T layout through LDS, round 6; 1 the four phases in lockstep; 0 the 32-deep slice
     ring), against the 128 x 128 kernel (SUTA_HBX=0),
     all without split-K (SUTA_SPLITK=0: a split sums k in another order): the same MFMA products in the same k order, so
     logits and adapted tensors are bitwise equal; and the large model's 20-step SUTA against the reference goldens g7
@@ -200,8 +201,8 @@ def test_bf16_hbx_slice_ring_kernel_bitwise_equals_128_tile(monkeypatch):
     steps = [int(s) for s in z["steps"]]
     waves = [synth.wave(32000, 82), synth.wave(20000, 83)]
     out, params = {}, {}
-    for mode, tr, form in (("0", "1", "2"), ("2", "1", "2"), ("2", "2", "2"), ("2", "2", "3"), ("2", "2", "1"),
-                           ("2", "2", "0"), ("2", "0", "2")):
+    for mode, tr, form in (("0", "1", "2"), ("2", "1", "2"), ("2", "2", "2"), ("2", "2", "3"), ("2", "2", "5"),
+                           ("2", "2", "1"), ("2", "2", "0"), ("2", "0", "2")):
         monkeypatch.setenv("SUTA_HBX", mode)
         monkeypatch.setenv("SUTA_HBX_T", tr)
         monkeypatch.setenv("SUTA_HBX_FORM", form)
@@ -219,7 +220,7 @@ def test_bf16_hbx_slice_ring_kernel_bitwise_equals_128_tile(monkeypatch):
         out[key], _, _ = eng.adapt_varlen(waves, 3, SutaHParams(), record=[0, 3])
         params[key] = {n: eng.get_param(1, n) for n in eng.trainable_names()}
         eng.close()
-    for key in ("212", "222", "223", "221", "220", "202"):
+    for key in ("212", "222", "223", "225", "221", "220", "202"):
         for r in (0, 3):
             for u in range(2):
                 assert np.array_equal(out[key][r][u], out["012"][r][u]), (key, r, u)

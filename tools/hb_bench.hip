@@ -56,10 +56,11 @@ int main(int argc, char** argv) {
     // (tile, ns, cb-capable, SUTA_HBX_T, SUTA_HBX_DBG): the DBG forms are diagnostics (wrong results): 1 no B DMA,
     // 2 no B fragment reads, 3 no DMA, 4 no fragment reads
     // + SUTA_HBX_FORM (6th): 1 the four-phase K-tile schedule (gemm_hbp_kernel), 2 the same with staggered wave groups
-    // 3: the four-phase schedule with three half-tiles of DMA in flight and one counted wait per K-tile
-    const int variants[][6] = {{8, 2, 1, 2, 0, 0}, {8, 2, 1, 2, 0, 2}, {8, 2, 1, 2, 0, 3}};
-    const char* vname[] = {"hbxTS", "hbpS ", "hbpD "};
-    constexpr int NV = 3;
+    // 3: the four-phase schedule with three half-tiles of DMA in flight and one counted wait per K-tile; 4: form 3 on
+    // 16x16x32 MFMAs
+    const int variants[][6] = {{8, 2, 1, 2, 0, 3}, {8, 2, 1, 2, 0, 4}};
+    const char* vname[] = {"hbpD ", "hbp16"};
+    constexpr int NV = 2;
     auto set_variant = [&](int v) {
         const char* tv[] = {"0", "1", "2", "3", "4", "5"};
         setenv("SUTA_HBX_T", tv[variants[v][3]], 1);
@@ -164,7 +165,7 @@ int main(int argc, char** argv) {
                 p.epi = 0;
                 p.preb = 0;
             }
-            const int evs[] = {0, 1, 2};
+            const int evs[] = {0, 1};
             std::vector<float> ms[NV];
             for (int rd = 0; rd < rounds; ++rd)
                 for (int v : evs) {
