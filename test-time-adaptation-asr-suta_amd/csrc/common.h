@@ -81,8 +81,7 @@ struct SutaSwitches {
     int hbx_form;         // SUTA_HBX_FORM (default 4): the 256 x 256 kernel's main loop with the C^T staged epilogue
                           // (SUTA_HBX_T=2) and K % 64 == 0: 2 four-phase 64-deep K-tiles with two wave groups one
                           // barrier apart + s_setprio (gemm_hbp_kernel), 1 the same in lockstep, 0 the 32-deep slice
-                          // ring, 3 form 2 with three half-tiles in flight, 4 form 3 on 16x16x32 MFMAs except the
-                          // N <= 1024, K <= 1024 shapes (form 3 there), 5 the 16x16x32 form on every shape
+                          // ring, 3 form 2 with three half-tiles in flight, 4 form 3 on 16x16x32 MFMAs
     int ln_rpw;           // SUTA_LN_RPW (default 2): rows per wave of the bf16-input (conv stack) LayerNorm forward; 1 = one
     int hbx_dbg;          // SUTA_HBX_DBG (tools/hb_bench diagnostics; wrong results): gemm_hbx with parts of its loop removed;
                           // honoured only by the tools build of gemm_hbx.hip (-DSUTA_HBX_DIAG), ignored by libsuta.so

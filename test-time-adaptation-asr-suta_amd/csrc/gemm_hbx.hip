@@ -1050,7 +1050,10 @@ void gemm_run_hbx(int variant, const GemmParams& p, dim3 grid, hipStream_t st) {
         throw std::invalid_argument("hbx: batched GEMMs only on the four-phase form with the staged C^T epilogue");
     if (p.segK > 0) {  // conv-A rows: the four-phase form's CONV instantiation (gemm.hip hbp_conv_ok)
         if (!hbp_conv_ok(p)) throw std::invalid_argument("hbx: conv-A GEMM outside the four-phase CONV form's conditions");
-        if (suta_switches().hbx_form >= 3) {  // (form 4's 16x16x32 shape only on the plain linears)
+        if (suta_switches().hbx_form >= 4) {
+            if (p.Cb) hipLaunchKernelGGL((gemm_hbp_kernel<true, XEM_A, 4, true>), grid, dim3(512), 0, st, p);
+            else hipLaunchKernelGGL((gemm_hbp_kernel<false, XEM_A, 4, true>), grid, dim3(512), 0, st, p);
+        } else if (suta_switches().hbx_form == 3) {
             if (p.Cb) hipLaunchKernelGGL((gemm_hbp_kernel<true, XEM_A, 3, true>), grid, dim3(512), 0, st, p);
             else hipLaunchKernelGGL((gemm_hbp_kernel<false, XEM_A, 3, true>), grid, dim3(512), 0, st, p);
         } else {
@@ -1070,12 +1073,10 @@ void gemm_run_hbx(int variant, const GemmParams& p, dim3 grid, hipStream_t st) {
     }
     const int tr = suta_switches().hbx_t;
     const int dbg = hbx_diag();
-    // SUTA_HBX_FORM 4 (default): the 16x16x32 form where it measured faster (tools/hb_bench, profiles/r6/hb16.txt:
-    // +8-14 % on the QKV, FFN1, FFN2 and dQKV shapes; the N = K = 1024 out-projection -4 %, which keeps form 3);
-    // 5: the 16x16x32 form on every shape (tests)
-    int form = suta_switches().hbx_form;
-    if (form == 4 && p.N <= 1024 && p.K <= 1024) form = 3;
-    else if (form == 5) form = 4;
+    // SUTA_HBX_FORM 4 (default): the 16x16x32 form on every shape (tools/hb_bench, profiles/r6/hb16.txt: +8-14 % on
+    // the QKV, FFN1, FFN2 and dQKV shapes, the N = K = 1024 out-projection -4 % alone; in the C4 loop every shape on
+    // form 4 measured +0.3 % over keeping form 3 for that one, profiles/r6/conv16)
+    const int form = suta_switches().hbx_form;
     if (form && tr == 2 && p.K % 64 == 0 && hbx_t_ok(p, true) && !dbg) {  // the four-phase K-tile schedule
         const bool cb = p.Cb != nullptr;
 #define HBP(EM_)                                                                                                   \

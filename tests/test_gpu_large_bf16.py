@@ -188,7 +188,7 @@ def test_bf16_hbx_slice_ring_kernel_bitwise_equals_128_tile(monkeypatch):
     edge tiles of a ragged pair: 198 and 124 rows of a 256-row tile), in every epilogue form (SUTA_HBX_T=1: C^T
     accumulators, row-per-lane 16-B stores; 2: the same staged through LDS into whole-line stores; 0: the
     column-per-lane form) and main loop (SUTA_HBX_FORM=2: four-phase 64-deep K-tiles, staggered wave groups; 3 the same
-    with three half-tiles of DMA in flight and one wait per K-tile; 5 form 3 on v_mfma_f32_16x16x32_bf16 with the
+    with three half-tiles of DMA in flight and one wait per K-tile; 4 form 3 on v_mfma_f32_16x16x32_bf16 with the
     accumulators remapped to the C^T layout through LDS, round 6; 1 the four phases in lockstep; 0 the 32-deep slice
     ring), against the 128 x 128 kernel (SUTA_HBX=0),
     all without split-K (SUTA_SPLITK=0: a split sums k in another order): the same MFMA products in the same k order, so
@@ -201,7 +201,7 @@ def test_bf16_hbx_slice_ring_kernel_bitwise_equals_128_tile(monkeypatch):
     steps = [int(s) for s in z["steps"]]
     waves = [synth.wave(32000, 82), synth.wave(20000, 83)]
     out, params = {}, {}
-    for mode, tr, form in (("0", "1", "2"), ("2", "1", "2"), ("2", "2", "2"), ("2", "2", "3"), ("2", "2", "5"),
+    for mode, tr, form in (("0", "1", "2"), ("2", "1", "2"), ("2", "2", "2"), ("2", "2", "3"), ("2", "2", "4"),
                            ("2", "2", "1"), ("2", "2", "0"), ("2", "0", "2")):
         monkeypatch.setenv("SUTA_HBX", mode)
         monkeypatch.setenv("SUTA_HBX_T", tr)
@@ -220,7 +220,7 @@ def test_bf16_hbx_slice_ring_kernel_bitwise_equals_128_tile(monkeypatch):
         out[key], _, _ = eng.adapt_varlen(waves, 3, SutaHParams(), record=[0, 3])
         params[key] = {n: eng.get_param(1, n) for n in eng.trainable_names()}
         eng.close()
-    for key in ("212", "222", "223", "225", "221", "220", "202"):
+    for key in ("212", "222", "223", "224", "221", "220", "202"):
         for r in (0, 3):
             for u in range(2):
                 assert np.array_equal(out[key][r][u], out["012"][r][u]), (key, r, u)
@@ -479,14 +479,14 @@ def test_batched_gemm_without_off32_epilogue_falls_back(monkeypatch):
         assert np.array_equal(v, params["0"][n]), n
 
 
-@pytest.mark.parametrize("form", ["2", "3"])
+@pytest.mark.parametrize("form", ["2", "3", "4"])
 def test_conv_input_gradients_on_256_tile_bitwise(monkeypatch, form):
     """The layer-norm conv stack's input gradients (conv-A rows m + seg - pad, per-tap weight segments; config C4's
     conv-seg GEMMs, one per output-row residue, Z = batch) on the four-phase 256 x 256 kernel's CONV form (per-segment
     row validity and weight-slice jumps in the DMA pointers; SUTA_HBP_CONV=1, default) against the 128 x 128 kernel
     (SUTA_HBP_CONV=0): the same MFMA products in the same k order, so logits and adapted tensors are bitwise equal.
     wav2vec2-large in bf16 mode, a ragged pair (per-utterance valid rows), the 256 x 256 kernel forced onto the small
-    grids (SUTA_HBX=2), no split-K, in both staggered main loops (SUTA_HBX_FORM 2 and 3)."""
+    grids (SUTA_HBX=2), no split-K, in the staggered main loops (SUTA_HBX_FORM 2, 3 and 4: 16x16x32 MFMAs)."""
     monkeypatch.setenv("SUTA_SPLITK", "0")
     monkeypatch.setenv("SUTA_HBX", "2")
     monkeypatch.setenv("SUTA_HBX_FORM", form)
