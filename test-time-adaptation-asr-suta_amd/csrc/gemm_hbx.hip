@@ -23,6 +23,7 @@
 // Requires K % 32 == 0 and K >= 128, no split-K, no conv-A rows, and Z == 1 except on the four-phase form
 // (gemm_hbp_kernel below, K % 64 == 0), which rebases its operands per batch (the dispatcher's conditions).
 #include "gemm_kernels.h"
+#include <algorithm>
 #include <cstdint>
 #include <cstdlib>
 #include <stdexcept>
@@ -297,7 +298,7 @@ __device__ __forceinline__ void epilogue_t_edge(const GemmParams& p, const f32x1
 // (chunk c of row r in slot c ^ (r & 7): conflict-free ds_write_b128 / ds_read_b128), read back row-contiguous
 // (8 lanes = one 128-B bf16 row of the wave tile, 16 lanes = one 256-B fp32 row) and stored with every lane of an
 // instruction in 8 whole lines.  Without ST a store instruction touches 32 rows.
-template <bool CB, int EM, bool ST>
+template <bool CB, int EM, bool ST, int NOST = 0>
 __device__ __forceinline__ void epilogue_t(const GemmParams& p, const f32x16 (&acc)[4][2], int rbase, int cbase,
                                            int lane, char* stage) {
     if (cbase + 64 > p.N) {
@@ -330,7 +331,8 @@ __device__ __forceinline__ void epilogue_t(const GemmParams& p, const f32x16 (&a
         for (int k = 0; k < 4; ++k) {
             const int r = 8 * k + (lane >> 3), c = lane & 7;
             const u32x4v w = *reinterpret_cast<const u32x4v*>(img + r * 128 + ((c ^ (r & 7)) << 4));
-            if (row0 + r < p.M) *reinterpret_cast<u32x4v*>(base + (long)(row0 + r) * ld + cbase + 8 * c) = w;
+            if constexpr (NOST != 0) asm volatile("" ::"v"(w));  // (tools diagnostics: no global store)
+            else if (row0 + r < p.M) *reinterpret_cast<u32x4v*>(base + (long)(row0 + r) * ld + cbase + 8 * c) = w;
         }
     };
     auto flush_f32 = [&](const char* img, float* base, long ld, int row0) {
@@ -477,6 +479,185 @@ __device__ __forceinline__ void epilogue_t(const GemmParams& p, const f32x16 (&a
                 p.delta[((long)b * p.dNH + cbase / 64) * p.dT + t] = l2 + other;
             }
         }
+    }
+}
+
+// Epilogue of the 16x16x32 accumulators in their own C^T layout (round 6; gemm_hbp_kernel form 4): acc[bm][bn] lane l
+// holds row 16 bm + (l & 15) of the wave tile and its 4 consecutive columns 16 bn + 4 (l >> 4) .. + 3, so bias, residual
+// and fp32 operands load as 16-B vectors and bf16 operands as 8-B vectors per lane, and the outputs enter the staging
+// images as 8-B (bf16) or 16-B (fp32) pieces straight from the registers -- no remap of the accumulators to the 32x32
+// layout (which cost 1.6 us of a 33-us K = 1024 tile: profiles/r6/hbp_diag2.txt) and no v_permlane32_swap.  Same
+// operations in the same order as epilogue_t per element.  Used for the bf16-C-plane bias / residual class only (see
+// NATIVE16 in hbp_tile); every flag is implemented so the A/B forms (tools DBG builds) stay comparable.  Images per 32-row band and wave (the buffers are free after
+// the main loop): bf16 [32][128 B] with 16-B chunk c of row r at slot c ^ ((r >> 1) & 7) (the 8-B writes of 16 rows x 2
+// halves and the 16-B flush reads both conflict-free), fp32 [32][256 B] with chunk c at c ^ (r & 15).  Classes without
+// EPI_DELTA (the delta epilogue's summation tree is the 32x32 layout's: its kernels keep the remap).
+template <bool CB, int EM>
+__device__ __forceinline__ void epilogue16t(const GemmParams& p, const f32x4 (&acc)[8][4], int rbase, int cbase,
+                                            int lane, char* stage) {
+    const int e = p.epi & EM;
+    const int l16 = lane & 15, g = lane >> 4;
+    const float alpha = p.alpha;
+    const int rlim = (e & EPI_ROWMASK) ? p.zrows[0] : 0x7fffffff;
+    const bool preb = CB && p.preb;
+    if (cbase + 64 > p.N) {  // column tiles past N: element by element (same arithmetic, bounds-checked stores)
+#pragma unroll
+        for (int bm = 0; bm < 8; ++bm) {
+            const int row = rbase + 16 * bm + l16;
+#pragma unroll
+            for (int bn = 0; bn < 4; ++bn)
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int col = cbase + 16 * bn + 4 * g + k;
+                    if (row >= p.M || col >= p.N) continue;
+                    float v = acc[bm][bn][k] * alpha;
+                    if (e & EPI_BIAS) v += p.bias[col];
+                    if (e & EPI_STORE_PRE) {
+                        if (preb) reinterpret_cast<__bf16*>(p.C2)[(long)row * p.ldc2 + col] = (__bf16)v;
+                        else p.C2[(long)row * p.ldc2 + col] = v;
+                    }
+                    if (e & EPI_GELU) v = (CB && p.fgelu) ? gelu2_bf16ep(f32x2v{v, v}).x : gelu_f(v);
+                    if (e & EPI_DGELU) {
+                        const float xa = preb ? (float)reinterpret_cast<const __bf16*>(p.aux)[(long)row * p.ldaux + col]
+                                              : p.aux[(long)row * p.ldaux + col];
+                        v *= (CB && p.fgelu) ? dgelu2_bf16ep(f32x2v{xa, xa}).x : dgelu_f(xa);
+                    }
+                    if (e & EPI_RESID) v += p.R[(long)row * p.ldr + col];
+                    if (row >= rlim) v = 0.f;
+                    if (!CB || p.C) p.C[(long)row * p.ldc + col] = v;
+                    if (CB) reinterpret_cast<__bf16*>(p.Cb)[(long)row * p.ldcb + col] = (__bf16)v;
+                }
+        }
+        return;
+    }
+    char* const s_pre = stage;          // bf16 pre-activation image
+    char* const s_c32 = stage + 4096;   // fp32 C image
+    char* const s_cb = stage + 12288;   // bf16 C plane image
+    const bool st_pre = (e & EPI_STORE_PRE) && preb;
+    const bool c32 = !CB || p.C;
+    auto bimg = [](char* img, int r, int c0) {  // 8-B piece of columns c0 .. c0 + 3 (c0 % 4 == 0) of image row r
+        const int ch = c0 >> 3;
+        return img + r * 128 + ((ch ^ ((r >> 1) & 7)) << 4) + 2 * (c0 & 7);
+    };
+    auto wave_sync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    auto flush_bf16 = [&](const char* img, __bf16* base, long ld, int row0) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int r = 8 * k + (lane >> 3), c = lane & 7;
+            const u32x4v w = *reinterpret_cast<const u32x4v*>(img + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+            if (row0 + r < p.M) *reinterpret_cast<u32x4v*>(base + (long)(row0 + r) * ld + cbase + 8 * c) = w;
+        }
+    };
+    auto flush_f32 = [&](const char* img, float* base, long ld, int row0) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int r = 4 * k + (lane >> 4), c = lane & 15;
+            const f32x4 w = *reinterpret_cast<const f32x4*>(img + r * 256 + ((c ^ (r & 15)) << 4));
+            if (row0 + r < p.M) *reinterpret_cast<f32x4*>(base + (long)(row0 + r) * ld + cbase + 4 * c) = w;
+        }
+    };
+    typedef __bf16 bf16x4v __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int b2 = 0; b2 < 2; ++b2) {
+            const int rl = 16 * b2 + l16;  // row within the band
+            const int row = rbase + 32 * i + rl;
+            const long rowc = min(row, p.M - 1);
+            const bool rok = row < p.M;
+            const bool zero = (e & EPI_ROWMASK) && row >= rlim;
+            // DGELU: the row block's pre-activation operands loaded before the first use (EM-specialised: only the
+            // GELU' class carries them)
+            bf16x4v xab[4];
+            f32x4 xaf[4];
+            if (e & EPI_DGELU) {
+#pragma unroll
+                for (int bn = 0; bn < 4; ++bn) {
+                    const int col = cbase + 16 * bn + 4 * g;
+                    if (preb) xab[bn] = *reinterpret_cast<const bf16x4v*>(reinterpret_cast<const __bf16*>(p.aux) +
+                                                                          rowc * p.ldaux + col);
+                    else xaf[bn] = *reinterpret_cast<const f32x4*>(p.aux + rowc * p.ldaux + col);
+                }
+            }
+#pragma unroll
+            for (int bn = 0; bn < 4; ++bn) {
+                const int cl = 16 * bn + 4 * g;  // column within the wave tile
+                const int col = cbase + cl;
+                float v[4], xa[4], xr[4];
+                if (e & EPI_DGELU) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) xa[k] = preb ? (float)xab[bn][k] : xaf[bn][k];
+                }
+                if (e & EPI_RESID) {
+                    const f32x4 w = *reinterpret_cast<const f32x4*>(p.R + rowc * p.ldr + col);
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) xr[k] = w[k];
+                }
+                f32x4 bj = {0.f, 0.f, 0.f, 0.f};
+                if (e & EPI_BIAS) bj = *reinterpret_cast<const f32x4*>(p.bias + col);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    v[k] = acc[2 * i + b2][bn][k] * alpha;
+                    if (e & EPI_BIAS) v[k] += bj[k];
+                }
+                if (e & EPI_STORE_PRE) {
+                    if (preb) {
+                        const bf16x4v w = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+                        *reinterpret_cast<bf16x4v*>(bimg(s_pre, rl, cl)) = w;
+                    } else if (rok) {
+                        *reinterpret_cast<f32x4*>(p.C2 + (long)row * p.ldc2 + col) = f32x4{v[0], v[1], v[2], v[3]};
+                    }
+                }
+                if ((e & EPI_GELU) && CB && p.fgelu) {
+#pragma unroll
+                    for (int r = 0; r < 4; r += 2) {
+                        const f32x2v g2 = gelu2_bf16ep(f32x2v{v[r], v[r + 1]});
+                        v[r] = g2.x;
+                        v[r + 1] = g2.y;
+                    }
+                } else if (e & EPI_GELU) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = gelu_f(v[r]);
+                }
+                if ((e & EPI_DGELU) && CB && p.fgelu) {
+#pragma unroll
+                    for (int r = 0; r < 4; r += 2) {
+                        const f32x2v g2 = dgelu2_bf16ep(f32x2v{xa[r], xa[r + 1]});
+                        v[r] *= g2.x;
+                        v[r + 1] *= g2.y;
+                    }
+                } else if (e & EPI_DGELU) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] *= dgelu_f(xa[r]);
+                }
+                if (e & EPI_RESID) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] += xr[r];
+                }
+                if (zero) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = 0.f;
+                }
+                if (c32) {
+                    const int ch = cl >> 2;
+                    *reinterpret_cast<f32x4*>(s_c32 + rl * 256 + ((ch ^ (rl & 15)) << 4)) = f32x4{v[0], v[1], v[2], v[3]};
+                }
+                if (CB) {
+                    const bf16x4v w = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+                    *reinterpret_cast<bf16x4v*>(bimg(s_cb, rl, cl)) = w;
+                }
+            }
+        }
+        wave_sync();
+        const int row0 = rbase + 32 * i;
+        if (st_pre) flush_bf16(s_pre, reinterpret_cast<__bf16*>(p.C2), p.ldc2, row0);
+        if (c32) flush_f32(s_c32, p.C, p.ldc, row0);
+        if (CB) flush_bf16(s_cb, reinterpret_cast<__bf16*>(p.Cb), p.ldcb, row0);
+        wave_sync();
     }
 }
 
@@ -658,11 +839,14 @@ __device__ __forceinline__ int hbp_swz(int r) { return (r >> 1) & 7; }
 // step is one row down and back to column 0), so only the row's validity changes per segment; the B address jumps by
 // sBseg - segK at each segment boundary.  Both are evaluated per DMA issue (segK % 64 == 0: a K-tile lies in one
 // segment), so the shifts live in the DMA pointers, not in per-element VALU work.
-template <bool CB, int EM, int FORM, bool CONV = false>
-__global__ __launch_bounds__(512, 1) void gemm_hbp_kernel(GemmParams p) {
-    __shared__ __attribute__((aligned(16))) float smem[8 * P_HALF / 4];
-    char* const lds = reinterpret_cast<char*>(smem);
-    const TileId tid = xcd_tile(p.order);
+// DBG (tools/hb_bench diagnostics only, -DSUTA_HBX_DIAG; wrong results): 1 no epilogue (accumulators kept live), 2 no
+// K loop (prologue DMA and epilogue only), 3 neither, 4 no global stores of the staged epilogue (with the remap), 8 no
+// LDS remap of the 16x16 accumulators (into epilogue_t), 16 the remap + epilogue_t instead of epilogue16t
+// one 256 x 256 output tile (a persistent kernel looping this body over its XCD's tiles, one block per CU with the next
+// tile's first K-tiles fetched while the epilogue's stores drain, measured 1-2 us per tile slower than one block per
+// tile: DESIGN.md section 8)
+template <bool CB, int EM, int FORM, bool CONV, int DBG>
+__device__ __forceinline__ void hbp_tile(const GemmParams& p, const TileId tid, char* const lds) {
     // batch z (Z-batched GEMMs, the conv stack's per-utterance forward): operand planes offset in bf16 elements, the
     // epilogue's operands through a rebased copy of the parameters (batch z of a Z = 1 view)
     const int z1 = tid.z / p.zdiv, z0 = tid.z % p.zdiv;
@@ -854,7 +1038,7 @@ __global__ __launch_bounds__(512, 1) void gemm_hbp_kernel(GemmParams p) {
         }
         if (wr == 1) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier behind group 0
         __builtin_amdgcn_s_barrier();
-        for (int t = 0; t < nk; ++t) {
+        for (int t = 0; t < ((DBG & 2) ? 0 : nk); ++t) {
             const int b = t & 1;
             const bool n1 = t + 1 < nk, n2 = t + 2 < nk;
             // phase 1: quadrant (0,0)
@@ -922,7 +1106,29 @@ __global__ __launch_bounds__(512, 1) void gemm_hbp_kernel(GemmParams p) {
         if (wr == 0) __builtin_amdgcn_s_barrier();  // the leading group's matching barrier
     }
     __syncthreads();  // every wave is done with the buffers: wave-private 16-KB staging images
-    if constexpr (M16) {
+    // the native 16x16 epilogue on the class where the C4 loop measured it faster than the remap + epilogue_t
+    // (profiles/r6/trab2: the bf16-C-plane bias / residual linears and conv GEMMs -2..-5 %); the GELU / GELU' classes
+    // measured 2-8 % slower with it and the fp32-only class 1 %, so they keep the remap
+    constexpr bool NATIVE16 = CB && EM == (EPI_BIAS | EPI_RESID | EPI_ROWMASK) && (DBG & 16) == 0;
+    if constexpr ((DBG & 1) != 0) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc16[i][j]));
+        return;
+    }
+    if constexpr (M16 && (DBG & 8) != 0) {  // (tools diagnostics: no remap, wrong results)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) acc[i][j][4 * g + k] = acc16[2 * i + (g >> 1)][2 * j + (g & 1)][k];
+    } else if constexpr (M16 && NATIVE16) {
+        // (the native 16x16 epilogue below)
+    } else if constexpr (M16) {
         // 16x16 C^T fragments -> the 32x32 C^T layout (lane l: row 32 i + (l & 31), register 4 g + k: column 32 j + 8 g +
         // 4 (l >> 5) + k), one 32-row band at a time through the wave's staging image: fp32 [32][64], 16-B chunk c of
         // row r at slot c ^ (r & 15) (conflict-free 16-B writes and reads)
@@ -969,8 +1175,17 @@ __global__ __launch_bounds__(512, 1) void gemm_hbp_kernel(GemmParams p) {
             q.C2 = preb ? reinterpret_cast<float*>(reinterpret_cast<__bf16*>(p.C2) + z1 * p.sC21 + z0 * p.sC20)
                         : p.C2 + z1 * p.sC21 + z0 * p.sC20;
         if (p.zrows) q.zrows = p.zrows + z1;
-        epilogue_t<CB, EM, true>(q, acc, m0 + wr * 128, n0 + wc * 64, lane, lds + wid * 16384);
+        if constexpr (M16 && NATIVE16 && (DBG & 8) == 0)
+            epilogue16t<CB, EM>(q, acc16, m0 + wr * 128, n0 + wc * 64, lane, lds + wid * 16384);
+        else
+            epilogue_t<CB, EM, true, (DBG & 4)>(q, acc, m0 + wr * 128, n0 + wc * 64, lane, lds + wid * 16384);
     }
+}
+
+template <bool CB, int EM, int FORM, bool CONV = false, int DBG = 0>
+__global__ __launch_bounds__(512, 1) void gemm_hbp_kernel(GemmParams p) {
+    __shared__ __attribute__((aligned(16))) float smem[8 * P_HALF / 4];
+    hbp_tile<CB, EM, FORM, CONV, DBG>(p, xcd_tile(p.order), reinterpret_cast<char*>(smem));
 }
 
 template <int MS, int EM, int TR = 0>
@@ -1103,6 +1318,22 @@ void gemm_run_hbx(int variant, const GemmParams& p, dim3 grid, hipStream_t st) {
 #undef HBP
     }
 #ifdef SUTA_HBX_DIAG
+    if (dbg >= 11 && dbg <= 16 && (e & ~XEM_A) == 0) {  // tools/hb_bench: gemm_hbp_kernel form 4 diagnostics
+        const bool cb = p.Cb != nullptr;
+#define HBP_DBG(D)                                                                                                 \
+        do {                                                                                                       \
+            if (cb) hipLaunchKernelGGL((gemm_hbp_kernel<true, XEM_A, 4, false, D>), grid, dim3(512), 0, st, p);    \
+            else hipLaunchKernelGGL((gemm_hbp_kernel<false, XEM_A, 4, false, D>), grid, dim3(512), 0, st, p);      \
+        } while (0)
+        if (dbg == 11) HBP_DBG(1);
+        else if (dbg == 12) HBP_DBG(2);
+        else if (dbg == 13) HBP_DBG(3);
+        else if (dbg == 14) HBP_DBG(20);
+        else if (dbg == 15) HBP_DBG(8);
+        else HBP_DBG(16);
+#undef HBP_DBG
+        return;
+    }
     if (dbg && tr == 2 && hbx_t_ok(p, true) && (e & ~XEM_A) == 0) {  // tools/hb_bench diagnostics
         const bool cb = p.Cb != nullptr;
 #define HBX_DBG(D)                                                                                                 \

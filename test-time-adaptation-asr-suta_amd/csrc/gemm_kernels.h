@@ -178,12 +178,8 @@ __device__ __forceinline__ float epi_value(const GemmParams& p, float acc, long 
 struct TileId {
     int x, y, z;
 };
-__device__ __forceinline__ TileId xcd_tile(int order = 0) {
-    const int gx = gridDim.x, gy = gridDim.y;
-    const int nwg = gx * gy * gridDim.z;
-    const int orig = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
-    const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
-    const int id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+// tile of remapped id `id` in a gx x gy (x Z) grid, in the tile order `order`
+__device__ __forceinline__ TileId tile_of_id(int id, int gx, int gy, int order) {
     if (order == 1) return TileId{(id / gy) % gx, id % gy, id / (gx * gy)};  // m fastest: an XCD keeps a B band
     if (order >= 2) {  // grouped: bands of `order` tile rows walked column by column (A and B panels both reused)
         const int zid = id / (gx * gy), i2 = id % (gx * gy);
@@ -191,6 +187,14 @@ __device__ __forceinline__ TileId xcd_tile(int order = 0) {
         return TileId{loc / gsz, fm + loc % gsz, zid};
     }
     return TileId{id % gx, (id / gx) % gy, id / (gx * gy)};
+}
+__device__ __forceinline__ TileId xcd_tile(int order = 0) {
+    const int gx = gridDim.x, gy = gridDim.y;
+    const int nwg = gx * gy * gridDim.z;
+    const int orig = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+    const int id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+    return tile_of_id(id, gx, gy, order);
 }
 
 // Interior-tile epilogue with 32-bit offsets (p.off32: every operand's rows x leading dimension fits 4 GiB):

@@ -44,7 +44,9 @@ int main(int argc, char** argv) {
     float *C, *R;
     CK(hipMalloc(&A, (size_t)M * 4096 * 2));
     CK(hipMalloc(&B, (size_t)4096 * 4096 * 2));
-    CK(hipMalloc(&C, (size_t)M * 4096 * 4));
+    // HB_PAD: extra elements per row of every output / epilogue-operand plane (leading dimension N + pad)
+    const int pad = getenv("HB_PAD") ? atoi(getenv("HB_PAD")) : 0;
+    CK(hipMalloc(&C, (size_t)M * (4096 + pad) * 4));
     CK(hipMalloc(&R, (size_t)M * 4096 * 4));
     hipLaunchKernelGGL(fillb, dim3((M * 4096L + 255) / 256), dim3(256), 0, 0, A, (long)M * 4096, 1u);
     hipLaunchKernelGGL(fillb, dim3((4096L * 4096 + 255) / 256), dim3(256), 0, 0, B, 4096L * 4096, 2u);
@@ -58,11 +60,18 @@ int main(int argc, char** argv) {
     // + SUTA_HBX_FORM (6th): 1 the four-phase K-tile schedule (gemm_hbp_kernel), 2 the same with staggered wave groups
     // 3: the four-phase schedule with three half-tiles of DMA in flight and one counted wait per K-tile; 4: form 3 on
     // 16x16x32 MFMAs
-    const int variants[][6] = {{8, 2, 1, 2, 0, 3}, {8, 2, 1, 2, 0, 4}};
-    const char* vname[] = {"hbpD ", "hbp16"};
-    constexpr int NV = 2;
+    // SUTA_HBX_FORM 5: form 4 persistent; SUTA_HBX_DBG 11 / 12 / 13 / 14 / 15 (HB_DIAG=1 only): form 4 without its epilogue / K loop / both / epilogue
+    // global stores / accumulator remap (profiles/r6/hbp_diag*.txt)
+    // SUTA_HBX_DBG 16: form 4 with the accumulators remapped to the 32x32 layout and epilogue_t (the first form 4);
+    // HB_DIAG=1: + SUTA_HBX_DBG 11 .. 15 on that form (tools build only; wrong results): without its epilogue / K loop /
+    // both / the epilogue's global stores / the accumulator remap (profiles/r6/hbp_diag*.txt)
+    const int variants[][6] = {{8, 2, 1, 2, 0, 3}, {8, 2, 1, 2, 0, 4}, {8, 2, 1, 2, 16, 4}, {8, 2, 1, 2, 11, 4},
+                               {8, 2, 1, 2, 12, 4}, {8, 2, 1, 2, 13, 4}, {8, 2, 1, 2, 14, 4}, {8, 2, 1, 2, 15, 4}};
+    const char* vname[] = {"hbpD ", "hbp16", "16-remap", "16-noepi", "16-noloop", "16-neither", "16-nostore",
+                           "16-noremap"};
+    const int NV = getenv("HB_DIAG") ? 8 : 3;
     auto set_variant = [&](int v) {
-        const char* tv[] = {"0", "1", "2", "3", "4", "5"};
+        const char* tv[] = {"0", "1", "2", "3", "4", "5", "6", "7", "8", "9", "10", "11", "12", "13", "14", "15", "16"};
         setenv("SUTA_HBX_T", tv[variants[v][3]], 1);
         setenv("SUTA_HBX_DBG", tv[variants[v][4]], 1);
         setenv("SUTA_HBX_FORM", tv[variants[v][5]], 1);
@@ -70,7 +79,7 @@ int main(int argc, char** argv) {
         gemm_set_variant(variants[v][0], variants[v][1]);
     };
     __bf16* Cb;
-    CK(hipMalloc(&Cb, (size_t)M * 4096 * 2));
+    CK(hipMalloc(&Cb, (size_t)M * (4096 + pad) * 2));
     for (auto& s : shapes) {
         GemmParams p;
         gemm_init(p);
@@ -79,9 +88,9 @@ int main(int argc, char** argv) {
         p.B = reinterpret_cast<const float*>(B);
         p.M = M; p.N = s.N; p.K = s.K;
         p.lda = s.K; p.ldb = s.K; p.tb = 1;
-        p.C = C; p.ldc = s.N;
+        p.C = C; p.ldc = s.N + pad;
         p.Ab = A; p.Bb = B; p.ldab = s.K; p.ldbb = s.K;
-        std::vector<float> ms[NV];
+        std::vector<float> ms[8];
         for (int rd = 0; rd < rounds; ++rd)
             for (int v = 0; v < NV; ++v) {
                 set_variant(v);
@@ -109,7 +118,7 @@ int main(int argc, char** argv) {
                     err = fmax(err, fabs(hc[(size_t)r * rstep * s.N + n] - hr[(size_t)r * s.N + n]));
             if (variants[v][2]) {   // the bf16 copy of C (epilogue CB path)
                 GemmParams q = p;
-                q.Cb = Cb; q.ldcb = s.N;
+                q.Cb = Cb; q.ldcb = s.N + pad;
                 gemm_launch(q, 0, nullptr, 0);
                 CK(hipDeviceSynchronize());
                 std::vector<__bf16> hb((size_t)M * s.N);
@@ -127,14 +136,51 @@ int main(int argc, char** argv) {
             fflush(stdout);
         }
     }
+    // K sweep (N = 4096, bf16 C plane only): time = fixed per-tile cost (prologue + epilogue) + K x loop rate
+    if (getenv("HB_KSWEEP")) {
+        for (int K : {128, 256, 512, 1024, 2048, 4096}) {
+            GemmParams p;
+            gemm_init(p);
+            p.mode = 2;
+            p.A = reinterpret_cast<const float*>(A);
+            p.B = reinterpret_cast<const float*>(B);
+            p.M = M; p.N = 4096; p.K = K;
+            p.lda = K; p.ldb = K; p.tb = 1;
+            p.C = nullptr; p.ldc = 4096;
+            p.Ab = A; p.Bb = B; p.ldab = K; p.ldbb = K;
+            p.Cb = Cb; p.ldcb = 4096 + pad;
+            std::vector<float> ms[8];
+            for (int rd = 0; rd < rounds; ++rd)
+                for (int v = 0; v < NV; ++v) {
+                    set_variant(v);
+                    for (int w = 0; w < 2; ++w) gemm_launch(p, 0, nullptr, 0);
+                    CK(hipEventRecord(e0, 0));
+                    for (int r = 0; r < reps; ++r) gemm_launch(p, 0, nullptr, 0);
+                    CK(hipEventRecord(e1, 0));
+                    CK(hipEventSynchronize(e1));
+                    float tt = 0;
+                    CK(hipEventElapsedTime(&tt, e0, e1));
+                    ms[v].push_back(tt / reps);
+                }
+            for (int v = 0; v < NV; ++v) {
+                std::vector<float> m = ms[v];
+                std::sort(m.begin(), m.end());
+                const double tf = 2.0 * M * 4096.0 * K / (m[m.size() / 2] * 1e-3) / 1e12;
+                printf("ksweep K%5d %s: median %.4f ms %.1f TF  per tile round %.2f us\n", K, vname[v], m[m.size() / 2], tf,
+                       m[m.size() / 2] * 1e3 / 16.0);
+                fflush(stdout);
+            }
+        }
+        return 0;
+    }
     // epilogue-heavy C4 shapes (bf16 C plane only, bf16 pre-activation operand): FFN1 forward (bias + GELU +
     // pre-activation store) and the FFN2 input gradient (x GELU'(u)); variants compared on their Cb outputs
     {
         float* bias;
         __bf16 *U, *Cref;
         CK(hipMalloc(&bias, 4096 * 4));
-        CK(hipMalloc(&U, (size_t)M * 4096 * 2));
-        CK(hipMalloc(&Cref, (size_t)M * 4096 * 2));
+        CK(hipMalloc(&U, (size_t)M * (4096 + pad) * 2));
+        CK(hipMalloc(&Cref, (size_t)M * (4096 + pad) * 2));
         hipLaunchKernelGGL(fillb, dim3((M * 4096L + 255) / 256), dim3(256), 0, 0, U, (long)M * 4096, 3u);
         std::vector<float> hbias(4096);
         for (int i = 0; i < 4096; ++i) hbias[i] = 0.01f * (i % 17) - 0.08f;
@@ -153,20 +199,20 @@ int main(int argc, char** argv) {
             p.lda = 1024; p.ldb = 1024; p.tb = 1;
             p.C = nullptr; p.ldc = 4096;
             p.Ab = A; p.Bb = B; p.ldab = 1024; p.ldbb = 1024;
-            p.Cb = Cb; p.ldcb = 4096; p.preb = 1;
+            p.Cb = Cb; p.ldcb = 4096 + pad; p.preb = 1;
             if (form == 0 || form == 2) {
                 p.epi = EPI_BIAS | EPI_STORE_PRE | (form == 0 ? EPI_GELU : 0);
                 p.bias = bias;
-                p.C2 = reinterpret_cast<float*>(U); p.ldc2 = 4096;
+                p.C2 = reinterpret_cast<float*>(U); p.ldc2 = 4096 + pad;
             } else if (form == 1) {
                 p.epi = EPI_DGELU;
-                p.aux = reinterpret_cast<const float*>(U); p.ldaux = 4096;
+                p.aux = reinterpret_cast<const float*>(U); p.ldaux = 4096 + pad;
             } else {
                 p.epi = 0;
                 p.preb = 0;
             }
-            const int evs[] = {0, 1};
-            std::vector<float> ms[NV];
+            const int evs[] = {0, 1, 2};
+            std::vector<float> ms[8];
             for (int rd = 0; rd < rounds; ++rd)
                 for (int v : evs) {
                     set_variant(v);
