@@ -91,6 +91,9 @@ struct SutaSwitches {
                           // 0 = the column-per-lane form shared with the 128 x 128 kernel
     int hbp_conv;         // SUTA_HBP_CONV (default 1): the conv stack's conv-seg input gradients on the four-phase 256 x 256
                           // kernel (gemm.hip use_hbp_conv); 0 = the 128 x 128 kernel
+    int hbt4;             // SUTA_HBT4 (default 1): the conv weight gradients (MN-contiguous bf16 planes) on the four-phase
+                          // 256 x 256 kernel's TN form (gemm_hbp_kernel) on grids of >= 256 tiles; 2 on every grid
+                          // (tests); 0 = gemm_hbt_kernel (128 x 128, two stages, split-K on small grids)
     int epi_fast;         // SUTA_EPI_FAST (default 1): 32-bit-offset GEMM epilogue where every operand fits 4 GiB (p.off32);
                           // 0 = the general epilogue everywhere
 };

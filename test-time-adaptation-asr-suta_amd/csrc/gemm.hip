@@ -251,14 +251,18 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
         throw std::invalid_argument("gemm: bf16 pre-activation operands need the bf16-plane kernel with a Cb plane, ldc2 even");
     if (hb && p.segK > 0 && (p.segK % 8 || p.pad < 0 || (p.segB && (p.sBseg % 8))))
         throw std::invalid_argument("gemm: conv-A bf16 planes need segK and the tap stride % 8 == 0");
-    int tile = hbt ? 0
+    // conv weight gradients: the four-phase 256 x 256 TN form on grids that fill the chip (>= 256 tiles of 256^2; a
+    // smaller grid keeps the 128 x 128 kernel with its split-K)
+    const bool hbt4 = hbt && g_force_tile < 0 && hbt4_ok(p) &&
+                      (suta_switches().hbt4 == 2 || (long)((p.M + 255) / 256) * ((p.N + 255) / 256) * p.Z >= 256);
+    int tile = hbt ? (hbt4 ? 8 : 0)
                : (hb && p.segK > 0) ? (g_force_tile < 0 && use_hbp_conv(p) ? 8 : 0)
                : g_force_tile >= 0 ? g_force_tile
                : hb            ? (use_hbx(p) ? 8 : choose_tile_hb(p.M, p.N, p.Z))
                : p.mode == 2   ? choose_tile_bf16(p.M, p.N, p.Z, !bf16_gbf)
                                : choose_tile(p.M, p.N, p.Z, p.K, p.mode);
     if ((tile == 8 || tile == 9) && !(hb && p.K % 32 == 0 && p.K >= 128 && p.segK == 0 && (p.Z == 1 || (tile == 8 && hbx_batch_ok(p)))) &&
-        !(tile == 8 && hb && p.segK > 0 && hbp_conv_ok(p)))
+        !(tile == 8 && hb && p.segK > 0 && hbp_conv_ok(p)) && !(tile == 8 && hbt))
         tile = 0;
     if (tile == 6 || tile == 7) tile = 0;  // (the removed 256 x 256 ping-pong and 160 x 128 tiles: DESIGN.md 8)
     // tiles 0 = 128x128, 1 = 128x64, 2 = 64x128, 3 = 64x64; bf16 mode also 4 = 256x128, 5 = 128x256
@@ -299,7 +303,10 @@ void gemm_launch(GemmParams p, hipStream_t st, float* ws, long ws_floats) {
         if (!hb && p.mode == 0 && splits == 1 && p.Z == 1 && gx >= 16) p.order = 8;
     }
     dim3 grid(gx, gy, p.Z * splits);
-    if (hbt) {
+    if (hbt && tile == 8) {
+        census("hbt4", BM, BN, p, splits);
+        gemm_run_hbt4(p, grid, st);
+    } else if (hbt) {
         census("hbt", BM, BN, p, splits);
         gemm_run_hbt(p, grid, st);
     } else if (hb) {

@@ -845,15 +845,25 @@ __device__ __forceinline__ int hbp_swz(int r) { return (r >> 1) & 7; }
 // one 256 x 256 output tile (a persistent kernel looping this body over its XCD's tiles, one block per CU with the next
 // tile's first K-tiles fetched while the epilogue's stores drain, measured 1-2 us per tile slower than one block per
 // tile: DESIGN.md section 8)
-template <bool CB, int EM, int FORM, bool CONV, int DBG>
+// TN (round 6, form 4 only): MN-contiguous operands (A(m, k) = Ab[k ldab + m], B(k, n) = Bb[k ldbb + n]: the conv
+// stack's weight gradients, im2col(a)^T dz, formerly gemm_hbt_kernel's 128 x 128 two-stage loop).  A half-tile image is
+// [64 k][128 columns] bf16 (256-B rows; columns = the half's 128 m or n in the same order as the k-contiguous form), its
+// 16-B chunk c of row r in slot c ^ tn_swz(r) (on the DMA source); a fragment's 8 consecutive k of one column are two
+// ds_read_b64_tr_b16 reads (per 16-lane group 4 rows x 16 columns delivered column-major: lane i gets column i), the
+// 8 rows a 32-lane half reads land on 8 disjoint 32-B slot pairs (conflict-free).  K need not be a multiple of 64: rows
+// past K read the zero page.  The quadrants, phases, waits and epilogue are form 4's.
+__device__ __forceinline__ int tn_swz(int r) { return 2 * ((r & 3) | (((r >> 3) & 1) << 2)); }
+
+template <bool CB, int EM, int FORM, bool CONV, int DBG, bool TN = false>
 __device__ __forceinline__ void hbp_tile(const GemmParams& p, const TileId tid, char* const lds) {
+    static_assert(!TN || (FORM == 4 && !CONV), "TN: form 4, no conv-A rows");
     // batch z (Z-batched GEMMs, the conv stack's per-utterance forward): operand planes offset in bf16 elements, the
     // epilogue's operands through a rebased copy of the parameters (batch z of a Z = 1 view)
     const int z1 = tid.z / p.zdiv, z0 = tid.z % p.zdiv;
     const __bf16* A = reinterpret_cast<const __bf16*>(p.Ab) + z1 * p.sA1 + z0 * p.sA0;
     const __bf16* B = reinterpret_cast<const __bf16*>(p.Bb) + z1 * p.sB1 + z0 * p.sB0;
     const int m0 = tid.y * 256, n0 = tid.x * 256;
-    const int nk = p.K / 64;
+    const int nk = TN ? (p.K + 63) / 64 : p.K / 64;
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wr = wid >> 2, wc = wid & 3;
@@ -864,10 +874,24 @@ __device__ __forceinline__ void hbp_tile(const GemmParams& p, const TileId tid, 
     int inc[4][2];
     int arow[2][2];  // CONV: source row m - pad of the A halves' pieces (segment 0)
     const int mv = CONV ? (p.zmvalid ? p.zmvalid[z1] : p.Mvalid) : 0;
+    int krow[2];  // TN: the k row (within a K-tile) of the lane's 16-B piece, per piece
 #pragma unroll
     for (int h = 0; h < 4; ++h)
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
+            if constexpr (TN) {  // piece = 4 image rows of 256 B; lane j: row 4 pc + j / 16, slot j % 16
+                const int pc = wid + 8 * i, kr = 4 * pc + (lane >> 4);
+                const int ch = (lane & 15) ^ tn_swz(kr);
+                const bool isa = h == 0 || h == 3;
+                const int q = h == 3 ? 1 : h == 2 ? 1 : 0;
+                const int gc = isa ? m0 + 128 * (ch >> 3) + 64 * q + 8 * (ch & 7) : n0 + 64 * (ch >> 2) + 32 * q + 8 * (ch & 3);
+                const bool ok = gc < (isa ? p.M : p.N);
+                const long ld = isa ? p.ldab : p.ldbb;
+                krow[i] = kr;
+                src[h][i] = ok ? (isa ? A : B) + (long)kr * ld + gc : reinterpret_cast<const __bf16*>(g_zero16);
+                inc[h][i] = ok ? (int)(64 * ld) : 0;
+                continue;
+            }
             const int pc = wid + 8 * i, lr = 8 * pc + (lane >> 3);
             const int c = (lane & 7) ^ hbp_swz(lr);
             const bool isa = h == 0 || h == 3;
@@ -912,6 +936,16 @@ __device__ __forceinline__ void hbp_tile(const GemmParams& p, const TileId tid, 
             }
             return;
         }
+        if constexpr (TN) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const __bf16* g = t * 64 + krow[i] < p.K ? src[h][i] : reinterpret_cast<const __bf16*>(g_zero16);
+                __builtin_amdgcn_global_load_lds(reinterpret_cast<const float*>(g),
+                                                 (lds_ptr_t)(dst + (wid + 8 * i) * 1024), 16, 0, 0);
+                src[h][i] += inc[h][i];
+            }
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             __builtin_amdgcn_global_load_lds(reinterpret_cast<const float*>(src[h][i]),
@@ -946,9 +980,29 @@ __device__ __forceinline__ void hbp_tile(const GemmParams& p, const TileId tid, 
         const int c = 4 * kk2 + (lane >> 4);
         return *reinterpret_cast<const bf16x8*>(img + lr * 128 + ((c ^ hbp_swz(lr)) << 4));
     };
+    // TN: 8 consecutive k (32 kk2 + 8 (lane >> 4) ..) of column 16 j + (lane & 15) of a [64][128] image
+    auto tr8 = [&](const char* img, int j, int kk2) {
+        typedef __attribute__((address_space(3))) fbf16x4_t* lp4;
+        const int gq = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+        bf16x8 v;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+            const int r = 32 * kk2 + 8 * gq + 4 * s2 + q;
+            const int slot = (2 * j + (pp >> 1)) ^ tn_swz(r);
+            const fbf16x4_t x = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lp4)(img + r * 256 + slot * 16 + 8 * (pp & 1)));
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[4 * s2 + e] = x[e];
+        }
+        return v;
+    };
     auto read_a = [&](int b, int qm) {
         const char* img = lds + (b * 4 + qm) * P_HALF;
-        if constexpr (M16) {
+        if constexpr (TN) {
+#pragma unroll
+            for (int bm = 0; bm < 4; ++bm)
+#pragma unroll
+                for (int kk2 = 0; kk2 < 2; ++kk2) fa[bm >> 1][2 * (bm & 1) + kk2] = tr8(img, 4 * wr + bm, kk2);
+        } else if constexpr (M16) {
 #pragma unroll
             for (int bm = 0; bm < 4; ++bm)
 #pragma unroll
@@ -963,7 +1017,12 @@ __device__ __forceinline__ void hbp_tile(const GemmParams& p, const TileId tid, 
     };
     auto read_b = [&](int b, int qn, bf16x8 (&fb)[4]) {
         const char* img = lds + (b * 4 + 2 + qn) * P_HALF;
-        if constexpr (M16) {
+        if constexpr (TN) {
+#pragma unroll
+            for (int bn = 0; bn < 2; ++bn)
+#pragma unroll
+                for (int kk2 = 0; kk2 < 2; ++kk2) fb[2 * bn + kk2] = tr8(img, 2 * wc + bn, kk2);
+        } else if constexpr (M16) {
 #pragma unroll
             for (int bn = 0; bn < 2; ++bn)
 #pragma unroll
@@ -1182,10 +1241,10 @@ __device__ __forceinline__ void hbp_tile(const GemmParams& p, const TileId tid, 
     }
 }
 
-template <bool CB, int EM, int FORM, bool CONV = false, int DBG = 0>
+template <bool CB, int EM, int FORM, bool CONV = false, int DBG = 0, bool TN = false>
 __global__ __launch_bounds__(512, 1) void gemm_hbp_kernel(GemmParams p) {
     __shared__ __attribute__((aligned(16))) float smem[8 * P_HALF / 4];
-    hbp_tile<CB, EM, FORM, CONV, DBG>(p, xcd_tile(p.order), reinterpret_cast<char*>(smem));
+    hbp_tile<CB, EM, FORM, CONV, DBG, TN>(p, xcd_tile(p.order), reinterpret_cast<char*>(smem));
 }
 
 template <int MS, int EM, int TR = 0>
@@ -1253,6 +1312,18 @@ constexpr int XEM_D = EPI_DGELU | EPI_ROWMASK;
 constexpr int XEM_L = EPI_DELTA;  // the attention out-projection's input gradient with the flash backward's delta
 
 }  // namespace
+
+// the conv stack's weight gradients (MN-contiguous bf16 planes, gemm.hip use_hbt4) on the four-phase 256 x 256 kernel's
+// TN form: fp32 C only, the plain / bias / residual class, no split-K, the staged C^T epilogue's operand conditions
+bool hbt4_ok(const GemmParams& p) {
+    return suta_switches().hbt4 && p.ta && !p.tb && p.Ab && p.Bb && !p.Cb && p.segK == 0 && p.zdiv == 1 &&
+           p.splits <= 1 && (p.epi & ~(EPI_BIAS | EPI_RESID | EPI_ROWMASK)) == 0 && hbx_t_ok(p, true);
+}
+void gemm_run_hbt4(const GemmParams& p, dim3 grid, hipStream_t st) {
+    if (!hbt4_ok(p)) throw std::invalid_argument("hbt4: outside the TN form's conditions");
+    hipLaunchKernelGGL((gemm_hbp_kernel<false, EPI_BIAS | EPI_RESID | EPI_ROWMASK, 4, false, 0, true>), grid, dim3(512),
+                       0, st, p);
+}
 
 // variant 1: v_mfma_f32_32x32x16_bf16 with the shared epilogue (class-specialised kernels for the linears' epilogue
 // classes, the generic one otherwise); 2: v_mfma_f32_16x16x32_bf16 with epilogue16 (the linears' classes only)

@@ -1799,6 +1799,8 @@ void gemm_run_gbf(int bk64, int nprod, int tile, const GemmParams& p, dim3 grid,
 void gemm_run_hb(int tile, int ns, const GemmParams& p, dim3 grid, hipStream_t st);                         // gemm_hb.hip
 void gemm_run_hbt(const GemmParams& p, dim3 grid, hipStream_t st);                                          // gemm_hb.hip
 void gemm_run_hbx(int variant, const GemmParams& p, dim3 grid, hipStream_t st);                             // gemm_hbx.hip
+void gemm_run_hbt4(const GemmParams& p, dim3 grid, hipStream_t st);                                         // gemm_hbx.hip
+bool hbt4_ok(const GemmParams& p);  // the conv weight gradients on the four-phase kernel's TN form (gemm_hbx.hip)
 // the row-per-lane (C^T accumulator) epilogue's operand conditions (gemm_hbx.hip)
 bool hbx_t_ok(const GemmParams& p, bool check_off32);
 // conv-A GEMM (segK > 0) eligible for the four-phase 256 x 256 kernel's CONV form (gemm_hbx.hip; p.off32 set)

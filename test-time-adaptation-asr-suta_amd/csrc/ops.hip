@@ -1941,6 +1941,8 @@ void suta_latch_switches() {
     s.ln_rpw = lrpw ? atoi(lrpw) : 2;
     const char* hform = std::getenv("SUTA_HBX_FORM");
     s.hbx_form = hform ? atoi(hform) : 4;
+    const char* ht4 = std::getenv("SUTA_HBT4");
+    s.hbt4 = ht4 ? atoi(ht4) : 1;
     const char* hdbg = std::getenv("SUTA_HBX_DBG");
     s.hbx_dbg = hdbg ? atoi(hdbg) : 0;
     const char* fnw = std::getenv("SUTA_FLASH_FWD_NW");

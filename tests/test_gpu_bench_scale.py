@@ -188,8 +188,8 @@ def test_c4_bench_layout_bf16():
     the 256 x 256 bf16-plane kernel (hbx) over ceil(B x 399 / 256) row tiles, the K = 32 lm_head input gradient on
     the 128 x 128 one over ceil(B x 399 / 128), the conv stack's per-utterance (Z = B) GEMMs on bf16 planes --
     forward and input gradients (conv-A rows, per-tap weight segments) on the four-phase 256 x 256 kernel (no
-    conv-seg launch left on the 128 x 128 one), weight gradients on
-    the MN-contiguous hbt kernel -- and the per-utterance feature-projection weight gradient.
+    conv-seg launch left on the 128 x 128 one), weight gradients (MN-contiguous planes) on the four-phase kernel's TN
+    form (round 6; formerly the 128 x 128 hbt kernel) -- and the per-utterance feature-projection weight gradient.
     Reference main.py:181,205 (forward and backward through the encoder)."""
     from oracle import w2v2_cpu as W
     import os
@@ -222,7 +222,7 @@ def test_c4_bench_layout_bf16():
     assert any(k.startswith("hbx 256x256 ") and z in k and k.endswith(" conv-seg") for k in census), txt
     assert not any(k.startswith("hb ") and z in k and k.endswith(" conv-seg") for k in census), txt
     assert any(k.startswith("hbx 256x256 ") and z in k and "conv" not in k for k in census), txt
-    assert any(k.startswith("hbt ") and z in k for k in census), txt                        # conv dW
+    assert any(k.startswith("hbt4 256x256 ") and z in k for k in census), txt             # conv dW (TN form)
     assert any(z in k and k.startswith(("gbf", "x6_1plane")) for k in census), txt
     eng.set_precision("fp32")
     for slot in _slots(B):

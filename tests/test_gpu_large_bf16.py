@@ -514,6 +514,37 @@ def test_conv_input_gradients_on_256_tile_bitwise(monkeypatch, form):
         assert np.array_equal(v, params["0"][n]), n
 
 
+def test_conv_weight_gradients_on_256_tile_tn_form_bitwise(monkeypatch):
+    """The layer-norm conv stack's weight gradients dW_i = im2col(a_{i-1})^T dz_i (MN-contiguous bf16 planes, Z = batch;
+    config C4's former gemm_hbt_kernel GEMMs) on the four-phase 256 x 256 kernel's TN form (transposed LDS reads of
+    [k][m] images, K tails read from the zero page; SUTA_HBT4=2 forces it onto the small test grids) against the
+    128 x 128 hbt kernel (SUTA_HBT4=0), no split-K: the same products summed in the same k order, so logits and adapted
+    tensors (the conv weights among them) are bitwise equal.  wav2vec2-large in bf16 mode, a ragged pair."""
+    monkeypatch.setenv("SUTA_SPLITK", "0")
+    cfg = get_config("wav2vec2-large")
+    sd = synth_weights(cfg)
+    waves = [synth.wave(32000, 76), synth.wave(20000, 77)]
+    out, params, dw = {}, {}, {}
+    for h4 in ("2", "0"):
+        monkeypatch.setenv("SUTA_HBT4", h4)
+        eng = SutaEngine(cfg, sd, max_batch=2, max_samples=32000)
+        eng.set_precision("bf16")
+        eng.set_census(True)
+        out[h4], _, _ = eng.adapt_varlen(waves, 2, SutaHParams(), record=[0, 2])
+        census = eng.get_census()
+        eng.set_census(False)
+        dw[h4] = [k for k in census if k.startswith("hbt")]
+        params[h4] = {n: eng.get_param(1, n) for n in eng.trainable_names()}
+        eng.close()
+    assert dw["2"] and all(k.startswith("hbt4 256x256 ") for k in dw["2"]), dw["2"]
+    assert dw["0"] and all(k.startswith("hbt 128x128 ") for k in dw["0"]), dw["0"]
+    for r in (0, 2):
+        for u in range(2):
+            assert np.array_equal(out["2"][r][u], out["0"][r][u]), (r, u)
+    for n, v in params["2"].items():
+        assert np.array_equal(v, params["0"][n]), n
+
+
 @pytest.mark.parametrize("model", ["wav2vec2-large", "wav2vec2-base"])
 def test_bf16_plane_flash_backward_ragged_edges(monkeypatch, model):
     """The bf16-plane flash backward (key-major dS image read back transposed for dQ, row-permuted Q / dO images, dQ
