@@ -70,7 +70,7 @@ GEMM_KERNELS_C4 = ("gemm_hb_kernel", "gemm_hbx_kernel", "gemm_hbp_kernel", "gemm
                    "flash_bwd_bf16p_kernel", "flash_fwd_bf16_kernel", "flash_bwd_bf16_kernel", "flash_dq_reduce",
                    "flash_dq_reduce_frag")
 # kernels of each family the C4 bench layout must have launched (a missing entry means a stale PMC table)
-C4_REQUIRED = ("gemm_hb_kernel", "gemm_hbp_kernel", "gemm_hbt_kernel", "flash_fwd_bf16p_kernel", "flash_bwd_bf16p_kernel",
+C4_REQUIRED = ("gemm_hb_kernel", "gemm_hbp_kernel", "flash_fwd_bf16p_kernel", "flash_bwd_bf16p_kernel",
                "flash_dq_reduce_frag")
 FRONT_KERNELS = ("conv0_gn_kernel", "col_stats_final", "gn_bwd_final", "conv0_dw_reduce")
 
@@ -407,7 +407,7 @@ def bench_c4(args, dev):
         gms, gn = t["gemm"]
         ach = flops_utt * B / (gms / 1000.0) / 1e12
         res["roofline"] = {"bound": "mfma", "achieved": round(ach, 3), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                           "frac": round(ach / BF16_PEAK_TFLOPS, 4), "kernel": "bf16 GEMM family (bf16-plane linears: gemm_hbp_kernel / gemm_hbx_kernel (256 x 256), gemm_hb_kernel (the K = 32 lm_head input gradient); the layer-norm conv stack's forward / input gradients: gemm_hb_kernel; conv weight gradients: gemm_hbt_kernel; per-utterance projection GEMMs: gemm_x6_kernel one-plane form / gemm_gbf_kernel; posconv_bf16_kernel; flash attention on bf16 MFMA)",
+                           "frac": round(ach / BF16_PEAK_TFLOPS, 4), "kernel": "bf16 GEMM family (bf16-plane linears: gemm_hbp_kernel (256 x 256, 16x16x32 MFMA since round 6) / gemm_hbx_kernel, gemm_hb_kernel (the K = 32 lm_head input gradient); the layer-norm conv stack's forward / input gradients: gemm_hbp_kernel (Z-batched / CONV forms); conv weight gradients: gemm_hbp_kernel TN form (round 6; gemm_hbt_kernel before); per-utterance projection GEMMs: gemm_x6_kernel one-plane form / gemm_gbf_kernel; posconv_bf16_kernel; flash attention on bf16 MFMA)",
                            "launches": int(gn), "avg_launch_ms": round(gms / max(1, gn), 5)}
         gx, ax = tex["gemm"], tex["attention"]
         talg = round((gx[2] + ax[2]) / max(1, gx[1] + ax[1]))
