@@ -298,7 +298,7 @@ __device__ __forceinline__ void epilogue_t_edge(const GemmParams& p, const f32x1
 // (chunk c of row r in slot c ^ (r & 7): conflict-free ds_write_b128 / ds_read_b128), read back row-contiguous
 // (8 lanes = one 128-B bf16 row of the wave tile, 16 lanes = one 256-B fp32 row) and stored with every lane of an
 // instruction in 8 whole lines.  Without ST a store instruction touches 32 rows.
-template <bool CB, int EM, bool ST, int NOST = 0>
+template <bool CB, int EM, bool ST, int NOST = 0, bool NT = false>
 __device__ __forceinline__ void epilogue_t(const GemmParams& p, const f32x16 (&acc)[4][2], int rbase, int cbase,
                                            int lane, char* stage) {
     if (cbase + 64 > p.N) {
@@ -332,7 +332,11 @@ __device__ __forceinline__ void epilogue_t(const GemmParams& p, const f32x16 (&a
             const int r = 8 * k + (lane >> 3), c = lane & 7;
             const u32x4v w = *reinterpret_cast<const u32x4v*>(img + r * 128 + ((c ^ (r & 7)) << 4));
             if constexpr (NOST != 0) asm volatile("" ::"v"(w));  // (tools diagnostics: no global store)
-            else if (row0 + r < p.M) *reinterpret_cast<u32x4v*>(base + (long)(row0 + r) * ld + cbase + 8 * c) = w;
+            else if (row0 + r < p.M) {
+                u32x4v* d = reinterpret_cast<u32x4v*>(base + (long)(row0 + r) * ld + cbase + 8 * c);
+                if constexpr (NT) __builtin_nontemporal_store(w, d);
+                else *d = w;
+            }
         }
     };
     auto flush_f32 = [&](const char* img, float* base, long ld, int row0) {
@@ -340,7 +344,11 @@ __device__ __forceinline__ void epilogue_t(const GemmParams& p, const f32x16 (&a
         for (int k = 0; k < 8; ++k) {
             const int r = 4 * k + (lane >> 4), c = lane & 15;
             const f32x4 w = *reinterpret_cast<const f32x4*>(img + r * 256 + ((c ^ (r & 7)) << 4));
-            if (row0 + r < p.M) *reinterpret_cast<f32x4*>(base + (long)(row0 + r) * ld + cbase + 4 * c) = w;
+            if (row0 + r < p.M) {
+                f32x4* d = reinterpret_cast<f32x4*>(base + (long)(row0 + r) * ld + cbase + 4 * c);
+                if constexpr (NT) __builtin_nontemporal_store(w, d);
+                else *d = w;
+            }
         }
     };
     auto wave_sync = [] {
@@ -348,6 +356,32 @@ __device__ __forceinline__ void epilogue_t(const GemmParams& p, const f32x16 (&a
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
+    // GELU' / residual operands one band ahead (issued once band i has consumed its own, before band i's stores: a wait
+    // for them never covers those stores; as epilogue16t)
+    struct OpsT {
+        u32x4v a[2][2];    // GELU' operand of the bf16 pre-activation plane (the 16 B of the run pair; an fp32
+                           // operand is loaded where it is used)
+        f32x4 r[2][2][2];  // residual [j][q][t]
+    };
+    auto load_ops = [&](int i, OpsT& o) {
+        const long rowc = min(rbase + 32 * i + l32, p.M - 1);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const int nb = cbase + 32 * j + 16 * q;
+                if ((e & EPI_DGELU) && preb)
+                    o.a[j][q] = *reinterpret_cast<const u32x4v*>(reinterpret_cast<const __bf16*>(p.aux) + rowc * p.ldaux +
+                                                                 nb + 8 * h);
+                if (e & EPI_RESID) {
+#pragma unroll
+                    for (int t = 0; t < 2; ++t)
+                        o.r[j][q][t] = *reinterpret_cast<const f32x4*>(p.R + rowc * p.ldr + nb + 8 * t + 4 * h);
+                }
+            }
+    };
+    OpsT o;
+    if (e & (EPI_DGELU | EPI_RESID)) load_ops(0, o);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int row = rbase + 32 * i + l32;
@@ -363,8 +397,7 @@ __device__ __forceinline__ void epilogue_t(const GemmParams& p, const f32x16 (&a
                 float v[8], xa[8], xr[8];
                 if (e & EPI_DGELU) {
                     if (preb) {
-                        const u32x4v w = *reinterpret_cast<const u32x4v*>(reinterpret_cast<const __bf16*>(p.aux) +
-                                                                           rowc * p.ldaux + nb + 8 * h);
+                        const u32x4v w = o.a[j][q];
                         unsigned x0 = w[0], y0 = w[1], x1 = w[2], y1 = w[3];
                         swap_runs(x0, y0, x1, y1);
                         xa[0] = bf16_lo(x0); xa[1] = bf16_hi(x0); xa[2] = bf16_lo(y0); xa[3] = bf16_hi(y0);
@@ -380,11 +413,9 @@ __device__ __forceinline__ void epilogue_t(const GemmParams& p, const f32x16 (&a
                 }
                 if (e & EPI_RESID) {
 #pragma unroll
-                    for (int t = 0; t < 2; ++t) {
-                        const f32x4 w = *reinterpret_cast<const f32x4*>(p.R + rowc * p.ldr + nb + 8 * t + 4 * h);
+                    for (int t = 0; t < 2; ++t)
 #pragma unroll
-                        for (int k = 0; k < 4; ++k) xr[4 * t + k] = w[k];
-                    }
+                        for (int k = 0; k < 4; ++k) xr[4 * t + k] = o.r[j][q][t][k];
                 }
 #pragma unroll
                 for (int t = 0; t < 2; ++t) {
@@ -439,8 +470,8 @@ __device__ __forceinline__ void epilogue_t(const GemmParams& p, const f32x16 (&a
                 if (e & EPI_DELTA) {
 #pragma unroll
                     for (int t = 0; t < 2; ++t) {
-                        const f32x4 o = *reinterpret_cast<const f32x4*>(p.dlt_o + rowc * p.ldo + nb + 8 * t + 4 * h);
-                        const float d4 = fmaf(v[4 * t + 3], o[3], fmaf(v[4 * t + 2], o[2], fmaf(v[4 * t + 1], o[1], v[4 * t] * o[0])));
+                        const f32x4 od = *reinterpret_cast<const f32x4*>(p.dlt_o + rowc * p.ldo + nb + 8 * t + 4 * h);
+                        const float d4 = fmaf(v[4 * t + 3], od[3], fmaf(v[4 * t + 2], od[2], fmaf(v[4 * t + 1], od[1], v[4 * t] * od[0])));
                         sg[2 * q + t] = j == 0 ? d4 : sg[2 * q + t] + d4;
                     }
                 }
@@ -461,6 +492,7 @@ __device__ __forceinline__ void epilogue_t(const GemmParams& p, const f32x16 (&a
                     store_bf16(reinterpret_cast<__bf16*>(p.Cb) + (long)row * p.ldcb + nb + 8 * h, v, rok,
                                ST ? s_cb : nullptr, 4 * j + 2 * q + h);
             }
+        if ((e & (EPI_DGELU | EPI_RESID)) && i + 1 < 4) load_ops(i + 1, o);
         if constexpr (ST) {
             wave_sync();
             const int row0 = rbase + 32 * i;
@@ -487,12 +519,12 @@ __device__ __forceinline__ void epilogue_t(const GemmParams& p, const f32x16 (&a
 // and fp32 operands load as 16-B vectors and bf16 operands as 8-B vectors per lane, and the outputs enter the staging
 // images as 8-B (bf16) or 16-B (fp32) pieces straight from the registers -- no remap of the accumulators to the 32x32
 // layout (which cost 1.6 us of a 33-us K = 1024 tile: profiles/r6/hbp_diag2.txt) and no v_permlane32_swap.  Same
-// operations in the same order as epilogue_t per element.  Used for the bf16-C-plane bias / residual class only (see
-// NATIVE16 in hbp_tile); every flag is implemented so the A/B forms (tools DBG builds) stay comparable.  Images per 32-row band and wave (the buffers are free after
+// operations in the same order as epilogue_t per element.  Used for the bias / residual class (see NATIVE16 in
+// hbp_tile); every flag is implemented so the A/B forms (tools DBG builds) stay comparable.  Images per 32-row band and wave (the buffers are free after
 // the main loop): bf16 [32][128 B] with 16-B chunk c of row r at slot c ^ ((r >> 1) & 7) (the 8-B writes of 16 rows x 2
 // halves and the 16-B flush reads both conflict-free), fp32 [32][256 B] with chunk c at c ^ (r & 15).  Classes without
 // EPI_DELTA (the delta epilogue's summation tree is the 32x32 layout's: its kernels keep the remap).
-template <bool CB, int EM>
+template <bool CB, int EM, bool NT = false>
 __device__ __forceinline__ void epilogue16t(const GemmParams& p, const f32x4 (&acc)[8][4], int rbase, int cbase,
                                             int lane, char* stage) {
     const int e = p.epi & EM;
@@ -549,7 +581,11 @@ __device__ __forceinline__ void epilogue16t(const GemmParams& p, const f32x4 (&a
         for (int k = 0; k < 4; ++k) {
             const int r = 8 * k + (lane >> 3), c = lane & 7;
             const u32x4v w = *reinterpret_cast<const u32x4v*>(img + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
-            if (row0 + r < p.M) *reinterpret_cast<u32x4v*>(base + (long)(row0 + r) * ld + cbase + 8 * c) = w;
+            if (row0 + r < p.M) {
+                u32x4v* d = reinterpret_cast<u32x4v*>(base + (long)(row0 + r) * ld + cbase + 8 * c);
+                if constexpr (NT) __builtin_nontemporal_store(w, d);
+                else *d = w;
+            }
         }
     };
     auto flush_f32 = [&](const char* img, float* base, long ld, int row0) {
@@ -557,52 +593,83 @@ __device__ __forceinline__ void epilogue16t(const GemmParams& p, const f32x4 (&a
         for (int k = 0; k < 8; ++k) {
             const int r = 4 * k + (lane >> 4), c = lane & 15;
             const f32x4 w = *reinterpret_cast<const f32x4*>(img + r * 256 + ((c ^ (r & 15)) << 4));
-            if (row0 + r < p.M) *reinterpret_cast<f32x4*>(base + (long)(row0 + r) * ld + cbase + 4 * c) = w;
+            if (row0 + r < p.M) {
+                f32x4* d = reinterpret_cast<f32x4*>(base + (long)(row0 + r) * ld + cbase + 4 * c);
+                if constexpr (NT) __builtin_nontemporal_store(w, d);
+                else *d = w;
+            }
         }
     };
     typedef __bf16 bf16x4v __attribute__((ext_vector_type(4)));
+    // Epilogue operands one 32-row band ahead: band i + 1's residual / GELU'-operand loads are issued as soon as band i
+    // has consumed its own (before band i's stores), so the wait for them never covers those stores (a counted vmcnt
+    // retires in order: loading right before use made every band wait for the previous band's stores and for each
+    // load's latency -- profiles/r6/hbp_resid*.txt).  The bias (the same for every band) is loaded once.
+    typedef unsigned u32x2v __attribute__((ext_vector_type(2)));
+    struct Ops {
+        f32x4 r[2][4];   // residual, [b2][bn]
+        u32x4v a[2][4];  // GELU' operand: 4 bf16 in words 0-1 (bf16 pre-activation plane) or 4 fp32
+    };
+    auto load_ops = [&](int i, Ops& o) {
+#pragma unroll
+        for (int b2 = 0; b2 < 2; ++b2) {
+            const long rowc = min(rbase + 32 * i + 16 * b2 + l16, p.M - 1);
+#pragma unroll
+            for (int bn = 0; bn < 4; ++bn) {
+                const int col = cbase + 16 * bn + 4 * g;
+                if (e & EPI_RESID) o.r[b2][bn] = *reinterpret_cast<const f32x4*>(p.R + rowc * p.ldr + col);
+                if (e & EPI_DGELU) {
+                    if (preb) {
+                        const u32x2v w = *reinterpret_cast<const u32x2v*>(reinterpret_cast<const __bf16*>(p.aux) +
+                                                                          rowc * p.ldaux + col);
+                        o.a[b2][bn] = u32x4v{w[0], w[1], 0u, 0u};
+                    } else {
+                        o.a[b2][bn] = *reinterpret_cast<const u32x4v*>(p.aux + rowc * p.ldaux + col);
+                    }
+                }
+            }
+        }
+    };
+    f32x4 bjv[4];
+    if (e & EPI_BIAS) {
+#pragma unroll
+        for (int bn = 0; bn < 4; ++bn) bjv[bn] = *reinterpret_cast<const f32x4*>(p.bias + cbase + 16 * bn + 4 * g);
+    }
+    Ops o;
+    load_ops(0, o);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
 #pragma unroll
         for (int b2 = 0; b2 < 2; ++b2) {
             const int rl = 16 * b2 + l16;  // row within the band
             const int row = rbase + 32 * i + rl;
-            const long rowc = min(row, p.M - 1);
             const bool rok = row < p.M;
             const bool zero = (e & EPI_ROWMASK) && row >= rlim;
-            // DGELU: the row block's pre-activation operands loaded before the first use (EM-specialised: only the
-            // GELU' class carries them)
-            bf16x4v xab[4];
-            f32x4 xaf[4];
-            if (e & EPI_DGELU) {
-#pragma unroll
-                for (int bn = 0; bn < 4; ++bn) {
-                    const int col = cbase + 16 * bn + 4 * g;
-                    if (preb) xab[bn] = *reinterpret_cast<const bf16x4v*>(reinterpret_cast<const __bf16*>(p.aux) +
-                                                                          rowc * p.ldaux + col);
-                    else xaf[bn] = *reinterpret_cast<const f32x4*>(p.aux + rowc * p.ldaux + col);
-                }
-            }
 #pragma unroll
             for (int bn = 0; bn < 4; ++bn) {
                 const int cl = 16 * bn + 4 * g;  // column within the wave tile
                 const int col = cbase + cl;
                 float v[4], xa[4], xr[4];
                 if (e & EPI_DGELU) {
+                    const u32x4v w = o.a[b2][bn];
+                    if (preb) {
+                        xa[0] = bf16_lo(w[0]);
+                        xa[1] = bf16_hi(w[0]);
+                        xa[2] = bf16_lo(w[1]);
+                        xa[3] = bf16_hi(w[1]);
+                    } else {
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) xa[k] = preb ? (float)xab[bn][k] : xaf[bn][k];
+                        for (int k = 0; k < 4; ++k) xa[k] = __uint_as_float(w[k]);
+                    }
                 }
                 if (e & EPI_RESID) {
-                    const f32x4 w = *reinterpret_cast<const f32x4*>(p.R + rowc * p.ldr + col);
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) xr[k] = w[k];
+                    for (int k = 0; k < 4; ++k) xr[k] = o.r[b2][bn][k];
                 }
-                f32x4 bj = {0.f, 0.f, 0.f, 0.f};
-                if (e & EPI_BIAS) bj = *reinterpret_cast<const f32x4*>(p.bias + col);
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     v[k] = acc[2 * i + b2][bn][k] * alpha;
-                    if (e & EPI_BIAS) v[k] += bj[k];
+                    if (e & EPI_BIAS) v[k] += bjv[bn][k];
                 }
                 if (e & EPI_STORE_PRE) {
                     if (preb) {
@@ -652,6 +719,7 @@ __device__ __forceinline__ void epilogue16t(const GemmParams& p, const f32x4 (&a
                 }
             }
         }
+        if (i + 1 < 4) load_ops(i + 1, o);  // (band i's operands are dead: issued before band i's stores)
         wave_sync();
         const int row0 = rbase + 32 * i;
         if (st_pre) flush_bf16(s_pre, reinterpret_cast<__bf16*>(p.C2), p.ldc2, row0);
@@ -841,7 +909,8 @@ __device__ __forceinline__ int hbp_swz(int r) { return (r >> 1) & 7; }
 // segment), so the shifts live in the DMA pointers, not in per-element VALU work.
 // DBG (tools/hb_bench diagnostics only, -DSUTA_HBX_DIAG; wrong results): 1 no epilogue (accumulators kept live), 2 no
 // K loop (prologue DMA and epilogue only), 3 neither, 4 no global stores of the staged epilogue (with the remap), 8 no
-// LDS remap of the 16x16 accumulators (into epilogue_t), 16 the remap + epilogue_t instead of epilogue16t
+// LDS remap of the 16x16 accumulators (into epilogue_t), 16 the remap + epilogue_t instead of epilogue16t, 32
+// nontemporal global stores in the epilogue
 // one 256 x 256 output tile (a persistent kernel looping this body over its XCD's tiles, one block per CU with the next
 // tile's first K-tiles fetched while the epilogue's stores drain, measured 1-2 us per tile slower than one block per
 // tile: DESIGN.md section 8)
@@ -1165,10 +1234,11 @@ __device__ __forceinline__ void hbp_tile(const GemmParams& p, const TileId tid, 
         if (wr == 0) __builtin_amdgcn_s_barrier();  // the leading group's matching barrier
     }
     __syncthreads();  // every wave is done with the buffers: wave-private 16-KB staging images
-    // the native 16x16 epilogue on the class where the C4 loop measured it faster than the remap + epilogue_t
-    // (profiles/r6/trab2: the bf16-C-plane bias / residual linears and conv GEMMs -2..-5 %); the GELU / GELU' classes
-    // measured 2-8 % slower with it and the fp32-only class 1 %, so they keep the remap
-    constexpr bool NATIVE16 = CB && EM == (EPI_BIAS | EPI_RESID | EPI_ROWMASK) && (DBG & 16) == 0;
+    // the native 16x16 epilogue on the class where the C4 loop measured it faster than the remap + epilogue_t: the bias /
+    // residual linears, conv GEMMs and conv weight gradients (profiles/r6/trace_ab/nat2_*: fp32-output residual linears
+    // -7 %, QKV -7 %, bf16-plane residual linears -2 %, with the band-ahead operand loads); the GELU / GELU' classes
+    // measured 2 % slower with it in the loop (though faster in tools/hb_bench) and keep the remap
+    constexpr bool NATIVE16 = EM == (EPI_BIAS | EPI_RESID | EPI_ROWMASK) && (DBG & 16) == 0;
     if constexpr ((DBG & 1) != 0) {
 #pragma unroll
         for (int i = 0; i < 8; ++i)
@@ -1235,9 +1305,10 @@ __device__ __forceinline__ void hbp_tile(const GemmParams& p, const TileId tid, 
                         : p.C2 + z1 * p.sC21 + z0 * p.sC20;
         if (p.zrows) q.zrows = p.zrows + z1;
         if constexpr (M16 && NATIVE16 && (DBG & 8) == 0)
-            epilogue16t<CB, EM>(q, acc16, m0 + wr * 128, n0 + wc * 64, lane, lds + wid * 16384);
+            epilogue16t<CB, EM, (DBG & 32) != 0>(q, acc16, m0 + wr * 128, n0 + wc * 64, lane, lds + wid * 16384);
         else
-            epilogue_t<CB, EM, true, (DBG & 4)>(q, acc, m0 + wr * 128, n0 + wc * 64, lane, lds + wid * 16384);
+            epilogue_t<CB, EM, true, (DBG & 4), (DBG & 32) != 0>(q, acc, m0 + wr * 128, n0 + wc * 64, lane,
+                                                                 lds + wid * 16384);
     }
 }
 
@@ -1389,7 +1460,7 @@ void gemm_run_hbx(int variant, const GemmParams& p, dim3 grid, hipStream_t st) {
 #undef HBP
     }
 #ifdef SUTA_HBX_DIAG
-    if (dbg >= 11 && dbg <= 16 && (e & ~XEM_A) == 0) {  // tools/hb_bench: gemm_hbp_kernel form 4 diagnostics
+    if (dbg >= 11 && dbg <= 17 && (e & ~XEM_A) == 0) {  // tools/hb_bench: gemm_hbp_kernel form 4 diagnostics
         const bool cb = p.Cb != nullptr;
 #define HBP_DBG(D)                                                                                                 \
         do {                                                                                                       \
@@ -1401,7 +1472,8 @@ void gemm_run_hbx(int variant, const GemmParams& p, dim3 grid, hipStream_t st) {
         else if (dbg == 13) HBP_DBG(3);
         else if (dbg == 14) HBP_DBG(20);
         else if (dbg == 15) HBP_DBG(8);
-        else HBP_DBG(16);
+        else if (dbg == 16) HBP_DBG(16);
+        else HBP_DBG(32);
 #undef HBP_DBG
         return;
     }

@@ -69,14 +69,22 @@ int main(int argc, char** argv) {
                                {8, 2, 1, 2, 12, 4}, {8, 2, 1, 2, 13, 4}, {8, 2, 1, 2, 14, 4}, {8, 2, 1, 2, 15, 4}};
     const char* vname[] = {"hbpD ", "hbp16", "16-remap", "16-noepi", "16-noloop", "16-neither", "16-nostore",
                            "16-noremap"};
-    const int NV = getenv("HB_DIAG") ? 8 : 3;
+    int NV = getenv("HB_DIAG") ? 8 : 3;
+    // HB_NT=1: form 4 (default epilogues) against the same with nontemporal epilogue stores (SUTA_HBX_DBG 17)
+    int vmap[8] = {0, 1, 2, 3, 4, 5, 6, 7};
+    static const int vnt[2][6] = {{8, 2, 1, 2, 0, 4}, {8, 2, 1, 2, 17, 4}};
+    const char* vnt_name[2] = {"hbp16", "16-NT"};
+    const bool ntmode = getenv("HB_NT") != nullptr;
+    if (ntmode) NV = 2;
+    (void)vmap;
+    auto vrow = [&](int v) -> const int* { return ntmode ? vnt[v] : variants[v]; };
     auto set_variant = [&](int v) {
-        const char* tv[] = {"0", "1", "2", "3", "4", "5", "6", "7", "8", "9", "10", "11", "12", "13", "14", "15", "16"};
-        setenv("SUTA_HBX_T", tv[variants[v][3]], 1);
-        setenv("SUTA_HBX_DBG", tv[variants[v][4]], 1);
-        setenv("SUTA_HBX_FORM", tv[variants[v][5]], 1);
+        const char* tv[] = {"0", "1", "2", "3", "4", "5", "6", "7", "8", "9", "10", "11", "12", "13", "14", "15", "16", "17"};
+        setenv("SUTA_HBX_T", tv[vrow(v)[3]], 1);
+        setenv("SUTA_HBX_DBG", tv[vrow(v)[4]], 1);
+        setenv("SUTA_HBX_FORM", tv[vrow(v)[5]], 1);
         suta_latch_switches();
-        gemm_set_variant(variants[v][0], variants[v][1]);
+        gemm_set_variant(vrow(v)[0], vrow(v)[1]);
     };
     __bf16* Cb;
     CK(hipMalloc(&Cb, (size_t)M * (4096 + pad) * 2));
@@ -116,7 +124,7 @@ int main(int argc, char** argv) {
             for (int r = 0; r < rows; ++r)
                 for (int n = 0; n < s.N; ++n)
                     err = fmax(err, fabs(hc[(size_t)r * rstep * s.N + n] - hr[(size_t)r * s.N + n]));
-            if (variants[v][2]) {   // the bf16 copy of C (epilogue CB path)
+            if (vrow(v)[2]) {   // the bf16 copy of C (epilogue CB path)
                 GemmParams q = p;
                 q.Cb = Cb; q.ldcb = s.N + pad;
                 gemm_launch(q, 0, nullptr, 0);
@@ -131,10 +139,55 @@ int main(int argc, char** argv) {
             const float med = m[m.size() / 2], mn = m[0];
             const double tf = 2.0 * M * s.N * (double)s.K / (med * 1e-3) / 1e12;
             const double tfb = 2.0 * M * s.N * (double)s.K / (mn * 1e-3) / 1e12;
-            printf("%s %s: median %.4f ms %.1f TF (best %.1f) maxerr %.2e bf16-copy relerr %.2e\n", s.name, vname[v], med, tf,
+            printf("%s %s: median %.4f ms %.1f TF (best %.1f) maxerr %.2e bf16-copy relerr %.2e\n", s.name, (ntmode ? vnt_name[v] : vname[v]), med, tf,
                    tfb, err, errb);
             fflush(stdout);
         }
+    }
+    // HB_RESID: the residual linears (out-projection and FFN2 forward: bias + residual, fp32 C; with and without the
+    // bf16 C plane)
+    if (getenv("HB_RESID")) {
+        float* bias;
+        CK(hipMalloc(&bias, 4096 * 4));
+        CK(hipMemset(bias, 0, 4096 * 4));
+        struct RS { const char* name; int K; bool cb; } rs[] = {{"outR  K1024 fp32", 1024, false}, {"outR  K1024 +Cb ", 1024, true},
+                                                               {"ffn2R K4096 fp32", 4096, false}};
+        for (auto& r : rs) {
+            GemmParams p;
+            gemm_init(p);
+            p.mode = 2;
+            p.A = reinterpret_cast<const float*>(A);
+            p.B = reinterpret_cast<const float*>(B);
+            p.M = M; p.N = 1024; p.K = r.K;
+            p.lda = r.K; p.ldb = r.K; p.tb = 1;
+            p.C = C; p.ldc = 1024;
+            p.Ab = A; p.Bb = B; p.ldab = r.K; p.ldbb = r.K;
+            p.epi = EPI_BIAS | EPI_RESID;
+            p.bias = bias;
+            p.R = R; p.ldr = 1024;
+            if (r.cb) { p.Cb = Cb; p.ldcb = 1024; }
+            std::vector<float> ms[8];
+            for (int rd = 0; rd < rounds; ++rd)
+                for (int v = 0; v < NV; ++v) {
+                    set_variant(v);
+                    for (int w = 0; w < 2; ++w) gemm_launch(p, 0, nullptr, 0);
+                    CK(hipEventRecord(e0, 0));
+                    for (int q = 0; q < reps; ++q) gemm_launch(p, 0, nullptr, 0);
+                    CK(hipEventRecord(e1, 0));
+                    CK(hipEventSynchronize(e1));
+                    float tt = 0;
+                    CK(hipEventElapsedTime(&tt, e0, e1));
+                    ms[v].push_back(tt / reps);
+                }
+            for (int v = 0; v < NV; ++v) {
+                std::vector<float> m = ms[v];
+                std::sort(m.begin(), m.end());
+                printf("%s %s: median %.4f ms %.1f TF  per tile round %.2f us\n", r.name, (ntmode ? vnt_name[v] : vname[v]),
+                       m[m.size() / 2], 2.0 * M * 1024.0 * r.K / (m[m.size() / 2] * 1e-3) / 1e12, m[m.size() / 2] * 1e3 / 4.0);
+                fflush(stdout);
+            }
+        }
+        return 0;
     }
     // K sweep (N = 4096, bf16 C plane only): time = fixed per-tile cost (prologue + epilogue) + K x loop rate
     if (getenv("HB_KSWEEP")) {
@@ -166,7 +219,7 @@ int main(int argc, char** argv) {
                 std::vector<float> m = ms[v];
                 std::sort(m.begin(), m.end());
                 const double tf = 2.0 * M * 4096.0 * K / (m[m.size() / 2] * 1e-3) / 1e12;
-                printf("ksweep K%5d %s: median %.4f ms %.1f TF  per tile round %.2f us\n", K, vname[v], m[m.size() / 2], tf,
+                printf("ksweep K%5d %s: median %.4f ms %.1f TF  per tile round %.2f us\n", K, (ntmode ? vnt_name[v] : vname[v]), m[m.size() / 2], tf,
                        m[m.size() / 2] * 1e3 / 16.0);
                 fflush(stdout);
             }
@@ -243,7 +296,7 @@ int main(int argc, char** argv) {
                 std::sort(m.begin(), m.end());
                 const double tf = 2.0 * M * 4096.0 * 1024.0 / (m[m.size() / 2] * 1e-3) / 1e12;
                 printf("%s %s: median %.4f ms %.1f TF (best %.1f) vs hb128 Cb relerr %.2e\n",
-                       fname[form], vname[v], m[m.size() / 2], tf,
+                       fname[form], (ntmode ? vnt_name[v] : vname[v]), m[m.size() / 2], tf,
                        2.0 * M * 4096.0 * 1024.0 / (m[0] * 1e-3) / 1e12, dmax);
                 fflush(stdout);
             }
