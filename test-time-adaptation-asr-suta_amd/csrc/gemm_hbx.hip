@@ -1239,6 +1239,11 @@ __device__ __forceinline__ void hbp_tile(const GemmParams& p, const TileId tid, 
     // -7 %, QKV -7 %, bf16-plane residual linears -2 %, with the band-ahead operand loads); the GELU / GELU' classes
     // measured 2 % slower with it in the loop (though faster in tools/hb_bench) and keep the remap
     constexpr bool NATIVE16 = EM == (EPI_BIAS | EPI_RESID | EPI_ROWMASK) && (DBG & 16) == 0;
+    // nontemporal epilogue stores: tools diagnostics (DBG 32) and the A/B library build (-DSUTA_EPI_NT=1)
+#ifndef SUTA_EPI_NT
+#define SUTA_EPI_NT 0
+#endif
+    constexpr bool NTST = (DBG & 32) != 0 || SUTA_EPI_NT != 0;
     if constexpr ((DBG & 1) != 0) {
 #pragma unroll
         for (int i = 0; i < 8; ++i)
@@ -1305,10 +1310,9 @@ __device__ __forceinline__ void hbp_tile(const GemmParams& p, const TileId tid, 
                         : p.C2 + z1 * p.sC21 + z0 * p.sC20;
         if (p.zrows) q.zrows = p.zrows + z1;
         if constexpr (M16 && NATIVE16 && (DBG & 8) == 0)
-            epilogue16t<CB, EM, (DBG & 32) != 0>(q, acc16, m0 + wr * 128, n0 + wc * 64, lane, lds + wid * 16384);
+            epilogue16t<CB, EM, NTST>(q, acc16, m0 + wr * 128, n0 + wc * 64, lane, lds + wid * 16384);
         else
-            epilogue_t<CB, EM, true, (DBG & 4), (DBG & 32) != 0>(q, acc, m0 + wr * 128, n0 + wc * 64, lane,
-                                                                 lds + wid * 16384);
+            epilogue_t<CB, EM, true, (DBG & 4), NTST>(q, acc, m0 + wr * 128, n0 + wc * 64, lane, lds + wid * 16384);
     }
 }
 
