@@ -1239,9 +1239,10 @@ __device__ __forceinline__ void hbp_tile(const GemmParams& p, const TileId tid, 
     // -7 %, QKV -7 %, bf16-plane residual linears -2 %, with the band-ahead operand loads); the GELU / GELU' classes
     // measured 2 % slower with it in the loop (though faster in tools/hb_bench) and keep the remap
     constexpr bool NATIVE16 = EM == (EPI_BIAS | EPI_RESID | EPI_ROWMASK) && (DBG & 16) == 0;
-    // nontemporal epilogue stores: tools diagnostics (DBG 32) and the A/B library build (-DSUTA_EPI_NT=1)
+    // nontemporal epilogue stores (round 6 default: the outputs stream past the caches on their way out; C4 +0.6 %,
+    // GEMM family -0.9 %, profiles/r6/ntab/summary.txt; -DSUTA_EPI_NT=0 builds the cached stores for A/B runs)
 #ifndef SUTA_EPI_NT
-#define SUTA_EPI_NT 0
+#define SUTA_EPI_NT 1
 #endif
     constexpr bool NTST = (DBG & 32) != 0 || SUTA_EPI_NT != 0;
     if constexpr ((DBG & 1) != 0) {
